@@ -1,0 +1,141 @@
+"""Prometheus instrumentation.
+
+HTTP metrics reproduce what `Instrumentator().instrument(app).expose(app)` gives the reference
+(`/root/reference/app.py:136-138`; prometheus-fastapi-instrumentator 7.0.0 defaults, SURVEY.md
+Appendix B.3):
+
+* `http_requests_total{method,status,handler}` — status grouped to `2xx`/`4xx`/...;
+* `http_request_size_bytes{handler}` / `http_response_size_bytes{handler}` — Summaries of the
+  Content-Length headers (0 when absent);
+* `http_request_duration_seconds{method,handler}` — buckets 0.1, 0.5, 1, +Inf;
+* `http_request_duration_highr_seconds` — unlabelled, 21 buckets 0.01 … 60;
+* default `process_*` / `python_*` collectors;
+* handler = route template (`none` for unmatched paths); `/metrics` itself is instrumented;
+  the middleware is outermost so 401/429/500 are counted.
+
+Engine/business metrics are added on top (SURVEY.md §5.5 target): cache hit/miss counters, LLM
+TTFT/TPOT/latency histograms, batch size, queue depth and KV-block usage gauges.
+
+Each app gets its own `CollectorRegistry` so that several apps can live in one process (tests,
+DP replicas) without duplicate-registration errors.
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, Optional
+
+from prometheus_client import (CollectorRegistry, Counter, GCCollector, Gauge, Histogram,
+                               PlatformCollector, ProcessCollector, Summary, generate_latest)
+
+CONTENT_TYPE = "text/plain; version=0.0.4; charset=utf-8"
+HIGHR_BUCKETS = (0.01, 0.025, 0.05, 0.075, 0.1, 0.25, 0.5, 0.75, 1, 1.5, 2, 2.5, 3, 3.5, 4, 4.5,
+                 5, 7.5, 10, 30, 60)
+LOWR_BUCKETS = (0.1, 0.5, 1)
+
+
+class ServiceMetrics:
+    def __init__(self, registry: Optional[CollectorRegistry] = None, default_collectors: bool = True):
+        r = self.registry = registry or CollectorRegistry(auto_describe=True)
+        if default_collectors:
+            ProcessCollector(registry=r)
+            PlatformCollector(registry=r)
+            GCCollector(registry=r)
+        self.requests_total = Counter(
+            "http_requests_total", "Total number of requests by method, status and handler.",
+            ("method", "status", "handler"), registry=r)
+        self.request_size = Summary(
+            "http_request_size_bytes",
+            "Content length of incoming requests by handler. Only value of header is respected. "
+            "Otherwise ignored. No percentile calculated. ", ("handler",), registry=r)
+        self.response_size = Summary(
+            "http_response_size_bytes",
+            "Content length of outgoing responses by handler. Only value of header is respected. "
+            "Otherwise ignored. No percentile calculated. ", ("handler",), registry=r)
+        self.latency_highr = Histogram(
+            "http_request_duration_highr_seconds",
+            "Latency with many buckets but no API specific labels. Made for more accurate "
+            "percentile calculations. ", buckets=HIGHR_BUCKETS, registry=r)
+        self.latency_lowr = Histogram(
+            "http_request_duration_seconds",
+            "Latency with only few buckets by handler. Made to be only used if aggregation by "
+            "handler is important. ", ("method", "handler"), buckets=LOWR_BUCKETS, registry=r)
+        # --- engine / business metrics (not in the reference) ---
+        self.cache_hits = Counter("kubectl_agent_cache_hits_total", "Response cache hits.", registry=r)
+        self.cache_misses = Counter("kubectl_agent_cache_misses_total", "Response cache misses.", registry=r)
+        self.llm_latency = Histogram("llm_request_seconds", "End-to-end LLM generation latency.",
+                                     buckets=HIGHR_BUCKETS, registry=r)
+        self.llm_ttft = Histogram("llm_ttft_seconds", "Time to first token.", buckets=HIGHR_BUCKETS, registry=r)
+        self.llm_tpot = Histogram("llm_tpot_seconds", "Time per output token after the first.",
+                                  buckets=(0.001, 0.002, 0.003, 0.005, 0.0075, 0.01, 0.02, 0.05, 0.1, 0.25),
+                                  registry=r)
+        self.llm_queue_wait = Histogram("llm_queue_wait_seconds", "Scheduler queue wait.",
+                                        buckets=HIGHR_BUCKETS, registry=r)
+        self.llm_batch_size = Gauge("llm_batch_size", "Sequences in the last engine step.", registry=r)
+        self.llm_queue_depth = Gauge("llm_queue_depth", "Requests waiting for the engine.", registry=r)
+        self.llm_kv_blocks_used = Gauge("llm_kv_blocks_used", "Paged-KV blocks in use.", registry=r)
+        self.llm_errors = Counter("llm_errors_total", "LLM failures by kind.", ("kind",), registry=r)
+        self.execute_duration = Histogram("execute_duration_seconds", "kubectl subprocess wall time.",
+                                          buckets=HIGHR_BUCKETS, registry=r)
+
+    def render(self) -> bytes:
+        return generate_latest(self.registry)
+
+
+def _route_name(scope, routes) -> str:
+    from starlette.routing import Match
+
+    partial = None
+    for route in routes:
+        match, _ = route.matches(scope)
+        if match == Match.FULL:
+            return route.path
+        if match == Match.PARTIAL and partial is None:
+            partial = route.path
+    return partial if partial is not None else "none"
+
+
+class PrometheusMiddleware:
+    """Pure-ASGI HTTP instrumentation (the Instrumentator middleware's observable behaviour)."""
+
+    def __init__(self, app, metrics: ServiceMetrics, routes: Callable[[], list]):
+        self.app = app
+        self.metrics = metrics
+        self.routes = routes
+
+    async def __call__(self, scope, receive, send):
+        if scope["type"] != "http":
+            await self.app(scope, receive, send)
+            return
+        start = time.perf_counter()
+        status = [500]
+        resp_len = [0]
+
+        async def send_wrapper(message):
+            if message["type"] == "http.response.start":
+                status[0] = message["status"]
+                for k, v in message.get("headers", ()):
+                    if k == b"content-length":
+                        resp_len[0] = int(v)
+                        break
+            await send(message)
+
+        try:
+            await self.app(scope, receive, send_wrapper)
+        finally:
+            dur = time.perf_counter() - start
+            handler = _route_name(scope, self.routes())
+            method = scope.get("method", "GET")
+            req_len = 0
+            for k, v in scope.get("headers", ()):
+                if k == b"content-length":
+                    try:
+                        req_len = int(v)
+                    except ValueError:
+                        req_len = 0
+                    break
+            m = self.metrics
+            m.requests_total.labels(method, "%dxx" % (status[0] // 100), handler).inc()
+            m.request_size.labels(handler).observe(req_len)
+            m.response_size.labels(handler).observe(resp_len[0])
+            m.latency_highr.observe(dur)
+            m.latency_lowr.labels(method, handler).observe(dur)
