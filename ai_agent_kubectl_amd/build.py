@@ -1,0 +1,98 @@
+"""Build the in-tree native artefacts.
+
+* `build_hip()`    — compiles every `csrc/*.hip` for gfx950 with hipcc into
+                     `ops/lib/libkagent_hip.so` (one object per source, compiled in parallel,
+                     then linked).  Cross-compiles without a GPU.
+* `build_runtime()`— compiles the C++ host runtime (`runtime/*.cpp`: tokenizer trie, paged-KV
+                     block manager, batch-metadata builder) into `runtime/_native*.so` via pybind11.
+
+Both are incremental (rebuild only when a source is newer than the output).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "ops", "lib")
+HIP_LIB = os.path.join(LIB_DIR, "libkagent_hip.so")
+RUNTIME_DIR = os.path.join(PKG, "runtime")
+ARCH = os.environ.get("KA_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _newer(srcs, out) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > t for s in srcs)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("command failed: %s\n%s" % (" ".join(cmd), r.stdout))
+    return r.stdout
+
+
+def build_hip(force: bool = False, verbose: bool = False, extra_flags=()) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    os.makedirs(LIB_DIR, exist_ok=True)
+    if not force and not _newer(srcs + headers, HIP_LIB):
+        return HIP_LIB
+    obj_dir = os.path.join(LIB_DIR, "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-Wno-unused-result", *extra_flags]
+
+    def compile_one(src):
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+        if force or _newer([src] + headers, obj):
+            _run([HIPCC, *flags, "-c", src, "-o", obj])
+        return obj
+
+    jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
+    with cf.ThreadPoolExecutor(max(1, jobs)) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = HIP_LIB + ".tmp"
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp])
+    os.replace(tmp, HIP_LIB)
+    if verbose:
+        print("built", HIP_LIB)
+    return HIP_LIB
+
+
+def build_runtime(force: bool = False, verbose: bool = False) -> str:
+    srcs = sorted(glob.glob(os.path.join(RUNTIME_DIR, "*.cpp")))
+    if not srcs:
+        return ""
+    import pybind11
+
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    out = os.path.join(RUNTIME_DIR, "_native" + suffix)
+    if not force and not _newer(srcs + glob.glob(os.path.join(RUNTIME_DIR, "*.h")), out):
+        return out
+    inc = [pybind11.get_include(), sysconfig.get_paths()["include"]]
+    cmd = ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", *srcs,
+           *[f"-I{i}" for i in inc], "-o", out + ".tmp"]
+    if os.environ.get("KA_SANITIZE"):
+        cmd[1:1] = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
+    _run(cmd)
+    os.replace(out + ".tmp", out)
+    if verbose:
+        print("built", out)
+    return out
+
+
+def build_all(force: bool = False, verbose: bool = True):
+    return build_hip(force, verbose), build_runtime(force, verbose)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

@@ -1,0 +1,368 @@
+// Paged attention on MFMA (K5 prefill, K6 decode) for head_dim 128, KV block size 16, GQA group G.
+//
+// Cache layouts (written by rope_kv_kernel in elementwise.hip):
+//   k_cache [NB, Hkv, 16, 128]  token-major: the K^T B-operand fragment of lane l (token l&15, dims
+//                               8*(l>>4)..+7 of a 32-wide k-step) is one contiguous 16-B load;
+//   v_cache [NB, Hkv, 128, 16]  dim-major:   the V B-operand fragment of lane l (tokens 8*(l>>4)..+7,
+//                               dim l&15 of an n-tile) is one contiguous 16-B load.
+// MFMA: v_mfma_f32_16x16x32_bf16.  A[row l&15][k 8*(l>>4)+j], B[k 8*(l>>4)+j][col l&15],
+//       C[row 4*(l>>4)+r][col l&15] (cdna_hip_programming.md §3).
+// Softmax is online (running max m, running sum l per query row) in the exp2 domain.
+//
+// Decode (one query token per sequence): one workgroup per (kv head, sequence); the G query heads
+// sharing the kv head are the 16 (zero-padded) MFMA rows; the 4 waves stride over 32-token chunks
+// of the context, K/V fragments go straight from HBM to VGPRs (guide §5 table, 'GEMV / M <= 16'
+// row: no reuse across waves, so an LDS round trip would be pure overhead), and the waves' partial
+// (m, l, O) are merged through LDS.  P is re-laid from the C layout to the A layout through a
+// per-wave LDS scratch.
+//
+// Prefill (varlen, with cached context for prefix caching / chunked prefill): one workgroup per
+// (64 query rows = 64/G tokens x G heads, kv head, sequence); 4 waves x 16 rows.  K and V^T tiles
+// of 32 tokens are shared by all 4 waves, so they are staged in LDS (XOR-swizzled against bank
+// conflicts, guide §5.5 T2) with the next tile's global loads issued into registers before the
+// current tile's MFMAs (T14 issue-early / write-late).
+#include "common.h"
+
+#define HD 128
+#define KBS 16
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
+                                                           const bf16_t* __restrict__ k_cache,
+                                                           const bf16_t* __restrict__ v_cache,
+                                                           const int* __restrict__ block_tables, int max_blocks,
+                                                           const int* __restrict__ ctx_lens, int hq, int hkv,
+                                                           float scale_log2) {
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int G = hq / hkv;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int ctx = ctx_lens[b];
+
+  __shared__ __attribute__((aligned(16))) float smem[4 * 16 * 2 + 4 * 16 * (HD + 4)];
+  __shared__ __attribute__((aligned(16))) bf16_t p_lds[4][16 * 32];
+  float* sm = smem;                 // [4][16]
+  float* sl = smem + 64;            // [4][16]
+  float* so = smem + 128;           // [4][16][HD+4]
+
+  bf16x8 qf[4];
+  {
+    const int row = col;
+    if (row < G) {
+      const bf16_t* qp = q + ((size_t)b * hq + h * G + row) * HD + 8 * grp;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(*reinterpret_cast<const uint4*>(qp + 32 * ks));
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(make_uint4(0, 0, 0, 0));
+    }
+  }
+  float m[4], l[4];
+  f32x4 o[8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m[r] = -INFINITY;
+    l[r] = 0.f;
+  }
+#pragma unroll
+  for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int* bt = block_tables + (size_t)b * max_blocks;
+  const int nchunks = (ctx + 31) >> 5;
+  const size_t head_stride = (size_t)KBS * HD;  // elements per (block, head)
+  bf16_t* pw = p_lds[wave];
+  for (int c = wave; c < nchunks; c += 4) {
+    const int t0 = c * 32;
+    const int blk0 = bt[2 * c];
+    const int blk1 = (t0 + 16 < ctx) ? bt[2 * c + 1] : blk0;
+    // ---- S = Q K^T for the two 16-token halves ----
+    f32x4 s[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int blk = j ? blk1 : blk0;
+      const bf16_t* kp = k_cache + ((size_t)blk * hkv + h) * head_stride + col * HD + 8 * grp;
+      uint4 kr[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) kr[ks] = *reinterpret_cast<const uint4*>(kp + 32 * ks);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) acc = mfma16x16x32(qf[ks], as_bf16x8(kr[ks]), acc);
+      s[j] = acc;
+    }
+    // ---- V fragments (issued before the softmax so their latency hides under it) ----
+    uint4 vr[8];
+    {
+      const int blk = (grp >> 1) ? blk1 : blk0;
+      const bf16_t* vp = v_cache + ((size_t)blk * hkv + h) * head_stride + col * KBS + 8 * (grp & 1);
+#pragma unroll
+      for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(vp + (size_t)n * 16 * KBS);
+    }
+    // ---- online softmax over this chunk ----
+    float alpha[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x0 = (t0 + col < ctx) ? s[0][r] * scale_log2 : -INFINITY;
+      float x1 = (t0 + 16 + col < ctx) ? s[1][r] * scale_log2 : -INFINITY;
+      const float mx = row16_max(fmaxf(x0, x1));
+      const float mn = fmaxf(m[r], mx);
+      alpha[r] = exp2f(m[r] - mn);
+      const float p0 = exp2f(x0 - mn), p1 = exp2f(x1 - mn);
+      l[r] = l[r] * alpha[r] + row16_sum(p0 + p1);
+      m[r] = mn;
+      const int prow = 4 * grp + r;
+      const int sw = (prow >> 2) & 3;
+      pw[prow * 32 + ((((col >> 3)) ^ sw) << 3) + (col & 7)] = f2bf(p0);
+      pw[prow * 32 + ((((16 + col) >> 3) ^ sw) << 3) + (col & 7)] = f2bf(p1);
+    }
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[n][r] *= alpha[r];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bf16x8 pf = as_bf16x8(*reinterpret_cast<const uint4*>(pw + col * 32 + ((grp ^ ((col >> 2) & 3)) << 3)));
+#pragma unroll
+    for (int n = 0; n < 8; ++n) o[n] = mfma16x16x32(pf, as_bf16x8(vr[n]), o[n]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // P scratch reads done before next chunk's writes
+  }
+
+  // ---- merge the 4 waves ----
+  if (col == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sm[wave * 16 + 4 * grp + r] = m[r];
+      sl[wave * 16 + 4 * grp + r] = l[r];
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) so[(wave * 16 + 4 * grp + r) * (HD + 4) + n * 16 + col] = o[n][r];
+  }
+  __syncthreads();
+  const int row = threadIdx.x >> 4;          // 16 rows
+  const int d0 = (threadIdx.x & 15) * 8;     // 8 dims per thread
+  if (row < G) {
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[w * 16 + row]);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float den = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float e = exp2f(sm[w * 16 + row] - M);
+        den += e * sl[w * 16 + row];
+        const float* src = so + (w * 16 + row) * (HD + 4) + d0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += e * src[k];
+      }
+    }
+    const float inv = den > 0.f ? 1.f / den : 0.f;
+    uint4 res = make_uint4(pack2(acc[0] * inv, acc[1] * inv), pack2(acc[2] * inv, acc[3] * inv),
+                           pack2(acc[4] * inv, acc[5] * inv), pack2(acc[6] * inv, acc[7] * inv));
+    *reinterpret_cast<uint4*>(out + ((size_t)b * hq + h * G + row) * HD + d0) = res;
+  }
+}
+
+extern "C" int ka_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache,
+                               const int* block_tables, int max_blocks, const int* ctx_lens, int batch, int hq,
+                               int hkv, int head_dim, int block_size, float scale, hipStream_t stream) {
+  if (batch <= 0) return 0;
+  if (head_dim != HD || block_size != KBS || hq % hkv != 0 || hq / hkv > 16) return (int)hipErrorInvalidValue;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(paged_decode_kernel, dim3(hkv, batch), dim3(256), 0, stream, static_cast<bf16_t*>(out),
+                     static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
+                     static_cast<const bf16_t*>(v_cache), block_tables, max_blocks, ctx_lens, hq, hkv, scale_log2);
+  KA_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Varlen paged prefill.  q/out [T, Hq, 128]; seq s owns query rows q_starts[s] .. q_starts[s+1]-1,
+// which are the LAST q_len positions of its ctx_lens[s]-token context (earlier positions are
+// already in the cache: shared prefix blocks or previous chunks).  Causal within the context.
+struct PrefillSmem {
+  uint4 k[32][16];        // [token][16-B chunk ^ (token & 15)]            8 KiB
+  uint4 v[HD][4];         // [dim][16-B chunk ^ ((dim >> 2) & 3)] tokens    8 KiB
+  bf16_t p[4][16 * 32];   // per-wave P scratch                             4 KiB
+};
+
+__device__ __forceinline__ void prefill_load_tile(uint4 (&kreg)[2], uint4 (&vreg)[2], const bf16_t* __restrict__ k_cache,
+                                                  const bf16_t* __restrict__ v_cache, const int* __restrict__ bt,
+                                                  int nblocks, int tile, int h, int hkv) {
+  const int tid = threadIdx.x;
+  const size_t head_stride = (size_t)KBS * HD;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = tid + 256 * i;           // 512 pieces of 16 B per operand
+    // K: token = p >> 4, chunk = p & 15
+    {
+      const int tok = p >> 4, ch = p & 15;
+      const int bi = 2 * tile + (tok >> 4);
+      const int blk = bi < nblocks ? bt[bi] : bt[0];
+      kreg[i] = *reinterpret_cast<const uint4*>(k_cache + ((size_t)blk * hkv + h) * head_stride + (tok & 15) * HD + ch * 8);
+    }
+    // V^T: dim = p >> 2, chunk = p & 3 (chunks 0,1 from the first block, 2,3 from the second)
+    {
+      const int dim = p >> 2, ch = p & 3;
+      const int bi = 2 * tile + (ch >> 1);
+      const int blk = bi < nblocks ? bt[bi] : bt[0];
+      vreg[i] = *reinterpret_cast<const uint4*>(v_cache + ((size_t)blk * hkv + h) * head_stride + dim * KBS + (ch & 1) * 8);
+    }
+  }
+}
+
+__device__ __forceinline__ void prefill_store_tile(PrefillSmem& s, const uint4 (&kreg)[2], const uint4 (&vreg)[2]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = tid + 256 * i;
+    const int tok = p >> 4, ch = p & 15;
+    s.k[tok][ch ^ (tok & 15)] = kreg[i];
+    const int dim = p >> 2, vc = p & 3;
+    s.v[dim][vc ^ ((dim >> 2) & 3)] = vreg[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void paged_prefill_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
+                                                            const bf16_t* __restrict__ k_cache,
+                                                            const bf16_t* __restrict__ v_cache,
+                                                            const int* __restrict__ block_tables, int max_blocks,
+                                                            const int* __restrict__ q_starts,
+                                                            const int* __restrict__ ctx_lens, int hq, int hkv,
+                                                            float scale_log2) {
+  const int qt = blockIdx.x, h = blockIdx.y, sq = blockIdx.z;
+  const int G = hq / hkv;
+  const int tpt = 64 / G;  // tokens per tile
+  const int q0 = q_starts[sq];
+  const int qlen = q_starts[sq + 1] - q0;
+  const int tile_tok0 = qt * tpt;
+  if (tile_tok0 >= qlen) return;
+  const int ctx = ctx_lens[sq];
+  const int base_pos = ctx - qlen;
+  const int last_tok = min(tile_tok0 + tpt, qlen) - 1;
+  const int kv_end = base_pos + last_tok + 1;
+  const int ntiles = (kv_end + 31) >> 5;
+  const int nblocks = (ctx + KBS - 1) / KBS;
+  const int* bt = block_tables + (size_t)sq * max_blocks;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  __shared__ PrefillSmem s;
+
+  // Q fragments for A rows (row = wave*16 + col)
+  bf16x8 qf[4];
+  {
+    const int row = wave * 16 + col;
+    const int tok = tile_tok0 + row / G;
+    const int g = row % G;
+    if (tok < qlen) {
+      const bf16_t* qp = q + ((size_t)(q0 + tok) * hq + h * G + g) * HD + 8 * grp;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(*reinterpret_cast<const uint4*>(qp + 32 * ks));
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(make_uint4(0, 0, 0, 0));
+    }
+  }
+  // query positions of this lane's 4 C rows
+  int qpos[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = wave * 16 + 4 * grp + r;
+    const int tok = tile_tok0 + row / G;
+    qpos[r] = tok < qlen ? base_pos + tok : kv_end - 1;
+  }
+  float m[4], l[4];
+  f32x4 o[8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m[r] = -INFINITY;
+    l[r] = 0.f;
+  }
+#pragma unroll
+  for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 kreg[2], vreg[2];
+  prefill_load_tile(kreg, vreg, k_cache, v_cache, bt, nblocks, 0, h, hkv);
+  bf16_t* pw = s.p[wave];
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();  // previous tile's LDS reads are done
+    prefill_store_tile(s, kreg, vreg);
+    __syncthreads();
+    if (t + 1 < ntiles) prefill_load_tile(kreg, vreg, k_cache, v_cache, bt, nblocks, t + 1, h, hkv);
+    const int t0 = t * 32;
+    f32x4 sc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int tok = 16 * j + col;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const uint4 kf = s.k[tok][(4 * ks + grp) ^ (tok & 15)];
+        acc = mfma16x16x32(qf[ks], as_bf16x8(kf), acc);
+      }
+      sc[j] = acc;
+    }
+    float alpha[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float x0 = (t0 + col <= qpos[r]) ? sc[0][r] * scale_log2 : -INFINITY;
+      const float x1 = (t0 + 16 + col <= qpos[r]) ? sc[1][r] * scale_log2 : -INFINITY;
+      const float mx = row16_max(fmaxf(x0, x1));
+      const float mn = fmaxf(m[r], mx);
+      // mn == -inf only if every key so far is masked for this row (not possible for t == 0)
+      alpha[r] = (mn == -INFINITY) ? 1.f : exp2f(m[r] - mn);
+      const float p0 = (mn == -INFINITY) ? 0.f : exp2f(x0 - mn);
+      const float p1 = (mn == -INFINITY) ? 0.f : exp2f(x1 - mn);
+      l[r] = l[r] * alpha[r] + row16_sum(p0 + p1);
+      m[r] = mn;
+      const int prow = 4 * grp + r;
+      const int sw = (prow >> 2) & 3;
+      pw[prow * 32 + (((col >> 3) ^ sw) << 3) + (col & 7)] = f2bf(p0);
+      pw[prow * 32 + ((((16 + col) >> 3) ^ sw) << 3) + (col & 7)] = f2bf(p1);
+    }
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[n][r] *= alpha[r];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bf16x8 pf = as_bf16x8(*reinterpret_cast<const uint4*>(pw + col * 32 + ((grp ^ ((col >> 2) & 3)) << 3)));
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int dim = n * 16 + col;
+      const uint4 vf = s.v[dim][grp ^ ((dim >> 2) & 3)];
+      o[n] = mfma16x16x32(pf, as_bf16x8(vf), o[n]);
+    }
+  }
+  // epilogue: rows 4*grp + r of this wave
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = wave * 16 + 4 * grp + r;
+    const int tok = tile_tok0 + row / G;
+    const int g = row % G;
+    if (tok >= qlen) continue;
+    const float inv = l[r] > 0.f ? 1.f / l[r] : 0.f;
+    bf16_t* op = out + ((size_t)(q0 + tok) * hq + h * G + g) * HD + col;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) op[n * 16] = f2bf(o[n][r] * inv);
+  }
+}
+
+extern "C" int ka_paged_prefill(void* out, const void* q, const void* k_cache, const void* v_cache,
+                                const int* block_tables, int max_blocks, const int* q_starts, const int* ctx_lens,
+                                int num_seqs, int max_q_len, int hq, int hkv, int head_dim, int block_size,
+                                float scale, hipStream_t stream) {
+  if (num_seqs <= 0 || max_q_len <= 0) return 0;
+  const int G = hkv > 0 ? hq / hkv : 0;
+  if (head_dim != HD || block_size != KBS || hq % hkv != 0 || G > 64 || 64 % G != 0) return (int)hipErrorInvalidValue;
+  const int tpt = 64 / G;
+  const int qtiles = (max_q_len + tpt - 1) / tpt;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(paged_prefill_kernel, dim3(qtiles, hkv, num_seqs), dim3(256), 0, stream,
+                     static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
+                     static_cast<const bf16_t*>(v_cache), block_tables, max_blocks, q_starts, ctx_lens, hq, hkv,
+                     scale_log2);
+  KA_CHECK_LAUNCH();
+}

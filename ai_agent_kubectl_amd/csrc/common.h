@@ -1,0 +1,71 @@
+// Shared helpers for the CDNA4 (gfx950, MI355X) kernels of the kubectl-agent inference engine.
+//
+// Conventions (see /opt/skills/guides/cdna_hip_programming.md):
+//   * wave = 64 lanes; every block size is a multiple of 64;
+//   * bf16 is moved as raw 16-bit words and converted with bit ops (round-to-nearest-even, the
+//     same rounding torch uses), loads/stores are 16 B per lane wherever the layout allows
+//     (Guideline 13: hipcc never vectorises scalar bf16 accesses);
+//   * every launcher is `extern "C"`, takes the HIP stream explicitly and returns the hipError_t
+//     of the launch, so the Python side (ops/_hip.py, ctypes) can be captured in hipGraphs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define KA_DEV __device__ __forceinline__
+
+KA_DEV float bf2f(bf16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
+
+KA_DEV bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+// two packed bf16 <-> two floats
+KA_DEV float lo_f(uint32_t w) { return __uint_as_float(w << 16); }
+KA_DEV float hi_f(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+KA_DEV uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+template <typename T>
+KA_DEV T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+KA_DEV T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// reduce over the 16 lanes that share (lane >> 4): the column index of an MFMA 16x16 C tile.
+KA_DEV float row16_max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 1, 64));
+  v = fmaxf(v, __shfl_xor(v, 2, 64));
+  v = fmaxf(v, __shfl_xor(v, 4, 64));
+  v = fmaxf(v, __shfl_xor(v, 8, 64));
+  return v;
+}
+KA_DEV float row16_sum(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
+KA_DEV f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+KA_DEV bf16x8 as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
+
+#define KA_CHECK_LAUNCH() return (int)hipGetLastError()

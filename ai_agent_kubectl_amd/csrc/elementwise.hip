@@ -1,0 +1,226 @@
+// Memory-bound kernels: fused residual-add + RMSNorm (K2), neox RoPE fused with the paged-KV append
+// (K4), SiLU*mul (K8 epilogue), embedding gather (K1).  All bf16 I/O is 16 B per lane.
+//
+// Layouts (shared with attention.hip and the torch references in ops/reference.py):
+//   qkv      [T, (Hq + 2*Hkv) * D]   output of the fused QKV projection
+//   cos_sin  [max_pos, D] f32        cos in [0, D/2), sin in [D/2, D) (host-precomputed, guide App. B)
+//   k_cache  [NB, Hkv, BS, D]        token-major blocks: a 16-token K block is one 4 KiB run
+//   v_cache  [NB, Hkv, D, BS]        dim-major blocks: 8 consecutive tokens of one dim are 16 B, which
+//                                    is exactly the B-operand fragment of the P*V MFMA
+//   slot_mapping[t] = block * BS + offset, or -1 for padding tokens (no cache write).
+#include "common.h"
+
+// ------------------------------------------------------------------------------------------------
+// RMSNorm, optionally fused with the residual add:   r = x (+ residual);  residual = r;
+//                                                  out = r * rsqrt(mean(r^2) + eps) * w
+template <int NT, int MAXV>
+__global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16_t* __restrict__ out, bf16_t* __restrict__ residual,
+                                                     const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                     int hidden, float eps) {
+  const int row = blockIdx.x;
+  const int nvec = hidden >> 3;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * hidden);
+  uint4* rr = residual ? reinterpret_cast<uint4*>(residual + (size_t)row * hidden) : nullptr;
+  float v[MAXV][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) {
+      uint4 a = xr[idx];
+      uint32_t aw[4] = {a.x, a.y, a.z, a.w};
+      if (rr) {
+        uint4 b = rr[idx];
+        uint32_t bw[4] = {b.x, b.y, b.z, b.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          // round the sum to bf16 first: the residual stream is stored in bf16
+          float s0 = bf2f(f2bf(lo_f(aw[k]) + lo_f(bw[k])));
+          float s1 = bf2f(f2bf(hi_f(aw[k]) + hi_f(bw[k])));
+          v[i][2 * k] = s0;
+          v[i][2 * k + 1] = s1;
+          o[k] = pack2(s0, s1);
+        }
+        rr[idx] = make_uint4(o[0], o[1], o[2], o[3]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[i][2 * k] = lo_f(aw[k]);
+          v[i][2 * k + 1] = hi_f(aw[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ss += v[i][k] * v[i][k];
+    }
+  }
+  __shared__ float red[NT / 64];
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) tot += red[i];
+  const float scale = rsqrtf(tot / (float)hidden + eps);
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * hidden);
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) {
+      uint4 g = wr[idx];
+      uint32_t gw[4] = {g.x, g.y, g.z, g.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        o[k] = pack2(v[i][2 * k] * scale * lo_f(gw[k]), v[i][2 * k + 1] * scale * hi_f(gw[k]));
+      orow[idx] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+extern "C" int ka_rmsnorm(void* out, void* residual, const void* x, const void* w, int rows, int hidden,
+                          float eps, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (hidden % 8 != 0 || hidden > 256 * 8 * 4) return (int)hipErrorInvalidValue;
+  const int nvec = hidden / 8;
+  auto* o = static_cast<bf16_t*>(out);
+  auto* r = static_cast<bf16_t*>(residual);
+  auto* xi = static_cast<const bf16_t*>(x);
+  auto* wi = static_cast<const bf16_t*>(w);
+  if (nvec <= 256)
+    hipLaunchKernelGGL((rmsnorm_kernel<256, 1>), dim3(rows), dim3(256), 0, stream, o, r, xi, wi, hidden, eps);
+  else if (nvec <= 512)
+    hipLaunchKernelGGL((rmsnorm_kernel<256, 2>), dim3(rows), dim3(256), 0, stream, o, r, xi, wi, hidden, eps);
+  else
+    hipLaunchKernelGGL((rmsnorm_kernel<256, 4>), dim3(rows), dim3(256), 0, stream, o, r, xi, wi, hidden, eps);
+  KA_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// RoPE (neox / rotate-half pairs (i, i + D/2)) on q and k, q -> q_out [T, Hq, D], k and v -> paged cache.
+__global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_cache,
+                                                      bf16_t* __restrict__ v_cache, const bf16_t* __restrict__ qkv,
+                                                      const int* __restrict__ positions,
+                                                      const float* __restrict__ cos_sin,
+                                                      const int* __restrict__ slot_mapping, int hq, int hkv, int d,
+                                                      int bs) {
+  const int t = blockIdx.x;
+  const int half = d >> 1;
+  const int qkv_stride = (hq + 2 * hkv) * d;
+  const bf16_t* row = qkv + (size_t)t * qkv_stride;
+  const int pos = positions[t];
+  const int slot = slot_mapping[t];
+  const float* cs = cos_sin + (size_t)pos * d;
+  const int chunks = half >> 2;  // 4 pairs per item
+  const int n_rot = (hq + hkv) * chunks;
+  const int blk = slot >= 0 ? slot / bs : 0;
+  const int off = slot >= 0 ? slot % bs : 0;
+  for (int it = threadIdx.x; it < n_rot; it += blockDim.x) {
+    const int h = it / chunks;
+    const int i = (it % chunks) * 4;
+    const bf16_t* src = row + h * d;  // q heads first, then k heads (contiguous in qkv)
+    uint2 a = *reinterpret_cast<const uint2*>(src + i);
+    uint2 b = *reinterpret_cast<const uint2*>(src + i + half);
+    float4 c = *reinterpret_cast<const float4*>(cs + i);
+    float4 s = *reinterpret_cast<const float4*>(cs + half + i);
+    float x1[4] = {lo_f(a.x), hi_f(a.x), lo_f(a.y), hi_f(a.y)};
+    float x2[4] = {lo_f(b.x), hi_f(b.x), lo_f(b.y), hi_f(b.y)};
+    float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
+    float o1[4], o2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o1[k] = x1[k] * cc[k] - x2[k] * ss[k];
+      o2[k] = x2[k] * cc[k] + x1[k] * ss[k];
+    }
+    uint2 r1 = make_uint2(pack2(o1[0], o1[1]), pack2(o1[2], o1[3]));
+    uint2 r2 = make_uint2(pack2(o2[0], o2[1]), pack2(o2[2], o2[3]));
+    bf16_t* dst;
+    if (h < hq) {
+      dst = q_out + ((size_t)t * hq + h) * d;
+    } else {
+      if (slot < 0) continue;
+      dst = k_cache + (((size_t)blk * hkv + (h - hq)) * bs + off) * d;
+    }
+    *reinterpret_cast<uint2*>(dst + i) = r1;
+    *reinterpret_cast<uint2*>(dst + i + half) = r2;
+  }
+  if (slot < 0) return;
+  const int vchunks = d >> 3;
+  const bf16_t* vsrc = row + (hq + hkv) * d;
+  for (int it = threadIdx.x; it < hkv * vchunks; it += blockDim.x) {
+    const int h = it / vchunks;
+    const int i = (it % vchunks) * 8;
+    uint4 v = *reinterpret_cast<const uint4*>(vsrc + h * d + i);
+    bf16_t e[8] = {(bf16_t)v.x, (bf16_t)(v.x >> 16), (bf16_t)v.y, (bf16_t)(v.y >> 16),
+                   (bf16_t)v.z, (bf16_t)(v.z >> 16), (bf16_t)v.w, (bf16_t)(v.w >> 16)};
+    bf16_t* dst = v_cache + (((size_t)blk * hkv + h) * d + i) * bs + off;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dst[(size_t)k * bs] = e[k];
+  }
+}
+
+extern "C" int ka_rope_kv(void* q_out, void* k_cache, void* v_cache, const void* qkv, const int* positions,
+                          const float* cos_sin, const int* slot_mapping, int tokens, int hq, int hkv, int d, int bs,
+                          hipStream_t stream) {
+  if (tokens <= 0) return 0;
+  if (d % 16 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(rope_kv_kernel, dim3(tokens), dim3(256), 0, stream, static_cast<bf16_t*>(q_out),
+                     static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache),
+                     static_cast<const bf16_t*>(qkv), positions, cos_sin, slot_mapping, hq, hkv, d, bs);
+  KA_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// out[t, :I] = silu(gu[t, :I]) * gu[t, I:2I]     (gate | up halves of the fused gate_up projection)
+__global__ __launch_bounds__(256) void silu_mul_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ gu,
+                                                       int inter, long total_vec) {
+  const int vpr = inter >> 3;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total_vec; i += (long)gridDim.x * blockDim.x) {
+    const long t = i / vpr;
+    const int c = (int)(i % vpr) * 8;
+    const bf16_t* r = gu + t * 2 * (long)inter;
+    uint4 g = *reinterpret_cast<const uint4*>(r + c);
+    uint4 u = *reinterpret_cast<const uint4*>(r + inter + c);
+    uint32_t gw[4] = {g.x, g.y, g.z, g.w}, uw[4] = {u.x, u.y, u.z, u.w}, o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float g0 = lo_f(gw[k]), g1 = hi_f(gw[k]);
+      float s0 = g0 / (1.f + __expf(-g0)), s1 = g1 / (1.f + __expf(-g1));
+      o[k] = pack2(s0 * lo_f(uw[k]), s1 * hi_f(uw[k]));
+    }
+    *reinterpret_cast<uint4*>(out + t * (long)inter + c) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+extern "C" int ka_silu_mul(void* out, const void* gu, int tokens, int inter, hipStream_t stream) {
+  if (tokens <= 0) return 0;
+  if (inter % 8 != 0) return (int)hipErrorInvalidValue;
+  const long total = (long)tokens * (inter / 8);
+  const int grid = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(grid), dim3(256), 0, stream, static_cast<bf16_t*>(out),
+                     static_cast<const bf16_t*>(gu), inter, total);
+  KA_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// out[t, :] = table[ids[t], :]   (ids outside [0, vocab) -> zeros; vocab-parallel shards pass an offset)
+__global__ __launch_bounds__(256) void embedding_kernel(bf16_t* __restrict__ out, const int* __restrict__ ids,
+                                                        const bf16_t* __restrict__ table, int hidden, int vocab,
+                                                        int vocab_offset) {
+  const int t = blockIdx.x;
+  const int id = ids[t] - vocab_offset;
+  const bool valid = id >= 0 && id < vocab;
+  const uint4* src = reinterpret_cast<const uint4*>(table + (size_t)(valid ? id : 0) * hidden);
+  uint4* dst = reinterpret_cast<uint4*>(out + (size_t)t * hidden);
+  for (int i = threadIdx.x; i < (hidden >> 3); i += blockDim.x) dst[i] = valid ? src[i] : make_uint4(0, 0, 0, 0);
+}
+
+extern "C" int ka_embedding(void* out, const int* ids, const void* table, int tokens, int hidden, int vocab,
+                            int vocab_offset, hipStream_t stream) {
+  if (tokens <= 0) return 0;
+  if (hidden % 8 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(embedding_kernel, dim3(tokens), dim3(256), 0, stream, static_cast<bf16_t*>(out), ids,
+                     static_cast<const bf16_t*>(table), hidden, vocab, vocab_offset);
+  KA_CHECK_LAUNCH();
+}

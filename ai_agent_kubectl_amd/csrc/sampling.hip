@@ -1,0 +1,123 @@
+// Greedy sampling with the SAFE_DECODE token mask (K10 epilogue) and the Mixtral router top-k (K11).
+//
+// masked_argmax: one workgroup per row; each lane scans 8 logits per 16-B load, skips tokens whose
+// bit is clear in the row's mask (mask_idx[row] < 0 = unmasked), keeps (max, lowest index), then a
+// wave shuffle + LDS reduction.  The same kernel serves the vocab-parallel LM head under TP: each
+// rank reports (value, global index = local + vocab_offset) and the ranks' winners are combined
+// after an all-gather (ops/__init__.py: tp_argmax).  temperature=0 in the reference (app.py:109).
+#include "common.h"
+
+template <int NT>
+__global__ __launch_bounds__(NT) void masked_argmax_kernel(int* __restrict__ out_idx, float* __restrict__ out_val,
+                                                           const bf16_t* __restrict__ logits,
+                                                           const uint32_t* __restrict__ mask_bits,
+                                                           const int* __restrict__ mask_idx, int vocab,
+                                                           int mask_words, int vocab_offset) {
+  const int row = blockIdx.x;
+  const bf16_t* lr = logits + (size_t)row * vocab;
+  const int mi = mask_idx ? mask_idx[row] : -1;
+  const uint32_t* mrow = mi >= 0 ? mask_bits + (size_t)mi * mask_words : nullptr;
+  float best = -INFINITY;
+  int bidx = 0x7fffffff;
+  const int nvec = vocab >> 3;
+  for (int v = threadIdx.x; v < nvec; v += NT) {
+    const int base = v << 3;
+    uint32_t bits = 0xffu;
+    if (mrow) {
+      const int gb = base + vocab_offset;  // mask is indexed by the global token id
+      bits = (mrow[gb >> 5] >> (gb & 31)) & 0xffu;
+      if (!bits) continue;
+    }
+    uint4 q = *reinterpret_cast<const uint4*>(lr + base);
+    uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float x = (k & 1) ? hi_f(w[k >> 1]) : lo_f(w[k >> 1]);
+      if (((bits >> k) & 1u) && x > best) {  // strict '>' keeps the lowest index within a lane
+        best = x;
+        bidx = base + k;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bidx, o, 64);
+    if (ob > best || (ob == best && oi < bidx)) {
+      best = ob;
+      bidx = oi;
+    }
+  }
+  __shared__ float sb[NT / 64];
+  __shared__ int si[NT / 64];
+  if ((threadIdx.x & 63) == 0) {
+    sb[threadIdx.x >> 6] = best;
+    si[threadIdx.x >> 6] = bidx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float b = sb[0];
+    int bi = si[0];
+    for (int i = 1; i < NT / 64; ++i)
+      if (sb[i] > b || (sb[i] == b && si[i] < bi)) {
+        b = sb[i];
+        bi = si[i];
+      }
+    if (bi == 0x7fffffff) bi = 0;  // fully masked row (cannot happen with a valid mask): token 0
+    out_idx[row] = bi + vocab_offset;
+    if (out_val) out_val[row] = b;
+  }
+}
+
+extern "C" int ka_masked_argmax(int* out_idx, float* out_val, const void* logits, const uint32_t* mask_bits,
+                                const int* mask_idx, int rows, int vocab, int mask_words, int vocab_offset,
+                                hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (vocab % 8 != 0 || vocab_offset % 8 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL((masked_argmax_kernel<512>), dim3(rows), dim3(512), 0, stream, out_idx, out_val,
+                     static_cast<const bf16_t*>(logits), mask_bits, mask_idx, vocab, mask_words, vocab_offset);
+  KA_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Mixtral router: softmax over E experts (fp32), top-k (ties -> lower expert id), renormalised.
+__global__ __launch_bounds__(256) void moe_topk_kernel(float* __restrict__ topk_w, int* __restrict__ topk_ids,
+                                                       const bf16_t* __restrict__ logits, int tokens, int experts,
+                                                       int k) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= tokens) return;
+  const bf16_t* l = logits + (size_t)t * experts;
+  float mx = -INFINITY;
+  for (int e = 0; e < experts; ++e) mx = fmaxf(mx, bf2f(l[e]));
+  float p[64];
+  float den = 0.f;
+  for (int e = 0; e < experts; ++e) {
+    p[e] = __expf(bf2f(l[e]) - mx);
+    den += p[e];
+  }
+  unsigned long long used = 0ull;
+  float wsum = 0.f;
+  for (int j = 0; j < k; ++j) {
+    int bi = -1;
+    float bv = -1.f;
+    for (int e = 0; e < experts; ++e)
+      if (!((used >> e) & 1ull) && p[e] > bv) {
+        bv = p[e];
+        bi = e;
+      }
+    used |= 1ull << bi;
+    topk_ids[t * k + j] = bi;
+    topk_w[t * k + j] = bv / den;
+    wsum += bv / den;
+  }
+  for (int j = 0; j < k; ++j) topk_w[t * k + j] /= wsum;
+}
+
+extern "C" int ka_moe_topk(float* topk_w, int* topk_ids, const void* logits, int tokens, int experts, int k,
+                           hipStream_t stream) {
+  if (tokens <= 0) return 0;
+  if (experts > 64 || k > experts) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(moe_topk_kernel, dim3((tokens + 255) / 256), dim3(256), 0, stream, topk_w, topk_ids,
+                     static_cast<const bf16_t*>(logits), tokens, experts, k);
+  KA_CHECK_LAUNCH();
+}

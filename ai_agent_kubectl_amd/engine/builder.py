@@ -1,0 +1,98 @@
+"""Assemble an engine (tokenizer, weights, KV pool, runner, scheduler) from `Settings`.
+
+KV sizing for 288 GB HBM3E per MI355X: after the weights (16 GB for Llama-3-8B bf16, 17.6 GB per
+GPU for 70B at TP=8) the pool gets `GPU_MEM_FRACTION` of what is left, capped by
+`KV_CACHE_TOKENS` (default 1M tokens = 128 GiB for 8B), so batch size is never KV-limited for this
+workload.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from ..models.config import get_config
+from ..models.weights import ParallelInfo, build_weights
+from .engine import LLMEngine
+from .runner import ModelRunner
+from .safe_decode import build_masks
+from .tokenizer import get_tokenizer
+
+logger = logging.getLogger("app.engine")
+
+
+@dataclass
+class EngineOptions:
+    model: str = "llama3-8b"
+    weights: str = "random:0"
+    device: str = "cuda"
+    tp_rank: int = 0
+    tp_size: int = 1
+    ep_size: int = 1
+    max_batch: int = 256
+    max_batched_tokens: int = 8192
+    max_model_len: int = 2048
+    block_size: int = 16
+    kv_cache_tokens: int = 1 << 18
+    gpu_mem_fraction: float = 0.90
+    graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256)
+    use_graphs: bool = True
+    safe_decode: bool = True
+    ignore_eos: bool = False
+    prefix_caching: bool = True
+
+    @classmethod
+    def from_settings(cls, s) -> "EngineOptions":
+        return cls(model=s.MODEL, weights=s.WEIGHTS, tp_size=s.TP, ep_size=s.EP, max_batch=s.MAX_BATCH,
+                   max_batched_tokens=s.MAX_NUM_BATCHED_TOKENS, block_size=s.KV_BLOCK_SIZE,
+                   gpu_mem_fraction=s.GPU_MEM_FRACTION,
+                   graph_buckets=tuple(b for b in s.graph_buckets() if b <= s.MAX_BATCH) or (1,),
+                   safe_decode=s.SAFE_DECODE, ignore_eos=s.IGNORE_EOS, prefix_caching=s.PREFIX_CACHING,
+                   kv_cache_tokens=int(os.environ.get("KV_CACHE_TOKENS", 1 << 18)),
+                   max_model_len=int(os.environ.get("MAX_MODEL_LEN", 2048)),
+                   device="cuda" if torch.cuda.is_available() else "cpu")
+
+
+def build_engine(opts: EngineOptions, comm=None, metrics=None) -> LLMEngine:
+    t0 = time.perf_counter()
+    cfg = get_config(opts.model)
+    tok = get_tokenizer(cfg.vocab_size, cfg.tokenizer)
+    dev = torch.device(opts.device)
+    if dev.type == "cuda":
+        from ..ops._hip import require
+        require()  # fail loudly: the GPU path never runs without the HIP kernels
+        torch.cuda.set_device(dev.index if dev.index is not None else torch.cuda.current_device())
+    dtype = torch.bfloat16
+    # MoE: experts are sharded over the tensor-parallel group (EP = TP); the all-reduce after the
+    # MoE block is the expert combine.  EP is therefore derived, not free (EP=1 with TP>1 would
+    # replicate experts and double-count them in that all-reduce).
+    ep_size = opts.tp_size if cfg.is_moe else 1
+    if cfg.is_moe and opts.ep_size not in (1, opts.tp_size):
+        raise ValueError("EP must equal TP (experts are sharded over the tensor-parallel group)")
+    par = ParallelInfo(opts.tp_rank, opts.tp_size, opts.tp_rank if ep_size > 1 else 0, ep_size)
+    weights = build_weights(opts.weights, cfg, par, device=dev, dtype=dtype)
+    # ---- KV pool size ----
+    per_block = cfg.num_layers * 2 * (cfg.num_kv_heads // opts.tp_size) * cfg.head_dim * opts.block_size * 2
+    want_blocks = max(opts.kv_cache_tokens // opts.block_size, opts.max_batch * (opts.max_model_len // opts.block_size + 1))
+    if dev.type == "cuda":
+        free, _total = torch.cuda.mem_get_info(dev)
+        budget = int(free * opts.gpu_mem_fraction) - (2 << 30)   # headroom for activations / graphs
+        num_blocks = max(64, min(want_blocks, budget // per_block))
+    else:
+        num_blocks = min(want_blocks, 4096)
+    masks = build_masks(tok, allow_eos=not opts.ignore_eos) if opts.safe_decode else None
+    runner = ModelRunner(cfg, weights, dev, num_blocks=num_blocks, block_size=opts.block_size,
+                         max_model_len=opts.max_model_len, graph_buckets=opts.graph_buckets, mask_bits=masks,
+                         comm=comm, tp_rank=opts.tp_rank, tp_size=opts.tp_size, ep_rank=par.ep_rank,
+                         ep_size=ep_size, use_graphs=opts.use_graphs)
+    eng = LLMEngine(runner, tok, max_batch=opts.max_batch, max_batched_tokens=opts.max_batched_tokens,
+                    max_model_len=opts.max_model_len, prefix_caching=opts.prefix_caching, metrics=metrics)
+    eng.options = opts
+    eng.build_seconds = time.perf_counter() - t0
+    logger.info("engine built: model=%s tp=%d blocks=%d (%.1f GiB KV) in %.1fs", cfg.name, opts.tp_size,
+                num_blocks, num_blocks * per_block / 2**30, eng.build_seconds)
+    return eng

@@ -1,0 +1,184 @@
+"""LLMEngine: request queue -> scheduler -> runner loop on a dedicated thread.
+
+The API process is asyncio (uvicorn); the GPU loop runs on one background thread so the event loop
+keeps serving cache hits, `/execute` and `/metrics` while tokens are generated.  The two sides meet
+through a thread-safe inbox and per-request callbacks (the asyncio side wraps them with
+`loop.call_soon_threadsafe`, llm/engine_backend.py).  This replaces `chain.ainvoke`
+(`/root/reference/app.py:184`).
+
+Per step: drain inbox/aborts -> `Scheduler.schedule()` -> `ModelRunner.execute()` -> append tokens,
+publish completed prefix blocks, stop on EOS / max_new_tokens -> callbacks.  Failures inside a step
+fail every in-flight request (HTTP 500/503) and mark the engine unhealthy instead of hanging.
+"""
+from __future__ import annotations
+
+import logging
+import queue
+import threading
+import time
+from typing import Callable, List, Optional
+
+from .block_manager import BlockManager
+from .runner import ModelRunner
+from .scheduler import Scheduler
+from .sequence import SamplingParams, Sequence, SeqStatus
+
+logger = logging.getLogger("app.engine")
+
+
+class LLMEngine:
+    def __init__(self, runner: ModelRunner, tokenizer, max_batch: int = 256, max_batched_tokens: int = 8192,
+                 max_model_len: int = 4096, prefix_caching: bool = True, metrics=None):
+        self.runner = runner
+        self.tokenizer = tokenizer
+        self.bm = BlockManager(runner.num_blocks, runner.block_size, enable_prefix_caching=prefix_caching)
+        self.scheduler = Scheduler(self.bm, max_batch=max_batch, max_batched_tokens=max_batched_tokens,
+                                   max_model_len=max_model_len)
+        self.metrics = metrics
+        self._inbox: "queue.SimpleQueue" = queue.SimpleQueue()
+        self._wake = threading.Event()
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self.healthy = True
+        self.last_error: Optional[BaseException] = None
+        self.steps = 0
+
+    # ------------------------------------------------------------------------------------------
+    def start(self) -> None:
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
+            self._thread.start()
+
+    def shutdown(self) -> None:
+        self._stop.set()
+        self._wake.set()
+        if self._thread is not None:
+            self._thread.join(timeout=30)
+            self._thread = None
+        try:
+            self.runner.stop_workers()
+        except Exception:  # pragma: no cover
+            pass
+
+    def submit(self, prompt_ids: List[int], params: SamplingParams, callback: Callable[[Sequence], None],
+               forced_prefix: Optional[List[int]] = None) -> Sequence:
+        seq = Sequence(prompt_ids=list(prompt_ids), params=params, callback=callback,
+                       forced_prefix=list(forced_prefix or []))
+        self._inbox.put(("add", seq))
+        self._wake.set()
+        return seq
+
+    def abort(self, seq: Sequence) -> None:
+        self._inbox.put(("abort", seq))
+        self._wake.set()
+
+    # ------------------------------------------------------------------------------------------
+    def _drain_inbox(self) -> None:
+        while True:
+            try:
+                op, seq = self._inbox.get_nowait()
+            except queue.Empty:
+                return
+            if op == "add":
+                if seq.finished:
+                    continue
+                try:
+                    self.scheduler.add(seq)
+                except ValueError as e:
+                    self._finish(seq, SeqStatus.ABORTED, "length", error=e)
+            elif op == "abort" and not seq.finished:
+                self.scheduler.abort(seq)
+                seq.finish_reason = "abort"
+
+    def _finish(self, seq: Sequence, status: SeqStatus, reason: str, error: Optional[BaseException] = None):
+        seq.status = status
+        seq.finish_reason = reason
+        seq.error = error
+        seq.t_finish = time.perf_counter()
+        if seq.block_table:
+            self.bm.free_table(seq.block_table)
+        if seq.callback is not None:
+            try:
+                seq.callback(seq)
+            except Exception:  # pragma: no cover
+                logger.exception("request callback failed")
+
+    def _apply(self, batch, tokens) -> None:
+        """Append sampled tokens, publish prefix blocks, finish sequences (EOS / max_new_tokens)."""
+        now = time.perf_counter()
+        m = self.metrics
+        for s, nq, tok in zip(batch.seqs, batch.num_query, tokens):
+            if s.finished:
+                continue
+            was_prefill = s in batch.prefill_seqs
+            s.num_computed += nq
+            s.output_ids.append(int(tok))
+            if was_prefill:
+                self.bm.register_computed(s.block_table, s.all_ids[:s.num_computed], s.block_hashes)
+                if s.t_first_token is None:
+                    s.t_first_token = now
+                    if m is not None:
+                        m.llm_ttft.observe(now - s.t_arrival)
+            eos = (not s.params.ignore_eos) and self.tokenizer.is_eos(int(tok))
+            if eos or s.num_generated >= s.params.max_new_tokens:
+                if m is not None and s.t_first_token is not None and s.num_generated > 1:
+                    m.llm_tpot.observe((now - s.t_first_token) / (s.num_generated - 1))
+                self._finish(s, SeqStatus.FINISHED, "stop" if eos else "length")
+
+    def step(self) -> int:
+        """Run one scheduler step; returns the number of sequences processed."""
+        self._drain_inbox()
+        if not self.scheduler.has_work():
+            return 0
+        batch = self.scheduler.schedule()
+        if not batch.seqs:
+            return 0
+        tokens = self.runner.execute(batch)
+        self._apply(batch, tokens)
+        self.scheduler.on_step_done(batch)
+        self.steps += 1
+        m = self.metrics
+        if m is not None:
+            m.llm_batch_size.set(len(batch.seqs))
+            m.llm_queue_depth.set(len(self.scheduler.waiting))
+            m.llm_kv_blocks_used.set(self.bm.num_used)
+        return len(batch.seqs)
+
+    def _fail_all(self, err: BaseException) -> None:
+        seqs = list(self.scheduler.running) + list(self.scheduler.waiting)
+        self.scheduler.running.clear()
+        self.scheduler.waiting.clear()
+        for s in seqs:
+            if not s.finished:
+                self._finish(s, SeqStatus.ABORTED, "error", error=err)
+
+    def _loop(self) -> None:
+        while not self._stop.is_set():
+            try:
+                n = self.step()
+            except Exception as e:  # engine fault: fail in-flight requests, stay alive but unhealthy
+                logger.exception("engine step failed")
+                self.healthy = False
+                self.last_error = e
+                self._fail_all(e)
+                n = 0
+            if n == 0 and not self.scheduler.has_work():
+                self._wake.wait(timeout=0.05)
+                self._wake.clear()
+
+    # ------------------------------------------------------------------------------------------
+    def generate_blocking(self, prompt_ids_list: List[List[int]], params: SamplingParams,
+                          forced_prefix: Optional[List[int]] = None) -> List[Sequence]:
+        """Synchronous batch generation on the caller's thread (tests, benchmarks)."""
+        seqs = [Sequence(prompt_ids=list(p), params=params, forced_prefix=list(forced_prefix or []))
+                for p in prompt_ids_list]
+        for s in seqs:
+            self.scheduler.add(s)
+        while any(not s.finished for s in seqs):
+            batch = self.scheduler.schedule()
+            if not batch.seqs:
+                raise RuntimeError("scheduler produced an empty batch (out of KV blocks?)")
+            tokens = self.runner.execute(batch)
+            self._apply(batch, tokens)
+            self.scheduler.on_step_done(batch)
+        return seqs

@@ -1,0 +1,252 @@
+"""Model runner: KV cache ownership, step metadata, eager prefill, hipGraph decode, TP fan-out.
+
+Decode steps dominate the request latency (one replay per output token, SURVEY.md §3.6 hot loop 1),
+so they are captured once per batch bucket (`HIPGRAPH_BUCKETS`) with `torch.cuda.CUDAGraph` (a
+hipGraph on ROCm): embedding -> 32 x (norm, QKV GEMM, RoPE+KV append, paged decode attention, O
+GEMM [+ all-reduce], norm, gate_up GEMM, SiLU*mul, down GEMM [+ all-reduce]) -> norm -> LM head ->
+masked argmax [+ all-gather].  All per-step inputs live in ONE device staging tensor at fixed
+offsets so a step is: one pinned host->device copy, one graph replay, one 4*B-byte readback.
+
+With TP > 1 the driver rank (rank 0) owns the scheduler; every step it broadcasts a small header
+and the packed metadata and all ranks run the same forward, the collectives
+inside it synchronising them.  Worker ranks sit in `worker_loop()`.
+"""
+from __future__ import annotations
+
+import bisect
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..models.config import ModelConfig
+from ..models.llama import AttnMeta, LlamaModel
+from ..parallel.comm import LocalComm
+from .safe_decode import mask_index_for
+from .scheduler import Batch
+
+KIND_STOP, KIND_DECODE, KIND_PREFILL = 0, 1, 2
+HDR = 8
+
+
+class ModelRunner:
+    def __init__(self, cfg: ModelConfig, weights: Dict[str, torch.Tensor], device: torch.device,
+                 num_blocks: int, block_size: int = 16, max_model_len: int = 4096, graph_buckets=(1, 2, 4, 8),
+                 mask_bits: Optional[np.ndarray] = None, comm=None, tp_rank: int = 0, tp_size: int = 1,
+                 ep_rank: int = 0, ep_size: int = 1, use_graphs: bool = True):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.comm = comm or LocalComm()
+        self.tp_rank, self.tp_size = tp_rank, tp_size
+        self.model = LlamaModel(cfg, weights, self.comm, tp_rank, tp_size, ep_rank, ep_size)
+        self.block_size = block_size
+        self.num_blocks = num_blocks
+        self.max_blocks = (max_model_len + block_size - 1) // block_size
+        hkv = cfg.num_kv_heads // tp_size
+        L, D = cfg.num_layers, cfg.head_dim
+        dt = weights["embed"].dtype
+        # zero-filled: stale slots read by masked lanes must be finite (attention.hip contract)
+        self.k_cache = torch.zeros((L, num_blocks, hkv, block_size, D), dtype=dt, device=self.device)
+        self.v_cache = torch.zeros((L, num_blocks, hkv, D, block_size), dtype=dt, device=self.device)
+        self.mask_bits = (torch.from_numpy(mask_bits.view(np.int32)).to(self.device)
+                          if mask_bits is not None else None)
+        self.buckets = sorted(set(int(b) for b in graph_buckets))
+        self.bmax = self.buckets[-1] if self.buckets else 1
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        # ---- decode staging: [ids | pos | slots | ctx | mask | block_tables] at fixed offsets ----
+        B = self.bmax
+        self._off = {"ids": 0, "pos": B, "slots": 2 * B, "ctx": 3 * B, "mask": 4 * B, "bt": 5 * B}
+        self._stage_len = 5 * B + B * self.max_blocks
+        self.d_stage = torch.zeros(self._stage_len, dtype=torch.int32, device=self.device)
+        pin = self.device.type == "cuda"
+        self.h_stage = torch.zeros(self._stage_len, dtype=torch.int32, pin_memory=pin)
+        self.h_np = self.h_stage.numpy()
+        self.d_logits_idx = torch.arange(B, dtype=torch.int64, device=self.device)
+        self.d_out = torch.zeros(B, dtype=torch.int32, device=self.device)
+        self.h_out = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
+        self.d_hdr = torch.zeros(HDR, dtype=torch.int32, device=self.device)
+        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.graph_pool = None
+        self.stats = {"decode_steps": 0, "prefill_steps": 0, "graph_replays": 0, "decode_ms": 0.0,
+                      "prefill_ms": 0.0, "prefill_tokens": 0}
+
+    # ------------------------------------------------------------------------------------------
+    def _view(self, name: str, n: int) -> torch.Tensor:
+        o = self._off[name]
+        if name == "bt":
+            return self.d_stage[o:o + n * self.max_blocks].view(n, self.max_blocks)
+        return self.d_stage[o:o + n]
+
+    def _decode_forward(self, B: int) -> None:
+        meta = AttnMeta(positions=self._view("pos", B), slot_mapping=self._view("slots", B),
+                        block_tables=self._view("bt", B), ctx_lens=self._view("ctx", B),
+                        logits_indices=self.d_logits_idx[:B], is_decode=True)
+        h = self.model.forward(self._view("ids", B), meta, self.k_cache, self.v_cache)
+        mask_idx = self._view("mask", B) if self.mask_bits is not None else None
+        tok = self.model.sample(h, self.mask_bits, mask_idx)
+        self.d_out[:B].copy_(tok)
+
+    @torch.inference_mode()
+    def capture_graphs(self) -> float:
+        """Capture one decode graph per bucket (largest first, sharing a memory pool)."""
+        if not self.use_graphs:
+            return 0.0
+        t0 = time.perf_counter()
+        self.h_np[:] = 0
+        o = self._off
+        for name in ("slots",):
+            self.h_np[o[name]:o[name] + self.bmax] = -1
+        self.h_np[o["mask"]:o["mask"] + self.bmax] = -1
+        self.d_stage.copy_(self.h_stage)
+        stream = torch.cuda.Stream(self.device)
+        stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(stream):
+            for B in reversed(self.buckets):
+                self._decode_forward(B)  # warm-up (hipBLASLt heuristics, allocator)
+        torch.cuda.current_stream(self.device).wait_stream(stream)
+        torch.cuda.synchronize(self.device)
+        for B in reversed(self.buckets):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.graph_pool):
+                self._decode_forward(B)
+            if self.graph_pool is None:
+                self.graph_pool = g.pool()
+            self.graphs[B] = g
+        torch.cuda.synchronize(self.device)
+        return time.perf_counter() - t0
+
+    # ------------------------------------------------------------------------------------------
+    def _slot(self, table: List[int], pos: int) -> int:
+        return table[pos // self.block_size] * self.block_size + pos % self.block_size
+
+    def _pack_decode(self, batch: Batch, Bp: int) -> None:
+        h, o, mb = self.h_np, self._off, self.max_blocks
+        B = len(batch.seqs)
+        for i, s in enumerate(batch.seqs):
+            pos = s.total_len - 1
+            h[o["ids"] + i] = s.all_ids[-1]
+            h[o["pos"] + i] = pos
+            h[o["slots"] + i] = self._slot(s.block_table, pos)
+            h[o["ctx"] + i] = s.total_len
+            h[o["mask"] + i] = mask_index_for(s.num_generated, s.params.safe_decode)
+            row = o["bt"] + i * mb
+            n = len(s.block_table)
+            h[row:row + n] = s.block_table
+        if Bp > B:  # padding rows: no cache write, empty context
+            for name, val in (("ids", 0), ("pos", 0), ("slots", -1), ("ctx", 0), ("mask", -1)):
+                h[o[name] + B:o[name] + Bp] = val
+
+    def _launch_decode(self, Bp: int, n_copy: int) -> None:
+        if self.tp_size > 1:
+            self.comm.broadcast(self.d_stage[:n_copy], src=0)
+        g = self.graphs.get(Bp)
+        if g is not None:
+            g.replay()
+            self.stats["graph_replays"] += 1
+        else:
+            self._decode_forward(Bp)
+
+    def _pack_prefill(self, batch: Batch) -> np.ndarray:
+        S = len(batch.seqs)
+        T = batch.num_tokens
+        mb = self.max_blocks
+        buf = np.zeros(3 * T + (S + 1) + 3 * S + S * mb, dtype=np.int32)
+        ids, pos, slots = buf[:T], buf[T:2 * T], buf[2 * T:3 * T]
+        o = 3 * T
+        q_starts = buf[o:o + S + 1]; o += S + 1
+        ctx = buf[o:o + S]; o += S
+        mask = buf[o:o + S]; o += S
+        lidx = buf[o:o + S]; o += S
+        bt = buf[o:o + S * mb].reshape(S, mb)
+        t = 0
+        for i, (s, nq) in enumerate(zip(batch.seqs, batch.num_query)):
+            q_starts[i] = t
+            start = s.total_len - nq
+            toks = s.all_ids[start:s.total_len]
+            ids[t:t + nq] = toks
+            p = np.arange(start, s.total_len, dtype=np.int32)
+            pos[t:t + nq] = p
+            tbl = np.asarray(s.block_table, dtype=np.int32)
+            slots[t:t + nq] = tbl[p // self.block_size] * self.block_size + p % self.block_size
+            ctx[i] = s.total_len
+            mask[i] = mask_index_for(s.num_generated, s.params.safe_decode)
+            bt[i, :len(tbl)] = tbl
+            t += nq
+            lidx[i] = t - 1
+        q_starts[S] = t
+        return buf
+
+    def _run_prefill(self, buf: torch.Tensor, T: int, S: int, max_q: int) -> torch.Tensor:
+        mb = self.max_blocks
+        ids, pos, slots = buf[:T], buf[T:2 * T], buf[2 * T:3 * T]
+        o = 3 * T
+        q_starts = buf[o:o + S + 1]; o += S + 1
+        ctx = buf[o:o + S]; o += S
+        mask = buf[o:o + S]; o += S
+        lidx = buf[o:o + S].long(); o += S
+        bt = buf[o:o + S * mb].view(S, mb)
+        meta = AttnMeta(positions=pos, slot_mapping=slots, block_tables=bt, ctx_lens=ctx, logits_indices=lidx,
+                        is_decode=False, q_starts=q_starts, max_q_len=max_q)
+        h = self.model.forward(ids, meta, self.k_cache, self.v_cache)
+        return self.model.sample(h, self.mask_bits, mask if self.mask_bits is not None else None)
+
+    # ------------------------------------------------------------------------------------------
+    def _bcast_header(self, kind: int, a: int = 0, b: int = 0, c: int = 0, d: int = 0) -> None:
+        if self.tp_size == 1:
+            return
+        self.d_hdr.copy_(torch.tensor([kind, a, b, c, d, 0, 0, 0], dtype=torch.int32))
+        self.comm.broadcast(self.d_hdr, src=0)
+
+    @torch.inference_mode()
+    def execute(self, batch: Batch) -> List[int]:
+        """Run one step for `batch` on every TP rank; returns the sampled token per sequence."""
+        B = len(batch.seqs)
+        if B == 0:
+            return []
+        t0 = time.perf_counter()
+        if batch.is_decode and B <= self.bmax:
+            i = bisect.bisect_left(self.buckets, B)
+            Bp = self.buckets[i] if (self.use_graphs and i < len(self.buckets)) else B
+            self._pack_decode(batch, Bp)
+            n_copy = self._off["bt"] + Bp * self.max_blocks
+            self._bcast_header(KIND_DECODE, Bp, n_copy)
+            self.d_stage[:n_copy].copy_(self.h_stage[:n_copy], non_blocking=True)
+            self._launch_decode(Bp, n_copy)
+            self.h_out[:B].copy_(self.d_out[:B], non_blocking=True)
+            if self.device.type == "cuda":
+                torch.cuda.current_stream(self.device).synchronize()
+            out = self.h_out[:B].tolist()
+            self.stats["decode_steps"] += 1
+            self.stats["decode_ms"] += (time.perf_counter() - t0) * 1e3
+            return out
+        host = self._pack_prefill(batch)
+        T, S, max_q = batch.num_tokens, B, max(batch.num_query)
+        self._bcast_header(KIND_PREFILL, T, S, max_q, host.shape[0])
+        buf = torch.from_numpy(host).to(self.device, non_blocking=False)
+        if self.tp_size > 1:
+            self.comm.broadcast(buf, src=0)
+        tok = self._run_prefill(buf, T, S, max_q)
+        out = tok.cpu().tolist()
+        self.stats["prefill_steps"] += 1
+        self.stats["prefill_tokens"] += T
+        self.stats["prefill_ms"] += (time.perf_counter() - t0) * 1e3
+        return out
+
+    @torch.inference_mode()
+    def worker_loop(self) -> None:
+        """Non-driver TP ranks: mirror every step of rank 0 until it broadcasts STOP."""
+        while True:
+            self.comm.broadcast(self.d_hdr, src=0)
+            kind, a, b, c, d = self.d_hdr[:5].tolist()
+            if kind == KIND_STOP:
+                return
+            if kind == KIND_DECODE:
+                self._launch_decode(a, b)
+            elif kind == KIND_PREFILL:
+                buf = torch.empty(d, dtype=torch.int32, device=self.device)
+                self.comm.broadcast(buf, src=0)
+                self._run_prefill(buf, a, b, c)
+
+    def stop_workers(self) -> None:
+        self._bcast_header(KIND_STOP)

@@ -1,0 +1,128 @@
+"""Continuous-batching scheduler.
+
+Each engine step runs ONE forward over a batch:
+* a prefill step when requests are waiting and KV blocks are available: as many waiting
+  sequences as fit the token budget (`MAX_NUM_BATCHED_TOKENS`) and the batch limit, with their
+  prefix-cache hits skipped (only the uncached tail of each prompt is computed), plus — so that
+  running sequences do not stall behind arrivals — every running sequence's next decode token
+  (a mixed varlen step; decode rows are one-token queries in the same paged prefill kernel);
+* otherwise a decode step over all running sequences (hipGraph replay in the runner).
+
+New sequences join the running set the step after their prefill; finished sequences leave
+immediately and free their blocks, so the batch composition changes every step.
+"""
+from __future__ import annotations
+
+import collections
+from dataclasses import dataclass, field
+from typing import Deque, List
+
+from .block_manager import BlockManager, NoFreeBlocks
+from .sequence import Sequence, SeqStatus
+
+
+@dataclass
+class Batch:
+    seqs: List[Sequence]
+    num_query: List[int]                 # tokens computed this step per sequence
+    is_decode: bool
+    prefill_seqs: List[Sequence] = field(default_factory=list)
+
+    @property
+    def num_tokens(self) -> int:
+        return sum(self.num_query)
+
+
+class Scheduler:
+    def __init__(self, block_manager: BlockManager, max_batch: int = 256, max_batched_tokens: int = 8192,
+                 max_model_len: int = 4096, mix_decode_into_prefill: bool = True):
+        self.bm = block_manager
+        self.max_batch = max_batch
+        self.max_batched_tokens = max_batched_tokens
+        self.max_model_len = max_model_len
+        self.mix = mix_decode_into_prefill
+        self.waiting: Deque[Sequence] = collections.deque()
+        self.running: List[Sequence] = []
+
+    def add(self, seq: Sequence) -> None:
+        if seq.total_len + seq.params.max_new_tokens > self.max_model_len:
+            raise ValueError(f"prompt ({len(seq.prompt_ids)}) + max_new_tokens exceeds max_model_len "
+                             f"{self.max_model_len}")
+        self.waiting.append(seq)
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def abort(self, seq: Sequence) -> None:
+        if seq in self.waiting:
+            self.waiting.remove(seq)
+        if seq in self.running:
+            self.running.remove(seq)
+        self.bm.free_table(seq.block_table)
+        seq.status = SeqStatus.ABORTED
+
+    # ------------------------------------------------------------------------------------------
+    def _admit(self) -> List[Sequence]:
+        admitted: List[Sequence] = []
+        budget = self.max_batched_tokens - (len(self.running) if self.mix else 0)
+        while self.waiting and len(self.running) + len(admitted) < self.max_batch:
+            seq = self.waiting[0]
+            try:
+                table, cached, hashes = self.bm.allocate_prompt(seq.all_ids)
+            except NoFreeBlocks:
+                break
+            q = seq.total_len - cached
+            if q > budget and admitted:
+                self.bm.free_table(table)
+                break
+            self.waiting.popleft()
+            seq.block_table, seq.block_hashes = table, hashes
+            seq.num_computed = cached
+            seq.num_cached_prompt = cached
+            seq.status = SeqStatus.RUNNING
+            admitted.append(seq)
+            budget -= q
+        return admitted
+
+    def schedule(self) -> Batch:
+        admitted = self._admit() if self.waiting else []
+        # decode rows need a slot for their next token
+        decodes: List[Sequence] = []
+        if not admitted or self.mix:
+            for seq in list(self.running):
+                if seq.status is not SeqStatus.RUNNING:
+                    continue  # preempted below while serving an earlier row
+                while True:
+                    try:
+                        self.bm.ensure_capacity(seq.block_table, seq.total_len)
+                        break
+                    except NoFreeBlocks:
+                        # preempt the newest running sequence (recomputed when re-admitted)
+                        victim = self.running[-1]
+                        self._preempt(victim)
+                        if victim in decodes:
+                            decodes.remove(victim)
+                        if victim is seq:
+                            break
+                if seq.status is SeqStatus.RUNNING:
+                    decodes.append(seq)
+        if admitted:
+            seqs = decodes + admitted
+            nq = [1] * len(decodes) + [s.total_len - s.num_computed for s in admitted]
+            return Batch(seqs, nq, is_decode=False, prefill_seqs=admitted)
+        return Batch(decodes, [1] * len(decodes), is_decode=True)
+
+    def _preempt(self, seq: Sequence) -> None:
+        """Recompute-style preemption: drop the KV, requeue; re-admission prefills all_ids."""
+        self.running.remove(seq)
+        self.bm.free_table(seq.block_table)
+        seq.block_hashes = []
+        seq.num_computed = 0
+        seq.status = SeqStatus.WAITING
+        self.waiting.appendleft(seq)
+
+    def on_step_done(self, batch: Batch) -> None:
+        for s in batch.prefill_seqs:
+            if not s.finished:
+                self.running.append(s)
+        self.running = [s for s in self.running if not s.finished]

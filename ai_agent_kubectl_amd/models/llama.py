@@ -1,0 +1,112 @@
+"""Llama-3 decoder (8B / 70B) and Mixtral-8x7B (MoE MLP) over the engine ops.
+
+This is what replaces the remote `ChatOpenAI` call (`/root/reference/app.py:117,184`): the
+forward pass of SURVEY.md §3.6 —
+  K1 embed -> per layer: K2 norm, K3 QKV GEMM, K4 RoPE+KV append, K5/K6 paged attention,
+  K7 O-proj (+A1 all-reduce), K2 norm, K8 gate_up GEMM + SiLU*mul (or K11/K12 MoE), K9 down
+  (+A2 all-reduce) -> final norm -> K10 vocab-parallel LM head -> masked greedy argmax (+A3).
+
+Tensor parallelism is Megatron-style (column-parallel QKV / gate_up, row-parallel O / down,
+vocab-parallel LM head); Mixtral experts are sharded over the same group (EP = TP group) and
+combined by the all-reduce that follows the MoE block.  Every op is shape-static for a given
+token count, so decode steps can be captured into hipGraphs by the runner.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..parallel.comm import LocalComm
+from .config import ModelConfig
+from .moe import moe_forward
+
+
+@dataclass
+class AttnMeta:
+    """Per-step metadata (device int32 tensors unless noted)."""
+    positions: torch.Tensor            # [T]
+    slot_mapping: torch.Tensor         # [T]   -1 = padding token
+    block_tables: torch.Tensor         # [S, max_blocks]
+    ctx_lens: torch.Tensor             # [S]   KV length after this step
+    logits_indices: torch.Tensor       # [S]   int64, row of each sequence's last token in [T]
+    is_decode: bool                    # all sequences contribute exactly one token
+    q_starts: Optional[torch.Tensor] = None   # [S+1] (prefill)
+    max_q_len: int = 1
+
+
+class LlamaModel:
+    def __init__(self, cfg: ModelConfig, weights: Dict[str, torch.Tensor], comm=None, tp_rank: int = 0,
+                 tp_size: int = 1, ep_rank: int = 0, ep_size: int = 1):
+        self.cfg = cfg
+        self.W = weights
+        self.comm = comm or LocalComm()
+        self.tp_rank, self.tp_size = tp_rank, tp_size
+        self.ep_rank, self.ep_size = ep_rank, ep_size
+        self.hq = cfg.num_heads // tp_size
+        self.hkv = cfg.num_kv_heads // tp_size
+        self.D = cfg.head_dim
+        self.scale = cfg.head_dim ** -0.5
+        self.vocab_local = weights["lm_head"].shape[0]
+        self.vocab_offset = tp_rank * self.vocab_local
+        dev = weights["embed"].device
+        self.device = dev
+        self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, device=dev)
+        self.layers = [self._layer(i) for i in range(cfg.num_layers)]
+
+    def _layer(self, i):
+        p = f"layers.{i}."
+        return {k: self.W[p + k] for k in ("wqkv", "wo", "ln1", "ln2", "w13", "w2", "router") if p + k in self.W}
+
+    # ------------------------------------------------------------------------------------------
+    def forward(self, input_ids: torch.Tensor, meta: AttnMeta, k_cache: torch.Tensor,
+                v_cache: torch.Tensor) -> torch.Tensor:
+        """Returns the final-normed hidden state of each sequence's last token: [S, H]."""
+        cfg = self.cfg
+        eps = cfg.norm_eps
+        h = ops.embedding(input_ids, self.W["embed"])
+        residual = None
+        T = input_ids.shape[0]
+        for li, L in enumerate(self.layers):
+            if residual is None:
+                residual = h
+                x = ops.rmsnorm(h, L["ln1"], eps)
+            else:
+                x = ops.rmsnorm(h, L["ln1"], eps, residual=residual)
+            qkv = F.linear(x, L["wqkv"])
+            q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, k_cache[li], v_cache[li],
+                                  self.hq, self.hkv, self.D)
+            if meta.is_decode:
+                a = ops.attention_decode(q, k_cache[li], v_cache[li], meta.block_tables, meta.ctx_lens, self.scale)
+            else:
+                a = ops.attention_prefill(q, k_cache[li], v_cache[li], meta.block_tables, meta.q_starts,
+                                          meta.ctx_lens, meta.max_q_len, self.scale)
+            h = F.linear(a.view(T, self.hq * self.D), L["wo"])
+            self.comm.all_reduce(h)
+            x = ops.rmsnorm(h, L["ln2"], eps, residual=residual)
+            if cfg.is_moe:
+                h = moe_forward(x, L, cfg, self.ep_rank, self.ep_size, meta.is_decode)
+            else:
+                h = F.linear(ops.silu_mul(F.linear(x, L["w13"])), L["w2"])
+            self.comm.all_reduce(h)
+        x = ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
+        return x.index_select(0, meta.logits_indices)
+
+    def logits(self, hidden_last: torch.Tensor) -> torch.Tensor:
+        """Vocab-parallel logits of this rank: [S, V / tp] (bf16)."""
+        return F.linear(hidden_last, self.W["lm_head"])
+
+    def sample(self, hidden_last: torch.Tensor, mask_bits: Optional[torch.Tensor],
+               mask_idx: Optional[torch.Tensor]) -> torch.Tensor:
+        """Greedy (temperature 0, app.py:109) next tokens under the SAFE_DECODE mask: [S] int32."""
+        logits = self.logits(hidden_last)
+        idx, val = ops.masked_argmax(logits, mask_bits, mask_idx, vocab_offset=self.vocab_offset)
+        if self.tp_size == 1:
+            return idx
+        vals = self.comm.all_gather(val)                       # [t, S]
+        idxs = self.comm.all_gather(idx)                       # [t, S]
+        best = torch.argmax(vals, dim=0)                       # first max = lowest rank = lowest id on ties
+        return idxs.gather(0, best.unsqueeze(0)).squeeze(0)

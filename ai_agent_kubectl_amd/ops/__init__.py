@@ -1,1 +1,145 @@
+"""Engine ops: one implementation per op on the GPU (hand-written HIP, `csrc/`), the fp32 torch
+reference (`ops/reference.py`) for CPU tensors.
 
+Dispatch is by tensor device only: a CUDA (HIP) tensor always goes to the HIP kernel and raises if
+the kernel library is missing; CPU tensors (tests, no-GPU development) go to the reference.
+GEMMs that are plain library GEMMs use `torch.nn.functional.linear` (hipBLASLt) except where a
+hand-written kernel wins (decode GEMV, MoE grouped GEMM).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import reference as ref
+from ._hip import check, require
+
+
+_FORCE_REF = False
+
+
+class force_reference:
+    """Test-only context: run the fp32 torch references even on GPU tensors (model-level parity)."""
+
+    def __enter__(self):
+        global _FORCE_REF
+        self._old, _FORCE_REF = _FORCE_REF, True
+
+    def __exit__(self, *exc):
+        global _FORCE_REF
+        _FORCE_REF = self._old
+
+
+def _ref(t: torch.Tensor) -> bool:
+    return _FORCE_REF or not t.is_cuda
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = rmsnorm(x (+ residual)) * w; when `residual` is given it is updated in place to x + residual."""
+    if _ref(x):
+        return ref.rmsnorm(x, w, eps, residual)
+    lib = require()
+    out = torch.empty_like(x) if out is None else out
+    rows, hidden = x.shape[0], x.shape[-1]
+    check(lib.ka_rmsnorm(_p(out), _p(residual), _p(x), _p(w), rows, hidden, float(eps), _stream()), "rmsnorm")
+    return out
+
+
+def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq: int, hkv: int, d: int,
+                  q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _ref(qkv):
+        return ref.rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq, hkv, d)
+    lib = require()
+    T = qkv.shape[0]
+    q_out = torch.empty((T, hq, d), dtype=qkv.dtype, device=qkv.device) if q_out is None else q_out
+    check(lib.ka_rope_kv(_p(q_out), _p(k_cache), _p(v_cache), _p(qkv), _p(positions), _p(cos_sin),
+                         _p(slot_mapping), T, hq, hkv, d, k_cache.shape[2], _stream()), "rope_kv")
+    return q_out
+
+
+def attention_prefill(q, k_cache, v_cache, block_tables, q_starts, ctx_lens, max_q_len: int, scale: float,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _ref(q):
+        return ref.attention_prefill(q, k_cache, v_cache, block_tables, q_starts, ctx_lens, scale)
+    lib = require()
+    out = torch.empty_like(q) if out is None else out
+    S = ctx_lens.shape[0]
+    check(lib.ka_paged_prefill(_p(out), _p(q), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.shape[1],
+                               _p(q_starts), _p(ctx_lens), S, int(max_q_len), q.shape[1], k_cache.shape[1],
+                               q.shape[2], k_cache.shape[2], float(scale), _stream()), "paged_prefill")
+    return out
+
+
+def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _ref(q):
+        return ref.attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
+    lib = require()
+    out = torch.empty_like(q) if out is None else out
+    check(lib.ka_paged_decode(_p(out), _p(q), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.shape[1],
+                              _p(ctx_lens), q.shape[0], q.shape[1], k_cache.shape[1], q.shape[2], k_cache.shape[2],
+                              float(scale), _stream()), "paged_decode")
+    return out
+
+
+def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _ref(gu):
+        return ref.silu_mul(gu)
+    lib = require()
+    T, two_i = gu.shape
+    out = torch.empty((T, two_i // 2), dtype=gu.dtype, device=gu.device) if out is None else out
+    check(lib.ka_silu_mul(_p(out), _p(gu), T, two_i // 2, _stream()), "silu_mul")
+    return out
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor, vocab_offset: int = 0,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _ref(table):
+        return ref.embedding(ids, table, vocab_offset)
+    lib = require()
+    T = ids.shape[0]
+    out = torch.empty((T, table.shape[1]), dtype=table.dtype, device=table.device) if out is None else out
+    check(lib.ka_embedding(_p(out), _p(ids), _p(table), T, table.shape[1], table.shape[0], int(vocab_offset),
+                           _stream()), "embedding")
+    return out
+
+
+def masked_argmax(logits: torch.Tensor, mask_bits: Optional[torch.Tensor], mask_idx: Optional[torch.Tensor],
+                  vocab_offset: int = 0, out_idx: Optional[torch.Tensor] = None,
+                  out_val: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Greedy token per row among tokens allowed by mask row `mask_idx[r]` (-1 = all)."""
+    if _ref(logits):
+        return ref.masked_argmax(logits, mask_bits, mask_idx, vocab_offset)
+    lib = require()
+    B, V = logits.shape
+    out_idx = torch.empty(B, dtype=torch.int32, device=logits.device) if out_idx is None else out_idx
+    out_val = torch.empty(B, dtype=torch.float32, device=logits.device) if out_val is None else out_val
+    words = mask_bits.shape[1] if mask_bits is not None else 0
+    check(lib.ka_masked_argmax(_p(out_idx), _p(out_val), _p(logits), _p(mask_bits),
+                               _p(mask_idx) if mask_bits is not None else None, B, V, words, int(vocab_offset),
+                               _stream()), "masked_argmax")
+    return out_idx, out_val
+
+
+def moe_topk(router_logits: torch.Tensor, k: int):
+    if _ref(router_logits):
+        return ref.moe_topk(router_logits, k)
+    lib = require()
+    T, E = router_logits.shape
+    w = torch.empty((T, k), dtype=torch.float32, device=router_logits.device)
+    ids = torch.empty((T, k), dtype=torch.int32, device=router_logits.device)
+    check(lib.ka_moe_topk(_p(w), _p(ids), _p(router_logits), T, E, k, _stream()), "moe_topk")
+    return w, ids
+
+
+rope_cos_sin = ref.rope_cos_sin

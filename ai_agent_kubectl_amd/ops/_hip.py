@@ -1,0 +1,81 @@
+"""ctypes binding to the in-tree HIP kernel library (`ops/lib/libkagent_hip.so`).
+
+The library is built by `ai_agent_kubectl_amd.build.build_hip()` (hipcc --offload-arch=gfx950) from
+`csrc/*.hip`.  Every kernel entry point is a plain `extern "C"` launcher that takes raw device
+pointers and the HIP stream, so calls made while torch is capturing a hipGraph
+(`torch.cuda.CUDAGraph`) are recorded into the graph like any torch kernel.
+
+There is deliberately no fallback: on a GPU the engine refuses to run without this library
+(`require()` raises), so a silent eager-PyTorch path can never masquerade as the HIP path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libkagent_hip.so")
+
+_lock = threading.Lock()
+_lib: Optional[ctypes.CDLL] = None
+_err: Optional[str] = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+F = ctypes.c_float
+
+_SIGS = {
+    "ka_rmsnorm": [P, P, P, P, I, I, F, P],
+    "ka_rope_kv": [P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "ka_silu_mul": [P, P, I, I, P],
+    "ka_embedding": [P, P, P, I, I, I, I, P],
+    "ka_masked_argmax": [P, P, P, P, P, I, I, I, I, P],
+    "ka_moe_topk": [P, P, P, I, I, I, P],
+    "ka_paged_decode": [P, P, P, P, P, I, P, I, I, I, I, I, F, P],
+    "ka_paged_prefill": [P, P, P, P, P, I, P, P, I, I, I, I, I, I, F, P],
+    "ka_gemv_bf16": [P, P, P, P, I, I, I, I, P],
+    "ka_moe_grouped_gemm": [P, P, P, P, P, P, I, I, I, I, I, I, P],
+    "ka_allreduce_oneshot": [P, P, P, I, I, I, I, P],
+}
+
+
+def load(path: str = LIB_PATH) -> Optional[ctypes.CDLL]:
+    """Load the library once; returns None (and remembers why) if it is missing."""
+    global _lib, _err
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            _err = f"HIP kernel library not built: {path} (run python -c 'import __graft_entry__ as g; g.build()')"
+            return None
+        try:
+            lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            _err = f"failed to load {path}: {e}"
+            return None
+        for name, argtypes in _SIGS.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        _lib = lib
+        return _lib
+
+
+def require() -> ctypes.CDLL:
+    lib = load()
+    if lib is None:
+        raise RuntimeError(_err or "HIP kernel library unavailable")
+    return lib
+
+
+def available() -> bool:
+    return load() is not None
+
+
+def check(code: int, what: str) -> None:
+    if code != 0:
+        raise RuntimeError(f"{what} failed with hipError {code}")

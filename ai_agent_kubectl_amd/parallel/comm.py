@@ -1,0 +1,79 @@
+"""Communicators for tensor / expert parallelism.
+
+One process per GPU (`torch.distributed`, backend "nccl" = RCCL over xGMI on ROCm; "gloo" on CPU for
+tests).  The model only needs three collectives:
+
+* `all_reduce(t)`   — sum, in place: row-parallel O-proj / down-proj outputs (A1, A2) and the
+                      expert-parallel MoE combine;
+* `all_gather(t)`   — vocab-parallel argmax winners (A3);
+* `broadcast(t)`    — per-step metadata from the driver rank (A4).
+
+All are issued on the current stream so that they are captured inside decode hipGraphs.
+`LocalComm` is the TP=1 no-op.  `TorchComm` wraps a process group.  A hand-written one-shot
+all-reduce over peer-mapped buffers (csrc/allreduce.hip) is used for small decode messages when
+enabled (parallel/custom_allreduce.py).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+
+class LocalComm:
+    world_size = 1
+    rank = 0
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        return t.unsqueeze(0)
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        return t
+
+    def barrier(self) -> None:
+        return None
+
+
+class TorchComm:
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.world_size = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.custom_ar = None  # optional one-shot all-reduce (parallel/custom_allreduce.py)
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world_size == 1:
+            return t
+        if self.custom_ar is not None and self.custom_ar.should_use(t):
+            return self.custom_ar.all_reduce(t)
+        self.dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        out = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        self.dist.broadcast(t, src=self.dist.get_global_rank(self.group, src) if self.group else src,
+                            group=self.group)
+        return t
+
+    def barrier(self) -> None:
+        self.dist.barrier(group=self.group)
+
+
+def make_comm(group=None):
+    import torch.distributed as dist
+
+    if not dist.is_available() or not dist.is_initialized():
+        return LocalComm()
+    if dist.get_world_size(group) == 1:
+        return LocalComm()
+    return TorchComm(group)

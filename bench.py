@@ -1,0 +1,166 @@
+"""Headline benchmark: requests/sec + p50 end-to-end latency of POST /kubectl-command backed by
+Llama-3-8B (bf16, random-init weights, synthetic queries) on N MI355X GPUs (BASELINE.json metric).
+
+One process per GPU (torchrun); every rank is a data-parallel replica running the full service
+in-process: ASGI app (auth, limiter, cache, Prometheus middleware, JSON) -> EngineLLM ->
+continuous-batching engine on its GPU.  A "step" is one wave of `--concurrency` concurrent cache-miss
+requests (distinct queries, so the TTL cache never answers) sent through httpx's ASGI transport,
+all completed.  W warm-up steps, then K timed steps bracketed by barrier + device sync; the job
+value is total requests / max-over-ranks elapsed (weak scaling: per-GPU work is fixed).
+
+  python bench.py                                   # 1 GPU, defaults
+  torchrun --nproc-per-node 8 bench.py --gpus 8     # driver form
+"""
+import argparse
+import asyncio
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "requests/sec + p50 e2e latency, /kubectl-command Llama-3-8B 1/2/4/8 GPU"
+# reference app.py, cache-miss /kubectl-command at concurrency 32 = 354 req/s
+# (plumbing floor with an instant stub LLM; the reference publishes no OpenAI-backed number).
+BASELINE_RPS = 354.0
+
+VERBS = ["list", "show", "get", "display", "find"]
+RES = ["pods", "services", "deployments", "nodes", "configmaps", "secrets", "jobs", "ingresses", "events",
+       "statefulsets", "daemonsets", "replicasets", "namespaces", "cronjobs", "endpoints"]
+MODS = ["in namespace", "with label app", "sorted by age in", "that are failing in", "running in cluster"]
+
+
+def make_query(rank, step, i):
+    v = VERBS[(step + i) % len(VERBS)]
+    r = RES[(i * 7 + step) % len(RES)]
+    m = MODS[(i + rank) % len(MODS)]
+    return f"{v} all {r} {m} team-{rank}-{step}-{i}"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--concurrency", type=int, default=int(os.environ.get("BENCH_CONCURRENCY", 128)))
+    ap.add_argument("--model", default=os.environ.get("BENCH_MODEL", "llama3-8b"))
+    ap.add_argument("--max-new-tokens", type=int, default=16)
+    ap.add_argument("--no-graphs", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import httpx
+    from ai_agent_kubectl_amd.api import create_app
+    from ai_agent_kubectl_amd.config import Settings
+    from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine
+    from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM
+
+    C = args.concurrency
+    buckets = tuple(b for b in (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 256) if b <= max(C, 1))
+    if C not in buckets:
+        buckets = tuple(sorted(set(buckets) | {C}))
+    opts = EngineOptions(model=args.model, device=str(dev), max_batch=max(C, 1), graph_buckets=buckets,
+                         kv_cache_tokens=max(65536, C * 256), max_model_len=512, use_graphs=not args.no_graphs,
+                         ignore_eos=True, max_batched_tokens=16384)
+    t_build = time.perf_counter()
+    eng = build_engine(opts)
+    cap_s = eng.runner.capture_graphs()
+    t_build = time.perf_counter() - t_build
+    backend = EngineLLM(eng, max_new_tokens=args.max_new_tokens, ignore_eos=True)
+    settings = Settings(RATE_LIMIT="100000000/minute", CACHE_MAXSIZE=100, LLM_TIMEOUT=600, LOG_LEVEL="WARNING")
+    import logging
+    logging.getLogger("app").setLevel(logging.WARNING)
+    app = create_app(settings, backend=backend)
+
+    lat = []
+
+    async def one(client, q, record):
+        t0 = time.perf_counter()
+        r = await client.post("/kubectl-command", json={"query": q})
+        dt = time.perf_counter() - t0
+        if r.status_code != 200:
+            raise RuntimeError(f"{r.status_code}: {r.text}")
+        body = r.json()
+        assert body["from_cache"] is False
+        if record:
+            lat.append(dt)
+        return body["kubectl_command"]
+
+    async def wave(client, step, record):
+        return await asyncio.gather(*[one(client, make_query(rank, step, i), record) for i in range(C)])
+
+    def sync_all():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    async def run():
+        await backend.start()
+        limits = httpx.Limits(max_connections=None, max_keepalive_connections=None)
+        async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://bench",
+                                     limits=limits, timeout=600) as client:
+            sample = None
+            for s in range(args.warmup):
+                sample = await wave(client, s, False)
+            sync_all()
+            st0 = dict(eng.runner.stats)
+            t0 = time.perf_counter()
+            for s in range(args.steps):
+                await wave(client, args.warmup + s, True)
+            sync_all()
+            el = time.perf_counter() - t0
+            st1 = dict(eng.runner.stats)
+        await backend.close()
+        return el, sample, {k: st1[k] - st0[k] for k in st1}
+
+    elapsed, sample, st = asyncio.run(run())
+    n_req = C * args.steps
+    p50 = statistics.median(lat) * 1e3
+    if world > 1:
+        t = torch.tensor([elapsed, p50], dtype=torch.float64, device=dev)
+        gathered = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(gathered, t)
+        elapsed = max(g[0].item() for g in gathered)
+        p50 = statistics.median([g[1].item() for g in gathered])
+    value = n_req * world / elapsed
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "req/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": round(value / BASELINE_RPS, 3),
+            "dtype": "bf16", "data": "synthetic queries, random-init weights",
+            "config": {"model": "Llama-3-8B-Instruct" if args.model == "llama3-8b" else args.model,
+                       "global_batch": C * world, "seq_len": len(backend.prompt_ids(make_query(0, 0, 0))) +
+                       args.max_new_tokens, "parallelism": f"dp{world}"},
+            "p50_ms": round(p50, 2),
+            "detail": {"concurrency_per_gpu": C, "new_tokens": args.max_new_tokens,
+                       "decode_steps": st.get("decode_steps"), "prefill_steps": st.get("prefill_steps"),
+                       "decode_ms_per_step": round(st["decode_ms"] / max(1, st["decode_steps"]), 3),
+                       "prefill_ms_per_step": round(st["prefill_ms"] / max(1, st["prefill_steps"]), 3),
+                       "prefill_tokens": st.get("prefill_tokens"), "graph_replays": st.get("graph_replays"),
+                       "prefix_cache_hit_rate": round(eng.bm.hits / max(1, eng.bm.queries), 3),
+                       "build_s": round(t_build, 1), "graph_capture_s": round(cap_s, 1),
+                       "sample_reply": sample[0] if sample else None,
+                       "baseline": "BASELINE.md reference plumbing floor, cache-miss conc 32 = 354 req/s"},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,163 @@
+"""HIP kernel numerics vs plain-PyTorch fp32 references (SURVEY.md §4.3 'kernel (GPU)' row).
+
+Every test asserts the HIP library is the code that ran (ops dispatch CUDA tensors to it and raises
+if it is missing).  Shapes cover the real head geometry (D=128, block 16), GQA 4 and 8, varlen
+prefill with cached context, and padding rows.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # collected on CPU with -m "not gpu" deselected anyway
+    pytest.skip("no GPU", allow_module_level=True)
+
+from ai_agent_kubectl_amd import ops  # noqa: E402
+from ai_agent_kubectl_amd.ops import _hip, reference as ref  # noqa: E402
+
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _lib():
+    _hip.require()
+    torch.manual_seed(0)
+
+
+def close(a, b, atol, rtol=0.02):
+    torch.testing.assert_close(a.float().cpu(), b.float().cpu(), atol=atol, rtol=rtol)
+
+
+@pytest.mark.parametrize("rows,hidden", [(1, 4096), (37, 4096), (5, 8192), (3, 256)])
+def test_rmsnorm(rows, hidden):
+    x = torch.randn(rows, hidden, device=DEV, dtype=BF)
+    w = (1 + 0.1 * torch.randn(hidden, device=DEV)).to(BF)
+    close(ops.rmsnorm(x, w, 1e-5), ref.rmsnorm(x, w, 1e-5), atol=2e-2)
+    res = torch.randn(rows, hidden, device=DEV, dtype=BF)
+    res2 = res.clone()
+    y = ops.rmsnorm(x, w, 1e-5, residual=res)
+    y2 = ref.rmsnorm(x, w, 1e-5, residual=res2)
+    close(res, res2, atol=1e-2)
+    close(y, y2, atol=3e-2)
+
+
+def _cache(nb, hkv, bs=16, d=128):
+    k = torch.randn(nb, hkv, bs, d, device=DEV, dtype=BF)
+    v = torch.randn(nb, hkv, d, bs, device=DEV, dtype=BF)
+    return k, v
+
+
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1)])
+def test_rope_kv_write(hq, hkv):
+    T, d = 23, 128
+    qkv = torch.randn(T, (hq + 2 * hkv) * d, device=DEV, dtype=BF)
+    cs = ref.rope_cos_sin(4096, d, 5e5, device=DEV)
+    pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(64 * 16, device=DEV)[:T].to(torch.int32)
+    slots[3] = -1
+    k1, v1 = _cache(64, hkv)
+    k2, v2 = k1.clone(), v1.clone()
+    q1 = ops.rope_kv_write(qkv, pos, cs, slots, k1, v1, hq, hkv, d)
+    q2 = ref.rope_kv_write(qkv, pos, cs, slots, k2, v2, hq, hkv, d)
+    close(q1, q2, atol=2e-2)
+    close(k1, k2, atol=2e-2)
+    assert torch.equal(v1, v2)
+
+
+def _tables(S, ctx_lens, nb_total, max_blocks, bs=16):
+    perm = torch.randperm(nb_total).tolist()
+    bt = torch.zeros(S, max_blocks, dtype=torch.int32)
+    k = 0
+    for s, c in enumerate(ctx_lens):
+        n = (c + bs - 1) // bs
+        bt[s, :n] = torch.tensor(perm[k:k + n], dtype=torch.int32)
+        k += n
+    return bt.to(DEV)
+
+
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (4, 1)])
+@pytest.mark.parametrize("ctx_lens", [[1, 17, 100, 129], [2048], [31, 32, 33]])
+def test_paged_decode(hq, hkv, ctx_lens):
+    S = len(ctx_lens)
+    kc, vc = _cache(400, hkv)
+    bt = _tables(S, ctx_lens, 400, 160)
+    q = torch.randn(S, hq, 128, device=DEV, dtype=BF)
+    ctx = torch.tensor(ctx_lens, dtype=torch.int32, device=DEV)
+    scale = 128 ** -0.5
+    close(ops.attention_decode(q, kc, vc, bt, ctx, scale), ref.attention_decode(q, kc, vc, bt, ctx, scale), atol=2e-2)
+
+
+def test_paged_decode_padding_rows_zero():
+    kc, vc = _cache(8, 8)
+    bt = torch.zeros(2, 4, dtype=torch.int32, device=DEV)
+    q = torch.randn(2, 32, 128, device=DEV, dtype=BF)
+    ctx = torch.tensor([5, 0], dtype=torch.int32, device=DEV)
+    out = ops.attention_decode(q, kc, vc, bt, ctx, 0.088)
+    assert torch.isfinite(out.float()).all()
+    assert out[1].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 8)])
+@pytest.mark.parametrize("qlens,ctxs", [([90], [90]), ([7, 1, 33, 20], [71, 130, 33, 84]), ([130, 1], [130, 5])])
+def test_paged_prefill(hq, hkv, qlens, ctxs):
+    S = len(qlens)
+    kc, vc = _cache(200, hkv)
+    bt = _tables(S, ctxs, 200, 16)
+    T = sum(qlens)
+    q = torch.randn(T, hq, 128, device=DEV, dtype=BF)
+    starts = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
+    ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    scale = 128 ** -0.5
+    got = ops.attention_prefill(q, kc, vc, bt, starts, ctx, max(qlens), scale)
+    want = ref.attention_prefill(q, kc, vc, bt, starts, ctx, scale)
+    close(got, want, atol=2e-2)
+
+
+def test_prefill_spike_forces_rescale():
+    # spike one key late in the context so the running max jumps at a later tile (guide §5.4 rule 26)
+    hq, hkv = 32, 8
+    kc, vc = _cache(32, hkv)
+    kc *= 0.1
+    bt = _tables(1, [200], 32, 16)
+    q = torch.randn(40, hq, 128, device=DEV, dtype=BF)
+    blk = bt[0, 190 // 16].item()
+    kc[blk, :, 190 % 16, :] = q[-1, ::4, :] * 4  # aligns with the last query's heads
+    starts = torch.tensor([0, 40], dtype=torch.int32, device=DEV)
+    ctx = torch.tensor([200], dtype=torch.int32, device=DEV)
+    got = ops.attention_prefill(q, kc, vc, bt, starts, ctx, 40, 128 ** -0.5)
+    want = ref.attention_prefill(q, kc, vc, bt, starts, ctx, 128 ** -0.5)
+    close(got, want, atol=3e-2)
+
+
+def test_silu_mul_and_embedding():
+    gu = torch.randn(19, 2 * 14336, device=DEV, dtype=BF)
+    close(ops.silu_mul(gu), ref.silu_mul(gu), atol=2e-2)
+    table = torch.randn(1000, 4096, device=DEV, dtype=BF)
+    ids = torch.tensor([0, 5, 999, 1000, -1], dtype=torch.int32, device=DEV)
+    assert torch.equal(ops.embedding(ids, table), ref.embedding(ids, table))
+
+
+@pytest.mark.parametrize("V,off", [(128256, 0), (16032, 16032 * 3), (32000, 0)])
+def test_masked_argmax(V, off):
+    import numpy as np
+    B = 9
+    logits = torch.randn(B, V, device=DEV, dtype=BF)
+    words = (V + off + 31) // 32
+    bits = torch.from_numpy(np.random.RandomState(0).randint(0, 2**32, size=(2, words), dtype=np.uint64)
+                            .astype(np.uint32).view(np.int32)).to(DEV)
+    midx = torch.tensor([0, 1, -1, 0, 1, -1, 0, 0, 1], dtype=torch.int32, device=DEV)
+    i1, v1 = ops.masked_argmax(logits, bits, midx, vocab_offset=off)
+    i2, v2 = ref.masked_argmax(logits.cpu(), bits.cpu(), midx.cpu(), vocab_offset=off)
+    assert torch.equal(i1.cpu(), i2.cpu())
+    close(v1, v2, atol=0, rtol=0)
+
+
+def test_moe_topk():
+    lg = torch.randn(50, 8, device=DEV, dtype=BF)
+    w1, i1 = ops.moe_topk(lg, 2)
+    w2, i2 = ref.moe_topk(lg, 2)
+    assert torch.equal(i1.cpu().sort(1).values, i2.cpu().sort(1).values)
+    close(w1.sort(1).values, w2.sort(1).values, atol=1e-5)

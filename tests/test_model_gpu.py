@@ -1,0 +1,133 @@
+"""Model / engine numerics on the GPU (SURVEY.md §4.3 'model (GPU)' and 'TP numerics' rows).
+
+* full forward (real Llama-3-8B layer geometry, 2 layers) through the HIP kernels vs the same
+  weights through the fp32 torch references;
+* hipGraph decode replay == eager decode, token for token;
+* prefix-cache hit == cold prefill (same tokens);
+* virtual TP: t shard-forwards summed in place of the all-reduce == TP=1 logits;
+* Mixtral (2 layers, 8 experts) HIP path vs reference.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from ai_agent_kubectl_amd import ops  # noqa: E402
+from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine  # noqa: E402
+from ai_agent_kubectl_amd.engine.sequence import SamplingParams  # noqa: E402
+from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM  # noqa: E402
+
+QUERIES = ["list all pods", "show services in namespace prod", "scale web to 3 replicas",
+           "get nodes with labels", "describe deployment api", "logs of pod api-1"]
+
+
+def _engine(model, graphs, buckets=(1, 2, 4, 8), **kw):
+    opts = EngineOptions(model=model, device="cuda", max_batch=8, graph_buckets=buckets, kv_cache_tokens=16384,
+                         max_model_len=512, use_graphs=graphs, **kw)
+    eng = build_engine(opts)
+    if graphs:
+        eng.runner.capture_graphs()
+    return eng
+
+
+def _prefill_hidden(eng, be, queries):
+    """Run one prefill step and return the runner's sampled tokens plus the last hidden states."""
+    from ai_agent_kubectl_amd.engine.scheduler import Batch
+    from ai_agent_kubectl_amd.engine.sequence import Sequence
+    seqs = [Sequence(prompt_ids=be.prompt_ids(q), params=be.params) for q in queries]
+    for s in seqs:
+        s.block_table, _, s.block_hashes = eng.bm.allocate_prompt(s.all_ids)
+    batch = Batch(seqs, [s.total_len for s in seqs], is_decode=False, prefill_seqs=seqs)
+    r = eng.runner
+    host = torch.from_numpy(r._pack_prefill(batch)).cuda()
+    T, S = batch.num_tokens, len(seqs)
+    from ai_agent_kubectl_amd.models.llama import AttnMeta
+    mb = r.max_blocks
+    o = 3 * T
+    meta = AttnMeta(positions=host[T:2 * T], slot_mapping=host[2 * T:3 * T],
+                    block_tables=host[o + 4 * S + 1:o + 4 * S + 1 + S * mb].view(S, mb),
+                    ctx_lens=host[o + S + 1:o + 2 * S + 1], logits_indices=host[o + 3 * S + 1:o + 4 * S + 1].long(),
+                    is_decode=False, q_starts=host[o:o + S + 1], max_q_len=max(batch.num_query))
+    h = r.model.forward(host[:T], meta, r.k_cache, r.v_cache)
+    for s in seqs:
+        eng.bm.free_table(s.block_table)
+    return h
+
+
+def test_llama_forward_hip_vs_reference():
+    eng = _engine("llama3-8b-2l", graphs=False)
+    be = EngineLLM(eng, max_new_tokens=8)
+    with torch.inference_mode():
+        h_hip = _prefill_hidden(eng, be, QUERIES[:3])
+        with ops.force_reference():
+            h_ref = _prefill_hidden(eng, be, QUERIES[:3])
+        lg_hip = eng.runner.model.logits(h_hip).float()
+        lg_ref = eng.runner.model.logits(h_ref).float()
+    cos = torch.nn.functional.cosine_similarity(lg_hip, lg_ref, dim=-1)
+    assert cos.min().item() > 0.995, cos
+    torch.testing.assert_close(h_hip.float(), h_ref.float(), atol=0.1, rtol=0.05)
+
+
+def test_graph_decode_equals_eager():
+    params = SamplingParams(max_new_tokens=12, ignore_eos=True)
+    outs = []
+    for graphs in (False, True):
+        eng = _engine("llama3-8b-2l", graphs=graphs)
+        be = EngineLLM(eng, max_new_tokens=12, ignore_eos=True)
+        seqs = eng.generate_blocking([be.prompt_ids(q) for q in QUERIES[:5]], params, forced_prefix=be._forced)
+        outs.append([s.output_ids for s in seqs])
+        if graphs:
+            assert eng.runner.stats["graph_replays"] > 0
+        del eng
+        torch.cuda.empty_cache()
+    assert outs[0] == outs[1]
+
+
+def test_prefix_cache_hit_matches_cold():
+    params = SamplingParams(max_new_tokens=8, ignore_eos=True)
+    eng = _engine("llama3-8b-2l", graphs=True)
+    be = EngineLLM(eng, max_new_tokens=8, ignore_eos=True)
+    cold = eng.generate_blocking([be.prompt_ids(QUERIES[0])], params, forced_prefix=be._forced)[0]
+    assert cold.num_cached_prompt == 0
+    warm = eng.generate_blocking([be.prompt_ids(QUERIES[0])], params, forced_prefix=be._forced)[0]
+    assert warm.num_cached_prompt >= 64
+    assert warm.output_ids == cold.output_ids
+
+
+def test_safe_decode_outputs_pass_validator():
+    from ai_agent_kubectl_amd.safety import is_safe_kubectl_command
+    eng = _engine("llama3-8b-2l", graphs=True)
+    be = EngineLLM(eng, max_new_tokens=16)
+    seqs = eng.generate_blocking([be.prompt_ids(q) for q in QUERIES], be.params, forced_prefix=be._forced)
+    for s in seqs:
+        txt = be.tok.decode([t for t in s.output_ids if not be.tok.is_eos(t)])
+        assert is_safe_kubectl_command(txt), txt
+
+
+def test_virtual_tp_matches_tp1():
+    """TP=2 shards run sequentially on one GPU with partial sums standing in for the all-reduce."""
+    from ai_agent_kubectl_amd.models.config import get_config
+    from ai_agent_kubectl_amd.models.llama import LlamaModel
+    from ai_agent_kubectl_amd.models.weights import ParallelInfo, random_weights
+    from tests.virtual_tp import virtual_tp_logits
+    cfg = get_config("llama3-8b-2l")
+    full = virtual_tp_logits(cfg, tp=1)
+    tp2 = virtual_tp_logits(cfg, tp=2)
+    cos = torch.nn.functional.cosine_similarity(full.float(), tp2.float(), dim=-1)
+    assert cos.min().item() > 0.999
+
+
+def test_mixtral_forward_hip_vs_reference():
+    eng = _engine("mixtral-2l", graphs=False)
+    be = EngineLLM(eng, max_new_tokens=8)
+    with torch.inference_mode():
+        h_hip = _prefill_hidden(eng, be, QUERIES[:2])
+        with ops.force_reference():
+            h_ref = _prefill_hidden(eng, be, QUERIES[:2])
+    torch.testing.assert_close(h_hip.float(), h_ref.float(), atol=0.1, rtol=0.05)
+    params = SamplingParams(max_new_tokens=6, ignore_eos=True)
+    seqs = eng.generate_blocking([be.prompt_ids(q) for q in QUERIES[:3]], params, forced_prefix=be._forced)
+    assert all(len(s.output_ids) == len(be._forced) + 6 for s in seqs)

@@ -1,0 +1,114 @@
+"""Virtual tensor parallelism on ONE device (SURVEY.md §4.3 'TP numerics (1 GPU)').
+
+RCCL refuses two ranks on one GPU, so the TP math is validated by running the t shard-models in t
+threads on the same device with a `VirtualComm` whose all-reduce sums the shards' partial outputs
+(barrier -> sum -> barrier -> copy back) and whose all-gather stacks them.  Because random weights
+are generated in parallel-invariant units (models/weights.py), shard r holds exactly the slice of
+the TP=1 weights that Megatron sharding assigns it.
+"""
+from __future__ import annotations
+
+import threading
+
+import torch
+
+from ai_agent_kubectl_amd.engine.runner import ModelRunner
+from ai_agent_kubectl_amd.engine.scheduler import Batch
+from ai_agent_kubectl_amd.engine.sequence import Sequence, SamplingParams
+from ai_agent_kubectl_amd.engine.tokenizer import get_tokenizer
+from ai_agent_kubectl_amd.models.llama import AttnMeta
+from ai_agent_kubectl_amd.models.weights import ParallelInfo, random_weights
+from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM
+
+
+class VirtualComm:
+    def __init__(self, world: int):
+        self.world_size = world
+        self._bar = threading.Barrier(world)
+        self._slots = [None] * world
+        self._out = None
+
+    def view(self, rank):
+        parent = self
+
+        class _R:
+            world_size = parent.world_size
+
+            def __init__(self):
+                self.rank = rank
+
+            def all_reduce(self, t):
+                parent._slots[rank] = t
+                parent._bar.wait()
+                if rank == 0:
+                    parent._out = torch.stack([s.float() for s in parent._slots]).sum(0)
+                parent._bar.wait()
+                t.copy_(parent._out.to(t.dtype))
+                parent._bar.wait()
+                return t
+
+            def all_gather(self, t):
+                parent._slots[rank] = t
+                parent._bar.wait()
+                out = torch.stack([s.clone() for s in parent._slots])
+                parent._bar.wait()
+                return out
+
+            def broadcast(self, t, src=0):
+                return t
+
+        return _R()
+
+
+class _TinyEngine:
+    """Just enough of LLMEngine for EngineLLM.prompt_ids()."""
+
+    def __init__(self, tok):
+        self.tokenizer = tok
+
+
+def _batch(cfg, queries, block_size=16):
+    tok = get_tokenizer(cfg.vocab_size, cfg.tokenizer)
+    be = EngineLLM(_TinyEngine(tok), max_new_tokens=4)
+    seqs = [Sequence(prompt_ids=be.prompt_ids(q), params=SamplingParams()) for q in queries]
+    nb = 0
+    for s in seqs:
+        n = (s.total_len + block_size - 1) // block_size
+        s.block_table = list(range(nb, nb + n))
+        nb += n
+    return Batch(seqs, [s.total_len for s in seqs], is_decode=False, prefill_seqs=seqs), nb
+
+
+def virtual_tp_logits(cfg, tp: int, device="cuda", queries=("list all pods", "get nodes in prod")):
+    batch, nb = _batch(cfg, queries)
+    vc = VirtualComm(tp)
+    runners = []
+    for r in range(tp):
+        ep = tp if cfg.is_moe else 1
+        W = random_weights(cfg, ParallelInfo(r, tp, r if ep > 1 else 0, ep), seed=0, device=device)
+        runners.append(ModelRunner(cfg, W, torch.device(device), num_blocks=nb + 4, max_model_len=512,
+                                   graph_buckets=(1,), comm=vc.view(r), tp_rank=r, tp_size=tp,
+                                   ep_rank=r if ep > 1 else 0, ep_size=ep, use_graphs=False))
+    results = [None] * tp
+
+    def run(r):
+        rn = runners[r]
+        host = torch.from_numpy(rn._pack_prefill(batch)).to(device)
+        T, S = batch.num_tokens, len(batch.seqs)
+        mb = rn.max_blocks
+        o = 3 * T
+        meta = AttnMeta(positions=host[T:2 * T], slot_mapping=host[2 * T:3 * T],
+                        block_tables=host[o + 4 * S + 1:o + 4 * S + 1 + S * mb].view(S, mb),
+                        ctx_lens=host[o + S + 1:o + 2 * S + 1],
+                        logits_indices=host[o + 3 * S + 1:o + 4 * S + 1].long(), is_decode=False,
+                        q_starts=host[o:o + S + 1], max_q_len=max(batch.num_query))
+        with torch.inference_mode():
+            h = rn.model.forward(host[:T], meta, rn.k_cache, rn.v_cache)
+            results[r] = rn.model.logits(h)
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(tp)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    return torch.cat(results, dim=-1)
