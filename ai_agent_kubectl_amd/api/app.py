@@ -124,6 +124,8 @@ def create_app(settings: Optional[Settings] = None, backend: Any = _UNSET,
         except Exception:
             logger.exception("Failed to initialize LLM backend.")  # app.py:119-122
             backend = None
+    if backend is not None and hasattr(backend, "attach_metrics"):
+        backend.attach_metrics(metrics)
     svc = KubectlService(settings, backend, metrics)
 
     if not settings.API_AUTH_KEY:

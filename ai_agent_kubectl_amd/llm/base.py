@@ -28,6 +28,10 @@ class LLMBackend(abc.ABC):
     async def close(self) -> None:  # pragma: no cover - trivial
         return None
 
+    def attach_metrics(self, metrics) -> None:
+        """Give the backend the app's metrics registry (engine TTFT/TPOT/queue gauges)."""
+        return None
+
     def healthy(self) -> bool:
         return True
 

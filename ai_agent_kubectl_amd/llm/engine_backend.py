@@ -69,6 +69,10 @@ class EngineLLM(LLMBackend):
     def healthy(self) -> bool:
         return self.engine.healthy
 
+    def attach_metrics(self, metrics) -> None:
+        if metrics is not None and getattr(self.engine, "metrics", None) is None:
+            self.engine.metrics = metrics
+
     async def generate(self, query: str) -> str:
         if not self._started:
             await self.start()

@@ -1,0 +1,187 @@
+"""Engine tests that run on CPU (reference ops, tiny models with the real vocab / head layout)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from ai_agent_kubectl_amd.engine.block_manager import BlockManager, NoFreeBlocks
+from ai_agent_kubectl_amd.engine.safe_decode import MASK_BODY, MASK_FIRST, build_masks, forced_prefix
+from ai_agent_kubectl_amd.engine.scheduler import Scheduler
+from ai_agent_kubectl_amd.engine.sequence import SamplingParams, Sequence, SeqStatus
+from ai_agent_kubectl_amd.engine.tokenizer import SyntheticTokenizer, get_tokenizer
+from ai_agent_kubectl_amd.prompt import PROMPT_PREFIX, render_prompt
+from ai_agent_kubectl_amd.safety import is_safe_kubectl_command
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ---------------- tokenizer ----------------
+@pytest.mark.parametrize("vocab,family", [(128256, "llama3"), (32000, "llama2")])
+def test_tokenizer_roundtrip_and_density(vocab, family):
+    tok = get_tokenizer(vocab, family)
+    p = render_prompt("list all pods in namespace prod ünïcode ✓")
+    ids = tok.encode(p)
+    assert tok.decode(ids) == p
+    assert all(0 <= i < vocab for i in ids)
+    assert 3.0 < len(p) / len(ids) < 6.0     # ~4 chars/token like a real BPE
+    chat = tok.encode_chat("hi")
+    assert chat[0] == tok.bos_id
+
+
+def test_tokenizer_specials():
+    tok = get_tokenizer(128256, "llama3")
+    assert tok.is_eos(128009) and tok.is_eos(128001) and tok.bos_id == 128000
+    assert tok.decode([128000, tok.encode("x")[0]]) == "x"
+
+
+# ---------------- safe decode ----------------
+def test_safe_masks_only_allow_validator_safe_tokens():
+    tok = get_tokenizer(128256, "llama3")
+    m = build_masks(tok)
+    bits = np.unpackbits(m.view(np.uint8), bitorder="little").reshape(2, -1)[:, :tok.vocab_size].astype(bool)
+    first = np.nonzero(bits[MASK_FIRST])[0]
+    body = np.nonzero(bits[MASK_BODY])[0]
+    assert len(first) > 1000 and len(body) > len(first)
+    rng = np.random.RandomState(0)
+    pre = tok.decode(forced_prefix(tok))
+    assert pre == "kubectl"
+    for _ in range(300):
+        toks = [rng.choice(first)] + list(rng.choice(body, size=rng.randint(0, 12)))
+        toks = [t for t in toks if not tok.is_eos(t)]
+        assert is_safe_kubectl_command(pre + tok.decode(toks))
+
+
+# ---------------- block manager ----------------
+def test_prefix_cache_sharing_and_eviction():
+    bm = BlockManager(num_blocks=12, block_size=4)
+    a = list(range(10))                       # 2 full blocks + partial
+    t1, c1, h1 = bm.allocate_prompt(a)
+    assert c1 == 0 and len(t1) == 3
+    bm.register_computed(t1, a, h1)
+    t2, c2, h2 = bm.allocate_prompt(a[:8] + [99, 98])
+    assert c2 == 8 and t2[:2] == t1[:2] and t2[2] != t1[2]
+    assert bm.ref[t1[0]] == 2
+    bm.free_table(t1)
+    bm.free_table(t2)
+    assert bm.num_free == 12
+    # cached blocks survive until memory pressure evicts them
+    t3, c3, _ = bm.allocate_prompt(a)
+    assert c3 == 8
+    bm.free_table(t3)
+    big, _, _ = bm.allocate_prompt(list(range(100, 148)))   # needs all 12 blocks -> evicts cache
+    assert len(big) == 12
+    with pytest.raises(NoFreeBlocks):
+        bm.allocate_prompt([1, 2, 3])
+    bm.free_table(big)
+    t4, c4, _ = bm.allocate_prompt(a)
+    assert c4 == 0
+
+
+def test_last_token_always_recomputed():
+    bm = BlockManager(num_blocks=8, block_size=4)
+    a = list(range(8))
+    t, _, h = bm.allocate_prompt(a)
+    bm.register_computed(t, a, h)
+    t2, c2, _ = bm.allocate_prompt(a)
+    assert c2 == 4        # the block holding the last prompt token is recomputed
+
+
+# ---------------- scheduler ----------------
+def _seq(n, new=4):
+    return Sequence(prompt_ids=list(range(1000, 1000 + n)), params=SamplingParams(max_new_tokens=new))
+
+
+def test_scheduler_budget_and_mixing():
+    bm = BlockManager(64, 4, enable_prefix_caching=False)
+    sch = Scheduler(bm, max_batch=3, max_batched_tokens=20)
+    seqs = [_seq(8), _seq(8), _seq(8), _seq(8)]
+    for s in seqs:
+        sch.add(s)
+    b = sch.schedule()
+    assert not b.is_decode and [len(x.all_ids) for x in b.prefill_seqs] == [8, 8]   # budget 20
+    for s, n in zip(b.seqs, b.num_query):
+        s.num_computed += n
+        s.output_ids.append(1)
+    sch.on_step_done(b)
+    b = sch.schedule()   # third admitted + two decode rows mixed in
+    assert len(b.prefill_seqs) == 1 and b.num_query == [1, 1, 8]
+
+
+def test_scheduler_preempts_when_out_of_blocks():
+    bm = BlockManager(5, 4, enable_prefix_caching=False)
+    sch = Scheduler(bm, max_batch=4, max_batched_tokens=100)
+    s1, s2 = _seq(8, new=8), _seq(8, new=8)
+    sch.add(s1)
+    sch.add(s2)
+    b = sch.schedule()
+    assert len(b.prefill_seqs) == 2 and bm.num_free == 1
+    for s, n in zip(b.seqs, b.num_query):
+        s.num_computed += n
+        s.output_ids.append(5)
+    sch.on_step_done(b)
+    b = sch.schedule()   # both need a 3rd block at length 9 -> one is preempted
+    assert b.is_decode and len(b.seqs) == 1
+    assert len(sch.waiting) == 1 and sch.waiting[0].status is SeqStatus.WAITING
+
+
+# ---------------- engine end to end (CPU) ----------------
+@pytest.fixture(scope="module")
+def tiny_engine():
+    from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine
+    from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM
+    eng = build_engine(EngineOptions(model="tiny-llama", device="cpu", max_batch=8, graph_buckets=(1, 2, 4, 8),
+                                     kv_cache_tokens=8192, max_model_len=512))
+    return eng, EngineLLM(eng, max_new_tokens=10)
+
+
+def test_engine_generates_safe_commands_and_hits_prefix_cache(tiny_engine):
+    eng, be = tiny_engine
+    qs = ["list pods", "show services in prod", "scale web to 3"]
+    seqs = eng.generate_blocking([be.prompt_ids(q) for q in qs], be.params, forced_prefix=be._forced)
+    for s in seqs:
+        txt = be.tok.decode([t for t in s.output_ids if not be.tok.is_eos(t)])
+        assert txt.startswith("kubectl ") and is_safe_kubectl_command(txt)
+    seqs2 = eng.generate_blocking([be.prompt_ids("get nodes")], be.params, forced_prefix=be._forced)
+    assert seqs2[0].num_cached_prompt >= 48
+    assert eng.bm.num_used == 0 or all(eng.bm.ref[b] == 0 for b in range(eng.bm.num_blocks))
+
+
+def test_prefix_cached_equals_cold(tiny_engine):
+    eng, be = tiny_engine
+    params = SamplingParams(max_new_tokens=6, ignore_eos=True)
+    ids = be.prompt_ids("describe deployment api")
+    eng.bm.reset_prefix_cache()
+    cold = eng.generate_blocking([ids], params, forced_prefix=be._forced)[0]
+    warm = eng.generate_blocking([ids], params, forced_prefix=be._forced)[0]
+    assert cold.num_cached_prompt == 0 and warm.num_cached_prompt > 0
+    assert cold.output_ids == warm.output_ids
+
+
+def test_api_with_engine_backend(tiny_engine):
+    from fastapi.testclient import TestClient
+    from ai_agent_kubectl_amd.api import create_app
+    from ai_agent_kubectl_amd.config import Settings
+    eng, be = tiny_engine
+    app = create_app(Settings(RATE_LIMIT="1000/minute"), backend=be)
+    with TestClient(app) as c:      # lifespan starts / stops the engine thread
+        r = c.post("/kubectl-command", json={"query": "list all pods"})
+        assert r.status_code == 200, r.text
+        assert is_safe_kubectl_command(r.json()["kubectl_command"])
+        assert c.post("/kubectl-command", json={"query": "list all pods"}).json()["from_cache"] is True
+        m = c.get("/metrics").text
+        assert "llm_ttft_seconds_count 1.0" in m
+
+
+# ---------------- tensor parallel numerics ----------------
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-mixtral"])
+def test_virtual_tp2_matches_tp1_cpu(model):
+    sys.path.insert(0, ROOT)
+    from tests.virtual_tp import virtual_tp_logits
+    from ai_agent_kubectl_amd.models.config import get_config
+    cfg = get_config(model)
+    a = virtual_tp_logits(cfg, 1, device="cpu").float()
+    b = virtual_tp_logits(cfg, 2, device="cpu").float()
+    assert torch.nn.functional.cosine_similarity(a, b, dim=-1).min() > 0.9999
+    assert torch.equal(a.argmax(-1), b.argmax(-1))
