@@ -187,7 +187,7 @@ struct PrefillSmem {
   bf16_t p[4][16 * 32];   // per-wave P scratch                             4 KiB
 };
 
-__device__ __forceinline__ void prefill_load_tile(uint4 (&kreg)[2], uint4 (&vreg)[2], const bf16_t* __restrict__ k_cache,
+__device__ __forceinline__ void prefill_load_tile(u32x4 (&kreg)[2], u32x4 (&vreg)[2], const bf16_t* __restrict__ k_cache,
                                                   const bf16_t* __restrict__ v_cache, const int* __restrict__ bt,
                                                   int nblocks, int tile, int h, int hkv) {
   const int tid = threadIdx.x;
@@ -200,27 +200,27 @@ __device__ __forceinline__ void prefill_load_tile(uint4 (&kreg)[2], uint4 (&vreg
       const int tok = p >> 4, ch = p & 15;
       const int bi = 2 * tile + (tok >> 4);
       const int blk = bi < nblocks ? bt[bi] : bt[0];
-      kreg[i] = *reinterpret_cast<const uint4*>(k_cache + ((size_t)blk * hkv + h) * head_stride + (tok & 15) * HD + ch * 8);
+      kreg[i] = *reinterpret_cast<const u32x4*>(k_cache + ((size_t)blk * hkv + h) * head_stride + (tok & 15) * HD + ch * 8);
     }
     // V^T: dim = p >> 2, chunk = p & 3 (chunks 0,1 from the first block, 2,3 from the second)
     {
       const int dim = p >> 2, ch = p & 3;
       const int bi = 2 * tile + (ch >> 1);
       const int blk = bi < nblocks ? bt[bi] : bt[0];
-      vreg[i] = *reinterpret_cast<const uint4*>(v_cache + ((size_t)blk * hkv + h) * head_stride + dim * KBS + (ch & 1) * 8);
+      vreg[i] = *reinterpret_cast<const u32x4*>(v_cache + ((size_t)blk * hkv + h) * head_stride + dim * KBS + (ch & 1) * 8);
     }
   }
 }
 
-__device__ __forceinline__ void prefill_store_tile(PrefillSmem& s, const uint4 (&kreg)[2], const uint4 (&vreg)[2]) {
+__device__ __forceinline__ void prefill_store_tile(PrefillSmem& s, const u32x4 (&kreg)[2], const u32x4 (&vreg)[2]) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int p = tid + 256 * i;
     const int tok = p >> 4, ch = p & 15;
-    s.k[tok][ch ^ (tok & 15)] = kreg[i];
+    reinterpret_cast<u32x4*>(s.k[tok])[ch ^ (tok & 15)] = kreg[i];
     const int dim = p >> 2, vc = p & 3;
-    s.v[dim][vc ^ ((dim >> 2) & 3)] = vreg[i];
+    reinterpret_cast<u32x4*>(s.v[dim])[vc ^ ((dim >> 2) & 3)] = vreg[i];
   }
 }
 
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256) void paged_prefill_kernel(bf16_t* __restrict__
 #pragma unroll
   for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 kreg[2], vreg[2];
+  u32x4 kreg[2], vreg[2];
   prefill_load_tile(kreg, vreg, k_cache, v_cache, bt, nblocks, 0, h, hkv);
   bf16_t* pw = s.p[wave];
   for (int t = 0; t < ntiles; ++t) {

@@ -1,0 +1,199 @@
+// Weight-streaming MFMA GEMM for decode (K13):  Y[M, N] = X[M, K] * W[N, K]^T,  M <= 256, bf16.
+//
+// In a decode step every weight byte is read exactly once, so the projections are HBM-bound on W
+// (Llama-3-8B: 16 GB per step); hipBLASLt's tiles for M <= 256 leave most CUs idle on N = 4096
+// (128 workgroups, K = 14336 streamed by each: 1.4-2 TB/s measured).  This kernel:
+//   * workgroup = 4 waves = 64 output columns (one 16-column MFMA tile per wave) x all M rows,
+//     over one K slice (split-K so that the grid covers the 256 CUs several times);
+//   * W is the MFMA A operand: lane l's fragment (row n = l&15, k = 8*(l>>4)..+7) is one contiguous
+//     16-B global load straight into VGPRs (no reuse across waves -> no LDS round trip), with a
+//     two-chunk-deep register ring (two named sets, ping-pong) so 4 KiB per wave stay in flight;
+//   * X (re-read by every column tile, L2/MALL-resident) is the B operand, staged per 64-k chunk
+//     in LDS by all 256 threads with an XOR swizzle (slot = chunk ^ (row & 7)) against the
+//     16-rows-same-column ds_read_b128 conflict (guide §5.5 T2), register-staged one chunk ahead;
+//   * C = 16 n x 16 m per MFMA: each lane owns 4 consecutive n of one m -> 8-B bf16 / 16-B fp32
+//     stores.  split == 1 writes bf16 Y; split > 1 writes fp32 partials P[split][M][N] that
+//     `ka_splitk_reduce` (or a fused consumer) sums.
+#include "common.h"
+
+#define NW 64  // output columns per workgroup
+
+// X staging: piece p -> row p >> 3, 16-B chunk p & 7 of a 64-k chunk; LDS slot = chunk ^ (row & 7)
+template <int MT>
+__device__ __forceinline__ void sk_load_x(u32x4 (&xr)[(MT * 128 + 255) / 256], const bf16_t* __restrict__ X, int M,
+                                          int K, int k_begin, int c, int tid) {
+  constexpr int PIECES = MT * 128;
+#pragma unroll
+  for (int i = 0; i < (PIECES + 255) / 256; ++i) {
+    const int p = tid + 256 * i;
+    if (PIECES % 256 == 0 || p < PIECES) {
+      const int row = min(p >> 3, M - 1);
+      xr[i] = *reinterpret_cast<const u32x4*>(X + (size_t)row * K + k_begin + c * 64 + (p & 7) * 8);
+    }
+  }
+}
+
+template <int MT>
+__device__ __forceinline__ void sk_store_x(const u32x4 (&xr)[(MT * 128 + 255) / 256], uint4* xs, int tid) {
+  constexpr int PIECES = MT * 128;
+#pragma unroll
+  for (int i = 0; i < (PIECES + 255) / 256; ++i) {
+    const int p = tid + 256 * i;
+    if (PIECES % 256 == 0 || p < PIECES)
+      reinterpret_cast<u32x4*>(xs)[(p >> 3) * 8 + ((p & 7) ^ ((p >> 3) & 7))] = xr[i];
+  }
+}
+
+__device__ __forceinline__ void sk_load_w(uint4& w0, uint4& w1, const bf16_t* __restrict__ wp, int c, int nchunks) {
+  c = min(c, nchunks - 1);
+  w0 = *reinterpret_cast<const uint4*>(wp + c * 64);
+  w1 = *reinterpret_cast<const uint4*>(wp + c * 64 + 32);
+}
+
+template <int MT>
+__device__ __forceinline__ void sk_compute(f32x4 (&acc)[MT], const uint4& w0, const uint4& w1, const uint4* xs,
+                                           int col, int grp) {
+  const bf16x8 a0 = as_bf16x8(w0), a1 = as_bf16x8(w1);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int row = mt * 16 + col;
+    acc[mt] = mfma16x16x32(a0, as_bf16x8(xs[row * 8 + (grp ^ (row & 7))]), acc[mt]);
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int row = mt * 16 + col;
+    acc[mt] = mfma16x16x32(a1, as_bf16x8(xs[row * 8 + ((4 + grp) ^ (row & 7))]), acc[mt]);
+  }
+}
+
+template <int MT>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                          bf16_t* __restrict__ Y, float* __restrict__ P, int M,
+                                                          int N, int K, int kps) {
+  constexpr int ROWS = MT * 16;
+  constexpr int XR = (MT * 128 + 255) / 256;        // 16-B X pieces per thread per 64-k chunk
+  __shared__ __attribute__((aligned(16))) uint4 xs[ROWS * 8];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int n0 = blockIdx.x * NW;
+  const int split = blockIdx.y;
+  const int k_begin = split * kps;
+  const int k_end = min(K, k_begin + kps);
+  const int nchunks = (k_end - k_begin) >> 6;
+
+  // W row this lane streams (clamped; out-of-range columns are computed but never stored)
+  const int wn = min(n0 + wave * 16 + col, N - 1);
+  const bf16_t* wp = W + (size_t)wn * K + k_begin + 8 * grp;
+
+  u32x4 xr[XR];
+  f32x4 acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 wa0 = make_uint4(0, 0, 0, 0), wa1 = wa0, wb0 = wa0, wb1 = wa0;  // two register sets
+  if (nchunks > 0) {
+    sk_load_w(wa0, wa1, wp, 0, nchunks);
+    sk_load_w(wb0, wb1, wp, 1, nchunks);
+    sk_load_x<MT>(xr, X, M, K, k_begin, 0, tid);
+    sk_store_x<MT>(xr, xs, tid);
+    __syncthreads();
+    int c = 0;
+    for (; c + 1 < nchunks; c += 2) {
+      sk_load_x<MT>(xr, X, M, K, k_begin, c + 1, tid);   // chunk c with set A
+      sk_compute<MT>(acc, wa0, wa1, xs, col, grp);
+      sk_load_w(wa0, wa1, wp, c + 2, nchunks);
+      __syncthreads();
+      sk_store_x<MT>(xr, xs, tid);
+      __syncthreads();
+      // chunk c + 1 with set B; loads past the end are clamped to the last chunk (harmless
+      // re-reads) so that no staging register is written under a branch (keeps xr in VGPRs)
+      sk_load_x<MT>(xr, X, M, K, k_begin, min(c + 2, nchunks - 1), tid);
+      sk_compute<MT>(acc, wb0, wb1, xs, col, grp);
+      sk_load_w(wb0, wb1, wp, c + 3, nchunks);
+      __syncthreads();
+      sk_store_x<MT>(xr, xs, tid);
+      __syncthreads();
+    }
+    if (c < nchunks) sk_compute<MT>(acc, wa0, wa1, xs, col, grp);  // odd tail (its X is in LDS)
+  }
+
+  // epilogue: lane holds n = n0 + wave*16 + 4*grp + r (r = 0..3) for m = mt*16 + col
+  const int nb = n0 + wave * 16 + 4 * grp;
+  if (nb >= N) return;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mt * 16 + col;
+    if (m >= M) continue;
+    if (P) {
+      float* dst = P + ((size_t)split * M + m) * N + nb;
+      if (nb + 3 < N) {
+        *reinterpret_cast<float4*>(dst) = make_float4(acc[mt][0], acc[mt][1], acc[mt][2], acc[mt][3]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (nb + r < N) dst[r] = acc[mt][r];
+      }
+    } else {
+      bf16_t* dst = Y + (size_t)m * N + nb;
+      if (nb + 3 < N) {
+        *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc[mt][0], acc[mt][1]), pack2(acc[mt][2], acc[mt][3]));
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (nb + r < N) dst[r] = f2bf(acc[mt][r]);
+      }
+    }
+  }
+}
+
+// Y[m, n] = bf16(sum_s P[s, m, n])
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(bf16_t* __restrict__ Y, const float* __restrict__ P,
+                                                            int split, long mn) {
+  for (long i = (blockIdx.x * (long)blockDim.x + threadIdx.x) * 4; i < mn; i += (long)gridDim.x * blockDim.x * 4) {
+    float4 s = *reinterpret_cast<const float4*>(P + i);
+    for (int k = 1; k < split; ++k) {
+      const float4 t = *reinterpret_cast<const float4*>(P + (size_t)k * mn + i);
+      s.x += t.x;
+      s.y += t.y;
+      s.z += t.z;
+      s.w += t.w;
+    }
+    *reinterpret_cast<uint2*>(Y + i) = make_uint2(pack2(s.x, s.y), pack2(s.z, s.w));
+  }
+}
+
+template <int MT>
+static void launch_mt(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int split, int kps,
+                      hipStream_t stream) {
+  dim3 grid((N + NW - 1) / NW, split);
+  hipLaunchKernelGGL(gemm_skinny_kernel<MT>, grid, dim3(256), 0, stream, X, W, Y, P, M, N, K, kps);
+}
+
+// split > 1 requires a workspace P of split * M * N floats; Y is then produced by the reduce kernel.
+extern "C" int ka_gemm_skinny(void* Y, const void* X, const void* W, void* workspace, int M, int N, int K, int split,
+                              hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > 256 || K % 64 != 0 || N % 4 != 0 || split < 1) return (int)hipErrorInvalidValue;
+  int kps = (K / split + 63) / 64 * 64;
+  split = (K + kps - 1) / kps;
+  auto* x = static_cast<const bf16_t*>(X);
+  auto* w = static_cast<const bf16_t*>(W);
+  auto* y = static_cast<bf16_t*>(Y);
+  float* p = split > 1 ? static_cast<float*>(workspace) : nullptr;
+  const int mt = (M + 15) / 16;
+  if (mt <= 1) launch_mt<1>(x, w, y, p, M, N, K, split, kps, stream);
+  else if (mt <= 2) launch_mt<2>(x, w, y, p, M, N, K, split, kps, stream);
+  else if (mt <= 4) launch_mt<4>(x, w, y, p, M, N, K, split, kps, stream);
+  else if (mt <= 6) launch_mt<6>(x, w, y, p, M, N, K, split, kps, stream);
+  else if (mt <= 8) launch_mt<8>(x, w, y, p, M, N, K, split, kps, stream);
+  else if (mt <= 12) launch_mt<12>(x, w, y, p, M, N, K, split, kps, stream);
+  else launch_mt<16>(x, w, y, p, M, N, K, split, kps, stream);
+  if (split > 1) {
+    const long mn = (long)M * N;
+    long blocks = (mn / 4 + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((int)blocks), dim3(256), 0, stream, y, p, split, mn);
+  }
+  KA_CHECK_LAUNCH();
+}

@@ -13,7 +13,9 @@ fail every in-flight request (HTTP 500/503) and mark the engine unhealthy instea
 from __future__ import annotations
 
 import logging
+import os
 import queue
+import sys
 import threading
 import time
 from typing import Callable, List, Optional
@@ -45,6 +47,10 @@ class LLMEngine:
 
     # ------------------------------------------------------------------------------------------
     def start(self) -> None:
+        # The GPU loop shares the GIL with the asyncio HTTP thread; the default 5 ms switch
+        # interval would let request handling delay the next kernel launch by up to 5 ms after
+        # every device sync.  A short interval hands the GIL back to the engine promptly.
+        sys.setswitchinterval(float(os.environ.get("KA_SWITCH_INTERVAL", "0.0002")))
         if self._thread is None:
             self._thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
             self._thread.start()
@@ -153,6 +159,22 @@ class LLMEngine:
                 self._finish(s, SeqStatus.ABORTED, "error", error=err)
 
     def _loop(self) -> None:
+        prof_path = os.environ.get("KA_PROFILE_ENGINE")
+        if prof_path:  # cProfile of the engine thread (diagnostics only)
+            import cProfile
+            import pstats
+            prof = cProfile.Profile()
+            prof.enable()
+            try:
+                self._loop_body()
+            finally:
+                prof.disable()
+                with open(prof_path, "w") as f:
+                    pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(60)
+            return
+        self._loop_body()
+
+    def _loop_body(self) -> None:
         while not self._stop.is_set():
             try:
                 n = self.step()

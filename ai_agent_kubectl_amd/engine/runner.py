@@ -87,12 +87,29 @@ class ModelRunner:
         tok = self.model.sample(h, self.mask_bits, mask_idx)
         self.d_out[:B].copy_(tok)
 
+    def autotune(self) -> dict:
+        """Pick hipBLASLt vs the hand-written decode GEMM per (bucket, N, K) on this model's weights."""
+        if self.device.type != "cuda":
+            return {}
+        from ..ops.autotune import tune_linear
+        groups = {}
+        for L in self.model.layers:
+            for k in ("wqkv", "wo", "w13", "w2"):
+                w = L.get(k)
+                if w is not None and w.dim() == 2:
+                    groups.setdefault(tuple(w.shape), []).append(w)
+        lm = self.model.W["lm_head"]
+        groups.setdefault(tuple(lm.shape), []).append(lm)
+        return tune_linear(groups, self.buckets)
+
     @torch.inference_mode()
-    def capture_graphs(self) -> float:
+    def capture_graphs(self, autotune: bool = True) -> float:
         """Capture one decode graph per bucket (largest first, sharing a memory pool)."""
         if not self.use_graphs:
             return 0.0
         t0 = time.perf_counter()
+        if autotune:
+            self.gemm_plan = self.autotune()
         self.h_np[:] = 0
         o = self._off
         for name in ("slots",):

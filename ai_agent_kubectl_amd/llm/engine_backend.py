@@ -58,6 +58,8 @@ class EngineLLM(LLMBackend):
 
     async def start(self) -> None:
         if not self._started:
+            from ..utils.runtime import tune_gc
+            tune_gc()
             self.engine.start()
             self._started = True
 

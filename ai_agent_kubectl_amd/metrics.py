@@ -81,17 +81,37 @@ class ServiceMetrics:
         return generate_latest(self.registry)
 
 
-def _route_name(scope, routes) -> str:
+_ROUTE_CACHE: dict = {}
+
+
+def match_route(scope, routes):
+    """(full_route, partial_route) for (method, path), memoised: the app's routes are static
+    and the paths they match are exact (no path parameters in this service)."""
+    key = (id(routes), scope.get("method"), scope.get("path"))
+    hit = _ROUTE_CACHE.get(key)
+    if hit is not None:
+        return hit
     from starlette.routing import Match
 
-    partial = None
+    full = partial = None
     for route in routes:
         match, _ = route.matches(scope)
         if match == Match.FULL:
-            return route.path
+            full = route
+            break
         if match == Match.PARTIAL and partial is None:
-            partial = route.path
-    return partial if partial is not None else "none"
+            partial = route
+    if len(_ROUTE_CACHE) > 4096:
+        _ROUTE_CACHE.clear()
+    _ROUTE_CACHE[key] = (full, partial)
+    return full, partial
+
+
+def _route_name(scope, routes) -> str:
+    full, partial = match_route(scope, routes)
+    if full is not None:
+        return full.path
+    return partial.path if partial is not None else "none"
 
 
 class PrometheusMiddleware:

@@ -76,7 +76,7 @@ class LlamaModel:
                 x = ops.rmsnorm(h, L["ln1"], eps)
             else:
                 x = ops.rmsnorm(h, L["ln1"], eps, residual=residual)
-            qkv = F.linear(x, L["wqkv"])
+            qkv = ops.linear(x, L["wqkv"])
             q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, k_cache[li], v_cache[li],
                                   self.hq, self.hkv, self.D)
             if meta.is_decode:
@@ -84,20 +84,20 @@ class LlamaModel:
             else:
                 a = ops.attention_prefill(q, k_cache[li], v_cache[li], meta.block_tables, meta.q_starts,
                                           meta.ctx_lens, meta.max_q_len, self.scale)
-            h = F.linear(a.view(T, self.hq * self.D), L["wo"])
+            h = ops.linear(a.view(T, self.hq * self.D), L["wo"])
             self.comm.all_reduce(h)
             x = ops.rmsnorm(h, L["ln2"], eps, residual=residual)
             if cfg.is_moe:
                 h = moe_forward(x, L, cfg, self.ep_rank, self.ep_size, meta.is_decode)
             else:
-                h = F.linear(ops.silu_mul(F.linear(x, L["w13"])), L["w2"])
+                h = ops.linear(ops.silu_mul(ops.linear(x, L["w13"])), L["w2"])
             self.comm.all_reduce(h)
         x = ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
         return x.index_select(0, meta.logits_indices)
 
     def logits(self, hidden_last: torch.Tensor) -> torch.Tensor:
         """Vocab-parallel logits of this rank: [S, V / tp] (bf16)."""
-        return F.linear(hidden_last, self.W["lm_head"])
+        return ops.linear(hidden_last, self.W["lm_head"])
 
     def sample(self, hidden_last: torch.Tensor, mask_bits: Optional[torch.Tensor],
                mask_idx: Optional[torch.Tensor]) -> torch.Tensor:

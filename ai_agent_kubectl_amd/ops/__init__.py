@@ -142,4 +142,44 @@ def moe_topk(router_logits: torch.Tensor, k: int):
     return w, ids
 
 
+# ---- decode GEMM (K13): hand-written weight-streaming split-K MFMA kernel for M <= 256 ----
+SKINNY_MAX_M = 256
+SKINNY_TARGET_WGS = int(__import__("os").environ.get("KA_SKINNY_WGS", "512"))
+
+
+def skinny_split(M: int, N: int, K: int, target_wgs: int = 0) -> int:
+    target = target_wgs or SKINNY_TARGET_WGS
+    tiles = (N + 63) // 64
+    split = max(1, min(target // max(tiles, 1), K // 256))
+    return split
+
+
+# (M, N, K) -> ("skinny", split) | ("blas", 0); filled by ops.autotune at engine start.
+GEMM_PLAN: dict = {}
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0) -> torch.Tensor:
+    """y = x @ w.T (w is [out, in]).  Decode-sized M goes to the hand-written weight-streaming
+    kernel or hipBLASLt, whichever the autotuned plan measured faster for this (M, N, K); larger M
+    (prefill) goes to hipBLASLt via F.linear."""
+    M, K = x.shape
+    N = w.shape[0]
+    if _ref(x) or M > SKINNY_MAX_M or K % 64 != 0 or N % 4 != 0 or not x.is_contiguous():
+        return torch.nn.functional.linear(x, w)
+    if not split:
+        plan = GEMM_PLAN.get((M, N, K))
+        if plan is not None:
+            if plan[0] == "blas":
+                return torch.nn.functional.linear(x, w)
+            split = plan[1]
+    lib = require()
+    split = split or skinny_split(M, N, K)
+    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    kps = ((K // split + 63) // 64) * 64
+    split = (K + kps - 1) // kps
+    ws = torch.empty((split, M, N), dtype=torch.float32, device=x.device) if split > 1 else None
+    check(lib.ka_gemm_skinny(_p(y), _p(x), _p(w), _p(ws), M, N, K, split, _stream()), "gemm_skinny")
+    return y
+
+
 rope_cos_sin = ref.rope_cos_sin

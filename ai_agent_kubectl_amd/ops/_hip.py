@@ -35,7 +35,7 @@ _SIGS = {
     "ka_moe_topk": [P, P, P, I, I, I, P],
     "ka_paged_decode": [P, P, P, P, P, I, P, I, I, I, I, I, F, P],
     "ka_paged_prefill": [P, P, P, P, P, I, P, P, I, I, I, I, I, I, F, P],
-    "ka_gemv_bf16": [P, P, P, P, I, I, I, I, P],
+    "ka_gemm_skinny": [P, P, P, P, I, I, I, I, P],
     "ka_moe_grouped_gemm": [P, P, P, P, P, P, I, I, I, I, I, I, P],
     "ka_allreduce_oneshot": [P, P, P, I, I, I, I, P],
 }

@@ -144,13 +144,10 @@ class RateLimitMiddleware:
         if scope["type"] != "http" or not self.limiter.enabled:
             await self.app(scope, receive, send)
             return
-        from starlette.routing import Match
+        from .metrics import match_route
 
-        handler = None
-        for route in self.routes():
-            match, _ = route.matches(scope)
-            if match == Match.FULL and hasattr(route, "endpoint"):
-                handler = route.endpoint
+        full, _ = match_route(scope, self.routes())
+        handler = getattr(full, "endpoint", None)
         if handler is not None:
             name = "%s.%s" % (handler.__module__, handler.__name__)
             if name not in self.exempt_endpoints():

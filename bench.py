@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--model", default=os.environ.get("BENCH_MODEL", "llama3-8b"))
     ap.add_argument("--max-new-tokens", type=int, default=16)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--client", choices=["asgi", "httpx"], default="asgi",
+                    help="asgi: minimal in-process ASGI client (default); httpx: httpx.ASGITransport")
     args = ap.parse_args()
 
     import torch
@@ -86,14 +88,46 @@ def main():
     app = create_app(settings, backend=backend)
 
     lat = []
+    headers = [(b"host", b"bench"), (b"content-type", b"application/json")]
+
+    async def asgi_post(path, body: bytes):
+        """Minimal in-process ASGI client: one HTTP/1.1 request through the full app stack
+        (Prometheus + rate-limit middleware, routing, auth dep, validation, handler, JSON)."""
+        scope = {"type": "http", "asgi": {"version": "3.0"}, "http_version": "1.1", "method": "POST",
+                 "scheme": "http", "path": path, "raw_path": path.encode(), "query_string": b"",
+                 "root_path": "", "headers": headers + [(b"content-length", str(len(body)).encode())],
+                 "client": ("127.0.0.1", 40000), "server": ("bench", 80)}
+        done = [False]
+
+        async def receive():
+            if not done[0]:
+                done[0] = True
+                return {"type": "http.request", "body": body, "more_body": False}
+            await asyncio.sleep(3600)
+            return {"type": "http.disconnect"}
+
+        out = {"status": 0, "body": []}
+
+        async def send(msg):
+            if msg["type"] == "http.response.start":
+                out["status"] = msg["status"]
+            elif msg["type"] == "http.response.body":
+                out["body"].append(msg.get("body", b""))
+
+        await app(scope, receive, send)
+        return out["status"], b"".join(out["body"])
 
     async def one(client, q, record):
         t0 = time.perf_counter()
-        r = await client.post("/kubectl-command", json={"query": q})
+        if client is None:
+            status, raw = await asgi_post("/kubectl-command", json.dumps({"query": q}).encode())
+            body = json.loads(raw)
+        else:
+            r = await client.post("/kubectl-command", json={"query": q})
+            status, body = r.status_code, r.json()
         dt = time.perf_counter() - t0
-        if r.status_code != 200:
-            raise RuntimeError(f"{r.status_code}: {r.text}")
-        body = r.json()
+        if status != 200:
+            raise RuntimeError(f"{status}: {body}")
         assert body["from_cache"] is False
         if record:
             lat.append(dt)
@@ -111,7 +145,8 @@ def main():
         await backend.start()
         limits = httpx.Limits(max_connections=None, max_keepalive_connections=None)
         async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://bench",
-                                     limits=limits, timeout=600) as client:
+                                     limits=limits, timeout=600) as hc:
+            client = hc if args.client == "httpx" else None
             sample = None
             for s in range(args.warmup):
                 sample = await wave(client, s, False)
@@ -126,7 +161,17 @@ def main():
         await backend.close()
         return el, sample, {k: st1[k] - st0[k] for k in st1}
 
-    elapsed, sample, st = asyncio.run(run())
+    if os.environ.get("KA_PROFILE_API"):
+        import cProfile
+        import pstats
+        prof = cProfile.Profile()
+        prof.enable()
+        elapsed, sample, st = asyncio.run(run())
+        prof.disable()
+        with open(os.environ["KA_PROFILE_API"], "w") as f:
+            pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(50)
+    else:
+        elapsed, sample, st = asyncio.run(run())
     n_req = C * args.steps
     p50 = statistics.median(lat) * 1e3
     if world > 1:

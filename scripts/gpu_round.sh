@@ -10,7 +10,17 @@ run_tests() { timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cachep
 run_smoke() { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; }
 run_bench() { timeout -k 10 600 python bench.py --steps ${BENCH_STEPS:-5} --warmup ${BENCH_WARMUP:-2} ${BENCH_ARGS} > gpurun_out/bench.log 2>&1; }
 run_prof() { cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 ${BENCH_ARGS} > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1; cd "$GRAFT_REPO_ROOT"; }
+run_cprof() { KA_PROFILE_ENGINE=gpurun_out/cprof_engine.txt KA_PROFILE_API=gpurun_out/cprof_api.txt timeout -k 10 600 python bench.py --steps 3 --warmup 1 ${BENCH_ARGS} > gpurun_out/bench_cprof.log 2>&1; }
+run_gemm() { timeout -k 10 600 python scripts/bench_gemm.py > gpurun_out/bench_gemm.log 2>&1; }
+run_ktest() { timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -x -q -p no:cacheprovider > gpurun_out/pytest_kernels.log 2>&1; }
+run_sweep() { for c in ${SWEEP:-64 128 256}; do timeout -k 10 600 python bench.py --steps 4 --warmup 2 --concurrency $c ${BENCH_ARGS} > gpurun_out/bench_c$c.log 2>&1 || return 1; done; }
 case "$STEP" in
+  sweep) run_sweep ;;
+  testsweep) run_tests && run_sweep ;;
+  gemm) run_ktest && run_gemm ;;
+  gemmbench) run_ktest && run_gemm && run_tests && run_bench ;;
+  cprof) run_cprof ;;
+  profall) run_bench && run_prof && run_cprof ;;
   tests) run_tests ;;
   smoke) run_smoke ;;
   bench) run_bench ;;

@@ -161,3 +161,14 @@ def test_moe_topk():
     w2, i2 = ref.moe_topk(lg, 2)
     assert torch.equal(i1.cpu().sort(1).values, i2.cpu().sort(1).values)
     close(w1.sort(1).values, w2.sort(1).values, atol=1e-5)
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 128, 200, 256])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (16032, 4096), (1000, 512)])
+def test_gemm_skinny(M, N, K):
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(BF)
+    want = x.float() @ w.float().t()
+    for split in (1, 3, 8):
+        got = ops.linear(x, w, split=split)
+        close(got, want, atol=3e-2, rtol=2e-2)
