@@ -53,6 +53,9 @@ def build_backend(settings, metrics=None) -> Optional[LLMBackend]:
         from .remote import OpenAIChatLLM
         return OpenAIChatLLM(settings)
     if kind == "engine":
+        if settings.DP > 1:
+            from ..parallel.dp import DPRouterLLM
+            return DPRouterLLM(settings, settings.DP)
         from .engine_backend import EngineLLM
         return EngineLLM.from_settings(settings, metrics=metrics)
     raise ValueError(f"unknown LLM_BACKEND {settings.LLM_BACKEND!r}")

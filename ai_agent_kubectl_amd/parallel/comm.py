@@ -56,9 +56,9 @@ class TorchComm:
         return t
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
-        out = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
-        return out
+        flat = torch.empty(self.world_size * t.numel(), dtype=t.dtype, device=t.device)
+        self.dist.all_gather_into_tensor(flat, t.contiguous().view(-1), group=self.group)
+        return flat.view((self.world_size,) + tuple(t.shape))
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         self.dist.broadcast(t, src=self.dist.get_global_rank(self.group, src) if self.group else src,

@@ -1,0 +1,225 @@
+"""Data parallelism for serving: N engine replicas (one process per GPU) behind one API process.
+
+SURVEY.md §2.5 DP row: the API process keeps the single TTL cache and rate limiter (so
+`from_cache` semantics match `/root/reference/app.py:312-322` exactly) and routes every cache miss to
+the replica with the fewest in-flight requests.  Replicas are spawned (multiprocessing "spawn")
+BEFORE the API process touches the GPU; each binds `cuda:i`, builds its engine (random-init or
+safetensors weights, hipGraph capture) and serves token-id requests from a queue.  Tokenisation
+and detokenisation stay in the API process; only int lists cross the process boundary.
+
+A replica that dies (or fails to start) is marked down; its in-flight requests fail with
+LLMUnavailableError (HTTP 503) and new requests go to the remaining replicas.
+"""
+from __future__ import annotations
+
+import asyncio
+import dataclasses
+import itertools
+import logging
+import multiprocessing as mp
+import threading
+import time
+from typing import Dict, List, Optional
+
+from ..llm.base import LLMBackend, LLMUnavailableError
+
+logger = logging.getLogger("app.dp")
+
+
+def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> None:
+    """Entry point of one replica process."""
+    import torch  # noqa: F401  (first CUDA use happens here, in the child)
+
+    from ..config import Settings
+    from ..engine.builder import EngineOptions, build_engine
+    from ..engine.safe_decode import forced_prefix
+    from ..engine.sequence import SamplingParams
+
+    try:
+        s = Settings(**settings_dict)
+        opts = EngineOptions.from_settings(s)
+        opts.device = device
+        eng = build_engine(opts)
+        if opts.use_graphs and device.startswith("cuda"):
+            eng.runner.capture_graphs()
+        from ..utils.runtime import tune_gc
+        tune_gc()
+        eng.start()
+        params = SamplingParams(max_new_tokens=s.MAX_NEW_TOKENS, ignore_eos=s.IGNORE_EOS, safe_decode=s.SAFE_DECODE)
+        forced = forced_prefix(eng.tokenizer) if s.SAFE_DECODE else []
+        resp_q.put(("ready", idx, None))
+    except Exception as e:  # pragma: no cover - reported to the router
+        resp_q.put(("dead", idx, repr(e)))
+        return
+
+    def done(seq, rid):
+        err = repr(seq.error) if seq.error is not None else None
+        resp_q.put(("done", rid, (seq.output_ids, err, seq.finish_reason)))
+
+    live = {}
+    while True:
+        msg = req_q.get()
+        if msg is None:
+            break
+        op, rid, payload = msg
+        if op == "gen":
+            seq = eng.submit(payload, params, lambda sq, rid=rid: done(sq, rid), forced_prefix=forced)
+            live[rid] = seq
+        elif op == "abort" and rid in live:
+            eng.abort(live.pop(rid))
+        if len(live) > 4096:
+            live = {k: v for k, v in live.items() if not v.finished}
+    eng.shutdown()
+
+
+@dataclasses.dataclass
+class _Replica:
+    idx: int
+    proc: mp.Process
+    req_q: object
+    inflight: int = 0
+    up: bool = False
+
+
+class DPRouterLLM(LLMBackend):
+    """LLM backend that fans requests out over DP engine replicas."""
+
+    name = "engine-dp"
+
+    def __init__(self, settings, dp: int, devices: Optional[List[str]] = None, start_timeout: float = 900):
+        from ..engine.tokenizer import get_tokenizer
+        from ..models.config import get_config
+        from ..prompt import PROMPT_PREFIX
+
+        cfg = get_config(settings.MODEL)
+        self.tok = get_tokenizer(cfg.vocab_size, cfg.tokenizer)
+        before, after = self.tok.chat_prefix_suffix()
+        self._prefix = before + self.tok.encode(PROMPT_PREFIX)
+        self._after = after
+        self.settings = settings
+        self.devices = devices or [f"cuda:{i}" for i in range(dp)]
+        ctx = mp.get_context("spawn")
+        self.resp_q = ctx.Queue()
+        sd = dataclasses.asdict(settings)
+        sd.update(TP=1, DP=1)
+        self.replicas: List[_Replica] = []
+        for i, dev in enumerate(self.devices):
+            rq = ctx.Queue()
+            p = ctx.Process(target=_replica_main, args=(i, dev, sd, rq, self.resp_q), daemon=True)
+            p.start()
+            self.replicas.append(_Replica(i, p, rq))
+        self._pending: Dict[int, tuple] = {}
+        self._ids = itertools.count()
+        self._lock = threading.Lock()
+        self._ready = threading.Event()
+        self._n_ready = 0
+        self._reader = threading.Thread(target=self._read_loop, name="dp-router", daemon=True)
+        self._reader.start()
+        self._start_timeout = start_timeout
+
+    # -----------------------------------------------------------------------------------------
+    def _read_loop(self) -> None:
+        while True:
+            try:
+                kind, a, b = self.resp_q.get(timeout=1.0)
+            except Exception:
+                self._check_alive()
+                continue
+            if kind == "ready":
+                self.replicas[a].up = True
+                self._n_ready += 1
+                if self._n_ready == len(self.replicas):
+                    self._ready.set()
+            elif kind == "dead":
+                logger.error("DP replica %d failed to start: %s", a, b)
+                self.replicas[a].up = False
+                self._n_ready += 1
+                if self._n_ready == len(self.replicas):
+                    self._ready.set()
+            elif kind == "done":
+                with self._lock:
+                    ent = self._pending.pop(a, None)
+                    if ent is not None:
+                        ent[2].inflight -= 1
+                if ent is not None:
+                    ent[0].call_soon_threadsafe(_set, ent[1], b)
+            elif kind == "stop":
+                return
+
+    def _check_alive(self) -> None:
+        for r in self.replicas:
+            if r.up and not r.proc.is_alive():
+                logger.error("DP replica %d died (exit %s)", r.idx, r.proc.exitcode)
+                r.up = False
+                with self._lock:
+                    dead = [(k, v) for k, v in self._pending.items() if v[2] is r]
+                    for k, _ in dead:
+                        self._pending.pop(k)
+                for _, (loop, fut, _) in dead:
+                    loop.call_soon_threadsafe(_set_exc, fut, LLMUnavailableError(f"replica {r.idx} died"))
+
+    def wait_ready(self, timeout: Optional[float] = None) -> bool:
+        return self._ready.wait(timeout if timeout is not None else self._start_timeout)
+
+    async def start(self) -> None:
+        loop = asyncio.get_running_loop()
+        await loop.run_in_executor(None, self.wait_ready)
+
+    async def close(self) -> None:
+        for r in self.replicas:
+            try:
+                r.req_q.put(None)
+            except Exception:
+                pass
+        for r in self.replicas:
+            r.proc.join(timeout=30)
+            if r.proc.is_alive():
+                r.proc.terminate()
+        self.resp_q.put(("stop", 0, None))
+
+    def healthy(self) -> bool:
+        return any(r.up for r in self.replicas)
+
+    def stats(self):
+        return {f"replica{r.idx}_inflight": r.inflight for r in self.replicas}
+
+    # -----------------------------------------------------------------------------------------
+    def prompt_ids(self, query: str) -> List[int]:
+        from ..prompt import PROMPT_SUFFIX
+        return self._prefix + self.tok.encode(query + PROMPT_SUFFIX) + self._after
+
+    async def generate(self, query: str) -> str:
+        if not self._ready.is_set():
+            await self.start()
+        live = [r for r in self.replicas if r.up]
+        if not live:
+            raise LLMUnavailableError("no live DP replica")
+        rep = min(live, key=lambda r: r.inflight)
+        rid = next(self._ids)
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        with self._lock:
+            self._pending[rid] = (loop, fut, rep)
+            rep.inflight += 1
+        rep.req_q.put(("gen", rid, self.prompt_ids(query)))
+        try:
+            out_ids, err, reason = await fut
+        except asyncio.CancelledError:
+            rep.req_q.put(("abort", rid, None))
+            with self._lock:
+                if self._pending.pop(rid, None) is not None:
+                    rep.inflight -= 1
+            raise
+        if err is not None:
+            raise LLMUnavailableError(err) if reason == "error" else RuntimeError(err)
+        return self.tok.decode([t for t in out_ids if not self.tok.is_eos(t)])
+
+
+def _set(fut, val):
+    if not fut.done():
+        fut.set_result(val)
+
+
+def _set_exc(fut, exc):
+    if not fut.done():
+        fut.set_exception(exc)
