@@ -84,7 +84,15 @@ class KubectlService:
             raise HTTPException(status_code=status.HTTP_503_SERVICE_UNAVAILABLE, detail="LLM Chain not initialized")
         timeout = self.settings.LLM_TIMEOUT
 
+        s = self.settings
+
         async def _chain() -> str:
+            if s.FAULT_LLM_DELAY_MS:          # fault injection: exercise 504 paths
+                await asyncio.sleep(s.FAULT_LLM_DELAY_MS / 1000.0)
+            if s.FAULT_LLM_ERROR:
+                if s.FAULT_LLM_ERROR == "unavailable":
+                    raise LLMUnavailableError("injected fault")
+                raise RuntimeError(s.FAULT_LLM_ERROR)
             return safety.parse_llm_output(await self.backend.generate(query))
 
         loop = asyncio.get_running_loop()
@@ -250,6 +258,15 @@ def create_app(settings: Optional[Settings] = None, backend: Any = _UNSET,
             svc.metrics.execute_duration.observe(execution_data["metadata"]["duration_ms"] / 1000.0)
         # COMPAT_STRICT_500: a result without metadata raises KeyError -> plain-text 500 (quirk Q1).
         return _json(_command_body(req.execute, False, execution_data))
+
+    @app.get("/ready", summary="Readiness: 200 once the LLM backend can serve, else 503")
+    async def readiness():
+        ok = svc.backend is not None and svc.backend.healthy()
+        body = {"status": "ready" if ok else "not ready", "backend": getattr(svc.backend, "name", None)}
+        return _json(body, status_code=200 if ok else 503)
+
+    from .openai_compat import install as _install_openai
+    _install_openai(app, svc, settings)
 
     @app.get("/metrics", include_in_schema=True)
     async def metrics_endpoint():

@@ -52,6 +52,7 @@ class LLMEngine:
         # every device sync.  A short interval hands the GIL back to the engine promptly.
         sys.setswitchinterval(float(os.environ.get("KA_SWITCH_INTERVAL", "0.0002")))
         if self._thread is None:
+            self._stop.clear()
             self._thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
             self._thread.start()
 

@@ -102,6 +102,42 @@ class EngineLLM(LLMBackend):
     def stats(self):
         return dict(self.engine.runner.stats)
 
+    # ---- OpenAI-compatible chat (api/openai_compat.py) ----------------------------------------
+    def chat_ids(self, messages) -> List[int]:
+        """Multi-turn chat template of the model family (Llama-3 header tokens / Llama-2 [INST])."""
+        tok = self.tok
+        if tok.family == "llama3":
+            s = tok.specials
+            ids = [s["<|begin_of_text|>"]]
+            for m in messages:
+                ids += [s["<|start_header_id|>"]] + tok.encode(m["role"]) + [s["<|end_header_id|>"]]
+                ids += tok.encode("\n\n" + m["content"]) + [s["<|eot_id|>"]]
+            ids += [s["<|start_header_id|>"]] + tok.encode("assistant") + [s["<|end_header_id|>"]] + tok.encode("\n\n")
+            return ids
+        text = "".join(f"[INST] {m['content']} [/INST]" if m["role"] != "assistant" else f" {m['content']} "
+                       for m in messages)
+        return [tok.bos_id] + tok.encode(text)
+
+    async def generate_chat(self, messages, max_tokens: int = 64, safe: bool = False):
+        """Returns (text, finish_reason, prompt_tokens, completion_tokens)."""
+        if not self._started:
+            await self.start()
+        loop = asyncio.get_running_loop()
+        fut: asyncio.Future = loop.create_future()
+        params = SamplingParams(max_new_tokens=max_tokens, ignore_eos=False, safe_decode=safe)
+        ids = self.chat_ids(messages)
+        seq = self.engine.submit(ids, params, lambda sq: loop.call_soon_threadsafe(_resolve, fut, sq),
+                                 forced_prefix=self._forced if safe else None)
+        try:
+            seq = await fut
+        except asyncio.CancelledError:
+            self.engine.abort(seq)
+            raise
+        if seq.error is not None:
+            raise LLMUnavailableError(str(seq.error))
+        out = [t for t in seq.output_ids if not self.tok.is_eos(t)]
+        return self.tok.decode(out), ("stop" if seq.finish_reason == "stop" else "length"), len(ids), len(seq.output_ids)
+
 
 def _resolve(fut: asyncio.Future, seq) -> None:
     if not fut.done():

@@ -240,3 +240,18 @@ def test_openapi_and_docs():
     assert set(spec["paths"]) >= {"/kubectl-command", "/execute", "/health", "/metrics"}
     assert c.get("/docs").status_code == 200
     assert c.get("/redoc").status_code == 200
+
+
+def test_fault_injection_and_ready():
+    c, _ = make(FAULT_LLM_ERROR="unavailable")
+    r = c.post("/kubectl-command", json={"query": "list pods"}, headers=H)
+    assert r.status_code == 503
+    c, _ = make(FAULT_LLM_DELAY_MS=1500, LLM_TIMEOUT=1)
+    r = c.post("/kubectl-command", json={"query": "list pods"}, headers=H)
+    assert (r.status_code, r.text) == (504, '{"detail":"LLM request timed out"}')
+    c, _ = make(FAULT_LLM_ERROR="kaboom")
+    assert c.post("/kubectl-command", json={"query": "x y z"}, headers=H).json() == {
+        "detail": "Error processing query with LLM: kaboom"}
+    assert c.get("/ready").status_code == 200
+    s = Settings(RATE_LIMIT="100/minute")
+    assert TestClient(create_app(s, backend=None)).get("/ready").status_code == 503

@@ -185,3 +185,20 @@ def test_virtual_tp2_matches_tp1_cpu(model):
     b = virtual_tp_logits(cfg, 2, device="cpu").float()
     assert torch.nn.functional.cosine_similarity(a, b, dim=-1).min() > 0.9999
     assert torch.equal(a.argmax(-1), b.argmax(-1))
+
+
+def test_openai_compatible_chat(tiny_engine):
+    from fastapi.testclient import TestClient
+    from ai_agent_kubectl_amd.api import create_app
+    from ai_agent_kubectl_amd.config import Settings
+    eng, be = tiny_engine
+    app = create_app(Settings(RATE_LIMIT="1000/minute", API_AUTH_KEY="k", MODEL="tiny-llama"), backend=be)
+    with TestClient(app) as c:
+        body = {"model": "tiny-llama", "messages": [{"role": "user", "content": "list pods"}], "max_tokens": 5}
+        assert c.post("/v1/chat/completions", json=body).status_code == 401
+        r = c.post("/v1/chat/completions", json=body, headers={"Authorization": "Bearer k"})
+        assert r.status_code == 200, r.text
+        j = r.json()
+        assert j["object"] == "chat.completion" and j["usage"]["completion_tokens"] <= 5
+        assert isinstance(j["choices"][0]["message"]["content"], str)
+        assert c.get("/v1/models", headers={"X-API-Key": "k"}).json()["data"][0]["id"] == "tiny-llama"
