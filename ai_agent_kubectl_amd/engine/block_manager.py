@@ -12,7 +12,7 @@ Invariants:
   dry; a block with ref 0 and no hash goes straight back to the free list;
 * at least one prompt token is always recomputed so the prefill produces logits.
 
-The C++ runtime (`runtime/block_manager.cpp`) implements the same structure for the scheduler hot
+The C++ runtime (`runtime/native.cpp`, `make_block_manager`) implements the same structure for the scheduler hot
 path when the native module is built; this Python class is the reference and the fallback.
 """
 from __future__ import annotations
@@ -79,6 +79,9 @@ class BlockManager:
                 self.free.append(b)
 
     # ------------------------------------------------------------------------------------------
+    def ref_count(self, b: int) -> int:
+        return self.ref[b]
+
     def blocks_needed(self, num_tokens: int) -> int:
         return (num_tokens + self.block_size - 1) // self.block_size
 
@@ -150,3 +153,14 @@ class BlockManager:
             self.free.append(b)
         self.evictable.clear()
         self.cached = {h: b for h, b in self.cached.items() if self.ref[b] > 0}
+
+
+def make_block_manager(num_blocks: int, block_size: int = 16, enable_prefix_caching: bool = True):
+    """The C++ allocator (runtime/native.cpp) when built, else this Python reference."""
+    try:
+        from ..runtime.native import NativeBlockManager, available
+        if available():
+            return NativeBlockManager(num_blocks, block_size, enable_prefix_caching)
+    except ImportError:
+        pass
+    return BlockManager(num_blocks, block_size, enable_prefix_caching)

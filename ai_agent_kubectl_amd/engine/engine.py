@@ -20,7 +20,7 @@ import threading
 import time
 from typing import Callable, List, Optional
 
-from .block_manager import BlockManager
+from .block_manager import make_block_manager
 from .runner import ModelRunner
 from .scheduler import Scheduler
 from .sequence import SamplingParams, Sequence, SeqStatus
@@ -33,7 +33,7 @@ class LLMEngine:
                  max_model_len: int = 4096, prefix_caching: bool = True, metrics=None):
         self.runner = runner
         self.tokenizer = tokenizer
-        self.bm = BlockManager(runner.num_blocks, runner.block_size, enable_prefix_caching=prefix_caching)
+        self.bm = make_block_manager(runner.num_blocks, runner.block_size, enable_prefix_caching=prefix_caching)
         self.scheduler = Scheduler(self.bm, max_batch=max_batch, max_batched_tokens=max_batched_tokens,
                                    max_model_len=max_model_len)
         self.metrics = metrics

@@ -145,7 +145,7 @@ def test_engine_generates_safe_commands_and_hits_prefix_cache(tiny_engine):
         assert txt.startswith("kubectl ") and is_safe_kubectl_command(txt)
     seqs2 = eng.generate_blocking([be.prompt_ids("get nodes")], be.params, forced_prefix=be._forced)
     assert seqs2[0].num_cached_prompt >= 48
-    assert eng.bm.num_used == 0 or all(eng.bm.ref[b] == 0 for b in range(eng.bm.num_blocks))
+    assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
 
 
 def test_prefix_cached_equals_cold(tiny_engine):
@@ -202,3 +202,63 @@ def test_openai_compatible_chat(tiny_engine):
         assert j["object"] == "chat.completion" and j["usage"]["completion_tokens"] <= 5
         assert isinstance(j["choices"][0]["message"]["content"], str)
         assert c.get("/v1/models", headers={"X-API-Key": "k"}).json()["data"][0]["id"] == "tiny-llama"
+
+
+def test_native_block_manager_matches_python():
+    import random
+    from ai_agent_kubectl_amd.runtime.native import NativeBlockManager, available
+    if not available():
+        pytest.skip("native runtime not built")
+    rng = random.Random(0)
+    py_bm, nv_bm = BlockManager(40, 4), NativeBlockManager(40, 4)
+    prefixes = [[rng.randrange(50) for _ in range(rng.randrange(4, 17))] for _ in range(4)]
+    live = []
+    for step in range(400):
+        op = rng.random()
+        if op < 0.5 and len(live) < 8:
+            toks = rng.choice(prefixes) + [rng.randrange(50) for _ in range(rng.randrange(1, 9))]
+            res = []
+            register = rng.random() < 0.8
+            for bm in (py_bm, nv_bm):
+                try:
+                    t, c, h = bm.allocate_prompt(toks)
+                    res.append((t, c))
+                    if register:
+                        bm.register_computed(t, toks, h)
+                except NoFreeBlocks:
+                    res.append(None)
+            assert res[0] == res[1], step
+            if res[0] is not None:
+                live.append([res[0][0], list(res[0][0]), toks])
+        elif op < 0.75 and live:
+            ent = rng.choice(live)
+            n = len(ent[2]) + rng.randrange(1, 6)
+            outs = []
+            for bm, tbl in ((py_bm, ent[0]), (nv_bm, ent[1])):
+                try:
+                    bm.ensure_capacity(tbl, n)
+                    outs.append(list(tbl))
+                except NoFreeBlocks:
+                    outs.append(None)
+            assert outs[0] == outs[1], step
+        elif live:
+            ent = live.pop(rng.randrange(len(live)))
+            py_bm.free_table(ent[0])
+            nv_bm.free_table(ent[1])
+        assert py_bm.num_free == nv_bm.num_free
+    assert py_bm.hits == nv_bm.hits and py_bm.queries == nv_bm.queries
+
+
+def test_native_tokenizer_matches_python():
+    from ai_agent_kubectl_amd.runtime.native import available
+    if not available():
+        pytest.skip("native runtime not built")
+    tok = get_tokenizer(128256, "llama3")
+    assert tok._native is not None
+    text = render_prompt("list all pods in namespace prod ünïcode ✓ --sort-by=.metadata.name")
+    native = tok.encode(text)
+    saved, tok._native = tok._native, None
+    try:
+        assert tok.encode(text) == native
+    finally:
+        tok._native = saved
