@@ -1,0 +1,200 @@
+// Mixtral MoE on MFMA (K12): route alignment -> grouped expert GEMMs -> weighted combine.
+// Shape-static for a given token count, so the whole block is captured in the decode hipGraphs.
+//
+//   moe_align:    topk_ids [T, k] -> per-local-expert row lists (rows r = t*k + j routed to local
+//                 expert e, e in [e0, e0 + El)); counts[El], lists[El][T*k] (order within a list is
+//                 irrelevant: every row is computed independently and the combine sums in j order).
+//   moe_gemm:     Y[r, :] = A[src(r), :] @ W[e]^T for every listed row r of expert e.  A row source
+//                 is r / k (the token, first GEMM) or r (the slot, second GEMM).  Structure of
+//                 gemm_skinny.hip: workgroup = 64 output columns x up to MT*16 rows of one expert,
+//                 W fragments streamed HBM -> VGPR with a two-chunk register ring, gathered A rows
+//                 staged through an XOR-swizzled LDS tile; expert weights are streamed once per
+//                 (column tile, row chunk).
+//   moe_combine:  out[t, :] = sum_j w[t, j] * Y[t*k + j, :] over local experts (EP partial; the
+//                 caller's TP/EP all-reduce completes the sum).
+#include "common.h"
+
+__global__ __launch_bounds__(256) void moe_align_kernel(int* __restrict__ counts, int* __restrict__ lists,
+                                                        const int* __restrict__ topk_ids, int rows, int e0, int el,
+                                                        int list_stride) {
+  __shared__ int cnt[64];
+  for (int e = threadIdx.x; e < el; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+    const int e = topk_ids[r] - e0;
+    if (e >= 0 && e < el) {
+      const int pos = atomicAdd(&cnt[e], 1);
+      lists[e * list_stride + pos] = r;
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < el; e += blockDim.x) counts[e] = cnt[e];
+}
+
+template <int MT>
+__global__ __launch_bounds__(256) void moe_gemm_kernel(bf16_t* __restrict__ Y, const bf16_t* __restrict__ A,
+                                                       const bf16_t* __restrict__ W, const int* __restrict__ counts,
+                                                       const int* __restrict__ lists, int list_stride, int N, int K,
+                                                       int src_div) {
+  constexpr int ROWS = MT * 16;
+  constexpr int PIECES = ROWS * 8;
+  constexpr int XR = (PIECES + 255) / 256;
+  __shared__ __attribute__((aligned(16))) u32x4 xs[ROWS * 8];
+  const int e = blockIdx.y;
+  const int count = counts[e];
+  const int r0 = blockIdx.z * ROWS;
+  if (r0 >= count) return;
+  const int nrows = min(ROWS, count - r0);
+  const int* list = lists + (size_t)e * list_stride + r0;
+  const bf16_t* We = W + (size_t)e * N * K;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int n0 = blockIdx.x * 64;
+  const int wn = min(n0 + wave * 16 + col, N - 1);
+  const bf16_t* wp = We + (size_t)wn * K + 8 * grp;
+  const int nchunks = K >> 6;
+
+  // per-thread source rows of the X staging pieces (fixed over the K loop)
+  int srow[XR];
+#pragma unroll
+  for (int i = 0; i < XR; ++i) {
+    const int p = tid + 256 * i;
+    const int rr = min(p >> 3, nrows - 1);
+    srow[i] = list[rr] / src_div;
+  }
+  u32x4 xr[XR];
+  f32x4 acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto load_x = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int p = tid + 256 * i;
+      xr[i] = *reinterpret_cast<const u32x4*>(A + (size_t)srow[i] * K + c * 64 + (p & 7) * 8);
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int p = tid + 256 * i;
+      if (PIECES % 256 == 0 || p < PIECES) xs[(p >> 3) * 8 + ((p & 7) ^ ((p >> 3) & 7))] = xr[i];
+    }
+  };
+  auto compute = [&](const uint4& w0, const uint4& w1) {
+    const bf16x8 a0 = as_bf16x8(w0), a1 = as_bf16x8(w1);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int row = mt * 16 + col;
+      acc[mt] = mfma16x16x32(a0, __builtin_bit_cast(bf16x8, xs[row * 8 + (grp ^ (row & 7))]), acc[mt]);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int row = mt * 16 + col;
+      acc[mt] = mfma16x16x32(a1, __builtin_bit_cast(bf16x8, xs[row * 8 + ((4 + grp) ^ (row & 7))]), acc[mt]);
+    }
+  };
+  auto load_w = [&](uint4& w0, uint4& w1, int c) {
+    c = min(c, nchunks - 1);
+    w0 = *reinterpret_cast<const uint4*>(wp + c * 64);
+    w1 = *reinterpret_cast<const uint4*>(wp + c * 64 + 32);
+  };
+
+  uint4 wa0, wa1, wb0, wb1;
+  load_w(wa0, wa1, 0);
+  load_w(wb0, wb1, 1);
+  load_x(0);
+  store_x();
+  __syncthreads();
+  int c = 0;
+  for (; c + 1 < nchunks; c += 2) {
+    load_x(c + 1);
+    compute(wa0, wa1);
+    load_w(wa0, wa1, c + 2);
+    __syncthreads();
+    store_x();
+    __syncthreads();
+    load_x(min(c + 2, nchunks - 1));
+    compute(wb0, wb1);
+    load_w(wb0, wb1, c + 3);
+    __syncthreads();
+    store_x();
+    __syncthreads();
+  }
+  if (c < nchunks) compute(wa0, wa1);
+
+  const int nb = n0 + wave * 16 + 4 * grp;
+  if (nb >= N) return;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mt * 16 + col;
+    if (m < nrows) {
+      bf16_t* dst = Y + (size_t)list[m] * N + nb;
+      *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc[mt][0], acc[mt][1]), pack2(acc[mt][2], acc[mt][3]));
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void moe_combine_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ Y,
+                                                          const float* __restrict__ topk_w,
+                                                          const int* __restrict__ topk_ids, int k, int H, int e0,
+                                                          int el) {
+  const int t = blockIdx.x;
+  for (int c = threadIdx.x * 8; c < H; c += blockDim.x * 8) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < k; ++j) {
+      const int e = topk_ids[t * k + j] - e0;
+      if (e < 0 || e >= el) continue;
+      const float w = topk_w[t * k + j];
+      const uint4 y = *reinterpret_cast<const uint4*>(Y + ((size_t)t * k + j) * H + c);
+      const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[2 * q] += w * lo_f(yw[q]);
+        acc[2 * q + 1] += w * hi_f(yw[q]);
+      }
+    }
+    *reinterpret_cast<uint4*>(out + (size_t)t * H + c) =
+        make_uint4(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]), pack2(acc[4], acc[5]), pack2(acc[6], acc[7]));
+  }
+}
+
+template <int MT>
+static void launch_gemm(bf16_t* Y, const bf16_t* A, const bf16_t* W, const int* counts, const int* lists, int stride,
+                        int el, int N, int K, int src_div, int max_rows, hipStream_t s) {
+  dim3 grid((N + 63) / 64, el, (max_rows + MT * 16 - 1) / (MT * 16));
+  hipLaunchKernelGGL(moe_gemm_kernel<MT>, grid, dim3(256), 0, s, Y, A, W, counts, lists, stride, N, K, src_div);
+}
+
+extern "C" int ka_moe_align(int* counts, int* lists, const int* topk_ids, int rows, int e0, int el, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (el > 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(256), 0, s, counts, lists, topk_ids, rows, e0, el, rows);
+  KA_CHECK_LAUNCH();
+}
+
+// Y [rows_total, N] (rows_total = T*k), A [T or T*k, K], W [el, N, K]; max_rows = T*k (worst case per expert)
+extern "C" int ka_moe_gemm(void* Y, const void* A, const void* W, const int* counts, const int* lists, int list_stride,
+                           int el, int N, int K, int src_div, int max_rows, hipStream_t s) {
+  if (max_rows <= 0) return 0;
+  if (K % 64 != 0 || N % 4 != 0) return (int)hipErrorInvalidValue;
+  auto* y = static_cast<bf16_t*>(Y);
+  auto* a = static_cast<const bf16_t*>(A);
+  auto* w = static_cast<const bf16_t*>(W);
+  const int mt = (max_rows + 15) / 16;  // rows per expert never exceed max_rows
+  if (mt <= 1) launch_gemm<1>(y, a, w, counts, lists, list_stride, el, N, K, src_div, max_rows, s);
+  else if (mt <= 2) launch_gemm<2>(y, a, w, counts, lists, list_stride, el, N, K, src_div, max_rows, s);
+  else if (mt <= 4) launch_gemm<4>(y, a, w, counts, lists, list_stride, el, N, K, src_div, max_rows, s);
+  else launch_gemm<8>(y, a, w, counts, lists, list_stride, el, N, K, src_div, max_rows, s);
+  KA_CHECK_LAUNCH();
+}
+
+extern "C" int ka_moe_combine(void* out, const void* Y, const float* topk_w, const int* topk_ids, int T, int k, int H,
+                              int e0, int el, hipStream_t s) {
+  if (T <= 0) return 0;
+  if (H % 8 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, s, static_cast<bf16_t*>(out),
+                     static_cast<const bf16_t*>(Y), topk_w, topk_ids, k, H, e0, el);
+  KA_CHECK_LAUNCH();
+}

@@ -224,7 +224,9 @@ class ModelRunner:
         t0 = time.perf_counter()
         if batch.is_decode and B <= self.bmax:
             i = bisect.bisect_left(self.buckets, B)
-            Bp = self.buckets[i] if (self.use_graphs and i < len(self.buckets)) else B
+            # pad to the bucket even when running eagerly: identical shapes -> identical GEMM plans
+            # and kernels as the captured graphs (graph replay == eager, token for token)
+            Bp = self.buckets[i] if i < len(self.buckets) else B
             self._pack_decode(batch, Bp)
             n_copy = self._off["bt"] + Bp * self.max_blocks
             self._bcast_header(KIND_DECODE, Bp, n_copy)

@@ -5,13 +5,13 @@ attention all-reduce already produced them), every rank computes the contributio
 experts, and the block output is summed across ranks by the all-reduce the caller issues right
 after (`LlamaModel.forward`) — the EP combine costs no extra collective.
 
-Two execution shapes:
-* grouped (`moe_grouped`): tokens are bucketed by expert and each expert runs its own GEMMs on
-  only its tokens — used for prefill (ragged, eager);
-* batched (`moe_batched`): every local expert processes the whole (small) decode batch with one
-  batched GEMM per projection and non-routed tokens get weight 0 — shape-static, so it is
-  captured into the decode hipGraphs.  At decode batch sizes every expert's weights are streamed
-  anyway, so the extra MFMA work rides under the weight stream.
+Execution shapes:
+* `moe_hip` (decode, T*k <= 512): device-side routing lists, grouped weight-streaming MFMA GEMMs
+  over only the routed rows and a weighted combine (csrc/moe.hip) — shape-static, captured in
+  the decode hipGraphs, every local expert's weights streamed once per step;
+* `moe_grouped` (prefill / CPU reference): tokens bucketed by expert on the host, hipBLASLt GEMMs
+  per expert (ragged, eager);
+* `moe_batched`: dense all-experts formulation, kept as a second reference.
 """
 from __future__ import annotations
 
@@ -56,7 +56,18 @@ def moe_grouped(x, L, cfg, ep_rank, ep_size):
     return out.to(x.dtype)
 
 
+MOE_HIP_MAX_ROWS = 512   # T * top_k handled by the HIP grouped kernel (decode buckets); larger -> grouped hipBLASLt
+
+
+def moe_hip(x, L, cfg, ep_rank, ep_size):
+    """Device-resident MoE block: K11 top-k + K12 align / grouped GEMMs / combine (csrc/moe.hip)."""
+    logits = ops.linear(x, L["router"])
+    w, ids = ops.moe_topk(logits, cfg.top_k)
+    el = cfg.num_experts // ep_size
+    return ops.moe_experts(x, L["w13"], L["w2"], w, ids, ep_rank * el)
+
+
 def moe_forward(x, L, cfg, ep_rank, ep_size, is_decode: bool):
-    if is_decode and x.is_cuda:
-        return moe_batched(x, L, cfg, ep_rank, ep_size)
+    if x.is_cuda and not ops._FORCE_REF and x.shape[0] * cfg.top_k <= MOE_HIP_MAX_ROWS:
+        return moe_hip(x, L, cfg, ep_rank, ep_size)
     return moe_grouped(x, L, cfg, ep_rank, ep_size)

@@ -182,4 +182,29 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0) -> torch.Tensor:
     return y
 
 
+# ---- Mixtral MoE (K12): device-side routing lists + grouped weight-streaming GEMM + combine ----
+def moe_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
+                topk_ids: torch.Tensor, e0: int) -> torch.Tensor:
+    """sum_j topk_w[t,j] * FFN_{e(t,j)}(x[t]) over this rank's experts [e0, e0 + El); [T, H] bf16."""
+    lib = require()
+    T, H = x.shape
+    k = topk_ids.shape[1]
+    El, two_i, _ = w13.shape
+    R = T * k
+    dev = x.device
+    counts = torch.empty(El, dtype=torch.int32, device=dev)
+    lists = torch.empty((El, R), dtype=torch.int32, device=dev)
+    st = _stream()
+    check(lib.ka_moe_align(_p(counts), _p(lists), _p(topk_ids), R, e0, El, st), "moe_align")
+    y1 = torch.empty((R, two_i), dtype=x.dtype, device=dev)
+    check(lib.ka_moe_gemm(_p(y1), _p(x), _p(w13), _p(counts), _p(lists), R, El, two_i, H, k, R, st), "moe_gemm1")
+    act = silu_mul(y1)
+    y2 = torch.empty((R, H), dtype=x.dtype, device=dev)
+    check(lib.ka_moe_gemm(_p(y2), _p(act), _p(w2), _p(counts), _p(lists), R, El, H, two_i // 2, 1, R, st),
+          "moe_gemm2")
+    out = torch.empty((T, H), dtype=x.dtype, device=dev)
+    check(lib.ka_moe_combine(_p(out), _p(y2), _p(topk_w), _p(topk_ids), T, k, H, e0, El, st), "moe_combine")
+    return out
+
+
 rope_cos_sin = ref.rope_cos_sin

@@ -76,7 +76,7 @@ def attention_prefill(q, k_cache, v_cache, block_tables, q_starts, ctx_lens, sca
     for s in range(len(cl)):
         q0, q1, ctx = qs[s], qs[s + 1], cl[s]
         qlen = q1 - q0
-        if qlen == 0:
+        if qlen == 0 or ctx == 0:      # ctx 0 = padding row of a bucketed decode batch
             continue
         k, v = _gather_kv(k_cache, v_cache, block_tables[s], ctx)
         k = k.repeat_interleave(G, dim=0)

@@ -172,3 +172,24 @@ def test_gemm_skinny(M, N, K):
     for split in (1, 3, 8):
         got = ops.linear(x, w, split=split)
         close(got, want, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("T", [1, 7, 64, 256])
+@pytest.mark.parametrize("e0,el", [(0, 8), (4, 4)])
+def test_moe_experts_vs_reference(T, e0, el):
+    E, H, I, k = 8, 512, 384, 2
+    x = torch.randn(T, H, device=DEV, dtype=BF)
+    w13 = (torch.randn(el, 2 * I, H, device=DEV) * 0.05).to(BF)
+    w2 = (torch.randn(el, H, I, device=DEV) * 0.05).to(BF)
+    logits = torch.randn(T, E, device=DEV, dtype=BF)
+    tw, tid = ops.moe_topk(logits, k)
+    got = ops.moe_experts(x, w13, w2, tw, tid, e0)
+    want = torch.zeros(T, H, device=DEV)
+    for t in range(T):
+        for j in range(k):
+            e = int(tid[t, j]) - e0
+            if 0 <= e < el:
+                g = x[t].float() @ w13[e].float().t()
+                a = (torch.nn.functional.silu(g[:I]) * g[I:]).to(BF).float()
+                want[t] += float(tw[t, j]) * (a @ w2[e].float().t())
+    close(got, want, atol=5e-2, rtol=5e-2)
