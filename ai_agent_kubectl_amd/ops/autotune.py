@@ -18,6 +18,14 @@ from . import GEMM_PLAN, linear, skinny_split
 logger = logging.getLogger("app.engine")
 
 
+import os as _os
+
+# TunableOp results for the decode GEMM shapes on MI355X (ROCm 7.x); loaded at start, extended
+# (and re-written) if new shapes appear.  Set KA_TUNABLEOP=0 to use hipBLASLt's heuristics only.
+DEFAULT_TUNABLEOP_FILE = _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "tuned",
+                                       "tunableop_mi355x.csv")
+
+
 def _time(fn, weights: List[torch.Tensor], reps: int = 12) -> float:
     for i in range(3):
         fn(weights[i % len(weights)])
@@ -31,9 +39,46 @@ def _time(fn, weights: List[torch.Tensor], reps: int = 12) -> float:
     return e0.elapsed_time(e1) / reps * 1e3
 
 
+def _tunableop_begin() -> bool:
+    """KA_TUNABLEOP=1: let torch TunableOp search hipBLASLt/rocBLAS solutions for the decode shapes
+    while we time them (results cached in KA_TUNABLEOP_FILE); tuning is switched off afterwards so
+    prefill's ragged shapes never trigger online tuning during serving."""
+    import os
+    if os.environ.get("KA_TUNABLEOP", "1") != "1":
+        return False
+    tun = torch.cuda.tunable
+    tun.enable(True)
+    fname = os.environ.get("KA_TUNABLEOP_FILE", DEFAULT_TUNABLEOP_FILE)
+    if fname:
+        tun.set_filename(fname)
+        if os.path.exists(fname):
+            tun.read_file(fname)
+    tun.tuning_enable(True)
+    tun.set_max_tuning_duration(int(os.environ.get("KA_TUNABLEOP_MS", "60")))
+    return True
+
+
+def _tunableop_end() -> None:
+    tun = torch.cuda.tunable
+    tun.tuning_enable(False)
+    try:
+        tun.write_file()
+    except Exception:  # pragma: no cover
+        pass
+
+
 @torch.inference_mode()
 def tune_linear(groups: Dict[Tuple[int, int], List[torch.Tensor]], Ms: Sequence[int]) -> Dict:
     """groups: (N, K) -> list of weight tensors of that shape (one per layer)."""
+    tunable = _tunableop_begin()
+    try:
+        return _tune(groups, Ms)
+    finally:
+        if tunable:
+            _tunableop_end()
+
+
+def _tune(groups, Ms) -> Dict:
     report = {}
     for (N, K), ws in groups.items():
         ws = ws[: max(2, min(len(ws), 16))]

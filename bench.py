@@ -34,10 +34,12 @@ MODS = ["in namespace", "with label app", "sorted by age in", "that are failing 
 
 
 def make_query(rank, step, i):
+    """Distinct natural-language query; the unique part comes first so that requests share only
+    the instruction template's KV blocks (no accidental cross-request query-prefix hits)."""
     v = VERBS[(step + i) % len(VERBS)]
     r = RES[(i * 7 + step) % len(RES)]
     m = MODS[(i + rank) % len(MODS)]
-    return f"{v} all {r} {m} team-{rank}-{step}-{i}"
+    return f"team-{rank}-{step}-{i}: {v} all {r} {m} prod"
 
 
 def main():

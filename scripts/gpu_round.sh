@@ -14,7 +14,9 @@ run_cprof() { KA_PROFILE_ENGINE=gpurun_out/cprof_engine.txt KA_PROFILE_API=gpuru
 run_gemm() { timeout -k 10 600 python scripts/bench_gemm.py > gpurun_out/bench_gemm.log 2>&1; }
 run_ktest() { timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -x -q -p no:cacheprovider > gpurun_out/pytest_kernels.log 2>&1; }
 run_sweep() { for c in ${SWEEP:-64 128 256}; do timeout -k 10 600 python bench.py --steps 4 --warmup 2 --concurrency $c ${BENCH_ARGS} > gpurun_out/bench_c$c.log 2>&1 || return 1; done; }
+run_tunab() { KA_TUNABLEOP=1 KA_TUNABLEOP_FILE=gpurun_out/tunableop_results.csv timeout -k 10 900 python bench.py --steps 4 --warmup 2 --concurrency ${C:-256} > gpurun_out/bench_tunable.log 2>&1; }
 case "$STEP" in
+  tunab) run_tunab && C=256 run_sweep ;;
   sweep) run_sweep ;;
   testsweep) run_tests && run_sweep ;;
   gemm) run_ktest && run_gemm ;;
