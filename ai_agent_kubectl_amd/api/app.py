@@ -141,6 +141,8 @@ def create_app(settings: Optional[Settings] = None, backend: Any = _UNSET,
 
     @contextlib.asynccontextmanager
     async def lifespan(app):
+        from ..utils.runtime import tune_gc
+        tune_gc()
         if svc.backend is not None:
             await svc.backend.start()
         try:

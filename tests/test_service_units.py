@@ -180,3 +180,38 @@ def test_executor_direct(fake_kubectl):
 def test_stub_rules(q, cmd):
     assert rule_translate(q) == cmd
     assert is_safe_kubectl_command(cmd)
+
+
+# ---------------- remote OpenAI-compatible backend ----------------
+def test_openai_backend_request_shape_and_retries():
+    import httpx
+    from ai_agent_kubectl_amd.llm.remote import OpenAIChatLLM
+    calls = []
+
+    def handler(request: httpx.Request):
+        calls.append(request)
+        if len(calls) == 1:
+            return httpx.Response(503, json={"error": "busy"})
+        body = __import__("json").loads(request.content)
+        assert body["temperature"] == 0 and body["model"] == "gpt-x"
+        assert body["messages"][0]["role"] == "user" and "User Request: list pods" in body["messages"][0]["content"]
+        return httpx.Response(200, json={"choices": [{"message": {"content": "kubectl get pods"}}]})
+
+    s = Settings(OPENAI_API_KEY="sk-test", OPENAI_MODEL="gpt-x", OPENAI_BASE_URL="http://llm.local/v1")
+    be = OpenAIChatLLM(s, transport=httpx.MockTransport(handler))
+    be_sleep = asyncio.sleep
+
+    async def run():
+        return await be.generate("list pods")
+
+    assert asyncio.run(run()) == "kubectl get pods"
+    assert len(calls) == 2 and calls[1].headers["authorization"] == "Bearer sk-test"
+    assert str(calls[1].url) == "http://llm.local/v1/chat/completions"
+
+
+def test_openai_backend_without_key_is_degraded_mode():
+    from fastapi.testclient import TestClient
+    from ai_agent_kubectl_amd.api import create_app
+    app = create_app(Settings(LLM_BACKEND="openai", RATE_LIMIT="100/minute"))
+    r = TestClient(app).post("/kubectl-command", json={"query": "list pods"})
+    assert (r.status_code, r.text) == (503, '{"detail":"LLM Chain not initialized"}')
