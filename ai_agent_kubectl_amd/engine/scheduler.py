@@ -14,6 +14,7 @@ immediately and free their blocks, so the batch composition changes every step.
 from __future__ import annotations
 
 import collections
+import time
 from dataclasses import dataclass, field
 from typing import Deque, List
 
@@ -35,7 +36,14 @@ class Batch:
 
 class Scheduler:
     def __init__(self, block_manager: BlockManager, max_batch: int = 256, max_batched_tokens: int = 8192,
-                 max_model_len: int = 4096, mix_decode_into_prefill: bool = True):
+                 max_model_len: int = 4096, mix_decode_into_prefill: bool = True,
+                 prefill_max_wait_s: float = 0.015, prefill_min_frac: float = 0.25):
+        # Prefill batching under continuous arrivals: a prefill step is an eager (non-graph) step,
+        # so while sequences are decoding, new arrivals are admitted together — when at least
+        # max(4, prefill_min_frac * running) are waiting or the oldest has waited
+        # prefill_max_wait_s — instead of turning every decode step into a mixed eager step.
+        self.prefill_max_wait_s = prefill_max_wait_s
+        self.prefill_min_frac = prefill_min_frac
         self.bm = block_manager
         self.max_batch = max_batch
         self.max_batched_tokens = max_batched_tokens
@@ -84,8 +92,19 @@ class Scheduler:
             budget -= q
         return admitted
 
+    def _should_prefill(self) -> bool:
+        if not self.waiting:
+            return False
+        if not self.running:
+            return True
+        if len(self.running) >= self.max_batch:
+            return False
+        if len(self.waiting) >= max(4, int(self.prefill_min_frac * len(self.running))):
+            return True
+        return time.perf_counter() - self.waiting[0].t_arrival >= self.prefill_max_wait_s
+
     def schedule(self) -> Batch:
-        admitted = self._admit() if self.waiting else []
+        admitted = self._admit() if self._should_prefill() else []
         # decode rows need a slot for their next token
         decodes: List[Sequence] = []
         if not admitted or self.mix:

@@ -95,7 +95,7 @@ def _seq(n, new=4):
 
 def test_scheduler_budget_and_mixing():
     bm = BlockManager(64, 4, enable_prefix_caching=False)
-    sch = Scheduler(bm, max_batch=3, max_batched_tokens=20)
+    sch = Scheduler(bm, max_batch=3, max_batched_tokens=20, prefill_max_wait_s=0.0)
     seqs = [_seq(8), _seq(8), _seq(8), _seq(8)]
     for s in seqs:
         sch.add(s)
@@ -111,7 +111,7 @@ def test_scheduler_budget_and_mixing():
 
 def test_scheduler_preempts_when_out_of_blocks():
     bm = BlockManager(5, 4, enable_prefix_caching=False)
-    sch = Scheduler(bm, max_batch=4, max_batched_tokens=100)
+    sch = Scheduler(bm, max_batch=4, max_batched_tokens=100, prefill_max_wait_s=0.0)
     s1, s2 = _seq(8, new=8), _seq(8, new=8)
     sch.add(s1)
     sch.add(s2)
@@ -262,3 +262,20 @@ def test_native_tokenizer_matches_python():
         assert tok.encode(text) == native
     finally:
         tok._native = saved
+
+
+def test_scheduler_batches_prefills_while_decoding():
+    bm = BlockManager(64, 4, enable_prefix_caching=False)
+    sch = Scheduler(bm, max_batch=16, max_batched_tokens=1000, prefill_max_wait_s=10.0)
+    first = _seq(8)
+    sch.add(first)
+    b = sch.schedule()
+    assert b.prefill_seqs == [first]          # nothing running -> admit immediately
+    first.num_computed, first.output_ids = 8, [1]
+    sch.on_step_done(b)
+    for _ in range(3):
+        sch.add(_seq(8))
+    assert sch.schedule().is_decode           # 3 waiting < 4 and young -> keep decoding
+    sch.add(_seq(8))
+    b = sch.schedule()
+    assert len(b.prefill_seqs) == 4           # batch of 4 admitted together (+1 decode row mixed)
