@@ -67,6 +67,15 @@ def _command_body(command: str, from_cache: bool, execution_data: Dict[str, Any]
     }
 
 
+async def _lag_probe(metrics, period: float = 0.05) -> None:
+    """Observe how late the event loop wakes a 50 ms sleeper (GIL / blocking-call diagnostics)."""
+    loop = asyncio.get_running_loop()
+    while True:
+        t0 = loop.time()
+        await asyncio.sleep(period)
+        metrics.loop_lag.observe(max(0.0, loop.time() - t0 - period))
+
+
 class KubectlService:
     """State shared by the routes: settings, cache, limiter, metrics and the LLM backend."""
 
@@ -145,9 +154,11 @@ def create_app(settings: Optional[Settings] = None, backend: Any = _UNSET,
         tune_gc()
         if svc.backend is not None:
             await svc.backend.start()
+        probe = asyncio.get_running_loop().create_task(_lag_probe(metrics))
         try:
             yield
         finally:
+            probe.cancel()
             if svc.backend is not None:
                 await svc.backend.close()
 

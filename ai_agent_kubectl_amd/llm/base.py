@@ -53,9 +53,11 @@ def build_backend(settings, metrics=None) -> Optional[LLMBackend]:
         from .remote import OpenAIChatLLM
         return OpenAIChatLLM(settings)
     if kind == "engine":
-        if settings.DP > 1:
+        if settings.DP > 1 or (settings.ENGINE_PROCESS and settings.TP == 1):
+            # engine replica process(es) behind this API process: HTTP handling and the GPU loop
+            # never contend for one GIL (SURVEY.md §7.3 hard part 6)
             from ..parallel.dp import DPRouterLLM
-            return DPRouterLLM(settings, settings.DP)
+            return DPRouterLLM(settings, max(1, settings.DP))
         from .engine_backend import EngineLLM
         return EngineLLM.from_settings(settings, metrics=metrics)
     raise ValueError(f"unknown LLM_BACKEND {settings.LLM_BACKEND!r}")

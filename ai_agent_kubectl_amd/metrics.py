@@ -76,6 +76,8 @@ class ServiceMetrics:
         self.llm_errors = Counter("llm_errors_total", "LLM failures by kind.", ("kind",), registry=r)
         self.execute_duration = Histogram("execute_duration_seconds", "kubectl subprocess wall time.",
                                           buckets=HIGHR_BUCKETS, registry=r)
+        self.loop_lag = Histogram("event_loop_lag_seconds", "asyncio event-loop scheduling delay (50 ms probe).",
+                                  buckets=(0.001, 0.002, 0.005, 0.01, 0.02, 0.05, 0.1, 0.2, 0.5, 1.0), registry=r)
 
     def render(self) -> bytes:
         return generate_latest(self.registry)

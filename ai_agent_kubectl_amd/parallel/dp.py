@@ -62,6 +62,13 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> 
         if msg is None:
             break
         op, rid, payload = msg
+        if op == "sync":           # barrier helper: all queued GPU work of this replica is done
+            import torch as _t
+            if device.startswith("cuda"):
+                _t.cuda.synchronize(device)
+            resp_q.put(("ctl", rid, dict(eng.runner.stats, prefix_hits=eng.bm.hits, prefix_queries=eng.bm.queries,
+                                         build_s=getattr(eng, "build_seconds", 0.0))))
+            continue
         if op == "gen":
             seq = eng.submit(payload, params, lambda sq, rid=rid: done(sq, rid), forced_prefix=forced)
             live[rid] = seq
@@ -143,6 +150,11 @@ class DPRouterLLM(LLMBackend):
                         ent[2].inflight -= 1
                 if ent is not None:
                     ent[0].call_soon_threadsafe(_set, ent[1], b)
+            elif kind == "ctl":
+                with self._lock:
+                    ent = self._pending.pop(a, None)
+                if ent is not None:
+                    ent[0].call_soon_threadsafe(_set, ent[1], b)
             elif kind == "stop":
                 return
 
@@ -183,6 +195,22 @@ class DPRouterLLM(LLMBackend):
     def stats(self):
         return {f"replica{r.idx}_inflight": r.inflight for r in self.replicas}
 
+    async def control(self, op: str = "sync") -> List[dict]:
+        """Send a control op to every live replica and gather the replies (sync = device barrier
+        + engine stats)."""
+        loop = asyncio.get_running_loop()
+        futs = []
+        for r in self.replicas:
+            if not r.up:
+                continue
+            rid = next(self._ids)
+            fut = loop.create_future()
+            with self._lock:
+                self._pending[rid] = (loop, fut, _Dummy())
+            r.req_q.put((op, rid, None))
+            futs.append(fut)
+        return list(await asyncio.gather(*futs))
+
     # -----------------------------------------------------------------------------------------
     def prompt_ids(self, query: str) -> List[int]:
         from ..prompt import PROMPT_SUFFIX
@@ -213,6 +241,10 @@ class DPRouterLLM(LLMBackend):
         if err is not None:
             raise LLMUnavailableError(err) if reason == "error" else RuntimeError(err)
         return self.tok.decode([t for t in out_ids if not self.tok.is_eos(t)])
+
+
+class _Dummy:
+    inflight = 0
 
 
 def _set(fut, val):

@@ -47,8 +47,10 @@ def main(argv=None) -> int:
 
     app = create_app(settings)
     log.info(f"Starting Uvicorn server on {args.host}:{args.port}")
+    # keep-alive longer than common client/LB pools so idle pooled connections are not reset
+    # under the client's feet (uvicorn's default is 5 s)
     uvicorn.run(app, host=args.host, port=args.port, reload=False, log_level=settings.LOG_LEVEL.lower(),
-                workers=1)
+                workers=1, timeout_keep_alive=int(os.environ.get("KEEP_ALIVE_S", "75")))
     return 0
 
 

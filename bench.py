@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--model", default=os.environ.get("BENCH_MODEL", "llama3-8b"))
     ap.add_argument("--max-new-tokens", type=int, default=16)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--in-process", action="store_true",
+                    help="run the engine in this process (default: its own process on the same GPU)")
     ap.add_argument("--client", choices=["asgi", "httpx"], default="asgi",
                     help="asgi: minimal in-process ASGI client (default); httpx: httpx.ASGITransport")
     args = ap.parse_args()
@@ -61,33 +63,53 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-
-    import httpx
-    from ai_agent_kubectl_amd.api import create_app
-    from ai_agent_kubectl_amd.config import Settings
-    from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine
-    from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM
-
     C = args.concurrency
-    buckets = tuple(b for b in (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 256) if b <= max(C, 1))
+    buckets = tuple(b for b in (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512)
+                    if b <= max(C, 1))
     if C not in buckets:
         buckets = tuple(sorted(set(buckets) | {C}))
-    opts = EngineOptions(model=args.model, device=str(dev), max_batch=max(C, 1), graph_buckets=buckets,
-                         kv_cache_tokens=max(65536, C * 256), max_model_len=512, use_graphs=not args.no_graphs,
-                         ignore_eos=True, max_batched_tokens=16384)
+
+    from ai_agent_kubectl_amd.api import create_app
+    from ai_agent_kubectl_amd.config import Settings
+
+    settings = Settings(RATE_LIMIT="100000000/minute", CACHE_MAXSIZE=100, LLM_TIMEOUT=600, LOG_LEVEL="WARNING",
+                        LLM_BACKEND="engine", MODEL=args.model, MAX_BATCH=max(C, 1), MAX_NEW_TOKENS=args.max_new_tokens,
+                        IGNORE_EOS=True, MAX_NUM_BATCHED_TOKENS=16384,
+                        HIPGRAPH_BUCKETS=",".join(str(b) for b in buckets))
+    os.environ.setdefault("KV_CACHE_TOKENS", str(max(65536, C * 256)))
+    os.environ.setdefault("MAX_MODEL_LEN", "512")
     t_build = time.perf_counter()
-    eng = build_engine(opts)
-    cap_s = eng.runner.capture_graphs()
+    if not args.in_process:
+        # Engine in its own process on cuda:LOCAL_RANK (spawned before this process touches the
+        # GPU); this process runs the ASGI app + load generator, so HTTP handling and the GPU loop
+        # never share a GIL.  Barriers use gloo; the device sync runs inside the engine process.
+        from ai_agent_kubectl_amd.parallel.dp import DPRouterLLM
+        backend = DPRouterLLM(settings, 1, devices=[os.environ.get("BENCH_DEVICE", f"cuda:{local}")])
+        if world > 1:
+            dist.init_process_group("gloo")
+        backend.wait_ready()
+        if not any(r.up for r in backend.replicas):
+            raise RuntimeError("engine process failed to start")
+        eng = None
+        cap_s = 0.0
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device(f"cuda:{local}")
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+        from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine
+        from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM
+        opts = EngineOptions(model=args.model, device=str(dev), max_batch=max(C, 1), graph_buckets=buckets,
+                             kv_cache_tokens=max(65536, C * 256), max_model_len=512,
+                             use_graphs=not args.no_graphs, ignore_eos=True, max_batched_tokens=16384)
+        eng = build_engine(opts)
+        cap_s = eng.runner.capture_graphs()
+        backend = EngineLLM(eng, max_new_tokens=args.max_new_tokens, ignore_eos=True)
     t_build = time.perf_counter() - t_build
-    backend = EngineLLM(eng, max_new_tokens=args.max_new_tokens, ignore_eos=True)
-    settings = Settings(RATE_LIMIT="100000000/minute", CACHE_MAXSIZE=100, LLM_TIMEOUT=600, LOG_LEVEL="WARNING")
     import logging
     logging.getLogger("app").setLevel(logging.WARNING)
     app = create_app(settings, backend=backend)
+    import httpx
 
     lat = []
     headers = [(b"host", b"bench"), (b"content-type", b"application/json")]
@@ -138,10 +160,16 @@ def main():
     async def wave(client, step, record):
         return await asyncio.gather(*[one(client, make_query(rank, step, i), record) for i in range(C)])
 
-    def sync_all():
-        torch.cuda.synchronize(dev)
+    async def sync_all():
+        """barrier + device synchronize: every engine's queued GPU work is complete"""
+        if eng is None:
+            st = (await backend.control("sync"))[0]
+        else:
+            torch.cuda.synchronize()
+            st = dict(eng.runner.stats, prefix_hits=eng.bm.hits, prefix_queries=eng.bm.queries)
         if world > 1:
             dist.barrier()
+        return st
 
     async def run():
         await backend.start()
@@ -152,16 +180,14 @@ def main():
             sample = None
             for s in range(args.warmup):
                 sample = await wave(client, s, False)
-            sync_all()
-            st0 = dict(eng.runner.stats)
+            st0 = await sync_all()
             t0 = time.perf_counter()
             for s in range(args.steps):
                 await wave(client, args.warmup + s, True)
-            sync_all()
+            st1 = await sync_all()
             el = time.perf_counter() - t0
-            st1 = dict(eng.runner.stats)
         await backend.close()
-        return el, sample, {k: st1[k] - st0[k] for k in st1}
+        return el, sample, {k: st1[k] - st0[k] for k in st1 if isinstance(st1[k], (int, float))}
 
     if os.environ.get("KA_PROFILE_API"):
         import cProfile
@@ -177,7 +203,8 @@ def main():
     n_req = C * args.steps
     p50 = statistics.median(lat) * 1e3
     if world > 1:
-        t = torch.tensor([elapsed, p50], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, p50], dtype=torch.float64,
+                         device="cpu" if eng is None else torch.device(f"cuda:{local}"))
         gathered = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(gathered, t)
         elapsed = max(g[0].item() for g in gathered)
@@ -198,8 +225,8 @@ def main():
                        "decode_ms_per_step": round(st["decode_ms"] / max(1, st["decode_steps"]), 3),
                        "prefill_ms_per_step": round(st["prefill_ms"] / max(1, st["prefill_steps"]), 3),
                        "prefill_tokens": st.get("prefill_tokens"), "graph_replays": st.get("graph_replays"),
-                       "prefix_cache_hit_rate": round(eng.bm.hits / max(1, eng.bm.queries), 3),
-                       "build_s": round(t_build, 1), "graph_capture_s": round(cap_s, 1),
+                       "prefix_cache_hit_rate": round(st.get("prefix_hits", 0) / max(1, st.get("prefix_queries", 0)), 3),
+                       "build_s": round(t_build, 1), "engine_process": eng is None,
                        "sample_reply": sample[0] if sample else None,
                        "baseline": "BASELINE.md reference plumbing floor, cache-miss conc 32 = 354 req/s"},
         }

@@ -146,12 +146,16 @@ async def mixed(base, conc, seconds):
         t0 = time.perf_counter()
         await asyncio.gather(scraper(), *[worker(i) for i in range(conc)])
         el = time.perf_counter() - t0
+        m = (await c.get("/metrics")).text
+        lag = [l for l in m.splitlines() if l.startswith("event_loop_lag_seconds_")]
     res = {"scenario": "mixed", "concurrency": conc, "seconds": round(el, 1),
            "total_rps": round(sum(len(v) for k, v in stats.items() if k != "metrics") / el, 1)}
     for k, v in stats.items():
         if v:
             res[f"{k}_n"] = len(v)
             res[f"{k}_p50_ms"] = round(statistics.median(v) * 1e3, 2)
+    res["loop_lag"] = {l.split("{")[1].split("}")[0] if "{" in l else l.split()[0]: float(l.split()[-1])
+                       for l in lag}
     print(json.dumps(res), flush=True)
     return res
 

@@ -19,6 +19,7 @@ run_big() { timeout -k 10 1200 python scripts/bigmodel_check.py ${BIG_MODELS} > 
 run_mixed() { timeout -k 10 600 python scripts/bench_service.py mixed --backend engine --concurrency ${C:-64} --seconds 20 > gpurun_out/mixed.log 2>&1; }
 case "$STEP" in
   big) run_big ;;
+  mixed) run_mixed ;;
   bigmixed) run_mixed && run_big ;;
   tunab) run_tunab && C=256 run_sweep ;;
   sweep) run_sweep ;;
