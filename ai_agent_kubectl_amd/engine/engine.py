@@ -44,6 +44,7 @@ class LLMEngine:
         self.healthy = True
         self.last_error: Optional[BaseException] = None
         self.steps = 0
+        self.step_end_hooks: List[Callable[[], None]] = []   # e.g. batched IPC flush (parallel/dp.py)
 
     # ------------------------------------------------------------------------------------------
     def start(self) -> None:
@@ -185,6 +186,8 @@ class LLMEngine:
                 self.last_error = e
                 self._fail_all(e)
                 n = 0
+            for hook in self.step_end_hooks:
+                hook()
             if n == 0 and not self.scheduler.has_work():
                 self._wake.wait(timeout=0.05)
                 self._wake.clear()

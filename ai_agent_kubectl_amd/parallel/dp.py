@@ -52,13 +52,38 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> 
         resp_q.put(("dead", idx, repr(e)))
         return
 
+    # completions are batched: the engine thread appends, and one message per engine step carries
+    # all of them back (a wave of 256 finishing together = 1 pickle + 1 pipe write, not 256)
+    done_buf = []
+    done_lock = __import__("threading").Lock()
+
     def done(seq, rid):
         err = repr(seq.error) if seq.error is not None else None
-        resp_q.put(("done", rid, (seq.output_ids, err, seq.finish_reason)))
+        with done_lock:
+            done_buf.append((rid, (seq.output_ids, err, seq.finish_reason)))
+
+    def flush():
+        nonlocal done_buf
+        if done_buf:
+            with done_lock:
+                batch, done_buf = done_buf, []
+            resp_q.put(("done_batch", 0, batch))
+
+    eng.step_end_hooks.append(flush)
+
+    def requests():
+        while True:
+            msg = req_q.get()
+            if msg is None:
+                yield None
+                return
+            if msg[0] == "batch":
+                yield from msg[2]
+            else:
+                yield msg
 
     live = {}
-    while True:
-        msg = req_q.get()
+    for msg in requests():
         if msg is None:
             break
         op, rid, payload = msg
@@ -86,6 +111,8 @@ class _Replica:
     req_q: object
     inflight: int = 0
     up: bool = False
+    outbox: list = dataclasses.field(default_factory=list)
+    flush_scheduled: bool = False
 
 
 class DPRouterLLM(LLMBackend):
@@ -143,13 +170,17 @@ class DPRouterLLM(LLMBackend):
                 self._n_ready += 1
                 if self._n_ready == len(self.replicas):
                     self._ready.set()
-            elif kind == "done":
+            elif kind in ("done", "done_batch"):
+                items = b if kind == "done_batch" else [(a, b)]
+                by_loop = {}
                 with self._lock:
-                    ent = self._pending.pop(a, None)
-                    if ent is not None:
-                        ent[2].inflight -= 1
-                if ent is not None:
-                    ent[0].call_soon_threadsafe(_set, ent[1], b)
+                    for rid, payload in items:
+                        ent = self._pending.pop(rid, None)
+                        if ent is not None:
+                            ent[2].inflight -= 1
+                            by_loop.setdefault(ent[0], []).append((ent[1], payload))
+                for loop, lst in by_loop.items():
+                    loop.call_soon_threadsafe(_set_many, lst)
             elif kind == "ctl":
                 with self._lock:
                     ent = self._pending.pop(a, None)
@@ -195,6 +226,21 @@ class DPRouterLLM(LLMBackend):
     def stats(self):
         return {f"replica{r.idx}_inflight": r.inflight for r in self.replicas}
 
+    def _send(self, rep, msg, loop) -> None:
+        """Queue a message for a replica; all messages queued in one event-loop tick go out as
+        one `batch` message (a burst of concurrent requests = one pickle + one pipe write)."""
+        rep.outbox.append(msg)
+        if not rep.flush_scheduled:
+            rep.flush_scheduled = True
+            loop.call_soon(self._flush, rep)
+
+    @staticmethod
+    def _flush(rep) -> None:
+        rep.flush_scheduled = False
+        if rep.outbox:
+            batch, rep.outbox = rep.outbox, []
+            rep.req_q.put(("batch", 0, batch) if len(batch) > 1 else batch[0])
+
     async def control(self, op: str = "sync") -> List[dict]:
         """Send a control op to every live replica and gather the replies (sync = device barrier
         + engine stats)."""
@@ -229,11 +275,11 @@ class DPRouterLLM(LLMBackend):
         with self._lock:
             self._pending[rid] = (loop, fut, rep)
             rep.inflight += 1
-        rep.req_q.put(("gen", rid, self.prompt_ids(query)))
+        self._send(rep, ("gen", rid, self.prompt_ids(query)), loop)
         try:
             out_ids, err, reason = await fut
         except asyncio.CancelledError:
-            rep.req_q.put(("abort", rid, None))
+            self._send(rep, ("abort", rid, None), loop)
             with self._lock:
                 if self._pending.pop(rid, None) is not None:
                     rep.inflight -= 1
@@ -245,6 +291,12 @@ class DPRouterLLM(LLMBackend):
 
 class _Dummy:
     inflight = 0
+
+
+def _set_many(lst):
+    for fut, val in lst:
+        if not fut.done():
+            fut.set_result(val)
 
 
 def _set(fut, val):

@@ -72,10 +72,15 @@ async def closed_loop(client, make_req, conc, total):
     q = iter(range(total))
 
     async def worker():
+        async with httpx.AsyncClient(base_url=str(client.base_url), timeout=60,
+                                     limits=httpx.Limits(max_connections=1, max_keepalive_connections=1)) as wc:
+            await _loop(wc)
+
+    async def _loop(wc):
         for i in q:
             method, path, body = make_req(i)
             t0 = time.perf_counter()
-            r = await client.request(method, path, json=body)
+            r = await wc.request(method, path, json=body)
             lat.append(time.perf_counter() - t0)
             if r.status_code != 200:
                 raise RuntimeError(f"{path}: {r.status_code} {r.text[:200]}")
@@ -113,14 +118,20 @@ async def mixed(base, conc, seconds):
     rng = random.Random(0)
     stats = {"miss": [], "hit": [], "execute": [], "metrics": []}
     hot = [f"list pods in namespace hot{i}" for i in range(50)]
-    stop = time.perf_counter() + seconds
     limits = httpx.Limits(max_connections=conc + 4, max_keepalive_connections=conc + 4)
     counter = [0]
     async with httpx.AsyncClient(base_url=base, limits=limits, timeout=600) as c:
-        for q in hot:  # warm the cache
-            await c.post("/kubectl-command", json={"query": q})
+        await asyncio.gather(*[c.post("/kubectl-command", json={"query": q}) for q in hot])  # warm the cache
+        stop = time.perf_counter() + seconds
 
         async def worker(wid):
+            # one single-connection client per worker: httpx's shared pool degrades badly with
+            # dozens of concurrent requests and would measure the load generator, not the server
+            async with httpx.AsyncClient(base_url=base, timeout=600,
+                                         limits=httpx.Limits(max_connections=1, max_keepalive_connections=1)) as wc:
+                await _worker_loop(wc, wid)
+
+        async def _worker_loop(c, wid):
             while time.perf_counter() < stop:
                 x = rng.random()
                 counter[0] += 1
@@ -148,16 +159,32 @@ async def mixed(base, conc, seconds):
         el = time.perf_counter() - t0
         m = (await c.get("/metrics")).text
         lag = [l for l in m.splitlines() if l.startswith("event_loop_lag_seconds_")]
+        srv = {}
+        for l in m.splitlines():   # server-side mean latency per handler (Prometheus histogram)
+            if l.startswith("http_request_duration_seconds_sum") or l.startswith("http_request_duration_seconds_count"):
+                h = l.split('handler="')[1].split('"')[0]
+                srv.setdefault(h, {})["sum" if "_sum" in l else "count"] = float(l.split()[-1])
     res = {"scenario": "mixed", "concurrency": conc, "seconds": round(el, 1),
            "total_rps": round(sum(len(v) for k, v in stats.items() if k != "metrics") / el, 1)}
     for k, v in stats.items():
         if v:
             res[f"{k}_n"] = len(v)
             res[f"{k}_p50_ms"] = round(statistics.median(v) * 1e3, 2)
+    res["cache_hit_ratio"] = round(_metric(m, "kubectl_agent_cache_hits_total") /
+                                   max(1.0, _metric(m, "kubectl_agent_cache_hits_total") +
+                                       _metric(m, "kubectl_agent_cache_misses_total")), 3)
+    res["server_mean_ms"] = {h: round(v["sum"] / max(1, v["count"]) * 1e3, 2) for h, v in srv.items() if "count" in v}
     res["loop_lag"] = {l.split("{")[1].split("}")[0] if "{" in l else l.split()[0]: float(l.split()[-1])
                        for l in lag}
     print(json.dumps(res), flush=True)
     return res
+
+
+def _metric(text, name):
+    for l in text.splitlines():
+        if l.startswith(name + " "):
+            return float(l.split()[-1])
+    return 0.0
 
 
 def main():
@@ -170,7 +197,10 @@ def main():
     a = ap.parse_args()
     port = _port()
     env = {"LLM_BACKEND": "stub" if a.mode == "plumbing" else a.backend, "MODEL": a.model,
-           "MAX_NEW_TOKENS": "16", "MAX_BATCH": str(max(64, a.concurrency))}
+           "MAX_NEW_TOKENS": "16", "MAX_BATCH": str(max(64, a.concurrency)),
+           # mixed: keep the hot set cached (the reference default of 100 entries would be
+           # flushed by the distinct misses and turn every "hit" into a miss)
+           "CACHE_MAXSIZE": "100" if a.mode == "plumbing" else "10000"}
     proc = start_server(env, port)
     try:
         base = f"http://127.0.0.1:{port}"
