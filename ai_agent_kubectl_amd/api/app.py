@@ -76,6 +76,88 @@ async def _lag_probe(metrics, period: float = 0.05) -> None:
         metrics.loop_lag.observe(max(0.0, loop.time() - t0 - period))
 
 
+class FastPathMiddleware:
+    """Pure-ASGI fast path for the two POST routes' common case.
+
+    FastAPI's per-request dependency solving, body-field validation and response plumbing cost
+    ~0.3 ms of Python per request — more than the rest of the handler — and every request of a
+    burst pays it serially on the event loop.  For a request that FastAPI would certainly accept
+    (JSON content type, a JSON object whose field is a str of the minimum length, valid or disabled
+    auth) this middleware calls the same handler function directly and renders errors exactly like
+    FastAPI's HTTPException / rate-limit handlers.  Anything else — missing/invalid key (401 before
+    422, Q-ordering), bad JSON, wrong types, other content types — is replayed untouched into the
+    FastAPI stack, so every error body stays byte-identical (tests/test_api_golden.py)."""
+
+    def __init__(self, app, settings: Settings, routes):
+        self.app = app
+        self.key = settings.API_AUTH_KEY
+        self.routes = routes
+        self.hits = 0
+
+    async def __call__(self, scope, receive, send):
+        ent = self.routes.get(scope.get("path")) if scope["type"] == "http" and scope["method"] == "POST" else None
+        if ent is None:
+            await self.app(scope, receive, send)
+            return
+        ctype = key = None
+        for k, v in scope["headers"]:
+            if k == b"content-type":
+                if ctype is None:
+                    ctype = v
+            elif k == b"x-api-key":
+                if key is None:
+                    key = v
+        if (ctype is None or ctype.split(b";")[0].strip().lower() != b"application/json"
+                or (self.key and (key is None or key.decode("latin-1") != self.key))):
+            await self.app(scope, receive, send)
+            return
+        chunks, tail = [], None
+        while True:
+            msg = await receive()
+            if msg["type"] != "http.request":
+                tail = msg
+                break
+            chunks.append(msg.get("body", b""))
+            if not msg.get("more_body", False):
+                break
+        body = b"".join(chunks)
+        field, min_len, handler = ent
+        value = None
+        if tail is None and body:
+            try:
+                obj = json.loads(body)
+                value = obj.get(field) if isinstance(obj, dict) else None
+            except ValueError:
+                value = None
+        if not isinstance(value, str) or len(value) < min_len:
+            await self.app(scope, _replay(body, tail, receive), send)
+            return
+        self.hits += 1
+        logger.debug("API key verified." if self.key else "API key auth disabled.")
+        try:
+            resp = await handler(value, scope)
+        except HTTPException as e:           # fastapi.exception_handlers.http_exception_handler
+            resp = _json({"detail": e.detail}, status_code=e.status_code)
+            if e.headers:
+                resp.headers.update(e.headers)
+        except RateLimitExceeded as e:       # the app's RateLimitExceeded handler
+            resp = Response(content=rate_limit_body(e), status_code=429, media_type="application/json")
+        await resp(scope, receive, send)
+
+
+def _replay(body: bytes, tail, receive):
+    sent = [False]
+
+    async def replay():
+        if not sent[0]:
+            sent[0] = True
+            return {"type": "http.request", "body": body, "more_body": False}
+        if tail is not None:
+            return tail
+        return await receive()
+    return replay
+
+
 class KubectlService:
     """State shared by the routes: settings, cache, limiter, metrics and the LLM backend."""
 
@@ -106,8 +188,26 @@ class KubectlService:
 
         loop = asyncio.get_running_loop()
         t0 = loop.time()
+        task = asyncio.current_task()
+        fired = []
+
+        def _expire():
+            fired.append(True)
+            task.cancel()
+
+        # asyncio.wait_for semantics without its per-call task: cancel this task at the deadline
+        # and turn that cancellation into the timeout (what asyncio.timeout does on 3.11+)
+        timer = loop.call_later(timeout, _expire) if timeout is not None else None
         try:
-            command = await asyncio.wait_for(_chain(), timeout=timeout)
+            try:
+                command = await _chain()
+            except asyncio.CancelledError:
+                if fired:
+                    raise asyncio.TimeoutError() from None
+                raise
+            finally:
+                if timer is not None:
+                    timer.cancel()
             self.metrics.llm_latency.observe(loop.time() - t0)
             logger.info(f"LLM generated command for query '{query}': {command}")
             return command
@@ -190,27 +290,12 @@ def create_app(settings: Optional[Settings] = None, backend: Any = _UNSET,
         decorated.add("%s.%s" % (fn.__module__, fn.__name__))
         return fn
 
-    @app.post("/kubectl-command",
-              response_model=CommandResponse,
-              dependencies=[Depends(verify_api_key)],
-              summary="Generate and optionally execute a kubectl command from natural language",
-              responses={
-                  200: {"description": "Command generated (and optionally executed)"},
-                  400: {"description": "Invalid input query"},
-                  401: {"description": "Unauthorized (Missing or invalid API Key)"},
-                  422: {"description": "Unsafe command generated by LLM"},
-                  429: {"description": "Rate limit exceeded"},
-                  500: {"description": "Internal server error"},
-                  503: {"description": "Service unavailable (LLM or execution issue)"},
-                  504: {"description": "Gateway timeout (LLM or execution)"},
-              })
-    @limited
-    async def get_kubectl_command(q: Query, request: Request):
-        """Takes a natural language query, generates a kubectl command using the on-node LLM,
-        validates it, and returns it (never executes; app.py:299-346)."""
-        svc.limiter.check(client_address(request.scope), "%s.get_kubectl_command" % __name__, svc.route_limits)
-        logger.info(f"Received query: '{q.query}'")
-        sanitized_query = safety.sanitize_query(q.query)
+    async def kubectl_command(query: str, scope) -> Response:
+        """POST /kubectl-command after auth + body validation (app.py:299-346); shared by the
+        FastAPI route and the fast path."""
+        svc.limiter.check(client_address(scope), "%s.get_kubectl_command" % __name__, svc.route_limits)
+        logger.info(f"Received query: '{query}'")
+        sanitized_query = safety.sanitize_query(query)
         from_cache = False
         try:
             cached = svc.cache.get(sanitized_query)
@@ -237,6 +322,40 @@ def create_app(settings: Optional[Settings] = None, backend: Any = _UNSET,
                                        "success": True}}
         return _json(_command_body(command, from_cache, execution_data))
 
+    async def execute(command: str, scope) -> Response:
+        """POST /execute after auth + body validation (app.py:369-389)."""
+        svc.limiter.check(client_address(scope), "%s.execute_kubectl_command" % __name__, svc.route_limits)
+        logger.info(f"Received execute request for command: '{command}'")
+        if not safety.is_safe_kubectl_command(command):
+            raise HTTPException(status_code=status.HTTP_400_BAD_REQUEST, detail="Command failed safety checks")
+        execution_data = await execute_command_async(
+            command, timeout=settings.EXECUTION_TIMEOUT, kubectl_bin=settings.KUBECTL_BIN,
+            strict_compat=settings.COMPAT_STRICT_500)
+        if "metadata" in execution_data:
+            svc.metrics.execute_duration.observe(execution_data["metadata"]["duration_ms"] / 1000.0)
+        # COMPAT_STRICT_500: a result without metadata raises KeyError -> plain-text 500 (quirk Q1).
+        return _json(_command_body(command, False, execution_data))
+
+    @app.post("/kubectl-command",
+              response_model=CommandResponse,
+              dependencies=[Depends(verify_api_key)],
+              summary="Generate and optionally execute a kubectl command from natural language",
+              responses={
+                  200: {"description": "Command generated (and optionally executed)"},
+                  400: {"description": "Invalid input query"},
+                  401: {"description": "Unauthorized (Missing or invalid API Key)"},
+                  422: {"description": "Unsafe command generated by LLM"},
+                  429: {"description": "Rate limit exceeded"},
+                  500: {"description": "Internal server error"},
+                  503: {"description": "Service unavailable (LLM or execution issue)"},
+                  504: {"description": "Gateway timeout (LLM or execution)"},
+              })
+    @limited
+    async def get_kubectl_command(q: Query, request: Request):
+        """Takes a natural language query, generates a kubectl command using the on-node LLM,
+        validates it, and returns it (never executes; app.py:299-346)."""
+        return await kubectl_command(q.query, request.scope)
+
     @app.get("/health",
              summary="Health check endpoint",
              status_code=status.HTTP_200_OK,
@@ -259,18 +378,7 @@ def create_app(settings: Optional[Settings] = None, backend: Any = _UNSET,
     @limited
     async def execute_kubectl_command(req: ExecuteRequest, request: Request):
         """Executes a provided kubectl command (app.py:369-389)."""
-        svc.limiter.check(client_address(request.scope), "%s.execute_kubectl_command" % __name__,
-                          svc.route_limits)
-        logger.info(f"Received execute request for command: '{req.execute}'")
-        if not safety.is_safe_kubectl_command(req.execute):
-            raise HTTPException(status_code=status.HTTP_400_BAD_REQUEST, detail="Command failed safety checks")
-        execution_data = await execute_command_async(
-            req.execute, timeout=settings.EXECUTION_TIMEOUT, kubectl_bin=settings.KUBECTL_BIN,
-            strict_compat=settings.COMPAT_STRICT_500)
-        if "metadata" in execution_data:
-            svc.metrics.execute_duration.observe(execution_data["metadata"]["duration_ms"] / 1000.0)
-        # COMPAT_STRICT_500: a result without metadata raises KeyError -> plain-text 500 (quirk Q1).
-        return _json(_command_body(req.execute, False, execution_data))
+        return await execute(req.execute, request.scope)
 
     @app.get("/ready", summary="Readiness: 200 once the LLM backend can serve, else 503")
     async def readiness():
@@ -285,7 +393,11 @@ def create_app(settings: Optional[Settings] = None, backend: Any = _UNSET,
     async def metrics_endpoint():
         return Response(content=svc.metrics.render(), headers={"Content-Type": CONTENT_TYPE})
 
-    # Middleware: rate-limit inner, Prometheus outermost (app.py:134 then :138).
+    # Middleware: fast path innermost, rate-limit, Prometheus outermost (app.py:134 then :138).
+    if settings.API_FAST_PATH:
+        app.add_middleware(FastPathMiddleware, settings=settings,
+                           routes={"/kubectl-command": ("query", 3, kubectl_command),
+                                   "/execute": ("execute", 0, execute)})
     app.add_middleware(RateLimitMiddleware, limiter=svc.limiter, exempt_endpoints=lambda: decorated,
                        routes=lambda: app.routes)
     app.add_middleware(PrometheusMiddleware, metrics=metrics, routes=lambda: app.routes)

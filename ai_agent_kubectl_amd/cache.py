@@ -19,7 +19,7 @@ from typing import Any, Callable, Hashable, Optional
 
 
 class TTLCache:
-    __slots__ = ("maxsize", "ttl", "timer", "_data", "hits", "misses")
+    __slots__ = ("maxsize", "ttl", "timer", "_data", "_exp", "hits", "misses")
 
     def __init__(self, maxsize: int, ttl: float, timer: Callable[[], float] = time.monotonic):
         self.maxsize = int(maxsize)
@@ -27,6 +27,9 @@ class TTLCache:
         self.timer = timer
         # key -> [value, expires]; order = LRU (first) ... MRU (last)
         self._data: "collections.OrderedDict[Hashable, list]" = collections.OrderedDict()
+        # (expires, key) in stamp order: with a constant ttl and a monotonic timer the stamps are
+        # non-decreasing, so expiry pops from the left instead of scanning every entry per insert
+        self._exp: "collections.deque" = collections.deque()
         self.hits = 0
         self.misses = 0
 
@@ -42,9 +45,14 @@ class TTLCache:
 
     def expire(self, now: Optional[float] = None) -> None:
         now = self.timer() if now is None else now
-        dead = [k for k, e in self._data.items() if not now < e[1]]
-        for k in dead:
-            del self._data[k]
+        exp, data = self._exp, self._data
+        while exp and not now < exp[0][0]:
+            t, k = exp.popleft()
+            ent = data.get(k)
+            if ent is not None and ent[1] == t:   # stale stamps (key re-set or evicted) are skipped
+                del data[k]
+        if len(exp) > 4 * max(16, len(data)):     # drop stale stamps left by re-sets / evictions
+            self._exp = collections.deque(sorted(((e[1], k) for k, e in data.items()), key=lambda x: x[0]))
 
     # -- mapping API -----------------------------------------------------------------------
     def get(self, key, default: Any = None) -> Any:
@@ -74,10 +82,12 @@ class TTLCache:
             ent[0] = value
             ent[1] = now + self.ttl
             self._data.move_to_end(key)
+            self._exp.append((ent[1], key))
             return
         while len(self._data) >= self.maxsize:
             self._data.popitem(last=False)
         self._data[key] = [value, now + self.ttl]
+        self._exp.append((now + self.ttl, key))
 
     def __delitem__(self, key) -> None:
         del self._data[key]
@@ -88,6 +98,7 @@ class TTLCache:
 
     def clear(self) -> None:
         self._data.clear()
+        self._exp.clear()
 
     @property
     def currsize(self) -> int:

@@ -101,6 +101,7 @@ class Settings:
     # --- behaviour flags ---
     COMPAT_STRICT_500: bool = False      # reproduce app.py:388 KeyError -> 500 text/plain
     KUBECTL_BIN: str = "kubectl"         # executable looked up on PATH (app.py:216)
+    API_FAST_PATH: bool = True           # pure-ASGI fast path for valid POSTs (api/app.py)
 
     # --- LLM backend selection ---
     LLM_BACKEND: str = "stub"            # stub | engine | openai

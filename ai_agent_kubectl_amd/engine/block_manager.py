@@ -12,6 +12,14 @@ Invariants:
   dry; a block with ref 0 and no hash goes straight back to the free list;
 * at least one prompt token is always recomputed so the prefill produces logits.
 
+Sub-block reuse (`reuse_partial`): the instruction prompt rarely ends on a block boundary (72
+tokens with the Llama-3 chat header = 4 full blocks + 8 tokens), so block-granular caching would
+recompute its tail in every request.  Each published block is also indexed under its PARENT hash
+with its 16 tokens; a new prompt whose next block shares a token prefix of length r with such a
+sibling pins the sibling and copies its KV into its own fresh block before the prefill (the copy
+is exact: causal attention makes the first r rows depend only on the shared chain), so only the
+tokens after r are computed.
+
 The C++ runtime (`runtime/native.cpp`, `make_block_manager`) implements the same structure for the scheduler hot
 path when the native module is built; this Python class is the reference and the fallback.
 """
@@ -37,6 +45,10 @@ class BlockManager:
         self.evictable: "collections.OrderedDict[int, None]" = collections.OrderedDict()  # LRU of ref-0 cached
         self.hits = 0
         self.queries = 0
+        self.partial_tokens = 0
+        self.children: Dict[int, "collections.deque[int]"] = {}   # parent hash -> recent child blocks
+        self.parent_of: List[Optional[int]] = [None] * num_blocks
+        self.block_toks: List[Optional[tuple]] = [None] * num_blocks
 
     # ------------------------------------------------------------------------------------------
     @property
@@ -134,6 +146,42 @@ class BlockManager:
             if h not in self.cached and self.block_hash[b] is None:
                 self.cached[h] = b
                 self.block_hash[b] = h
+                self.parent_of[b] = hashes[-2] if len(hashes) > 1 else 0
+                self.block_toks[b] = tuple(tokens[i * bs:(i + 1) * bs])
+                self.children.setdefault(self.parent_of[b], collections.deque(maxlen=4)).append(b)
+
+    def reuse_partial(self, table: List[int], tokens: Sequence[int], cached: int,
+                      hashes: List[int]) -> Optional[tuple]:
+        """Find a published sibling of the first uncached block sharing a token prefix with it.
+
+        Returns (src_block, r): the caller copies src's KV into table[cached // bs] and treats the
+        first r tokens of that block as computed; src is pinned until `unpin(src)`."""
+        if not self.prefix_caching:
+            return None
+        bs = self.block_size
+        maxr = min(bs, len(tokens) - 1 - cached)
+        if maxr <= 0:
+            return None
+        parent = hashes[-1] if hashes else 0
+        want = tokens[cached:cached + maxr]
+        best, best_r = -1, 0
+        for b in self.children.get(parent, ()):
+            if self.block_hash[b] is None or self.parent_of[b] != parent:
+                continue   # evicted (or re-published elsewhere) since it was indexed
+            bt = self.block_toks[b]
+            r = 0
+            while r < maxr and bt[r] == want[r]:
+                r += 1
+            if r > best_r:
+                best, best_r = b, r
+        if best_r == 0:
+            return None
+        self._acquire(best)
+        self.partial_tokens += best_r
+        return best, best_r
+
+    def unpin(self, b: int) -> None:
+        self._release(b)
 
     def ensure_capacity(self, table: List[int], num_tokens: int) -> None:
         """Grow a table so that it can hold `num_tokens` tokens (decode appends)."""

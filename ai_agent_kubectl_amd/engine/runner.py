@@ -168,7 +168,12 @@ class ModelRunner:
         S = len(batch.seqs)
         T = batch.num_tokens
         mb = self.max_blocks
-        buf = np.zeros(3 * T + (S + 1) + 3 * S + S * mb, dtype=np.int32)
+        nc = len(batch.copies)
+        buf = np.zeros(3 * T + (S + 1) + 3 * S + S * mb + 2 * nc, dtype=np.int32)
+        if nc:   # trailing [src... | dst...] block-copy list (sub-block prefix reuse)
+            cp = np.asarray(batch.copies, dtype=np.int32)
+            buf[len(buf) - 2 * nc:len(buf) - nc] = cp[:, 0]
+            buf[len(buf) - nc:] = cp[:, 1]
         ids, pos, slots = buf[:T], buf[T:2 * T], buf[2 * T:3 * T]
         o = 3 * T
         q_starts = buf[o:o + S + 1]; o += S + 1
@@ -194,8 +199,13 @@ class ModelRunner:
         q_starts[S] = t
         return buf
 
-    def _run_prefill(self, buf: torch.Tensor, T: int, S: int, max_q: int) -> torch.Tensor:
+    def _run_prefill(self, buf: torch.Tensor, T: int, S: int, max_q: int, nc: int = 0) -> torch.Tensor:
         mb = self.max_blocks
+        if nc:
+            n = buf.shape[0]
+            src, dst = buf[n - 2 * nc:n - nc].long(), buf[n - nc:].long()
+            self.k_cache[:, dst] = self.k_cache[:, src]
+            self.v_cache[:, dst] = self.v_cache[:, src]
         ids, pos, slots = buf[:T], buf[T:2 * T], buf[2 * T:3 * T]
         o = 3 * T
         q_starts = buf[o:o + S + 1]; o += S + 1
@@ -209,10 +219,10 @@ class ModelRunner:
         return self.model.sample(h, self.mask_bits, mask if self.mask_bits is not None else None)
 
     # ------------------------------------------------------------------------------------------
-    def _bcast_header(self, kind: int, a: int = 0, b: int = 0, c: int = 0, d: int = 0) -> None:
+    def _bcast_header(self, kind: int, a: int = 0, b: int = 0, c: int = 0, d: int = 0, e: int = 0) -> None:
         if self.tp_size == 1:
             return
-        self.d_hdr.copy_(torch.tensor([kind, a, b, c, d, 0, 0, 0], dtype=torch.int32))
+        self.d_hdr.copy_(torch.tensor([kind, a, b, c, d, e, 0, 0], dtype=torch.int32))
         self.comm.broadcast(self.d_hdr, src=0)
 
     @torch.inference_mode()
@@ -240,12 +250,12 @@ class ModelRunner:
             self.stats["decode_ms"] += (time.perf_counter() - t0) * 1e3
             return out
         host = self._pack_prefill(batch)
-        T, S, max_q = batch.num_tokens, B, max(batch.num_query)
-        self._bcast_header(KIND_PREFILL, T, S, max_q, host.shape[0])
+        T, S, max_q, nc = batch.num_tokens, B, max(batch.num_query), len(batch.copies)
+        self._bcast_header(KIND_PREFILL, T, S, max_q, host.shape[0], nc)
         buf = torch.from_numpy(host).to(self.device, non_blocking=False)
         if self.tp_size > 1:
             self.comm.broadcast(buf, src=0)
-        tok = self._run_prefill(buf, T, S, max_q)
+        tok = self._run_prefill(buf, T, S, max_q, nc)
         out = tok.cpu().tolist()
         self.stats["prefill_steps"] += 1
         self.stats["prefill_tokens"] += T
@@ -257,7 +267,7 @@ class ModelRunner:
         """Non-driver TP ranks: mirror every step of rank 0 until it broadcasts STOP."""
         while True:
             self.comm.broadcast(self.d_hdr, src=0)
-            kind, a, b, c, d = self.d_hdr[:5].tolist()
+            kind, a, b, c, d, e = self.d_hdr[:6].tolist()
             if kind == KIND_STOP:
                 return
             if kind == KIND_DECODE:
@@ -265,7 +275,7 @@ class ModelRunner:
             elif kind == KIND_PREFILL:
                 buf = torch.empty(d, dtype=torch.int32, device=self.device)
                 self.comm.broadcast(buf, src=0)
-                self._run_prefill(buf, a, b, c)
+                self._run_prefill(buf, a, b, c, e)
 
     def stop_workers(self) -> None:
         self._bcast_header(KIND_STOP)

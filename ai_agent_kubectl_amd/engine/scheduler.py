@@ -28,6 +28,7 @@ class Batch:
     num_query: List[int]                 # tokens computed this step per sequence
     is_decode: bool
     prefill_seqs: List[Sequence] = field(default_factory=list)
+    copies: List[tuple] = field(default_factory=list)     # (src, dst) KV block copies before the step
 
     @property
     def num_tokens(self) -> int:
@@ -37,7 +38,8 @@ class Batch:
 class Scheduler:
     def __init__(self, block_manager: BlockManager, max_batch: int = 256, max_batched_tokens: int = 8192,
                  max_model_len: int = 4096, mix_decode_into_prefill: bool = True,
-                 prefill_max_wait_s: float = 0.015, prefill_min_frac: float = 0.25):
+                 prefill_max_wait_s: float = 0.015, prefill_min_frac: float = 0.25,
+                 partial_block_reuse: bool = True):
         # Prefill batching under continuous arrivals: a prefill step is an eager (non-graph) step,
         # so while sequences are decoding, new arrivals are admitted together — when at least
         # max(4, prefill_min_frac * running) are waiting or the oldest has waited
@@ -49,6 +51,7 @@ class Scheduler:
         self.max_batched_tokens = max_batched_tokens
         self.max_model_len = max_model_len
         self.mix = mix_decode_into_prefill
+        self.partial_reuse = partial_block_reuse and hasattr(block_manager, "reuse_partial")
         self.waiting: Deque[Sequence] = collections.deque()
         self.running: List[Sequence] = []
 
@@ -70,7 +73,7 @@ class Scheduler:
         seq.status = SeqStatus.ABORTED
 
     # ------------------------------------------------------------------------------------------
-    def _admit(self) -> List[Sequence]:
+    def _admit(self, copies: List[tuple]) -> List[Sequence]:
         admitted: List[Sequence] = []
         budget = self.max_batched_tokens - (len(self.running) if self.mix else 0)
         while self.waiting and len(self.running) + len(admitted) < self.max_batch:
@@ -79,10 +82,16 @@ class Scheduler:
                 table, cached, hashes = self.bm.allocate_prompt(seq.all_ids)
             except NoFreeBlocks:
                 break
-            q = seq.total_len - cached
+            part = self.bm.reuse_partial(table, seq.all_ids, cached, hashes) if self.partial_reuse else None
+            q = seq.total_len - cached - (part[1] if part else 0)
             if q > budget and admitted:
+                if part:
+                    self.bm.unpin(part[0])
                 self.bm.free_table(table)
                 break
+            if part:   # sub-block reuse: copy the sibling's KV rows, skip its first r tokens
+                copies.append((part[0], table[cached // self.bm.block_size]))
+                cached += part[1]
             self.waiting.popleft()
             seq.block_table, seq.block_hashes = table, hashes
             seq.num_computed = cached
@@ -104,7 +113,8 @@ class Scheduler:
         return time.perf_counter() - self.waiting[0].t_arrival >= self.prefill_max_wait_s
 
     def schedule(self) -> Batch:
-        admitted = self._admit() if self._should_prefill() else []
+        copies: List[tuple] = []
+        admitted = self._admit(copies) if self._should_prefill() else []
         # decode rows need a slot for their next token
         decodes: List[Sequence] = []
         if not admitted or self.mix:
@@ -128,7 +138,7 @@ class Scheduler:
         if admitted:
             seqs = decodes + admitted
             nq = [1] * len(decodes) + [s.total_len - s.num_computed for s in admitted]
-            return Batch(seqs, nq, is_decode=False, prefill_seqs=admitted)
+            return Batch(seqs, nq, is_decode=False, prefill_seqs=admitted, copies=copies)
         return Batch(decodes, [1] * len(decodes), is_decode=True)
 
     def _preempt(self, seq: Sequence) -> None:
@@ -141,6 +151,8 @@ class Scheduler:
         self.waiting.appendleft(seq)
 
     def on_step_done(self, batch: Batch) -> None:
+        for src, _ in batch.copies:   # the copy is enqueued before the step's kernels: release the pin
+            self.bm.unpin(src)
         for s in batch.prefill_seqs:
             if not s.finished:
                 self.running.append(s)

@@ -123,6 +123,7 @@ class PrometheusMiddleware:
         self.app = app
         self.metrics = metrics
         self.routes = routes
+        self._children = {}
 
     async def __call__(self, scope, receive, send):
         if scope["type"] != "http":
@@ -155,9 +156,16 @@ class PrometheusMiddleware:
                     except ValueError:
                         req_len = 0
                     break
-            m = self.metrics
-            m.requests_total.labels(method, "%dxx" % (status[0] // 100), handler).inc()
-            m.request_size.labels(handler).observe(req_len)
-            m.response_size.labels(handler).observe(resp_len[0])
-            m.latency_highr.observe(dur)
-            m.latency_lowr.labels(method, handler).observe(dur)
+            key = (method, status[0] // 100, handler)
+            children = self._children.get(key)
+            if children is None:   # labelled children are resolved once per (method, class, handler)
+                m = self.metrics
+                children = (m.requests_total.labels(method, "%dxx" % key[1], handler), m.request_size.labels(handler),
+                            m.response_size.labels(handler), m.latency_lowr.labels(method, handler))
+                if len(self._children) < 4096:
+                    self._children[key] = children
+            children[0].inc()
+            children[1].observe(req_len)
+            children[2].observe(resp_len[0])
+            self.metrics.latency_highr.observe(dur)
+            children[3].observe(dur)

@@ -23,6 +23,8 @@ from typing import Dict, List, Optional
 
 from ..llm.base import LLMBackend, LLMUnavailableError
 
+FLUSH_EVERY = 16   # requests per engine-bound IPC message within one event-loop tick
+
 logger = logging.getLogger("app.dp")
 
 
@@ -92,6 +94,7 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> 
             if device.startswith("cuda"):
                 _t.cuda.synchronize(device)
             resp_q.put(("ctl", rid, dict(eng.runner.stats, prefix_hits=eng.bm.hits, prefix_queries=eng.bm.queries,
+                                         partial_tokens=getattr(eng.bm, "partial_tokens", 0),
                                          build_s=getattr(eng, "build_seconds", 0.0))))
             continue
         if op == "gen":
@@ -230,7 +233,11 @@ class DPRouterLLM(LLMBackend):
         """Queue a message for a replica; all messages queued in one event-loop tick go out as
         one `batch` message (a burst of concurrent requests = one pickle + one pipe write)."""
         rep.outbox.append(msg)
-        if not rep.flush_scheduled:
+        if len(rep.outbox) >= FLUSH_EVERY:
+            # a burst larger than this is handed over in chunks so the engine starts on the first
+            # requests while this process is still parsing the rest (the scheduler re-batches)
+            self._flush(rep)
+        elif not rep.flush_scheduled:
             rep.flush_scheduled = True
             loop.call_soon(self._flush, rep)
 

@@ -10,6 +10,7 @@
 #include <pybind11/stl.h>
 
 #include <cstdint>
+#include <algorithm>
 #include <deque>
 #include <list>
 #include <stdexcept>
@@ -88,7 +89,8 @@ class BlockManager {
  public:
   BlockManager(int num_blocks, int block_size, bool prefix_caching)
       : num_blocks_(num_blocks), bs_(block_size), prefix_(prefix_caching), ref_(num_blocks, 0),
-        hash_(num_blocks, 0), has_hash_(num_blocks, 0), lru_pos_(num_blocks) {
+        hash_(num_blocks, 0), has_hash_(num_blocks, 0), lru_pos_(num_blocks), parent_(num_blocks, 0),
+        btoks_(num_blocks) {
     for (int b = 0; b < num_blocks; ++b) free_.push_back(b);
   }
 
@@ -148,10 +150,40 @@ class BlockManager {
         cached_[h] = b;
         hash_[b] = h;
         has_hash_[b] = 1;
+        const uint64_t par = i > 0 ? hashes[i - 1] : 0;
+        parent_[b] = par;
+        btoks_[b].assign(toks.begin() + (size_t)i * bs_, toks.begin() + (size_t)(i + 1) * bs_);
+        auto& kids = children_[par];
+        if (kids.size() >= 4) kids.erase(kids.begin());
+        kids.push_back(b);
       }
     }
     return hashes;
   }
+
+  // sub-block reuse (engine/block_manager.py reuse_partial): returns (src, r) or (-1, 0)
+  std::pair<int, int> reuse_partial(const std::vector<int>& toks, int cached, const std::vector<uint64_t>& hashes) {
+    if (!prefix_) return {-1, 0};
+    const int maxr = std::min(bs_, (int)toks.size() - 1 - cached);
+    if (maxr <= 0) return {-1, 0};
+    const uint64_t par = hashes.empty() ? 0 : hashes.back();
+    auto it = children_.find(par);
+    if (it == children_.end()) return {-1, 0};
+    int best = -1, best_r = 0;
+    for (int b : it->second) {
+      if (!has_hash_[b] || parent_[b] != par) continue;
+      int r = 0;
+      while (r < maxr && btoks_[b][r] == toks[cached + r]) ++r;
+      if (r > best_r) { best = b; best_r = r; }
+    }
+    if (best_r == 0) return {-1, 0};
+    acquire(best);
+    partial_ += best_r;
+    return {best, best_r};
+  }
+
+  void unpin(int b) { release(b); }
+  long partial_tokens() const { return partial_; }
 
   std::vector<int> ensure_capacity(std::vector<int> table, int ntok) {
     while ((int)table.size() * bs_ < ntok) {
@@ -240,7 +272,10 @@ class BlockManager {
   std::vector<std::list<int>::iterator> lru_pos_;
   std::unordered_map<int, char> in_lru_;
   std::unordered_map<uint64_t, int> cached_;
-  long hits_ = 0, queries_ = 0;
+  std::vector<uint64_t> parent_;                           // parent hash of a published block
+  std::vector<std::vector<int>> btoks_;                    // its tokens (sub-block reuse)
+  std::unordered_map<uint64_t, std::vector<int>> children_;  // parent hash -> up to 4 recent children
+  long hits_ = 0, queries_ = 0, partial_ = 0;
 };
 
 PYBIND11_MODULE(_native, m) {
@@ -264,6 +299,9 @@ PYBIND11_MODULE(_native, m) {
       .def("num_used", &BlockManager::num_used)
       .def("ref", &BlockManager::ref)
       .def("reset_prefix_cache", &BlockManager::reset_prefix_cache)
+      .def("reuse_partial", &BlockManager::reuse_partial)
+      .def("unpin", &BlockManager::unpin)
+      .def("partial_tokens", &BlockManager::partial_tokens)
       .def("hits", &BlockManager::hits)
       .def("queries", &BlockManager::queries)
       .def_static("chain_hash", &BlockManager::chain_hash);

@@ -107,3 +107,14 @@ class NativeBlockManager:
 
     def reset_prefix_cache(self) -> None:
         self._m.reset_prefix_cache()
+
+    def reuse_partial(self, table: List[int], tokens: Sequence[int], cached: int, hashes: List[int]):
+        src, r = self._m.reuse_partial(list(tokens), cached, hashes)
+        return (src, r) if r > 0 else None
+
+    def unpin(self, b: int) -> None:
+        self._m.unpin(b)
+
+    @property
+    def partial_tokens(self) -> int:
+        return self._m.partial_tokens()

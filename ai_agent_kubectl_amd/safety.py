@@ -45,6 +45,8 @@ def is_safe_kubectl_command(command: str) -> bool:
         if bad in command:
             logger.warning(f"Generated command contains potentially unsafe characters: {command}")
             return False
+    if "'" not in command and '"' not in command and "\\" not in command:
+        return True   # shlex.split raises only on an unclosed quote or a trailing escape
     try:
         shlex.split(command)
     except ValueError as e:

@@ -34,12 +34,13 @@ MODS = ["in namespace", "with label app", "sorted by age in", "that are failing 
 
 
 def make_query(rank, step, i):
-    """Distinct natural-language query; the unique part comes first so that requests share only
-    the instruction template's KV blocks (no accidental cross-request query-prefix hits)."""
+    """Distinct natural-language query; the unique part comes first (request index before step
+    and rank) so that requests share only the instruction template's full KV blocks — the
+    computed token count per request is then independent of arrival timing and process mode."""
     v = VERBS[(step + i) % len(VERBS)]
     r = RES[(i * 7 + step) % len(RES)]
     m = MODS[(i + rank) % len(MODS)]
-    return f"team-{rank}-{step}-{i}: {v} all {r} {m} prod"
+    return f"{i}.{step}.{rank} team: {v} all {r} {m} prod"
 
 
 def main():
@@ -166,7 +167,8 @@ def main():
             st = (await backend.control("sync"))[0]
         else:
             torch.cuda.synchronize()
-            st = dict(eng.runner.stats, prefix_hits=eng.bm.hits, prefix_queries=eng.bm.queries)
+            st = dict(eng.runner.stats, prefix_hits=eng.bm.hits, prefix_queries=eng.bm.queries,
+                      partial_tokens=getattr(eng.bm, "partial_tokens", 0))
         if world > 1:
             dist.barrier()
         return st
@@ -226,6 +228,7 @@ def main():
                        "prefill_ms_per_step": round(st["prefill_ms"] / max(1, st["prefill_steps"]), 3),
                        "prefill_tokens": st.get("prefill_tokens"), "graph_replays": st.get("graph_replays"),
                        "prefix_cache_hit_rate": round(st.get("prefix_hits", 0) / max(1, st.get("prefix_queries", 0)), 3),
+                       "sub_block_reused_tokens": st.get("partial_tokens", 0),
                        "build_s": round(t_build, 1), "engine_process": eng is None,
                        "sample_reply": sample[0] if sample else None,
                        "baseline": "BASELINE.md reference plumbing floor, cache-miss conc 32 = 354 req/s"},

@@ -13,7 +13,7 @@ run_prof() { cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$
 run_cprof() { KA_PROFILE_ENGINE=gpurun_out/cprof_engine.txt KA_PROFILE_API=gpurun_out/cprof_api.txt timeout -k 10 600 python bench.py --steps 3 --warmup 1 ${BENCH_ARGS} > gpurun_out/bench_cprof.log 2>&1; }
 run_gemm() { timeout -k 10 600 python scripts/bench_gemm.py > gpurun_out/bench_gemm.log 2>&1; }
 run_ktest() { timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -x -q -p no:cacheprovider > gpurun_out/pytest_kernels.log 2>&1; }
-run_sweep() { for c in ${SWEEP:-64 128 256}; do timeout -k 10 600 python bench.py --steps 4 --warmup 2 --concurrency $c ${BENCH_ARGS} > gpurun_out/bench_c$c.log 2>&1 || return 1; done; }
+run_sweep() { for c in ${SWEEP:-64 128 256}; do timeout -k 10 600 python bench.py --steps 4 --warmup 2 --concurrency $c ${BENCH_ARGS} > gpurun_out/bench_c$c${TAG}.log 2>&1 || return 1; done; }
 run_tunab() { KA_TUNABLEOP=1 KA_TUNABLEOP_FILE=gpurun_out/tunableop_results.csv timeout -k 10 900 python bench.py --steps 4 --warmup 2 --concurrency ${C:-256} > gpurun_out/bench_tunable.log 2>&1; }
 run_big() { timeout -k 10 1200 python scripts/bigmodel_check.py ${BIG_MODELS} > gpurun_out/bigmodel.log 2>&1; }
 run_mixed() { timeout -k 10 600 python scripts/bench_service.py mixed --backend engine --concurrency ${C:-64} --seconds 20 > gpurun_out/mixed.log 2>&1; }
@@ -23,6 +23,7 @@ case "$STEP" in
   bigmixed) run_mixed && run_big ;;
   tunab) run_tunab && C=256 run_sweep ;;
   sweep) run_sweep ;;
+  modes) SWEEP="128 256" run_sweep && SWEEP="128 256" TAG=_inproc BENCH_ARGS="--in-process" run_sweep && C=64 run_mixed ;;
   testsweep) run_tests && run_sweep ;;
   gemm) run_ktest && run_gemm ;;
   gemmbench) run_ktest && run_gemm && run_tests && run_bench ;;

@@ -79,6 +79,39 @@ def test_prefix_cache_sharing_and_eviction():
     assert c4 == 0
 
 
+@pytest.mark.parametrize("native", [False, True])
+def test_sub_block_reuse(native):
+    if native:
+        from ai_agent_kubectl_amd.runtime.native import NativeBlockManager, available
+        if not available():
+            pytest.skip("native runtime not built")
+        bm = NativeBlockManager(num_blocks=12, block_size=4)
+    else:
+        bm = BlockManager(num_blocks=12, block_size=4)
+    a = list(range(1, 13))                    # 3 full blocks once computed
+    t1, c1, h1 = bm.allocate_prompt(a)
+    bm.register_computed(t1, a, h1)
+    b = a[:10] + [77, 78, 79]                 # shares 2 full blocks + 2 tokens of the third
+    t2, c2, h2 = bm.allocate_prompt(b)
+    assert c2 == 8
+    src, r = bm.reuse_partial(t2, b, c2, h2)
+    assert (src, r) == (t1[2], 2) and src not in t2
+    assert bm.ref_count(src) == 2             # pinned (t1 + the pending copy)
+    bm.unpin(src)
+    assert bm.ref_count(src) == 1
+    # never reaches the last prompt token, nothing shared -> no reuse
+    assert bm.reuse_partial(t2, a[:9], 8, h2) is None
+    c = a[:8] + [50, 51, 52]
+    t3, c3, h3 = bm.allocate_prompt(c)
+    assert bm.reuse_partial(t3, c, c3, h3) is None
+    # an evicted sibling is never offered
+    for t in (t1, t2, t3):
+        bm.free_table(t)
+    bm.reset_prefix_cache()
+    t4, c4, h4 = bm.allocate_prompt(b)
+    assert c4 == 0 and bm.reuse_partial(t4, b, c4, h4) is None
+
+
 def test_last_token_always_recomputed():
     bm = BlockManager(num_blocks=8, block_size=4)
     a = list(range(8))
@@ -159,6 +192,23 @@ def test_prefix_cached_equals_cold(tiny_engine):
     assert cold.output_ids == warm.output_ids
 
 
+def test_sub_block_reuse_equals_cold(tiny_engine):
+    """KV rows copied from a sibling block give the same tokens as computing them."""
+    eng, be = tiny_engine
+    params = SamplingParams(max_new_tokens=6, ignore_eos=True)
+    q1, q2 = be.prompt_ids("list pods in prod"), be.prompt_ids("list services in dev")
+    eng.bm.reset_prefix_cache()
+    cold = eng.generate_blocking([q2], params, forced_prefix=be._forced)[0]
+    eng.bm.reset_prefix_cache()
+    eng.generate_blocking([q1], params, forced_prefix=be._forced)
+    before = eng.bm.partial_tokens
+    warm = eng.generate_blocking([q2], params, forced_prefix=be._forced)[0]
+    assert eng.bm.partial_tokens > before
+    assert warm.num_cached_prompt > cold.num_cached_prompt
+    assert cold.output_ids == warm.output_ids
+    assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
+
+
 def test_api_with_engine_backend(tiny_engine):
     from fastapi.testclient import TestClient
     from ai_agent_kubectl_amd.api import create_app
@@ -222,7 +272,10 @@ def test_native_block_manager_matches_python():
             for bm in (py_bm, nv_bm):
                 try:
                     t, c, h = bm.allocate_prompt(toks)
-                    res.append((t, c))
+                    part = bm.reuse_partial(t, toks, c, h)
+                    if part:
+                        bm.unpin(part[0])
+                    res.append((t, c, part))
                     if register:
                         bm.register_computed(t, toks, h)
                 except NoFreeBlocks:
@@ -247,6 +300,7 @@ def test_native_block_manager_matches_python():
             nv_bm.free_table(ent[1])
         assert py_bm.num_free == nv_bm.num_free
     assert py_bm.hits == nv_bm.hits and py_bm.queries == nv_bm.queries
+    assert py_bm.partial_tokens == nv_bm.partial_tokens > 0
 
 
 def test_native_tokenizer_matches_python():
