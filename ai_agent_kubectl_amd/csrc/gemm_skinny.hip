@@ -163,6 +163,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(bf16_t* __restrict__
   }
 }
 
+// Y[mn] = sum_k P[k][mn] in bf16 (also used by gemm_tile.hip's split-K path)
+extern "C" void ka_splitk_reduce_launch(bf16_t* Y, const float* P, int split, long mn, hipStream_t stream) {
+  long blocks = (mn / 4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((int)blocks), dim3(256), 0, stream, Y, P, split, mn);
+}
+
 template <int MT>
 static void launch_mt(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int split, int kps,
                       hipStream_t stream) {
@@ -189,11 +196,6 @@ extern "C" int ka_gemm_skinny(void* Y, const void* X, const void* W, void* works
   else if (mt <= 8) launch_mt<8>(x, w, y, p, M, N, K, split, kps, stream);
   else if (mt <= 12) launch_mt<12>(x, w, y, p, M, N, K, split, kps, stream);
   else launch_mt<16>(x, w, y, p, M, N, K, split, kps, stream);
-  if (split > 1) {
-    const long mn = (long)M * N;
-    long blocks = (mn / 4 + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((int)blocks), dim3(256), 0, stream, y, p, split, mn);
-  }
+  if (split > 1) ka_splitk_reduce_launch(y, p, split, (long)M * N, stream);
   KA_CHECK_LAUNCH();
 }

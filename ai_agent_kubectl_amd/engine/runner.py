@@ -14,6 +14,7 @@ inside it synchronising them.  Worker ranks sit in `worker_loop()`.
 from __future__ import annotations
 
 import bisect
+import os
 import time
 from typing import Dict, List, Optional
 
@@ -38,6 +39,8 @@ class ModelRunner:
         self.cfg = cfg
         self.device = torch.device(device)
         self.comm = comm or LocalComm()
+        # mixed steps: decode rows through the decode kernel (KA_SPLIT_MIXED_ATTN=0: all varlen)
+        self.split_mixed_attention = os.environ.get("KA_SPLIT_MIXED_ATTN", "1") == "1"
         self.tp_rank, self.tp_size = tp_rank, tp_size
         self.model = LlamaModel(cfg, weights, self.comm, tp_rank, tp_size, ep_rank, ep_size)
         self.block_size = block_size
@@ -199,7 +202,7 @@ class ModelRunner:
         q_starts[S] = t
         return buf
 
-    def _run_prefill(self, buf: torch.Tensor, T: int, S: int, max_q: int, nc: int = 0) -> torch.Tensor:
+    def _run_prefill(self, buf: torch.Tensor, T: int, S: int, max_q: int, nc: int = 0, nd: int = 0) -> torch.Tensor:
         mb = self.max_blocks
         if nc:
             n = buf.shape[0]
@@ -214,15 +217,16 @@ class ModelRunner:
         lidx = buf[o:o + S].long(); o += S
         bt = buf[o:o + S * mb].view(S, mb)
         meta = AttnMeta(positions=pos, slot_mapping=slots, block_tables=bt, ctx_lens=ctx, logits_indices=lidx,
-                        is_decode=False, q_starts=q_starts, max_q_len=max_q)
+                        is_decode=False, q_starts=q_starts, max_q_len=max_q, num_decode=nd)
         h = self.model.forward(ids, meta, self.k_cache, self.v_cache)
         return self.model.sample(h, self.mask_bits, mask if self.mask_bits is not None else None)
 
     # ------------------------------------------------------------------------------------------
-    def _bcast_header(self, kind: int, a: int = 0, b: int = 0, c: int = 0, d: int = 0, e: int = 0) -> None:
+    def _bcast_header(self, kind: int, a: int = 0, b: int = 0, c: int = 0, d: int = 0, e: int = 0,
+                      f: int = 0) -> None:
         if self.tp_size == 1:
             return
-        self.d_hdr.copy_(torch.tensor([kind, a, b, c, d, e, 0, 0], dtype=torch.int32))
+        self.d_hdr.copy_(torch.tensor([kind, a, b, c, d, e, f, 0], dtype=torch.int32))
         self.comm.broadcast(self.d_hdr, src=0)
 
     @torch.inference_mode()
@@ -251,11 +255,12 @@ class ModelRunner:
             return out
         host = self._pack_prefill(batch)
         T, S, max_q, nc = batch.num_tokens, B, max(batch.num_query), len(batch.copies)
-        self._bcast_header(KIND_PREFILL, T, S, max_q, host.shape[0], nc)
+        nd = B - len(batch.prefill_seqs) if self.split_mixed_attention else 0
+        self._bcast_header(KIND_PREFILL, T, S, max_q, host.shape[0], nc, nd)
         buf = torch.from_numpy(host).to(self.device, non_blocking=False)
         if self.tp_size > 1:
             self.comm.broadcast(buf, src=0)
-        tok = self._run_prefill(buf, T, S, max_q, nc)
+        tok = self._run_prefill(buf, T, S, max_q, nc, nd)
         out = tok.cpu().tolist()
         self.stats["prefill_steps"] += 1
         self.stats["prefill_tokens"] += T
@@ -267,7 +272,7 @@ class ModelRunner:
         """Non-driver TP ranks: mirror every step of rank 0 until it broadcasts STOP."""
         while True:
             self.comm.broadcast(self.d_hdr, src=0)
-            kind, a, b, c, d, e = self.d_hdr[:6].tolist()
+            kind, a, b, c, d, e, f = self.d_hdr[:7].tolist()
             if kind == KIND_STOP:
                 return
             if kind == KIND_DECODE:
@@ -275,7 +280,7 @@ class ModelRunner:
             elif kind == KIND_PREFILL:
                 buf = torch.empty(d, dtype=torch.int32, device=self.device)
                 self.comm.broadcast(buf, src=0)
-                self._run_prefill(buf, a, b, c, e)
+                self._run_prefill(buf, a, b, c, e, f)
 
     def stop_workers(self) -> None:
         self._bcast_header(KIND_STOP)

@@ -14,9 +14,10 @@ immediately and free their blocks, so the batch composition changes every step.
 from __future__ import annotations
 
 import collections
+import os
 import time
 from dataclasses import dataclass, field
-from typing import Deque, List
+from typing import Deque, List, Optional
 
 from .block_manager import BlockManager, NoFreeBlocks
 from .sequence import Sequence, SeqStatus
@@ -38,12 +39,16 @@ class Batch:
 class Scheduler:
     def __init__(self, block_manager: BlockManager, max_batch: int = 256, max_batched_tokens: int = 8192,
                  max_model_len: int = 4096, mix_decode_into_prefill: bool = True,
-                 prefill_max_wait_s: float = 0.015, prefill_min_frac: float = 0.25,
+                 prefill_max_wait_s: Optional[float] = None, prefill_min_frac: Optional[float] = None,
                  partial_block_reuse: bool = True):
         # Prefill batching under continuous arrivals: a prefill step is an eager (non-graph) step,
         # so while sequences are decoding, new arrivals are admitted together — when at least
         # max(4, prefill_min_frac * running) are waiting or the oldest has waited
         # prefill_max_wait_s — instead of turning every decode step into a mixed eager step.
+        if prefill_max_wait_s is None:
+            prefill_max_wait_s = float(os.environ.get("KA_PREFILL_MAX_WAIT_MS", "15")) / 1000.0
+        if prefill_min_frac is None:
+            prefill_min_frac = float(os.environ.get("KA_PREFILL_MIN_FRAC", "0.25"))
         self.prefill_max_wait_s = prefill_max_wait_s
         self.prefill_min_frac = prefill_min_frac
         self.bm = block_manager

@@ -36,6 +36,7 @@ class AttnMeta:
     is_decode: bool                    # all sequences contribute exactly one token
     q_starts: Optional[torch.Tensor] = None   # [S+1] (prefill)
     max_q_len: int = 1
+    num_decode: int = 0                # mixed step: the first num_decode sequences are 1-token decode rows
 
 
 class LlamaModel:
@@ -81,6 +82,14 @@ class LlamaModel:
                                   self.hq, self.hkv, self.D)
             if meta.is_decode:
                 a = ops.attention_decode(q, k_cache[li], v_cache[li], meta.block_tables, meta.ctx_lens, self.scale)
+            elif meta.num_decode:
+                # mixed step: prompt rows through the varlen prefill kernel, the leading decode rows
+                # through the decode kernel (a 1-row query would waste a 64-row prefill tile)
+                nd = meta.num_decode
+                a = ops.attention_prefill(q, k_cache[li], v_cache[li], meta.block_tables[nd:], meta.q_starts[nd:],
+                                          meta.ctx_lens[nd:], meta.max_q_len, self.scale, out=torch.empty_like(q))
+                ops.attention_decode(q[:nd], k_cache[li], v_cache[li], meta.block_tables[:nd], meta.ctx_lens[:nd],
+                                     self.scale, out=a[:nd])
             else:
                 a = ops.attention_prefill(q, k_cache[li], v_cache[li], meta.block_tables, meta.q_starts,
                                           meta.ctx_lens, meta.max_q_len, self.scale)

@@ -70,7 +70,12 @@ def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq: i
 def attention_prefill(q, k_cache, v_cache, block_tables, q_starts, ctx_lens, max_q_len: int, scale: float,
                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if _ref(q):
-        return ref.attention_prefill(q, k_cache, v_cache, block_tables, q_starts, ctx_lens, scale)
+        r = ref.attention_prefill(q, k_cache, v_cache, block_tables, q_starts, ctx_lens, scale)
+        if out is None:
+            return r
+        for i in range(ctx_lens.shape[0]):   # only this call's sequences' rows, like the kernel
+            out[int(q_starts[i]):int(q_starts[i + 1])] = r[int(q_starts[i]):int(q_starts[i + 1])]
+        return out
     lib = require()
     out = torch.empty_like(q) if out is None else out
     S = ctx_lens.shape[0]
@@ -83,7 +88,11 @@ def attention_prefill(q, k_cache, v_cache, block_tables, q_starts, ctx_lens, max
 def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float,
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if _ref(q):
-        return ref.attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
+        r = ref.attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
+        if out is None:
+            return r
+        out.copy_(r)
+        return out
     lib = require()
     out = torch.empty_like(q) if out is None else out
     check(lib.ka_paged_decode(_p(out), _p(q), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.shape[1],
@@ -154,24 +163,33 @@ def skinny_split(M: int, N: int, K: int, target_wgs: int = 0) -> int:
     return split
 
 
-# (M, N, K) -> ("skinny", split) | ("blas", 0); filled by ops.autotune at engine start.
+# (M, N, K) -> ("skinny", split) | ("tile", split, cfg) | ("blas", 0); filled by ops.autotune at
+# engine start for the decode batch buckets.
 GEMM_PLAN: dict = {}
+TILE_MAX_M = 512
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0) -> torch.Tensor:
     """y = x @ w.T (w is [out, in]).  Decode-sized M goes to the hand-written weight-streaming
-    kernel or hipBLASLt, whichever the autotuned plan measured faster for this (M, N, K); larger M
-    (prefill) goes to hipBLASLt via F.linear."""
+    kernel (M <= 256), the LDS-tiled MFMA kernel (M <= 512) or hipBLASLt, whichever the autotuned
+    plan measured fastest for this (M, N, K); other shapes (prefill) go to hipBLASLt via F.linear."""
     M, K = x.shape
     N = w.shape[0]
-    if _ref(x) or M > SKINNY_MAX_M or K % 64 != 0 or N % 4 != 0 or not x.is_contiguous():
+    if _ref(x) or M > TILE_MAX_M or K % 64 != 0 or N % 4 != 0 or not x.is_contiguous():
         return torch.nn.functional.linear(x, w)
     if not split:
         plan = GEMM_PLAN.get((M, N, K))
-        if plan is not None:
-            if plan[0] == "blas":
+        if plan is None:
+            if M > SKINNY_MAX_M:
                 return torch.nn.functional.linear(x, w)
+        elif plan[0] == "blas":
+            return torch.nn.functional.linear(x, w)
+        elif plan[0] == "tile":
+            return linear_tile(x, w, plan[2], plan[1])
+        else:
             split = plan[1]
+    if M > SKINNY_MAX_M:
+        return torch.nn.functional.linear(x, w)
     lib = require()
     split = split or skinny_split(M, N, K)
     y = torch.empty((M, N), dtype=x.dtype, device=x.device)
@@ -179,6 +197,35 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0) -> torch.Tensor:
     split = (K + kps - 1) // kps
     ws = torch.empty((split, M, N), dtype=torch.float32, device=x.device) if split > 1 else None
     check(lib.ka_gemm_skinny(_p(y), _p(x), _p(w), _p(ws), M, N, K, split, _stream()), "gemm_skinny")
+    return y
+
+
+TILE_CFGS = tuple(range(10))   # csrc/gemm_tile.hip configurations (BN x BM tiles; >= 5: W in VGPRs)
+
+
+def tile_k_quantum(cfg: int) -> int:
+    return 128 if cfg >= 5 else 64
+
+
+def tile_shape(cfg: int):
+    """(BN, BM) of a gemm_tile configuration."""
+    lib = require()
+    return lib.ka_gemm_tile_bn(cfg), lib.ka_gemm_tile_bm(cfg)
+
+
+def linear_tile(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1) -> torch.Tensor:
+    """y = x @ w.T through the LDS-tiled MFMA kernel (csrc/gemm_tile.hip), split-K `split`."""
+    M, K = x.shape
+    N = w.shape[0]
+    kq = tile_k_quantum(cfg)
+    if K % kq or N % 16:
+        raise ValueError(f"gemm_tile cfg {cfg} needs K % {kq} == 0 and N % 16 == 0, got N={N} K={K}")
+    lib = require()
+    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    kps = ((K // split + kq - 1) // kq) * kq
+    split = (K + kps - 1) // kps
+    ws = torch.empty((split, M, N), dtype=torch.float32, device=x.device) if split > 1 else None
+    check(lib.ka_gemm_tile(_p(y), _p(x), _p(w), _p(ws), M, N, K, split, cfg, _stream()), "gemm_tile")
     return y
 
 

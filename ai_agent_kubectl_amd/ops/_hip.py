@@ -36,6 +36,9 @@ _SIGS = {
     "ka_paged_decode": [P, P, P, P, P, I, P, I, I, I, I, I, F, P],
     "ka_paged_prefill": [P, P, P, P, P, I, P, P, I, I, I, I, I, I, F, P],
     "ka_gemm_skinny": [P, P, P, P, I, I, I, I, P],
+    "ka_gemm_tile": [P, P, P, P, I, I, I, I, I, P],
+    "ka_gemm_tile_bm": [I],
+    "ka_gemm_tile_bn": [I],
     "ka_moe_align": [P, P, P, I, I, I, P],
     "ka_moe_gemm": [P, P, P, P, P, I, I, I, I, I, I, P],
     "ka_moe_combine": [P, P, P, P, I, I, I, I, I, P],

@@ -13,7 +13,8 @@ from typing import Dict, List, Sequence, Tuple
 
 import torch
 
-from . import GEMM_PLAN, linear, skinny_split
+from . import (GEMM_PLAN, SKINNY_MAX_M, TILE_CFGS, TILE_MAX_M, linear, linear_tile, skinny_split, tile_k_quantum,
+               tile_shape)
 
 logger = logging.getLogger("app.engine")
 
@@ -55,6 +56,9 @@ def _tunableop_begin() -> bool:
             tun.read_file(fname)
     tun.tuning_enable(True)
     tun.set_max_tuning_duration(int(os.environ.get("KA_TUNABLEOP_MS", "60")))
+    # time candidates with operands rotated through a buffer larger than the 256 MB MALL, so the
+    # choice reflects decode conditions (every layer's weights stream cold from HBM)
+    tun.set_rotating_buffer_size(int(os.environ.get("KA_TUNABLEOP_ROTATING_MB", "1024")))
     return True
 
 
@@ -78,23 +82,54 @@ def tune_linear(groups: Dict[Tuple[int, int], List[torch.Tensor]], Ms: Sequence[
             _tunableop_end()
 
 
+# configurations worth timing on MI355X (bench_gemm_tile.py: the W-in-VGPR variants 5-8 and the
+# 64x128-per-wave cfg 3 never made the top three for the Llama/Mixtral projection shapes)
+TUNE_CFGS = (0, 1, 2, 4, 9)
+
+
+def tile_candidates(M: int, N: int, K: int):
+    """(cfg, split) pairs of the LDS-tiled kernel worth timing for this shape: tiles no taller than
+    twice M, split-K so that the grid lands between ~1/2 and ~4 waves of workgroups on 256 CUs."""
+    out = []
+    if M < 48 or K % 64 or N % 16:
+        return out
+    for cfg in TUNE_CFGS:
+        bn, bm = tile_shape(cfg)
+        if bm > 2 * M and bm > 128:
+            continue
+        tiles = ((N + bn - 1) // bn) * ((M + bm - 1) // bm)
+        for split in (1, 2, 3, 4, 6, 8):
+            if K % (tile_k_quantum(cfg) * split) or K // split < 256:
+                continue
+            if split > 1 and tiles * split > 1024:
+                continue
+            if tiles * split < 96 and split < 8:
+                continue
+            out.append((cfg, split))
+    return out
+
+
 def _tune(groups, Ms) -> Dict:
     report = {}
     for (N, K), ws in groups.items():
         ws = ws[: max(2, min(len(ws), 16))]
-        for M in sorted(set(int(m) for m in Ms if m <= 256)):
+        for M in sorted(set(int(m) for m in Ms if m <= TILE_MAX_M)):
             x = torch.randn(M, K, device=ws[0].device, dtype=ws[0].dtype)
             GEMM_PLAN.pop((M, N, K), None)
             t_blas = _time(lambda w: torch.nn.functional.linear(x, w), ws)
-            best = ("blas", 0, t_blas)
-            if K % 64 == 0 and N % 4 == 0:
+            best = ("blas", 0, 0, t_blas)
+            if M <= SKINNY_MAX_M and K % 64 == 0 and N % 4 == 0:
                 cands = sorted({skinny_split(M, N, K, t) for t in (256, 512, 1024, 2048)})
                 for sp in cands:
                     t = _time(lambda w: linear(x, w, split=sp), ws)
-                    if t < best[2]:
-                        best = ("skinny", sp, t)
-            GEMM_PLAN[(M, N, K)] = (best[0], best[1])
-            report[(M, N, K)] = {"choice": best[0], "split": best[1], "us": round(best[2], 1),
+                    if t < best[3]:
+                        best = ("skinny", sp, 0, t)
+            for cfg, sp in tile_candidates(M, N, K):
+                t = _time(lambda w: linear_tile(x, w, cfg, sp), ws)
+                if t < best[3]:
+                    best = ("tile", sp, cfg, t)
+            GEMM_PLAN[(M, N, K)] = (best[0], best[1], best[2])
+            report[(M, N, K)] = {"choice": best[0], "split": best[1], "cfg": best[2], "us": round(best[3], 1),
                                  "blas_us": round(t_blas, 1)}
     logger.info("gemm plan: %s", report)
     return report

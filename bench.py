@@ -1,12 +1,14 @@
 """Headline benchmark: requests/sec + p50 end-to-end latency of POST /kubectl-command backed by
 Llama-3-8B (bf16, random-init weights, synthetic queries) on N MI355X GPUs (BASELINE.json metric).
 
-One process per GPU (torchrun); every rank is a data-parallel replica running the full service
-in-process: ASGI app (auth, limiter, cache, Prometheus middleware, JSON) -> EngineLLM ->
-continuous-batching engine on its GPU.  A "step" is one wave of `--concurrency` concurrent cache-miss
-requests (distinct queries, so the TTL cache never answers) sent through httpx's ASGI transport,
-all completed.  W warm-up steps, then K timed steps bracketed by barrier + device sync; the job
-value is total requests / max-over-ranks elapsed (weak scaling: per-GPU work is fixed).
+One process per GPU (torchrun); every rank is a data-parallel replica: this process runs the full
+ASGI app (auth, limiter, cache, Prometheus middleware, JSON) and the load generator, the engine runs
+in its own process on the rank's GPU (`--in-process` keeps it in this one).  Load is a closed loop
+of `--concurrency` clients per GPU, each sending its next distinct cache-miss query as soon as the
+previous reply arrives (BASELINE.md's concurrency-N method).  A "step" is C completed requests: W
+warm-up steps, then barrier + device sync, exactly K*C timed completions, sync + barrier; the job
+value is total timed requests / max-over-ranks elapsed (weak scaling: per-GPU work is fixed).
+`--waves` runs lock-step waves instead (C requests start together; the next wave after the last).
 
   python bench.py                                   # 1 GPU, defaults
   torchrun --nproc-per-node 8 bench.py --gpus 8     # driver form
@@ -48,12 +50,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--concurrency", type=int, default=int(os.environ.get("BENCH_CONCURRENCY", 128)))
+    ap.add_argument("--concurrency", type=int, default=int(os.environ.get("BENCH_CONCURRENCY", 256)))
     ap.add_argument("--model", default=os.environ.get("BENCH_MODEL", "llama3-8b"))
     ap.add_argument("--max-new-tokens", type=int, default=16)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--in-process", action="store_true",
                     help="run the engine in this process (default: its own process on the same GPU)")
+    ap.add_argument("--ramp-s", type=float, default=float(os.environ.get("BENCH_RAMP_S", 0.0)),
+                    help="closed loop: client start times spread uniformly over this many seconds")
+    ap.add_argument("--waves", action="store_true",
+                    help="lock-step waves (all C requests start together, the next wave after the "
+                         "slowest) instead of the default closed loop of C clients")
     ap.add_argument("--client", choices=["asgi", "httpx"], default="asgi",
                     help="asgi: minimal in-process ASGI client (default); httpx: httpx.ASGITransport")
     args = ap.parse_args()
@@ -173,21 +180,78 @@ def main():
             dist.barrier()
         return st
 
+    async def sync_barrier():
+        """device sync + cross-rank barrier, run off the event loop so in-flight load keeps moving"""
+        loop = asyncio.get_running_loop()
+        if eng is None:
+            st = (await backend.control("sync"))[0]
+        else:
+            await loop.run_in_executor(None, torch.cuda.synchronize)
+            st = dict(eng.runner.stats, prefix_hits=eng.bm.hits, prefix_queries=eng.bm.queries,
+                      partial_tokens=getattr(eng.bm, "partial_tokens", 0))
+        if world > 1:
+            await loop.run_in_executor(None, dist.barrier)
+        return st
+
+    async def closed_loop(client):
+        """C concurrent clients, each sending its next request as soon as the previous reply
+        arrives (the closed-loop method BASELINE.md's concurrency-32 rows use).  W*C completions
+        warm up; then barrier + device sync, exactly K*C completions are timed, sync + barrier."""
+        import random
+        state = {"done": 0, "target": args.warmup * C, "record": False, "stop": False}
+        reached = asyncio.Event()
+        sample = []
+
+        async def worker(i):
+            await asyncio.sleep(random.Random(i).uniform(0, args.ramp_s))   # de-phase the first arrivals
+            n = 0
+            while not state["stop"]:
+                t_start = time.perf_counter()
+                cmd = await one(client, make_query(rank, n, i), False)
+                n += 1
+                if state["stop"]:
+                    break
+                if not sample:
+                    sample.append(cmd)
+                state["done"] += 1
+                if state["record"]:
+                    lat.append(time.perf_counter() - t_start)
+                if state["done"] >= state["target"] and not reached.is_set():
+                    reached.set()
+
+        tasks = [asyncio.ensure_future(worker(i)) for i in range(C)]
+        if state["target"] > 0:
+            await reached.wait()
+        st0 = await sync_barrier()
+        reached.clear()
+        state.update(done=0, target=args.steps * C, record=True)
+        t0 = time.perf_counter()
+        await reached.wait()
+        state["record"] = False
+        st1 = await sync_barrier()
+        el = time.perf_counter() - t0
+        state["stop"] = True
+        await asyncio.gather(*tasks)
+        return el, sample, st0, st1
+
+    async def waves(client):
+        sample = None
+        for s in range(args.warmup):
+            sample = await wave(client, s, False)
+        st0 = await sync_all()
+        t0 = time.perf_counter()
+        for s in range(args.steps):
+            await wave(client, args.warmup + s, True)
+        st1 = await sync_all()
+        return time.perf_counter() - t0, sample, st0, st1
+
     async def run():
         await backend.start()
         limits = httpx.Limits(max_connections=None, max_keepalive_connections=None)
         async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://bench",
                                      limits=limits, timeout=600) as hc:
             client = hc if args.client == "httpx" else None
-            sample = None
-            for s in range(args.warmup):
-                sample = await wave(client, s, False)
-            st0 = await sync_all()
-            t0 = time.perf_counter()
-            for s in range(args.steps):
-                await wave(client, args.warmup + s, True)
-            st1 = await sync_all()
-            el = time.perf_counter() - t0
+            el, sample, st0, st1 = await (waves(client) if args.waves else closed_loop(client))
         await backend.close()
         return el, sample, {k: st1[k] - st0[k] for k in st1 if isinstance(st1[k], (int, float))}
 
@@ -223,6 +287,8 @@ def main():
                        args.max_new_tokens, "parallelism": f"dp{world}"},
             "p50_ms": round(p50, 2),
             "detail": {"concurrency_per_gpu": C, "new_tokens": args.max_new_tokens,
+                       "load": "waves" if args.waves else "closed-loop",
+                       "p99_ms": round(sorted(lat)[int(0.99 * (len(lat) - 1))] * 1e3, 2) if lat else None,
                        "decode_steps": st.get("decode_steps"), "prefill_steps": st.get("prefill_steps"),
                        "decode_ms_per_step": round(st["decode_ms"] / max(1, st["decode_steps"]), 3),
                        "prefill_ms_per_step": round(st["prefill_ms"] / max(1, st["prefill_steps"]), 3),

@@ -17,7 +17,10 @@ run_sweep() { for c in ${SWEEP:-64 128 256}; do timeout -k 10 600 python bench.p
 run_tunab() { KA_TUNABLEOP=1 KA_TUNABLEOP_FILE=gpurun_out/tunableop_results.csv timeout -k 10 900 python bench.py --steps 4 --warmup 2 --concurrency ${C:-256} > gpurun_out/bench_tunable.log 2>&1; }
 run_big() { timeout -k 10 1200 python scripts/bigmodel_check.py ${BIG_MODELS} > gpurun_out/bigmodel.log 2>&1; }
 run_mixed() { timeout -k 10 600 python scripts/bench_service.py mixed --backend engine --concurrency ${C:-64} --seconds 20 > gpurun_out/mixed.log 2>&1; }
+run_phase() { timeout -k 10 600 python scripts/phase_profile.py --concurrency ${C:-256} > gpurun_out/phase_profile.log 2>&1; }
 case "$STEP" in
+  phase) run_phase ;;
+  policy) SWEEP="256" TAG=_p025 run_sweep && KA_PREFILL_MIN_FRAC=0 KA_PREFILL_MAX_WAIT_MS=0 SWEEP="256 384" TAG=_p0 run_sweep && KA_PREFILL_MIN_FRAC=0.1 KA_PREFILL_MAX_WAIT_MS=5 SWEEP="256" TAG=_p01 run_sweep && KA_SPLIT_MIXED_ATTN=0 KA_PREFILL_MIN_FRAC=0 KA_PREFILL_MAX_WAIT_MS=0 SWEEP="256" TAG=_p0nosplit run_sweep ;;
   big) run_big ;;
   mixed) run_mixed ;;
   bigmixed) run_mixed && run_big ;;

@@ -1,0 +1,102 @@
+"""Per-phase GPU profile of the bench workload: one prefill step admitting C requests at once
+(prefix-cached instruction blocks, sub-block reuse) and C-row decode steps (hipGraph replay).
+
+Drives the engine step by step on this thread and wraps each phase in torch.profiler, printing
+wall ms per phase and the top kernels by GPU time, so prefill and decode costs can be attributed
+separately (a whole-run rocprofv3 trace mixes in model build, autotune and warm-up).
+
+  python scripts/phase_profile.py [--concurrency 256] [--model llama3-8b]
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine  # noqa: E402
+from ai_agent_kubectl_amd.engine.sequence import SamplingParams, Sequence  # noqa: E402
+from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM  # noqa: E402
+import bench  # noqa: E402
+
+
+def table(prof, n=25):
+    rows = []
+    for e in prof.key_averages():
+        t = getattr(e, "device_time_total", None) or getattr(e, "cuda_time_total", 0)
+        if t > 0 and e.key and not e.key.startswith("ProfilerStep"):
+            rows.append((t, e.count, e.key))
+    rows.sort(reverse=True)
+    tot = sum(r[0] for r in rows if not r[2].startswith("aten::") and not r[2].startswith("cuda"))
+    out = [f"  device total (kernels) {tot / 1e3:.2f} ms"]
+    for t, c, k in rows[:n]:
+        out.append(f"  {t / 1e3:9.3f} ms  n={c:5d}  avg={t / max(1, c):8.1f} us  {k[:100]}")
+    return "\n".join(out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--concurrency", type=int, default=256)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--decode-steps", type=int, default=8)
+    a = ap.parse_args()
+    C = a.concurrency
+    buckets = tuple(b for b in (1, 8, 16, 32, 64, 128, 192, 256, 384, 512) if b <= C) + ((C,) if C not in (1, 8, 16, 32, 64, 128, 192, 256, 384, 512) else ())
+    eng = build_engine(EngineOptions(model=a.model, device="cuda:0", max_batch=C, graph_buckets=buckets,
+                                     kv_cache_tokens=max(65536, C * 256), max_model_len=512, ignore_eos=True,
+                                     max_batched_tokens=16384))
+    eng.runner.capture_graphs()
+    be = EngineLLM(eng, max_new_tokens=16, ignore_eos=True)
+    params = SamplingParams(max_new_tokens=16, ignore_eos=True)
+    for w in range(2):   # warm: publish the instruction blocks, exercise the plans
+        eng.generate_blocking([be.prompt_ids(bench.make_query(0, w, i)) for i in range(C)], params,
+                              forced_prefix=be._forced)
+    seqs = [Sequence(prompt_ids=be.prompt_ids(bench.make_query(0, 9, i)), params=params,
+                     forced_prefix=list(be._forced)) for i in range(C)]
+    for s in seqs:
+        eng.scheduler.add(s)
+    acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
+
+    def one_step():
+        batch = eng.scheduler.schedule()
+        toks = eng.runner.execute(batch)
+        eng._apply(batch, toks)
+        eng.scheduler.on_step_done(batch)
+        return batch
+
+    torch.cuda.synchronize()
+    with torch.profiler.profile(activities=acts) as prof_p:
+        t0 = time.perf_counter()
+        b = one_step()
+        torch.cuda.synchronize()
+        tp = time.perf_counter() - t0
+    print(f"PREFILL step: {len(b.seqs)} seqs, {b.num_tokens} tokens, {len(b.copies)} block copies, "
+          f"wall {tp * 1e3:.2f} ms ({b.num_tokens / tp:.0f} tok/s)")
+    print(table(prof_p))
+    one_step()   # (the first decode step after admission)
+    torch.cuda.synchronize()
+    with torch.profiler.profile(activities=acts) as prof_d:
+        t0 = time.perf_counter()
+        for _ in range(a.decode_steps):
+            b = one_step()
+        torch.cuda.synchronize()
+        td = (time.perf_counter() - t0) / a.decode_steps
+    print(f"DECODE steps: B={len(b.seqs)} decode={b.is_decode} wall {td * 1e3:.3f} ms/step")
+    print(table(prof_d, 30))
+    # eager (non-graph) decode for per-kernel attribution inside the graph
+    graphs = eng.runner.graphs
+    eng.runner.graphs = {}
+    with torch.profiler.profile(activities=acts) as prof_e:
+        t0 = time.perf_counter()
+        for _ in range(2):
+            one_step()
+        torch.cuda.synchronize()
+        te = (time.perf_counter() - t0) / 2
+    eng.runner.graphs = graphs
+    print(f"DECODE eager (attribution): {te * 1e3:.3f} ms/step")
+    print(table(prof_e, 30))
+
+
+if __name__ == "__main__":
+    main()

@@ -209,6 +209,23 @@ def test_sub_block_reuse_equals_cold(tiny_engine):
     assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
 
 
+def test_mixed_step_split_attention_matches(tiny_engine):
+    from tests.engine_helpers import run_staggered
+    eng, be = tiny_engine
+    params = SamplingParams(max_new_tokens=6, ignore_eos=True)
+    prompts = [be.prompt_ids(q) for q in ("list pods", "get nodes -o wide", "describe svc api", "top pods")]
+    alone = [eng.generate_blocking([p], params, forced_prefix=be._forced)[0].output_ids for p in prompts]
+    outs = {}
+    for split in (False, True):
+        eng.runner.split_mixed_attention = split
+        try:
+            outs[split] = run_staggered(eng, prompts, params, be._forced)
+            assert run_staggered.mixed >= 3
+        finally:
+            eng.runner.split_mixed_attention = True
+    assert outs[True] == outs[False] == alone
+
+
 def test_api_with_engine_backend(tiny_engine):
     from fastapi.testclient import TestClient
     from ai_agent_kubectl_amd.api import create_app

@@ -116,6 +116,25 @@ def test_paged_prefill(hq, hkv, qlens, ctxs):
     close(got, want, atol=2e-2)
 
 
+def test_mixed_step_split_attention():
+    """Mixed step: leading 1-token decode rows through the decode kernel, prompt rows through the
+    varlen prefill kernel (subset metadata, absolute q_starts, shared output) == reference."""
+    hq, hkv = 32, 8
+    qlens, ctxs = [1, 1, 1, 30, 17], [40, 93, 7, 30, 81]
+    S, nd = len(qlens), 3
+    kc, vc = _cache(200, hkv)
+    bt = _tables(S, ctxs, 200, 16)
+    T = sum(qlens)
+    q = torch.randn(T, hq, 128, device=DEV, dtype=BF)
+    starts = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
+    ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    scale = 128 ** -0.5
+    out = ops.attention_prefill(q, kc, vc, bt[nd:], starts[nd:], ctx[nd:], max(qlens), scale,
+                                out=torch.empty_like(q))
+    ops.attention_decode(q[:nd], kc, vc, bt[:nd], ctx[:nd], scale, out=out[:nd])
+    close(out, ref.attention_prefill(q, kc, vc, bt, starts, ctx, scale), atol=2e-2)
+
+
 def test_prefill_spike_forces_rescale():
     # spike one key late in the context so the running max jumps at a later tile (guide §5.4 rule 26)
     hq, hkv = 32, 8
@@ -172,6 +191,31 @@ def test_gemm_skinny(M, N, K):
     for split in (1, 3, 8):
         got = ops.linear(x, w, split=split)
         close(got, want, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [48, 128, 200, 256, 384, 512])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1040, 512)])
+def test_gemm_tile(M, N, K):
+    """LDS-tiled MFMA GEMM, every configuration, with and without split-K, ragged M and N tiles."""
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(BF)
+    want = x.float() @ w.float().t()
+    for cfg in ops.TILE_CFGS:
+        for split in (1, 2, 4):
+            got = ops.linear_tile(x, w, cfg, split)
+            close(got, want, atol=3e-2, rtol=2e-2)
+
+
+def test_gemm_tile_autotune_plan_dispatch():
+    from ai_agent_kubectl_amd.ops.autotune import tune_linear
+    ws = [(torch.randn(6144, 4096, device=DEV) * 0.02).to(BF) for _ in range(3)]
+    rep = tune_linear({(6144, 4096): ws}, [1, 64, 256, 320])
+    assert set(k[0] for k in rep) == {1, 64, 256, 320}
+    x = torch.randn(320, 4096, device=DEV, dtype=BF)
+    close(ops.linear(x, ws[0]), x.float() @ ws[0].float().t(), atol=3e-2, rtol=2e-2)
+    for key in list(ops.GEMM_PLAN):
+        if key[1:] == (6144, 4096):
+            ops.GEMM_PLAN.pop(key)
 
 
 @pytest.mark.parametrize("T", [1, 7, 64, 256])

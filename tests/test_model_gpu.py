@@ -99,6 +99,21 @@ def test_prefix_cache_hit_matches_cold():
     assert warm.output_ids == cold.output_ids
 
 
+def test_mixed_steps_split_attention_matches_unsplit():
+    from tests.engine_helpers import run_staggered
+    params = SamplingParams(max_new_tokens=8, ignore_eos=True)
+    eng = _engine("llama3-8b-2l", graphs=True)
+    be = EngineLLM(eng, max_new_tokens=8, ignore_eos=True)
+    prompts = [be.prompt_ids(q) for q in QUERIES]
+    outs = {}
+    for split in (False, True):
+        eng.runner.split_mixed_attention = split
+        outs[split] = run_staggered(eng, prompts, params, be._forced)
+        assert run_staggered.mixed >= 4
+    eng.runner.split_mixed_attention = True
+    assert outs[True] == outs[False]
+
+
 def test_safe_decode_outputs_pass_validator():
     from ai_agent_kubectl_amd.safety import is_safe_kubectl_command
     eng = _engine("llama3-8b-2l", graphs=True)
