@@ -1,0 +1,131 @@
+// One-shot all-reduce (sum, bf16) over IPC-mapped peer buffers, for the small tensor-parallel
+// decode messages (8-16 KB x batch, latency-bound; a ring is
+// per-link bound on xGMI while a one-shot read of all peers uses every link at once).
+//
+// Every rank owns one fine-grained *uncached* allocation (hipDeviceMallocUncached, so peer reads and
+// flag polls see memory, not a stale L2 line) mapped into every other rank with hipIpc handles:
+//   [ data half 0 : cap elems ][ data half 1 : cap elems ][ flags : AR_MAX_BLOCKS x AR_MAX_RANKS u32 ]
+//   [ ctr : u32 ][ done : u32 ][ err : i32 ]
+// Block b of every rank owns the same element chunk b.  One call (epoch e = ctr + 1, half = e & 1):
+//   1. copy chunk b of the input into my half;  2. system-scope release, then store e into
+//   flags[b][me] of every peer;  3. wait until my flags[b][p] >= e for every p (acquire, bounded
+//   spin -> err instead of a hang);  4. sum chunk b over all ranks' halves in fp32, write the output;
+//   5. the last block to finish stores ctr = e.
+// The epoch lives in device memory, so the launch can be captured once in a hipGraph and replayed.
+// Halves alternate by epoch parity: a rank rewrites half h in call e + 2 only after every peer has
+// signalled call e + 1, i.e. after every peer's call e (which read h) has completed on its stream.
+#include <cstring>
+
+#include "common.h"
+
+#define AR_MAX_RANKS 8
+#define AR_MAX_BLOCKS 64
+
+struct ArArgs {
+  bf16_t* data[AR_MAX_RANKS];
+  unsigned* flags[AR_MAX_RANKS];
+};
+
+__global__ __launch_bounds__(512) void allreduce_oneshot_kernel(ArArgs a, const bf16_t* __restrict__ in,
+                                                                bf16_t* out, unsigned* ctr, unsigned* done,
+                                                                int* err, int rank, int world, int n, int cap) {
+  __shared__ unsigned s_epoch;
+  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+  const size_t half = (size_t)(epoch & 1u) * cap;
+  const int chunk = ((n + (int)gridDim.x - 1) / (int)gridDim.x + 7) / 8 * 8;
+  const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
+
+  bf16_t* mine = a.data[rank] + half;
+  for (int i = beg + threadIdx.x * 8; i < end; i += blockDim.x * 8)
+    *reinterpret_cast<u32x4*>(mine + i) = *reinterpret_cast<const u32x4*>(in + i);
+  __threadfence_system();
+  __syncthreads();
+  if ((int)threadIdx.x < world) {
+    const int p = threadIdx.x;
+    __hip_atomic_store(a.flags[p] + blockIdx.x * AR_MAX_RANKS + rank, epoch, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned* f = a.flags[rank] + blockIdx.x * AR_MAX_RANKS + p;
+    int spins = 0;
+    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      if (++spins > (1 << 22)) {   // ~1 s: a peer never arrived -> report, never hang the GPU
+        atomicExch(err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+
+  for (int i = beg + threadIdx.x * 8; i < end; i += blockDim.x * 8) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < world; ++p) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(a.data[p] + half + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[2 * j] += lo_f(v[j]);
+        s[2 * j + 1] += hi_f(v[j]);
+      }
+    }
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = pack2(s[2 * j], s[2 * j + 1]);
+    *reinterpret_cast<u32x4*>(out + i) = o;
+  }
+
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned prev = atomicAdd(done, 1u);
+    if (prev == gridDim.x - 1) {   // every block has read ctr and finished: publish the epoch
+      *done = 0u;
+      __hip_atomic_store(ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ---- host helpers (ops/_hip.py ctypes; parallel/custom_allreduce.py) ----
+extern "C" int ka_ar_alloc(void** ptr, size_t bytes) {
+  hipError_t e = hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipMemset(*ptr, 0, bytes);
+}
+
+extern "C" int ka_ar_free(void* ptr) { return (int)hipFree(ptr); }
+
+extern "C" int ka_ar_get_handle(void* ptr, void* out64) {
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, ptr);
+  if (e == hipSuccess) memcpy(out64, &h, sizeof(h));
+  return (int)e;
+}
+
+extern "C" int ka_ar_open_handle(const void* in64, void** ptr) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, in64, sizeof(h));
+  return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+extern "C" int ka_ar_close_handle(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+
+// data / flags: host arrays of `world` device pointers (rank order); ctr/done/err: this rank's
+// counters.  n must be a multiple of 8 and <= cap.
+extern "C" int ka_allreduce_oneshot(void* out, const void* in, void* const* data, void* const* flags, void* ctr,
+                                    void* done, void* err, int rank, int world, int n, int cap, int nblocks,
+                                    hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n % 8 || n > cap || nblocks < 1 ||
+      nblocks > AR_MAX_BLOCKS)
+    return (int)hipErrorInvalidValue;
+  ArArgs a;
+  for (int p = 0; p < AR_MAX_RANKS; ++p) {
+    a.data[p] = p < world ? static_cast<bf16_t*>(data[p]) : nullptr;
+    a.flags[p] = p < world ? static_cast<unsigned*>(flags[p]) : nullptr;
+  }
+  // nblocks must be identical on every rank (block b of each rank owns chunk b)
+  hipLaunchKernelGGL(allreduce_oneshot_kernel, dim3(nblocks), dim3(512), 0, stream, a,
+                     static_cast<const bf16_t*>(in), static_cast<bf16_t*>(out), static_cast<unsigned*>(ctr),
+                     static_cast<unsigned*>(done), static_cast<int*>(err), rank, world, n, cap);
+  KA_CHECK_LAUNCH();
+}

@@ -85,6 +85,9 @@ def build_engine(opts: EngineOptions, comm=None, metrics=None) -> LLMEngine:
     else:
         num_blocks = min(want_blocks, 4096)
     masks = build_masks(tok, allow_eos=not opts.ignore_eos) if opts.safe_decode else None
+    if comm is not None and opts.tp_size > 1:
+        from ..parallel.custom_allreduce import maybe_enable
+        maybe_enable(comm, dev)   # KA_CUSTOM_AR=1: one-shot all-reduce for the small decode messages
     runner = ModelRunner(cfg, weights, dev, num_blocks=num_blocks, block_size=opts.block_size,
                          max_model_len=opts.max_model_len, graph_buckets=opts.graph_buckets, mask_bits=masks,
                          comm=comm, tp_rank=opts.tp_rank, tp_size=opts.tp_size, ep_rank=par.ep_rank,

@@ -42,7 +42,12 @@ _SIGS = {
     "ka_moe_align": [P, P, P, I, I, I, P],
     "ka_moe_gemm": [P, P, P, P, P, I, I, I, I, I, I, P],
     "ka_moe_combine": [P, P, P, P, I, I, I, I, I, P],
-    "ka_allreduce_oneshot": [P, P, P, I, I, I, I, P],
+    "ka_allreduce_oneshot": [P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "ka_ar_alloc": [P, ctypes.c_size_t],
+    "ka_ar_free": [P],
+    "ka_ar_get_handle": [P, P],
+    "ka_ar_open_handle": [P, P],
+    "ka_ar_close_handle": [P],
 }
 
 

@@ -9,9 +9,9 @@ tests).  The model only needs three collectives:
 * `broadcast(t)`    — per-step metadata from the driver rank (A4).
 
 All are issued on the current stream so that they are captured inside decode hipGraphs.
-`LocalComm` is the TP=1 no-op.  `TorchComm` wraps a process group.  A hand-written one-shot
-all-reduce over peer-mapped buffers (csrc/allreduce.hip) is used for small decode messages when
-enabled (parallel/custom_allreduce.py).
+`LocalComm` is the TP=1 no-op.  `TorchComm` wraps a process group.  With KA_CUSTOM_AR=1 a
+hand-written one-shot all-reduce over IPC-mapped peer buffers (csrc/allreduce.hip,
+parallel/custom_allreduce.py) takes the small bf16 decode messages; RCCL keeps the rest.
 """
 from __future__ import annotations
 

@@ -218,6 +218,7 @@ def test_mixed_step_split_attention_matches(tiny_engine):
     outs = {}
     for split in (False, True):
         eng.runner.split_mixed_attention = split
+        eng.bm.reset_prefix_cache()
         try:
             outs[split] = run_staggered(eng, prompts, params, be._forced)
             assert run_staggered.mixed >= 3
