@@ -28,6 +28,50 @@ FLUSH_EVERY = 16   # requests per engine-bound IPC message within one event-loop
 logger = logging.getLogger("app.dp")
 
 
+class _Obs:
+    """Histogram stand-in: records observations for shipping to the API process."""
+
+    def __init__(self, sink: list):
+        self.sink = sink
+
+    def observe(self, v: float) -> None:
+        self.sink.append(v)
+
+
+class _Gauge:
+    def __init__(self, store: dict, name: str):
+        self.store, self.name = store, name
+
+    def set(self, v) -> None:
+        self.store[self.name] = v
+
+
+class EngineMetricsProxy:
+    """The engine's metrics interface inside a replica process.  TTFT / TPOT observations and the
+    batch / queue / KV gauges ride back to the API process on the batched completion messages and
+    are replayed into its Prometheus registry (DPRouterLLM._apply_obs), so /metrics shows the engine
+    even though it runs in another process."""
+
+    def __init__(self):
+        self.ttft: list = []
+        self.tpot: list = []
+        self.gauges: dict = {}
+        self.llm_ttft = _Obs(self.ttft)
+        self.llm_tpot = _Obs(self.tpot)
+        self.llm_batch_size = _Gauge(self.gauges, "llm_batch_size")
+        self.llm_queue_depth = _Gauge(self.gauges, "llm_queue_depth")
+        self.llm_kv_blocks_used = _Gauge(self.gauges, "llm_kv_blocks_used")
+
+    def take(self):
+        if not (self.ttft or self.tpot or self.gauges):
+            return None
+        out = {"ttft": self.ttft[:], "tpot": self.tpot[:], "gauges": dict(self.gauges)}
+        self.ttft.clear()
+        self.tpot.clear()
+        self.gauges.clear()
+        return out
+
+
 def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> None:
     """Entry point of one replica process."""
     import torch  # noqa: F401  (first CUDA use happens here, in the child)
@@ -42,6 +86,7 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> 
         opts = EngineOptions.from_settings(s)
         opts.device = device
         eng = build_engine(opts)
+        eng.metrics = EngineMetricsProxy()
         if opts.use_graphs and device.startswith("cuda"):
             eng.runner.capture_graphs()
         from ..utils.runtime import tune_gc
@@ -64,12 +109,18 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> 
         with done_lock:
             done_buf.append((rid, (seq.output_ids, err, seq.finish_reason)))
 
+    last_obs = [0.0]
+
     def flush():
         nonlocal done_buf
-        if done_buf:
-            with done_lock:
-                batch, done_buf = done_buf, []
-            resp_q.put(("done_batch", 0, batch))
+        now = time.perf_counter()
+        if done_buf or now - last_obs[0] > 0.05:
+            obs = eng.metrics.take()
+            if done_buf or obs is not None:
+                with done_lock:
+                    batch, done_buf = done_buf, []
+                last_obs[0] = now
+                resp_q.put(("done_batch", idx, (batch, obs)))
 
     eng.step_end_hooks.append(flush)
 
@@ -150,6 +201,8 @@ class DPRouterLLM(LLMBackend):
         self._lock = threading.Lock()
         self._ready = threading.Event()
         self._n_ready = 0
+        self._metrics = None
+        self._gauges: Dict[int, dict] = {}
         self._reader = threading.Thread(target=self._read_loop, name="dp-router", daemon=True)
         self._reader.start()
         self._start_timeout = start_timeout
@@ -174,7 +227,12 @@ class DPRouterLLM(LLMBackend):
                 if self._n_ready == len(self.replicas):
                     self._ready.set()
             elif kind in ("done", "done_batch"):
-                items = b if kind == "done_batch" else [(a, b)]
+                if kind == "done_batch":
+                    items, obs = b
+                    if obs is not None and self._metrics is not None:
+                        self._apply_obs(a, obs)
+                else:
+                    items = [(a, b)]
                 by_loop = {}
                 with self._lock:
                     for rid, payload in items:
@@ -191,6 +249,20 @@ class DPRouterLLM(LLMBackend):
                     ent[0].call_soon_threadsafe(_set, ent[1], b)
             elif kind == "stop":
                 return
+
+    def attach_metrics(self, metrics) -> None:
+        self._metrics = metrics
+
+    def _apply_obs(self, idx: int, obs: dict) -> None:
+        m = self._metrics
+        for v in obs["ttft"]:
+            m.llm_ttft.observe(v)
+        for v in obs["tpot"]:
+            m.llm_tpot.observe(v)
+        if obs["gauges"]:
+            self._gauges[idx] = {**self._gauges.get(idx, {}), **obs["gauges"]}
+            for name in ("llm_batch_size", "llm_queue_depth", "llm_kv_blocks_used"):
+                getattr(m, name).set(sum(g.get(name, 0) for g in self._gauges.values()))
 
     def _check_alive(self) -> None:
         for r in self.replicas:

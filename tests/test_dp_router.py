@@ -39,3 +39,13 @@ def test_api_over_dp_router():
         r2 = c.post("/kubectl-command", json={"query": "get nodes"})
         assert r1.status_code == 200 and r1.json()["from_cache"] is False
         assert r2.json()["from_cache"] is True   # one global cache in the API process
+        # engine metrics recorded in the replica processes reach the API's /metrics
+        import time
+        deadline = time.time() + 10
+        while time.time() < deadline:
+            m = c.get("/metrics").text
+            if "llm_ttft_seconds_count 1.0" in m:
+                break
+            time.sleep(0.2)
+        assert "llm_ttft_seconds_count 1.0" in m and "llm_tpot_seconds_count 1.0" in m
+        assert "llm_kv_blocks_used" in m
