@@ -13,10 +13,14 @@
 // ------------------------------------------------------------------------------------------------
 // RMSNorm, optionally fused with the residual add:   r = x (+ residual);  residual = r;
 //                                                  out = r * rsqrt(mean(r^2) + eps) * w
+// and optionally with the split-K reduction of the GEMM that produced x: x = bf16(sum_k P[k]) where P
+// holds `split` fp32 partial slabs of [rows, hidden] (gemm_skinny / gemm_tile with no output), so
+// the projection's reduce kernel and its bf16 round trip through HBM disappear.
 template <int NT, int MAXV>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16_t* __restrict__ out, bf16_t* __restrict__ residual,
                                                      const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
-                                                     int hidden, float eps) {
+                                                     int hidden, float eps, const float* __restrict__ P, int split,
+                                                     size_t pstride) {
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
   const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * hidden);
@@ -27,7 +31,18 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16_t* __restrict__ out, b
   for (int i = 0; i < MAXV; ++i) {
     const int idx = threadIdx.x + i * NT;
     if (idx < nvec) {
-      uint4 a = xr[idx];
+      uint4 a;
+      if (P != nullptr) {
+        const float* pr = P + (size_t)row * hidden + idx * 8;
+        f32x4 s0 = *reinterpret_cast<const f32x4*>(pr), s1 = *reinterpret_cast<const f32x4*>(pr + 4);
+        for (int k = 1; k < split; ++k) {
+          s0 += *reinterpret_cast<const f32x4*>(pr + k * pstride);
+          s1 += *reinterpret_cast<const f32x4*>(pr + k * pstride + 4);
+        }
+        a = make_uint4(pack2(s0[0], s0[1]), pack2(s0[2], s0[3]), pack2(s1[0], s1[1]), pack2(s1[2], s1[3]));
+      } else {
+        a = xr[idx];
+      }
       uint32_t aw[4] = {a.x, a.y, a.z, a.w};
       if (rr) {
         uint4 b = rr[idx];
@@ -88,12 +103,41 @@ extern "C" int ka_rmsnorm(void* out, void* residual, const void* x, const void* 
   auto* r = static_cast<bf16_t*>(residual);
   auto* xi = static_cast<const bf16_t*>(x);
   auto* wi = static_cast<const bf16_t*>(w);
+  const float* P = nullptr;
+  const int split = 0;
+  const size_t pstride = 0;
   if (nvec <= 256)
-    hipLaunchKernelGGL((rmsnorm_kernel<256, 1>), dim3(rows), dim3(256), 0, stream, o, r, xi, wi, hidden, eps);
+    hipLaunchKernelGGL((rmsnorm_kernel<256, 1>), dim3(rows), dim3(256), 0, stream, o, r, xi, wi, hidden, eps, P,
+                       split, pstride);
   else if (nvec <= 512)
-    hipLaunchKernelGGL((rmsnorm_kernel<256, 2>), dim3(rows), dim3(256), 0, stream, o, r, xi, wi, hidden, eps);
+    hipLaunchKernelGGL((rmsnorm_kernel<256, 2>), dim3(rows), dim3(256), 0, stream, o, r, xi, wi, hidden, eps, P,
+                       split, pstride);
   else
-    hipLaunchKernelGGL((rmsnorm_kernel<256, 4>), dim3(rows), dim3(256), 0, stream, o, r, xi, wi, hidden, eps);
+    hipLaunchKernelGGL((rmsnorm_kernel<256, 4>), dim3(rows), dim3(256), 0, stream, o, r, xi, wi, hidden, eps, P,
+                       split, pstride);
+  KA_CHECK_LAUNCH();
+}
+
+// out = rmsnorm(bf16(sum_k P[k]) (+ residual)) * w; P = split fp32 slabs of [rows, hidden]
+extern "C" int ka_rmsnorm_splitk(void* out, void* residual, const void* P, int split, const void* w, int rows,
+                                 int hidden, float eps, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (hidden % 8 != 0 || hidden > 256 * 8 * 4 || split < 1) return (int)hipErrorInvalidValue;
+  const int nvec = hidden / 8;
+  auto* o = static_cast<bf16_t*>(out);
+  auto* r = static_cast<bf16_t*>(residual);
+  auto* p = static_cast<const float*>(P);
+  auto* wi = static_cast<const bf16_t*>(w);
+  const size_t ps = (size_t)rows * hidden;
+  if (nvec <= 256)
+    hipLaunchKernelGGL((rmsnorm_kernel<256, 1>), dim3(rows), dim3(256), 0, stream, o, r, nullptr, wi, hidden, eps,
+                       p, split, ps);
+  else if (nvec <= 512)
+    hipLaunchKernelGGL((rmsnorm_kernel<256, 2>), dim3(rows), dim3(256), 0, stream, o, r, nullptr, wi, hidden, eps,
+                       p, split, ps);
+  else
+    hipLaunchKernelGGL((rmsnorm_kernel<256, 4>), dim3(rows), dim3(256), 0, stream, o, r, nullptr, wi, hidden, eps,
+                       p, split, ps);
   KA_CHECK_LAUNCH();
 }
 

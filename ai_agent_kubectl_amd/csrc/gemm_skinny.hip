@@ -196,6 +196,7 @@ extern "C" int ka_gemm_skinny(void* Y, const void* X, const void* W, void* works
   else if (mt <= 8) launch_mt<8>(x, w, y, p, M, N, K, split, kps, stream);
   else if (mt <= 12) launch_mt<12>(x, w, y, p, M, N, K, split, kps, stream);
   else launch_mt<16>(x, w, y, p, M, N, K, split, kps, stream);
-  if (split > 1) ka_splitk_reduce_launch(y, p, split, (long)M * N, stream);
+  // Y == nullptr: leave the fp32 partials for a fused consumer (ka_rmsnorm_splitk)
+  if (split > 1 && y != nullptr) ka_splitk_reduce_launch(y, p, split, (long)M * N, stream);
   KA_CHECK_LAUNCH();
 }

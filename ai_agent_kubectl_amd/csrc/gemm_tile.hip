@@ -353,6 +353,7 @@ extern "C" int ka_gemm_tile(void* Y, const void* X, const void* W, void* workspa
     case 8: launch_wide<1, 4, 8>(x, w, y, p, M, N, K, split, kps, stream); break;
     case 9: launch_wide<4, 2, 8>(x, w, y, p, M, N, K, split, kps, stream); break;
   }
-  if (split > 1) ka_splitk_reduce_launch(y, p, split, (long)M * N, stream);
+  // Y == nullptr: leave the fp32 partials for a fused consumer (ka_rmsnorm_splitk)
+  if (split > 1 && y != nullptr) ka_splitk_reduce_launch(y, p, split, (long)M * N, stream);
   KA_CHECK_LAUNCH();
 }

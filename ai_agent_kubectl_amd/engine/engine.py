@@ -176,10 +176,38 @@ class LLMEngine:
             return
         self._loop_body()
 
+    def _torch_profile_hook(self):
+        """KA_TORCH_PROFILE=<trace.json>[:<steps>]: torch.profiler (CPU + GPU activities) over the
+        first <steps> busy engine steps (default 50), exported as a Chrome trace."""
+        spec = os.environ.get("KA_TORCH_PROFILE")
+        if not spec:
+            return None
+        path, _, steps = spec.partition(":")
+        import torch
+        acts = [torch.profiler.ProfilerActivity.CPU]
+        if torch.cuda.is_available():
+            acts.append(torch.profiler.ProfilerActivity.CUDA)
+        prof = torch.profiler.profile(activities=acts)
+        prof.start()
+        state = {"left": int(steps or 50), "prof": prof}
+
+        def on_step(n: int) -> None:
+            if state["prof"] is None or n == 0:
+                return
+            state["left"] -= 1
+            if state["left"] <= 0:
+                state["prof"].stop()
+                state["prof"].export_chrome_trace(path)
+                state["prof"] = None
+        return on_step
+
     def _loop_body(self) -> None:
+        tprof = self._torch_profile_hook()
         while not self._stop.is_set():
             try:
                 n = self.step()
+                if tprof is not None:
+                    tprof(n)
             except Exception as e:  # engine fault: fail in-flight requests, stay alive but unhealthy
                 logger.exception("engine step failed")
                 self.healthy = False

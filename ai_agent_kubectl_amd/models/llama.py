@@ -46,6 +46,7 @@ class LlamaModel:
         self.W = weights
         self.comm = comm or LocalComm()
         self.tp_rank, self.tp_size = tp_rank, tp_size
+        self._local_comm = isinstance(self.comm, LocalComm)   # no all-reduce between GEMM and norm
         self.ep_rank, self.ep_size = ep_rank, ep_size
         self.hq = cfg.num_heads // tp_size
         self.hkv = cfg.num_kv_heads // tp_size
@@ -93,13 +94,16 @@ class LlamaModel:
             else:
                 a = ops.attention_prefill(q, k_cache[li], v_cache[li], meta.block_tables, meta.q_starts,
                                           meta.ctx_lens, meta.max_q_len, self.scale)
-            h = ops.linear(a.view(T, self.hq * self.D), L["wo"])
+            # TP = 1: the projections feeding a norm leave their split-K partials to the fused
+            # reduce + residual + RMSNorm kernel (ops.SplitK); with TP the all-reduce needs bf16
+            fuse = self._local_comm
+            h = ops.linear(a.view(T, self.hq * self.D), L["wo"], defer_reduce=fuse)
             self.comm.all_reduce(h)
             x = ops.rmsnorm(h, L["ln2"], eps, residual=residual)
             if cfg.is_moe:
                 h = moe_forward(x, L, cfg, self.ep_rank, self.ep_size, meta.is_decode)
             else:
-                h = ops.linear(ops.silu_mul(ops.linear(x, L["w13"])), L["w2"])
+                h = ops.linear(ops.silu_mul(ops.linear(x, L["w13"])), L["w2"], defer_reduce=fuse)
             self.comm.all_reduce(h)
         x = ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
         return x.index_select(0, meta.logits_indices)

@@ -8,7 +8,7 @@ hand-written kernel wins (decode GEMV, MoE grouped GEMM).
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import Optional, Tuple, NamedTuple
 
 import torch
 
@@ -43,9 +43,31 @@ def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
-def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+class SplitK(NamedTuple):
+    """fp32 split-K partials of a projection whose reduction is deferred to the consumer (rmsnorm)."""
+    P: torch.Tensor          # [split, M, N] fp32
+    split: int
+
+    @property
+    def shape(self):
+        return self.P.shape[1:]
+
+    def resolve(self) -> torch.Tensor:
+        """bf16 [M, N] (for consumers without a fused path)."""
+        return self.P.sum(0).to(torch.bfloat16)
+
+
+def rmsnorm(x, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
             out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out = rmsnorm(x (+ residual)) * w; when `residual` is given it is updated in place to x + residual."""
+    """out = rmsnorm(x (+ residual)) * w; when `residual` is given it is updated in place to x + residual.
+    `x` may be a `SplitK` (partials of the producing GEMM): the reduction is fused into the norm."""
+    if isinstance(x, SplitK):
+        lib = require()
+        rows, hidden = x.shape
+        out = torch.empty((rows, hidden), dtype=w.dtype, device=w.device) if out is None else out
+        check(lib.ka_rmsnorm_splitk(_p(out), _p(residual), _p(x.P), x.split, _p(w), rows, hidden, float(eps),
+                                    _stream()), "rmsnorm_splitk")
+        return out
     if _ref(x):
         return ref.rmsnorm(x, w, eps, residual)
     lib = require()
@@ -169,10 +191,12 @@ GEMM_PLAN: dict = {}
 TILE_MAX_M = 512
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0) -> torch.Tensor:
+def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool = False):
     """y = x @ w.T (w is [out, in]).  Decode-sized M goes to the hand-written weight-streaming
     kernel (M <= 256), the LDS-tiled MFMA kernel (M <= 512) or hipBLASLt, whichever the autotuned
-    plan measured fastest for this (M, N, K); other shapes (prefill) go to hipBLASLt via F.linear."""
+    plan measured fastest for this (M, N, K); other shapes (prefill) go to hipBLASLt via F.linear.
+    defer_reduce: when the chosen kernel splits K, return its fp32 partials as a `SplitK` for a
+    consumer that fuses the reduction (rmsnorm) instead of running the reduce kernel."""
     M, K = x.shape
     N = w.shape[0]
     if _ref(x) or M > TILE_MAX_M or K % 64 != 0 or N % 4 != 0 or not x.is_contiguous():
@@ -185,17 +209,20 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0) -> torch.Tensor:
         elif plan[0] == "blas":
             return torch.nn.functional.linear(x, w)
         elif plan[0] == "tile":
-            return linear_tile(x, w, plan[2], plan[1])
+            return linear_tile(x, w, plan[2], plan[1], defer_reduce)
         else:
             split = plan[1]
     if M > SKINNY_MAX_M:
         return torch.nn.functional.linear(x, w)
     lib = require()
     split = split or skinny_split(M, N, K)
-    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
     kps = ((K // split + 63) // 64) * 64
     split = (K + kps - 1) // kps
     ws = torch.empty((split, M, N), dtype=torch.float32, device=x.device) if split > 1 else None
+    if defer_reduce and split > 1:
+        check(lib.ka_gemm_skinny(None, _p(x), _p(w), _p(ws), M, N, K, split, _stream()), "gemm_skinny")
+        return SplitK(ws, split)
+    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
     check(lib.ka_gemm_skinny(_p(y), _p(x), _p(w), _p(ws), M, N, K, split, _stream()), "gemm_skinny")
     return y
 
@@ -213,7 +240,7 @@ def tile_shape(cfg: int):
     return lib.ka_gemm_tile_bn(cfg), lib.ka_gemm_tile_bm(cfg)
 
 
-def linear_tile(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1) -> torch.Tensor:
+def linear_tile(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, defer_reduce: bool = False):
     """y = x @ w.T through the LDS-tiled MFMA kernel (csrc/gemm_tile.hip), split-K `split`."""
     M, K = x.shape
     N = w.shape[0]
@@ -221,10 +248,13 @@ def linear_tile(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1) -> t
     if K % kq or N % 16:
         raise ValueError(f"gemm_tile cfg {cfg} needs K % {kq} == 0 and N % 16 == 0, got N={N} K={K}")
     lib = require()
-    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
     kps = ((K // split + kq - 1) // kq) * kq
     split = (K + kps - 1) // kps
     ws = torch.empty((split, M, N), dtype=torch.float32, device=x.device) if split > 1 else None
+    if defer_reduce and split > 1:
+        check(lib.ka_gemm_tile(None, _p(x), _p(w), _p(ws), M, N, K, split, cfg, _stream()), "gemm_tile")
+        return SplitK(ws, split)
+    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
     check(lib.ka_gemm_tile(_p(y), _p(x), _p(w), _p(ws), M, N, K, split, cfg, _stream()), "gemm_tile")
     return y
 

@@ -36,6 +36,7 @@ _SIGS = {
     "ka_paged_decode": [P, P, P, P, P, I, P, I, I, I, I, I, F, P],
     "ka_paged_prefill": [P, P, P, P, P, I, P, P, I, I, I, I, I, I, F, P],
     "ka_gemm_skinny": [P, P, P, P, I, I, I, I, P],
+    "ka_rmsnorm_splitk": [P, P, P, I, P, I, I, F, P],
     "ka_gemm_tile": [P, P, P, P, I, I, I, I, I, P],
     "ka_gemm_tile_bm": [I],
     "ka_gemm_tile_bn": [I],

@@ -193,6 +193,30 @@ def test_gemm_skinny(M, N, K):
         close(got, want, atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("rows,hidden,split", [(1, 4096, 2), (37, 4096, 8), (256, 4096, 4), (5, 8192, 3)])
+def test_rmsnorm_fused_splitk_reduce(rows, hidden, split):
+    """rmsnorm(SplitK partials, residual) == rmsnorm(bf16(sum partials), residual)."""
+    P = torch.randn(split, rows, hidden, device=DEV) * 0.5
+    w = (torch.rand(hidden, device=DEV) + 0.5).to(BF)
+    res0 = torch.randn(rows, hidden, device=DEV).to(BF)
+    r1, r2 = res0.clone(), res0.clone()
+    got = ops.rmsnorm(ops.SplitK(P, split), w, 1e-5, residual=r1)
+    want = ref.rmsnorm(P.sum(0).to(BF), w, 1e-5, r2)
+    close(got, want, atol=2e-2)
+    close(r1, r2, atol=1e-2)
+
+
+def test_linear_defer_reduce_roundtrip():
+    x = torch.randn(64, 4096, device=DEV, dtype=BF)
+    w = (torch.randn(4096, 4096, device=DEV) * 0.02).to(BF)
+    sk = ops.linear_tile(x, w, 2, 4, defer_reduce=True)
+    assert isinstance(sk, ops.SplitK) and sk.split == 4
+    close(sk.resolve(), x.float() @ w.float().t(), atol=3e-2, rtol=2e-2)
+    sk2 = ops.linear(x, w, split=4, defer_reduce=True)
+    assert isinstance(sk2, ops.SplitK)
+    close(sk2.resolve(), x.float() @ w.float().t(), atol=3e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("M", [48, 128, 200, 256, 384, 512])
 @pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1040, 512)])
 def test_gemm_tile(M, N, K):
