@@ -268,3 +268,36 @@ extern "C" int ka_embedding(void* out, const int* ids, const void* table, int to
                      static_cast<const bf16_t*>(table), hidden, vocab, vocab_offset);
   KA_CHECK_LAUNCH();
 }
+
+// ------------------------------------------------------------------------------------------------
+// Paged-KV block copy for sub-block prefix reuse (engine/block_manager.py reuse_partial): for every
+// (src, dst) pair and every layer, copy the whole K block and V block (Hkv * BS * D bf16 each).
+// Rows past the reused prefix are overwritten by the same step's prefill (stream order).
+// grid = (pairs, layers); each block streams 2 * Hkv * BS * D * 2 bytes with 16-B accesses.
+__global__ __launch_bounds__(256) void kv_block_copy_kernel(bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
+                                                            const int* __restrict__ src, const int* __restrict__ dst,
+                                                            long layer_stride, long block_elems) {
+  const long l = blockIdx.y;
+  const long s = (long)src[blockIdx.x] * block_elems + l * layer_stride;
+  const long d = (long)dst[blockIdx.x] * block_elems + l * layer_stride;
+  const int nvec = (int)(block_elems / 8);
+  const u32x4* ks = reinterpret_cast<const u32x4*>(kc + s);
+  u32x4* kd = reinterpret_cast<u32x4*>(kc + d);
+  const u32x4* vs = reinterpret_cast<const u32x4*>(vc + s);
+  u32x4* vd = reinterpret_cast<u32x4*>(vc + d);
+  for (int i = threadIdx.x; i < nvec; i += 256) {
+    const u32x4 a = ks[i], b = vs[i];
+    kd[i] = a;
+    vd[i] = b;
+  }
+}
+
+extern "C" int ka_kv_block_copy(void* k_cache, void* v_cache, const void* src, const void* dst, int pairs,
+                                int layers, long layer_stride, long block_elems, hipStream_t stream) {
+  if (pairs <= 0) return 0;
+  if (block_elems % 8 != 0 || layer_stride % 8 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kv_block_copy_kernel, dim3(pairs, layers), dim3(256), 0, stream, static_cast<bf16_t*>(k_cache),
+                     static_cast<bf16_t*>(v_cache), static_cast<const int*>(src), static_cast<const int*>(dst),
+                     layer_stride, block_elems);
+  KA_CHECK_LAUNCH();
+}

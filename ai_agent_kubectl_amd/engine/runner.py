@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from ..models.config import ModelConfig
+from .. import ops
 from ..models.llama import AttnMeta, LlamaModel
 from ..parallel.comm import LocalComm
 from .safe_decode import mask_index_for
@@ -206,9 +207,7 @@ class ModelRunner:
         mb = self.max_blocks
         if nc:
             n = buf.shape[0]
-            src, dst = buf[n - 2 * nc:n - nc].long(), buf[n - nc:].long()
-            self.k_cache[:, dst] = self.k_cache[:, src]
-            self.v_cache[:, dst] = self.v_cache[:, src]
+            ops.kv_block_copy(self.k_cache, self.v_cache, buf[n - 2 * nc:n - nc], buf[n - nc:])
         ids, pos, slots = buf[:T], buf[T:2 * T], buf[2 * T:3 * T]
         o = 3 * T
         q_starts = buf[o:o + S + 1]; o += S + 1

@@ -77,6 +77,21 @@ def rmsnorm(x, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = N
     return out
 
 
+def kv_block_copy(k_cache: torch.Tensor, v_cache: torch.Tensor, src: torch.Tensor, dst: torch.Tensor) -> None:
+    """k_cache[:, dst] = k_cache[:, src] and the same for v_cache ([L, NB, ...] paged caches; src/dst
+    int32 device tensors of equal length) — the sub-block prefix-reuse copy."""
+    if _ref(k_cache):
+        s, d = src.long(), dst.long()
+        k_cache[:, d] = k_cache[:, s]
+        v_cache[:, d] = v_cache[:, s]
+        return
+    lib = require()
+    L, NB = k_cache.shape[0], k_cache.shape[1]
+    block_elems = k_cache[0, 0].numel()
+    check(lib.ka_kv_block_copy(_p(k_cache), _p(v_cache), _p(src), _p(dst), src.shape[0], L, NB * block_elems,
+                               block_elems, _stream()), "kv_block_copy")
+
+
 def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq: int, hkv: int, d: int,
                   q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if _ref(qkv):

@@ -206,6 +206,19 @@ def test_rmsnorm_fused_splitk_reduce(rows, hidden, split):
     close(r1, r2, atol=1e-2)
 
 
+def test_kv_block_copy():
+    L, NB, hkv = 4, 40, 8
+    kc = torch.randn(L, NB, hkv, 16, 128, device=DEV).to(BF)
+    vc = torch.randn(L, NB, hkv, 128, 16, device=DEV).to(BF)
+    src = torch.tensor([3, 7, 11], dtype=torch.int32, device=DEV)
+    dst = torch.tensor([20, 21, 39], dtype=torch.int32, device=DEV)
+    k2, v2 = kc.clone(), vc.clone()
+    k2[:, dst.long()] = k2[:, src.long()]
+    v2[:, dst.long()] = v2[:, src.long()]
+    ops.kv_block_copy(kc, vc, src, dst)
+    assert torch.equal(kc, k2) and torch.equal(vc, v2)
+
+
 def test_linear_defer_reduce_roundtrip():
     x = torch.randn(64, 4096, device=DEV, dtype=BF)
     w = (torch.randn(4096, 4096, device=DEV) * 0.02).to(BF)
