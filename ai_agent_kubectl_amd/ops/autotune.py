@@ -63,12 +63,17 @@ def _tunableop_begin() -> bool:
 
 
 def _tunableop_end() -> None:
+    """Stop tuning.  Results are written back only with KA_TUNABLEOP_WRITE=1 (to KA_TUNABLEOP_FILE):
+    with one engine process per GPU, eight processes would otherwise rewrite the same file while
+    others read it at start-up."""
+    import os
     tun = torch.cuda.tunable
     tun.tuning_enable(False)
-    try:
-        tun.write_file()
-    except Exception:  # pragma: no cover
-        pass
+    if os.environ.get("KA_TUNABLEOP_WRITE", "0") == "1":
+        try:
+            tun.write_file()
+        except Exception:  # pragma: no cover
+            pass
 
 
 @torch.inference_mode()

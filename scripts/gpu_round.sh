@@ -14,7 +14,7 @@ run_cprof() { KA_PROFILE_ENGINE=gpurun_out/cprof_engine.txt KA_PROFILE_API=gpuru
 run_gemm() { timeout -k 10 600 python scripts/bench_gemm.py > gpurun_out/bench_gemm.log 2>&1; }
 run_ktest() { timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -x -q -p no:cacheprovider > gpurun_out/pytest_kernels.log 2>&1; }
 run_sweep() { for c in ${SWEEP:-64 128 256}; do timeout -k 10 600 python bench.py --steps 4 --warmup 2 --concurrency $c ${BENCH_ARGS} > gpurun_out/bench_c$c${TAG}.log 2>&1 || return 1; done; }
-run_tunab() { KA_TUNABLEOP=1 KA_TUNABLEOP_FILE=gpurun_out/tunableop_results.csv timeout -k 10 900 python bench.py --steps 4 --warmup 2 --concurrency ${C:-256} > gpurun_out/bench_tunable.log 2>&1; }
+run_tunab() { KA_TUNABLEOP=1 KA_TUNABLEOP_WRITE=1 KA_TUNABLEOP_FILE=gpurun_out/tunableop_results.csv timeout -k 10 900 python bench.py --steps 4 --warmup 2 --concurrency ${C:-256} > gpurun_out/bench_tunable.log 2>&1; }
 run_big() { timeout -k 10 1200 python scripts/bigmodel_check.py ${BIG_MODELS} > gpurun_out/bigmodel.log 2>&1; }
 run_mixed() { timeout -k 10 600 python scripts/bench_service.py mixed --backend engine --concurrency ${C:-64} --seconds 20 > gpurun_out/mixed.log 2>&1; }
 run_phase() { timeout -k 10 600 python scripts/phase_profile.py --concurrency ${C:-256} > gpurun_out/phase_profile.log 2>&1; }
