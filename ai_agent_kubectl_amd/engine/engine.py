@@ -45,6 +45,10 @@ class LLMEngine:
         self.last_error: Optional[BaseException] = None
         self.steps = 0
         self.step_end_hooks: List[Callable[[], None]] = []   # e.g. batched IPC flush (parallel/dp.py)
+        # overlapped decode: one decode step in flight while the host applies the previous one
+        self.overlap = os.environ.get("KA_OVERLAP", "1") == "1"
+        self._inflight = None
+        self.chained_steps = 0
 
     # ------------------------------------------------------------------------------------------
     def start(self) -> None:
@@ -133,18 +137,51 @@ class LLMEngine:
                     m.llm_tpot.observe((now - s.t_first_token) / (s.num_generated - 1))
                 self._finish(s, SeqStatus.FINISHED, "stop" if eos else "length")
 
-    def step(self) -> int:
-        """Run one scheduler step; returns the number of sequences processed."""
-        self._drain_inbox()
-        if not self.scheduler.has_work():
-            return 0
-        batch = self.scheduler.schedule()
-        if not batch.seqs:
-            return 0
-        tokens = self.runner.execute(batch)
+    def _chain(self, prev):
+        """The decode step after `prev` (in flight, tokens not applied), or None when the batch
+        composition could change: an admission is due, a sequence reaches max_new_tokens with
+        `prev`, a sequence finished / was aborted, or KV capacity for one more token is missing.
+        (An EOS sampled by `prev` is only seen at collect: that row's next token is discarded.)"""
+        sch = self.scheduler
+        if sch.waiting and sch._should_prefill():
+            return None
+        for s in prev.seqs:
+            if s.finished or s.num_generated + 1 >= s.params.max_new_tokens:
+                return None
+        try:
+            for s in prev.seqs:
+                self.bm.ensure_capacity(s.block_table, s.total_len + 1)
+        except Exception:
+            return None
+        from .scheduler import Batch
+        return Batch(list(prev.seqs), [1] * len(prev.seqs), is_decode=True)
+
+    def _finish_step(self, batch, tokens) -> None:
         self._apply(batch, tokens)
         self.scheduler.on_step_done(batch)
         self.steps += 1
+
+    def step(self) -> int:
+        """Run one scheduler step; returns the number of sequences processed."""
+        self._drain_inbox()
+        if self._inflight is not None:
+            prev, handle = self._inflight
+            nxt = self._chain(prev)
+            nh = self.runner.launch_decode_async(nxt, chained=True) if nxt is not None else None
+            self.chained_steps += nxt is not None
+            self._finish_step(prev, self.runner.collect(handle))
+            self._inflight = (nxt, nh) if nxt is not None else None
+            batch = prev
+        else:
+            if not self.scheduler.has_work():
+                return 0
+            batch = self.scheduler.schedule()
+            if not batch.seqs:
+                return 0
+            if self.overlap and batch.is_decode and self.runner.can_overlap(len(batch.seqs)):
+                self._inflight = (batch, self.runner.launch_decode_async(batch))
+                return len(batch.seqs)
+            self._finish_step(batch, self.runner.execute(batch))
         m = self.metrics
         if m is not None:
             m.llm_batch_size.set(len(batch.seqs))
@@ -153,6 +190,7 @@ class LLMEngine:
         return len(batch.seqs)
 
     def _fail_all(self, err: BaseException) -> None:
+        self._inflight = None
         seqs = list(self.scheduler.running) + list(self.scheduler.waiting)
         self.scheduler.running.clear()
         self.scheduler.waiting.clear()
@@ -219,6 +257,13 @@ class LLMEngine:
             if n == 0 and not self.scheduler.has_work():
                 self._wake.wait(timeout=0.05)
                 self._wake.clear()
+        if self._inflight is not None:   # stopping with a step in flight: finish it cleanly
+            prev, handle = self._inflight
+            self._inflight = None
+            try:
+                self._finish_step(prev, self.runner.collect(handle))
+            except Exception:  # pragma: no cover
+                logger.exception("in-flight step failed at shutdown")
 
     # ------------------------------------------------------------------------------------------
     def generate_blocking(self, prompt_ids_list: List[List[int]], params: SamplingParams,

@@ -66,6 +66,11 @@ class ModelRunner:
         pin = self.device.type == "cuda"
         self.h_stage = torch.zeros(self._stage_len, dtype=torch.int32, pin_memory=pin)
         self.h_np = self.h_stage.numpy()
+        # overlapped decode (launch_decode_async): second pinned staging / output buffers so step
+        # t+1 can be packed and queued while step t's copies are still in flight
+        self._h_stages = [self.h_stage, torch.zeros(self._stage_len, dtype=torch.int32, pin_memory=pin)]
+        self._h_outs = [torch.zeros(B, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self._flip = 0
         self.d_logits_idx = torch.arange(B, dtype=torch.int64, device=self.device)
         self.d_out = torch.zeros(B, dtype=torch.int32, device=self.device)
         self.h_out = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
@@ -141,22 +146,67 @@ class ModelRunner:
     def _slot(self, table: List[int], pos: int) -> int:
         return table[pos // self.block_size] * self.block_size + pos % self.block_size
 
-    def _pack_decode(self, batch: Batch, Bp: int) -> None:
-        h, o, mb = self.h_np, self._off, self.max_blocks
+    def _pack_decode(self, batch: Batch, Bp: int, h: Optional[np.ndarray] = None, ahead: int = 0) -> None:
+        """Fill the decode staging image.  ahead = 1: for the step after the one in flight (its token
+        is not appended yet; ids then come from the device, launch_decode_async)."""
+        h = self.h_np if h is None else h
+        o, mb = self._off, self.max_blocks
         B = len(batch.seqs)
         for i, s in enumerate(batch.seqs):
-            pos = s.total_len - 1
-            h[o["ids"] + i] = s.all_ids[-1]
+            L = s.total_len + ahead
+            pos = L - 1
+            h[o["ids"] + i] = s.all_ids[-1] if not ahead else 0
             h[o["pos"] + i] = pos
             h[o["slots"] + i] = self._slot(s.block_table, pos)
-            h[o["ctx"] + i] = s.total_len
-            h[o["mask"] + i] = mask_index_for(s.num_generated, s.params.safe_decode)
+            h[o["ctx"] + i] = L
+            h[o["mask"] + i] = mask_index_for(s.num_generated + ahead, s.params.safe_decode)
             row = o["bt"] + i * mb
             n = len(s.block_table)
             h[row:row + n] = s.block_table
         if Bp > B:  # padding rows: no cache write, empty context
             for name, val in (("ids", 0), ("pos", 0), ("slots", -1), ("ctx", 0), ("mask", -1)):
                 h[o[name] + B:o[name] + Bp] = val
+
+    def can_overlap(self, B: int) -> bool:
+        # (on CPU the "async" launch simply runs synchronously: same code path, testable)
+        return self.tp_size == 1 and B <= self.bmax
+
+    @torch.inference_mode()
+    def launch_decode_async(self, batch: Batch, chained: bool = False):
+        """Queue one decode step without waiting for it (TP = 1).  chained: `batch` is the step after
+        the one in flight (same sequences, same row order): its input ids are copied on the device
+        from the previous step's sampled tokens.  Returns a handle for `collect`."""
+        B = len(batch.seqs)
+        i = bisect.bisect_left(self.buckets, B)
+        Bp = self.buckets[i] if i < len(self.buckets) else B
+        t0 = time.perf_counter()
+        k = self._flip
+        self._flip ^= 1
+        hs, ho = self._h_stages[k], self._h_outs[k]
+        self._pack_decode(batch, Bp, hs.numpy(), ahead=1 if chained else 0)
+        n_copy = self._off["bt"] + Bp * self.max_blocks
+        self.d_stage[:n_copy].copy_(hs[:n_copy], non_blocking=True)
+        if chained:
+            o = self._off["ids"]
+            self.d_stage[o:o + B].copy_(self.d_out[:B])
+        self._launch_decode(Bp, n_copy)
+        ho[:B].copy_(self.d_out[:B], non_blocking=True)
+        ev = None
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+        return (ev, ho, B, t0)
+
+    def collect(self, handle) -> List[int]:
+        ev, ho, B, t0 = handle
+        if ev is not None:
+            ev.synchronize()
+        now = time.perf_counter()
+        # wall time attributed to this step: from its launch (or the previous collect, if later)
+        self.stats["decode_ms"] += (now - max(t0, getattr(self, "_last_collect", t0))) * 1e3
+        self._last_collect = now
+        self.stats["decode_steps"] += 1
+        return ho[:B].tolist()
 
     def _launch_decode(self, Bp: int, n_copy: int) -> None:
         if self.tp_size > 1:

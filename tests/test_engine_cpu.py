@@ -227,6 +227,56 @@ def test_mixed_step_split_attention_matches(tiny_engine):
     assert outs[True] == outs[False] == alone
 
 
+def _run_thread(eng, prompts, params, forced, abort_idx=None):
+    import threading
+    done = {}
+    ev = threading.Event()
+
+    want = len(prompts) - (abort_idx is not None)   # an abort completes without a callback
+
+    def cb(seq):
+        done[seq.seq_id] = seq
+        if len(done) == want:
+            ev.set()
+
+    eng.start()
+    try:
+        seqs = [eng.submit(p, params, cb, forced_prefix=forced) for p in prompts]
+        if abort_idx is not None:
+            eng.abort(seqs[abort_idx])
+        assert ev.wait(60)
+        if abort_idx is not None:
+            import time
+            time.sleep(0.2)
+    finally:
+        eng.shutdown()
+    return seqs
+
+
+def test_overlapped_decode_matches_sync(tiny_engine):
+    """One decode step in flight while the host applies the previous one (engine._chain) gives the
+    same tokens as the synchronous loop, with EOS stops, length stops and an abort mid-flight."""
+    eng, be = tiny_engine
+    prompts = [be.prompt_ids(q) for q in ("list pods", "get svc -A", "top nodes", "describe pod web-1",
+                                          "logs api", "get deploy")]
+    outs = {}
+    for overlap in (False, True):
+        eng.overlap = overlap
+        eng.bm.reset_prefix_cache()
+        for ignore_eos in (True, False):
+            params = SamplingParams(max_new_tokens=7, ignore_eos=ignore_eos)
+            seqs = _run_thread(eng, prompts, params, be._forced)
+            outs[(overlap, ignore_eos)] = [s.output_ids for s in seqs]
+            assert all(s.finish_reason in ("stop", "length") for s in seqs)
+        seqs = _run_thread(eng, prompts, SamplingParams(max_new_tokens=7, ignore_eos=True), be._forced, abort_idx=2)
+        assert seqs[2].finish_reason == "abort"
+    eng.overlap = True
+    assert eng.chained_steps > 0
+    assert outs[(True, True)] == outs[(False, True)]
+    assert outs[(True, False)] == outs[(False, False)]
+    assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
+
+
 def test_api_with_engine_backend(tiny_engine):
     from fastapi.testclient import TestClient
     from ai_agent_kubectl_amd.api import create_app
