@@ -49,6 +49,7 @@ class LLMEngine:
         self.overlap = os.environ.get("KA_OVERLAP", "1") == "1"
         self._inflight = None
         self.chained_steps = 0
+        self.idle_s = 0.0          # time the loop slept with no work (waiting for requests)
 
     # ------------------------------------------------------------------------------------------
     def start(self) -> None:
@@ -119,10 +120,11 @@ class LLMEngine:
         """Append sampled tokens, publish prefix blocks, finish sequences (EOS / max_new_tokens)."""
         now = time.perf_counter()
         m = self.metrics
+        prefill = {id(s) for s in batch.prefill_seqs}
         for s, nq, tok in zip(batch.seqs, batch.num_query, tokens):
             if s.finished:
                 continue
-            was_prefill = s in batch.prefill_seqs
+            was_prefill = id(s) in prefill
             s.num_computed += nq
             s.output_ids.append(int(tok))
             if was_prefill:
@@ -255,8 +257,10 @@ class LLMEngine:
             for hook in self.step_end_hooks:
                 hook()
             if n == 0 and not self.scheduler.has_work():
+                t_idle = time.perf_counter()
                 self._wake.wait(timeout=0.05)
                 self._wake.clear()
+                self.idle_s += time.perf_counter() - t_idle
         if self._inflight is not None:   # stopping with a step in flight: finish it cleanly
             prev, handle = self._inflight
             self._inflight = None

@@ -24,7 +24,7 @@ class SamplingParams:
     safe_decode: bool = True      # SAFE_DECODE token mask (engine/safe_decode.py)
 
 
-@dataclass
+@dataclass(eq=False)   # identity semantics: `seq in list` / `remove` must not compare token lists
 class Sequence:
     prompt_ids: List[int]
     params: SamplingParams

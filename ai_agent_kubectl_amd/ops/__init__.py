@@ -39,7 +39,15 @@ def _p(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_cur_device = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def _stream() -> int:
+    """Current HIP stream handle (the capture stream inside hipGraph capture).  The raw C accessor
+    costs ~0.3 us; torch.cuda.current_stream() ~8 us, paid per kernel launch in eager steps."""
+    if _raw_stream is not None:
+        return _raw_stream(_cur_device())
     return torch.cuda.current_stream().cuda_stream
 
 

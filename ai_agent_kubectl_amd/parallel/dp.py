@@ -146,7 +146,7 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> 
                 _t.cuda.synchronize(device)
             resp_q.put(("ctl", rid, dict(eng.runner.stats, prefix_hits=eng.bm.hits, prefix_queries=eng.bm.queries,
                                          partial_tokens=getattr(eng.bm, "partial_tokens", 0),
-                                         chained_steps=eng.chained_steps,
+                                         chained_steps=eng.chained_steps, engine_idle_s=eng.idle_s,
                                          build_s=getattr(eng, "build_seconds", 0.0))))
             continue
         if op == "gen":

@@ -175,7 +175,8 @@ def main():
         else:
             torch.cuda.synchronize()
             st = dict(eng.runner.stats, prefix_hits=eng.bm.hits, prefix_queries=eng.bm.queries,
-                      partial_tokens=getattr(eng.bm, "partial_tokens", 0), chained_steps=eng.chained_steps)
+                      partial_tokens=getattr(eng.bm, "partial_tokens", 0), chained_steps=eng.chained_steps,
+                      engine_idle_s=eng.idle_s)
         if world > 1:
             dist.barrier()
         return st
@@ -188,7 +189,8 @@ def main():
         else:
             await loop.run_in_executor(None, torch.cuda.synchronize)
             st = dict(eng.runner.stats, prefix_hits=eng.bm.hits, prefix_queries=eng.bm.queries,
-                      partial_tokens=getattr(eng.bm, "partial_tokens", 0), chained_steps=eng.chained_steps)
+                      partial_tokens=getattr(eng.bm, "partial_tokens", 0), chained_steps=eng.chained_steps,
+                      engine_idle_s=eng.idle_s)
         if world > 1:
             await loop.run_in_executor(None, dist.barrier)
         return st
@@ -296,6 +298,7 @@ def main():
                        "prefix_cache_hit_rate": round(st.get("prefix_hits", 0) / max(1, st.get("prefix_queries", 0)), 3),
                        "sub_block_reused_tokens": st.get("partial_tokens", 0),
                        "overlapped_decode_steps": st.get("chained_steps", 0),
+                       "engine_idle_ms_per_step": round(st.get("engine_idle_s", 0.0) * 1e3 / args.steps, 2),
                        "build_s": round(t_build, 1), "engine_process": eng is None,
                        "sample_reply": sample[0] if sample else None,
                        "baseline": "BASELINE.md reference plumbing floor, cache-miss conc 32 = 354 req/s"},

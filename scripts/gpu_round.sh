@@ -9,7 +9,7 @@ STEP="${1:-all}"
 run_tests() { timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; }
 run_smoke() { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; }
 run_bench() { timeout -k 10 600 python bench.py --steps ${BENCH_STEPS:-5} --warmup ${BENCH_WARMUP:-2} ${BENCH_ARGS} > gpurun_out/bench.log 2>&1; }
-run_prof() { rm -rf /tmp/ka_prof && cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/ka_prof -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 ${BENCH_ARGS} > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1; rc=$?; cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/prof && find /tmp/ka_prof -name "*stats.csv" -exec cp {} gpurun_out/prof/ \; ; return $rc; }
+run_prof() { rm -rf /tmp/ka_prof && cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/ka_prof -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 ${BENCH_ARGS} > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1; rc=$?; cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/prof && find /tmp/ka_prof -name "*stats.csv" -exec cp {} gpurun_out/prof/ \; ; python scripts/trace_busy.py /tmp/ka_prof --window ${TRACE_WINDOW:-2.0} > gpurun_out/trace_busy.txt 2>&1; return $rc; }
 run_cprof() { KA_PROFILE_ENGINE=gpurun_out/cprof_engine.txt KA_PROFILE_API=gpurun_out/cprof_api.txt timeout -k 10 600 python bench.py --steps 3 --warmup 1 ${BENCH_ARGS} > gpurun_out/bench_cprof.log 2>&1; }
 run_gemm() { timeout -k 10 600 python scripts/bench_gemm.py > gpurun_out/bench_gemm.log 2>&1; }
 run_ktest() { timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -x -q -p no:cacheprovider > gpurun_out/pytest_kernels.log 2>&1; }
