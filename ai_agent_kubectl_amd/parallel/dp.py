@@ -17,6 +17,7 @@ import dataclasses
 import itertools
 import logging
 import multiprocessing as mp
+import sys
 import threading
 import time
 from typing import Dict, List, Optional
@@ -26,6 +27,20 @@ from ..llm.base import LLMBackend, LLMUnavailableError
 FLUSH_EVERY = 16   # requests per engine-bound IPC message within one event-loop tick
 
 logger = logging.getLogger("app.dp")
+
+
+class _PipeSender:
+    """Request channel API process -> replica.  `put` pickles and writes on the calling thread
+    (mp.Queue hands both to a feeder thread, which waits for the GIL while the event loop turns a
+    burst of replies into new requests: measured as ~15 ms of engine idle per wave)."""
+
+    def __init__(self, conn):
+        self.conn = conn
+        self.lock = threading.Lock()
+
+    def put(self, obj) -> None:
+        with self.lock:
+            self.conn.send(obj)
 
 
 class _Obs:
@@ -124,9 +139,14 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> 
 
     eng.step_end_hooks.append(flush)
 
+    recv = req_q.recv if hasattr(req_q, "recv") else req_q.get
+
     def requests():
         while True:
-            msg = req_q.get()
+            try:
+                msg = recv()
+            except EOFError:   # the API process went away
+                msg = None
             if msg is None:
                 yield None
                 return
@@ -193,10 +213,13 @@ class DPRouterLLM(LLMBackend):
         sd.update(TP=1, DP=1)
         self.replicas: List[_Replica] = []
         for i, dev in enumerate(self.devices):
-            rq = ctx.Queue()
-            p = ctx.Process(target=_replica_main, args=(i, dev, sd, rq, self.resp_q), daemon=True)
+            r_end, w_end = ctx.Pipe(duplex=False)
+            p = ctx.Process(target=_replica_main, args=(i, dev, sd, r_end, self.resp_q), daemon=True)
             p.start()
-            self.replicas.append(_Replica(i, p, rq))
+            r_end.close()
+            self.replicas.append(_Replica(i, p, _PipeSender(w_end)))
+        # the reply-reader thread must get the GIL promptly while the event loop is busy
+        sys.setswitchinterval(min(sys.getswitchinterval(), 0.001))
         self._pending: Dict[int, tuple] = {}
         self._ids = itertools.count()
         self._lock = threading.Lock()
@@ -270,12 +293,15 @@ class DPRouterLLM(LLMBackend):
             if r.up and not r.proc.is_alive():
                 logger.error("DP replica %d died (exit %s)", r.idx, r.proc.exitcode)
                 r.up = False
-                with self._lock:
-                    dead = [(k, v) for k, v in self._pending.items() if v[2] is r]
-                    for k, _ in dead:
-                        self._pending.pop(k)
-                for _, (loop, fut, _) in dead:
-                    loop.call_soon_threadsafe(_set_exc, fut, LLMUnavailableError(f"replica {r.idx} died"))
+                self._fail_replica(r)
+
+    def _fail_replica(self, r) -> None:
+        with self._lock:
+            dead = [(k, v) for k, v in self._pending.items() if v[2] is r]
+            for k, _ in dead:
+                self._pending.pop(k)
+        for _, (loop, fut, _) in dead:
+            loop.call_soon_threadsafe(_set_exc, fut, LLMUnavailableError(f"replica {r.idx} died"))
 
     def wait_ready(self, timeout: Optional[float] = None) -> bool:
         return self._ready.wait(timeout if timeout is not None else self._start_timeout)
@@ -314,12 +340,16 @@ class DPRouterLLM(LLMBackend):
             rep.flush_scheduled = True
             loop.call_soon(self._flush, rep)
 
-    @staticmethod
-    def _flush(rep) -> None:
+    def _flush(self, rep) -> None:
         rep.flush_scheduled = False
         if rep.outbox:
             batch, rep.outbox = rep.outbox, []
-            rep.req_q.put(("batch", 0, batch) if len(batch) > 1 else batch[0])
+            try:
+                rep.req_q.put(("batch", 0, batch) if len(batch) > 1 else batch[0])
+            except (OSError, ValueError) as e:   # replica died: fail what was just routed to it
+                logger.error("DP replica %d unreachable: %s", rep.idx, e)
+                rep.up = False
+                self._fail_replica(rep)
 
     async def control(self, op: str = "sync") -> List[dict]:
         """Send a control op to every live replica and gather the replies (sync = device barrier
