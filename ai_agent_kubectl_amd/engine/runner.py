@@ -42,6 +42,8 @@ class ModelRunner:
         self.comm = comm or LocalComm()
         # mixed steps: decode rows through the decode kernel (KA_SPLIT_MIXED_ATTN=0: all varlen)
         self.split_mixed_attention = os.environ.get("KA_SPLIT_MIXED_ATTN", "1") == "1"
+        self.prefill_pad = int(os.environ.get("KA_PREFILL_PAD", "256"))
+        self.prefill_pad_min = int(os.environ.get("KA_PREFILL_PAD_MIN", "1024"))
         self.tp_rank, self.tp_size = tp_rank, tp_size
         self.model = LlamaModel(cfg, weights, self.comm, tp_rank, tp_size, ep_rank, ep_size)
         self.block_size = block_size
@@ -218,9 +220,16 @@ class ModelRunner:
         else:
             self._decode_forward(Bp)
 
-    def _pack_prefill(self, batch: Batch) -> np.ndarray:
+    def padded_tokens(self, T: int) -> int:
+        """Prefill steps of >= 1024 tokens run padded to a multiple of KA_PREFILL_PAD (256): hipBLASLt
+        is up to ~10% faster per token on whole 256-row tiles (scripts/bench_prefill_gemm.py: M=4000
+        1.31 PFLOP/s vs M=4096 1.45).  Padding rows write no KV (slot -1) and are never sampled."""
+        q = self.prefill_pad
+        return T if q <= 1 or T < self.prefill_pad_min else (T + q - 1) // q * q
+
+    def _pack_prefill(self, batch: Batch, pad: bool = False) -> np.ndarray:
         S = len(batch.seqs)
-        T = batch.num_tokens
+        T = self.padded_tokens(batch.num_tokens) if pad else batch.num_tokens
         mb = self.max_blocks
         nc = len(batch.copies)
         buf = np.zeros(3 * T + (S + 1) + 3 * S + S * mb + 2 * nc, dtype=np.int32)
@@ -229,6 +238,7 @@ class ModelRunner:
             buf[len(buf) - 2 * nc:len(buf) - nc] = cp[:, 0]
             buf[len(buf) - nc:] = cp[:, 1]
         ids, pos, slots = buf[:T], buf[T:2 * T], buf[2 * T:3 * T]
+        slots[batch.num_tokens:] = -1          # padding rows (if any): no cache write
         o = 3 * T
         q_starts = buf[o:o + S + 1]; o += S + 1
         ctx = buf[o:o + S]; o += S
@@ -253,7 +263,8 @@ class ModelRunner:
         q_starts[S] = t
         return buf
 
-    def _run_prefill(self, buf: torch.Tensor, T: int, S: int, max_q: int, nc: int = 0, nd: int = 0) -> torch.Tensor:
+    def _run_prefill(self, buf: torch.Tensor, T: int, S: int, max_q: int, nc: int = 0, nd: int = 0,
+                     t_real: int = 0) -> torch.Tensor:
         mb = self.max_blocks
         if nc:
             n = buf.shape[0]
@@ -266,16 +277,17 @@ class ModelRunner:
         lidx = buf[o:o + S].long(); o += S
         bt = buf[o:o + S * mb].view(S, mb)
         meta = AttnMeta(positions=pos, slot_mapping=slots, block_tables=bt, ctx_lens=ctx, logits_indices=lidx,
-                        is_decode=False, q_starts=q_starts, max_q_len=max_q, num_decode=nd)
+                        is_decode=False, q_starts=q_starts, max_q_len=max_q, num_decode=nd,
+                        num_tokens=t_real or T)
         h = self.model.forward(ids, meta, self.k_cache, self.v_cache)
         return self.model.sample(h, self.mask_bits, mask if self.mask_bits is not None else None)
 
     # ------------------------------------------------------------------------------------------
     def _bcast_header(self, kind: int, a: int = 0, b: int = 0, c: int = 0, d: int = 0, e: int = 0,
-                      f: int = 0) -> None:
+                      f: int = 0, g: int = 0) -> None:
         if self.tp_size == 1:
             return
-        self.d_hdr.copy_(torch.tensor([kind, a, b, c, d, e, f, 0], dtype=torch.int32))
+        self.d_hdr.copy_(torch.tensor([kind, a, b, c, d, e, f, g], dtype=torch.int32))
         self.comm.broadcast(self.d_hdr, src=0)
 
     @torch.inference_mode()
@@ -302,14 +314,14 @@ class ModelRunner:
             self.stats["decode_steps"] += 1
             self.stats["decode_ms"] += (time.perf_counter() - t0) * 1e3
             return out
-        host = self._pack_prefill(batch)
-        T, S, max_q, nc = batch.num_tokens, B, max(batch.num_query), len(batch.copies)
+        host = self._pack_prefill(batch, pad=True)
+        T, S, max_q, nc = self.padded_tokens(batch.num_tokens), B, max(batch.num_query), len(batch.copies)
         nd = B - len(batch.prefill_seqs) if self.split_mixed_attention else 0
-        self._bcast_header(KIND_PREFILL, T, S, max_q, host.shape[0], nc, nd)
+        self._bcast_header(KIND_PREFILL, T, S, max_q, host.shape[0], nc, nd, batch.num_tokens)
         buf = torch.from_numpy(host).to(self.device, non_blocking=False)
         if self.tp_size > 1:
             self.comm.broadcast(buf, src=0)
-        tok = self._run_prefill(buf, T, S, max_q, nc, nd)
+        tok = self._run_prefill(buf, T, S, max_q, nc, nd, batch.num_tokens)
         out = tok.cpu().tolist()
         self.stats["prefill_steps"] += 1
         self.stats["prefill_tokens"] += T
@@ -321,7 +333,7 @@ class ModelRunner:
         """Non-driver TP ranks: mirror every step of rank 0 until it broadcasts STOP."""
         while True:
             self.comm.broadcast(self.d_hdr, src=0)
-            kind, a, b, c, d, e, f = self.d_hdr[:7].tolist()
+            kind, a, b, c, d, e, f, g = self.d_hdr[:8].tolist()
             if kind == KIND_STOP:
                 return
             if kind == KIND_DECODE:
@@ -329,7 +341,7 @@ class ModelRunner:
             elif kind == KIND_PREFILL:
                 buf = torch.empty(d, dtype=torch.int32, device=self.device)
                 self.comm.broadcast(buf, src=0)
-                self._run_prefill(buf, a, b, c, e, f)
+                self._run_prefill(buf, a, b, c, e, f, g)
 
     def stop_workers(self) -> None:
         self._bcast_header(KIND_STOP)

@@ -37,6 +37,7 @@ class AttnMeta:
     q_starts: Optional[torch.Tensor] = None   # [S+1] (prefill)
     max_q_len: int = 1
     num_decode: int = 0                # mixed step: the first num_decode sequences are 1-token decode rows
+    num_tokens: int = 0                # real tokens when the step is padded (rows beyond are padding)
 
 
 class LlamaModel:
@@ -94,6 +95,8 @@ class LlamaModel:
             else:
                 a = ops.attention_prefill(q, k_cache[li], v_cache[li], meta.block_tables, meta.q_starts,
                                           meta.ctx_lens, meta.max_q_len, self.scale)
+            if 0 < meta.num_tokens < T and not meta.is_decode:
+                a[meta.num_tokens:].zero_()   # padding rows: no sequence's attention writes them
             # TP = 1: the projections feeding a norm leave their split-K partials to the fused
             # reduce + residual + RMSNorm kernel (ops.SplitK); with TP the all-reduce needs bf16
             fuse = self._local_comm

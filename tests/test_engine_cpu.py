@@ -253,6 +253,22 @@ def _run_thread(eng, prompts, params, forced, abort_idx=None):
     return seqs
 
 
+def test_padded_prefill_matches_unpadded(tiny_engine):
+    """Prefill steps padded to a tile multiple (slot -1 rows, zeroed attention) sample the same tokens."""
+    eng, be = tiny_engine
+    params = SamplingParams(max_new_tokens=5, ignore_eos=True)
+    prompts = [be.prompt_ids(q) for q in ("list pods", "get svc -A", "top nodes")]
+    r = eng.runner
+    outs = []
+    for pad, pmin in ((0, 1 << 30), (64, 1)):
+        r.prefill_pad, r.prefill_pad_min = pad, pmin
+        eng.bm.reset_prefix_cache()
+        outs.append([s.output_ids for s in eng.generate_blocking(prompts, params, forced_prefix=be._forced)])
+    r.prefill_pad, r.prefill_pad_min = 256, 1024
+    assert r.padded_tokens(1000) == 1000 and r.padded_tokens(1030) == 1280
+    assert outs[0] == outs[1]
+
+
 def test_overlapped_decode_matches_sync(tiny_engine):
     """One decode step in flight while the host applies the previous one (engine._chain) gives the
     same tokens as the synchronous loop, with EOS stops, length stops and an abort mid-flight."""
