@@ -20,7 +20,7 @@ from ..models.weights import ParallelInfo, build_weights
 from .engine import LLMEngine
 from .runner import ModelRunner
 from .safe_decode import build_masks
-from .tokenizer import get_tokenizer
+from .tokenizer import get_tokenizer, tokenizer_path
 
 logger = logging.getLogger("app.engine")
 
@@ -60,7 +60,7 @@ class EngineOptions:
 def build_engine(opts: EngineOptions, comm=None, metrics=None) -> LLMEngine:
     t0 = time.perf_counter()
     cfg = get_config(opts.model)
-    tok = get_tokenizer(cfg.vocab_size, cfg.tokenizer)
+    tok = get_tokenizer(cfg.vocab_size, cfg.tokenizer, tokenizer_path(opts.weights))
     dev = torch.device(opts.device)
     if dev.type == "cuda":
         from ..ops._hip import require

@@ -19,6 +19,7 @@ built).  `encode_chat` implements each family's chat template with one user turn
 from __future__ import annotations
 
 import functools
+import os
 import random
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -202,6 +203,121 @@ class SyntheticTokenizer:
         return before + self.encode(prompt) + after
 
 
+def _byte_decoder() -> Dict[str, int]:
+    """Inverse of the GPT-2 / tiktoken byte-level BPE alphabet (printable stand-ins for bytes)."""
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("\xa1"), ord("\xac") + 1)) + \
+        list(range(ord("\xae"), ord("\xff") + 1))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return {chr(c): b for b, c in zip(bs, cs)}
+
+
+class HFTokenizer:
+    """A real checkpoint's `tokenizer.json` (HF `tokenizers`) behind the engine's tokenizer interface.
+
+    Llama-3 is byte-level BPE (token strings use the GPT-2 byte alphabet); Llama-2 / Mixtral are
+    SentencePiece BPE (`▁` = space, `<0xNN>` byte fallback).  `id_to_bytes` gives the exact bytes of
+    every regular token (the SAFE_DECODE masks are built from it); added tokens are specials."""
+
+    def __init__(self, path: str, vocab_size: int, family: str):
+        from tokenizers import Tokenizer
+        if os.path.isdir(path):
+            path = os.path.join(path, "tokenizer.json")
+        self.tk = Tokenizer.from_file(path)
+        self.vocab_size = vocab_size
+        self.family = family
+        added = {t.content: i for i, t in self.tk.get_added_tokens_decoder().items()} \
+            if hasattr(self.tk, "get_added_tokens_decoder") else {}
+        self.specials: Dict[str, int] = dict(added)
+        self.id_to_special = {v: k for k, v in self.specials.items()}
+        vocab = self.tk.get_vocab(with_added_tokens=False)
+        byte_level = any(ch in tok for tok in list(vocab)[:2000] for ch in ("\u0120", "\u010a"))
+        dec = _byte_decoder()
+        self.id_to_bytes: List[Optional[bytes]] = [None] * vocab_size
+        for tok, i in vocab.items():
+            if i >= vocab_size or i in self.id_to_special:
+                continue
+            if byte_level:
+                try:
+                    self.id_to_bytes[i] = bytes(dec[c] for c in tok)
+                except KeyError:
+                    self.id_to_bytes[i] = tok.encode("utf-8")
+            elif len(tok) == 6 and tok.startswith("<0x") and tok.endswith(">"):
+                self.id_to_bytes[i] = bytes([int(tok[3:5], 16)])
+            else:
+                self.id_to_bytes[i] = tok.replace("\u2581", " ").encode("utf-8")
+        sp = self.specials
+        if family == "llama3":
+            self.bos_id = sp.get("<|begin_of_text|>", 128000)
+            self.eos_ids = tuple(sp[n] for n in ("<|eot_id|>", "<|end_of_text|>") if n in sp) or (128009,)
+        else:
+            self.bos_id = sp.get("<s>", 1)
+            self.eos_ids = (sp.get("</s>", 2),)
+        self.eos_id = self.eos_ids[0]
+
+    def encode(self, text: str) -> List[int]:
+        return self.tk.encode(text, add_special_tokens=False).ids
+
+    def token_bytes(self, tid: int) -> bytes:
+        p = self.id_to_bytes[tid] if 0 <= tid < self.vocab_size else None
+        return p if p is not None else b""
+
+    def token_text(self, tid: int) -> str:
+        if tid in self.id_to_special:
+            return self.id_to_special[tid]
+        return self.token_bytes(tid).decode("utf-8", errors="replace")
+
+    def decode(self, ids: Sequence[int], skip_special: bool = True) -> str:
+        buf = bytearray()
+        for t in ids:
+            p = self.id_to_bytes[t] if 0 <= t < self.vocab_size else None
+            if p is None:
+                if not skip_special and t in self.id_to_special:
+                    buf += self.id_to_special[t].encode()
+                continue
+            buf += p
+        return buf.decode("utf-8", errors="replace")
+
+    def is_eos(self, tid: int) -> bool:
+        return tid in self.eos_ids
+
+    def chat_prefix_suffix(self) -> Tuple[List[int], List[int]]:
+        if self.family == "llama3":
+            s = self.specials
+            before = [s["<|begin_of_text|>"], s["<|start_header_id|>"]] + self.encode("user") + \
+                [s["<|end_header_id|>"]] + self.encode("\n\n")
+            after = [s["<|eot_id|>"], s["<|start_header_id|>"]] + self.encode("assistant") + \
+                [s["<|end_header_id|>"]] + self.encode("\n\n")
+        else:
+            before = [self.bos_id] + self.encode("[INST] ")
+            after = self.encode(" [/INST]")
+        return before, after
+
+    def encode_chat(self, prompt: str) -> List[int]:
+        before, after = self.chat_prefix_suffix()
+        return before + self.encode(prompt) + after
+
+
+def tokenizer_path(weights: Optional[str]) -> Optional[str]:
+    """TOKENIZER env, else <WEIGHTS dir>/tokenizer.json when the weights are a local checkpoint."""
+    p = os.environ.get("TOKENIZER")
+    if p:
+        return p
+    if weights and not weights.startswith("random") and os.path.isdir(weights):
+        f = os.path.join(weights, "tokenizer.json")
+        if os.path.exists(f):
+            return f
+    return None
+
+
 @functools.lru_cache(maxsize=4)
-def get_tokenizer(vocab_size: int, family: str) -> SyntheticTokenizer:
+def get_tokenizer(vocab_size: int, family: str, path: Optional[str] = None):
+    """The checkpoint's real tokenizer when `path` is given, else the synthetic one (random weights)."""
+    if path:
+        return HFTokenizer(path, vocab_size, family)
     return SyntheticTokenizer(vocab_size=vocab_size, family=family)

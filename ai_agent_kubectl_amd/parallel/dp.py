@@ -196,12 +196,12 @@ class DPRouterLLM(LLMBackend):
     name = "engine-dp"
 
     def __init__(self, settings, dp: int, devices: Optional[List[str]] = None, start_timeout: float = 900):
-        from ..engine.tokenizer import get_tokenizer
+        from ..engine.tokenizer import get_tokenizer, tokenizer_path
         from ..models.config import get_config
         from ..prompt import PROMPT_PREFIX
 
         cfg = get_config(settings.MODEL)
-        self.tok = get_tokenizer(cfg.vocab_size, cfg.tokenizer)
+        self.tok = get_tokenizer(cfg.vocab_size, cfg.tokenizer, tokenizer_path(settings.WEIGHTS))
         before, after = self.tok.chat_prefix_suffix()
         self._prefix = before + self.tok.encode(PROMPT_PREFIX)
         self._after = after
