@@ -35,6 +35,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16_t* __restrict__ out, b
       if (P != nullptr) {
         const float* pr = P + (size_t)row * hidden + idx * 8;
         f32x4 s0 = *reinterpret_cast<const f32x4*>(pr), s1 = *reinterpret_cast<const f32x4*>(pr + 4);
+#pragma unroll 4
         for (int k = 1; k < split; ++k) {
           s0 += *reinterpret_cast<const f32x4*>(pr + k * pstride);
           s1 += *reinterpret_cast<const f32x4*>(pr + k * pstride + 4);
@@ -109,6 +110,9 @@ extern "C" int ka_rmsnorm(void* out, void* residual, const void* x, const void* 
   if (nvec <= 256)
     hipLaunchKernelGGL((rmsnorm_kernel<256, 1>), dim3(rows), dim3(256), 0, stream, o, r, xi, wi, hidden, eps, P,
                        split, pstride);
+  else if (nvec <= 512 && rows <= 1024)   // decode-sized: one 16-B vector per thread, 8 waves per row
+    hipLaunchKernelGGL((rmsnorm_kernel<512, 1>), dim3(rows), dim3(512), 0, stream, o, r, xi, wi, hidden, eps, P,
+                       split, pstride);
   else if (nvec <= 512)
     hipLaunchKernelGGL((rmsnorm_kernel<256, 2>), dim3(rows), dim3(256), 0, stream, o, r, xi, wi, hidden, eps, P,
                        split, pstride);
@@ -131,6 +135,9 @@ extern "C" int ka_rmsnorm_splitk(void* out, void* residual, const void* P, int s
   const size_t ps = (size_t)rows * hidden;
   if (nvec <= 256)
     hipLaunchKernelGGL((rmsnorm_kernel<256, 1>), dim3(rows), dim3(256), 0, stream, o, r, nullptr, wi, hidden, eps,
+                       p, split, ps);
+  else if (nvec <= 512)   // the split slabs are read once: 8 waves per row keep more loads in flight
+    hipLaunchKernelGGL((rmsnorm_kernel<512, 1>), dim3(rows), dim3(512), 0, stream, o, r, nullptr, wi, hidden, eps,
                        p, split, ps);
   else if (nvec <= 512)
     hipLaunchKernelGGL((rmsnorm_kernel<256, 2>), dim3(rows), dim3(256), 0, stream, o, r, nullptr, wi, hidden, eps,
