@@ -27,7 +27,7 @@
 #define KBS 16
 
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
+__global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
                                                            const bf16_t* __restrict__ k_cache,
                                                            const bf16_t* __restrict__ v_cache,
                                                            const int* __restrict__ block_tables, int max_blocks,
@@ -165,12 +165,147 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(bf16_t* __restrict__ 
   }
 }
 
+
+// Decode variant: one WAVE per (sequence, kv head), 4 independent pairs per workgroup.  The wave
+// walks all of its context's 32-token chunks (next chunk's K/V prefetched into registers) with the
+// same online softmax: no cross-wave merge, no workgroup barrier.  Measured slightly slower than
+// the split kernel at B = 256, ctx 120-1024 (26.0 vs 23.1 us at ctx 120), so it is opt-in
+// (KA_DECODE_WAVE_MIN = minimum B * Hkv).
+__global__ __launch_bounds__(256) void paged_decode_wave_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
+                                                                const bf16_t* __restrict__ k_cache,
+                                                                const bf16_t* __restrict__ v_cache,
+                                                                const int* __restrict__ block_tables, int max_blocks,
+                                                                const int* __restrict__ ctx_lens, int batch, int hq,
+                                                                int hkv, float scale_log2) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int pair = blockIdx.x * 4 + wave;
+  if (pair >= batch * hkv) return;            // whole wave exits; no block-level sync below
+  const int b = pair / hkv, h = pair % hkv;
+  const int G = hq / hkv;
+  const int col = lane & 15, grp = lane >> 4;
+  const int ctx = ctx_lens[b];
+  __shared__ __attribute__((aligned(16))) bf16_t p_lds[4][16 * 32];
+  bf16_t* pw = p_lds[wave];
+
+  bf16x8 qf[4];
+  if (col < G) {
+    const bf16_t* qp = q + ((size_t)b * hq + h * G + col) * HD + 8 * grp;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(*reinterpret_cast<const uint4*>(qp + 32 * ks));
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(make_uint4(0, 0, 0, 0));
+  }
+  float m[4], l[4];
+  f32x4 o[8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m[r] = -INFINITY;
+    l[r] = 0.f;
+  }
+#pragma unroll
+  for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int* bt = block_tables + (size_t)b * max_blocks;
+  const int nchunks = (ctx + 31) >> 5;
+  const size_t head_stride = (size_t)KBS * HD;
+  // register double buffer: chunk c+1's K and V fragments are loaded before chunk c is computed
+  uint4 kr[2][4], vr[8];
+  auto load_k = [&](int c, uint4 (&kk)[2][4]) {
+    const int t0 = c * 32;
+    const int blk0 = bt[2 * c];
+    const int blk1 = (t0 + 16 < ctx) ? bt[2 * c + 1] : blk0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bf16_t* kp = k_cache + ((size_t)(j ? blk1 : blk0) * hkv + h) * head_stride + col * HD + 8 * grp;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) kk[j][ks] = *reinterpret_cast<const uint4*>(kp + 32 * ks);
+    }
+  };
+  auto load_v = [&](int c, uint4 (&vv)[8]) {
+    const int t0 = c * 32;
+    const int blk = (grp >> 1) ? ((t0 + 16 < ctx) ? bt[2 * c + 1] : bt[2 * c]) : bt[2 * c];
+    const bf16_t* vp = v_cache + ((size_t)blk * hkv + h) * head_stride + col * KBS + 8 * (grp & 1);
+#pragma unroll
+    for (int n = 0; n < 8; ++n) vv[n] = *reinterpret_cast<const uint4*>(vp + (size_t)n * 16 * KBS);
+  };
+  if (nchunks > 0) {
+    load_k(0, kr);
+    load_v(0, vr);
+  }
+  for (int c = 0; c < nchunks; ++c) {
+    const int t0 = c * 32;
+    f32x4 s[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) acc = mfma16x16x32(qf[ks], as_bf16x8(kr[j][ks]), acc);
+      s[j] = acc;
+    }
+    uint4 vc[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) vc[n] = vr[n];
+    if (c + 1 < nchunks) {   // wave-uniform: issue the next chunk's loads under this chunk's math
+      load_k(c + 1, kr);
+      load_v(c + 1, vr);
+    }
+    float alpha[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x0 = (t0 + col < ctx) ? s[0][r] * scale_log2 : -INFINITY;
+      float x1 = (t0 + 16 + col < ctx) ? s[1][r] * scale_log2 : -INFINITY;
+      const float mx = row16_max(fmaxf(x0, x1));
+      const float mn = fmaxf(m[r], mx);
+      alpha[r] = exp2f(m[r] - mn);
+      const float p0 = exp2f(x0 - mn), p1 = exp2f(x1 - mn);
+      l[r] = l[r] * alpha[r] + row16_sum(p0 + p1);
+      m[r] = mn;
+      const int prow = 4 * grp + r;
+      const int sw = (prow >> 2) & 3;
+      pw[prow * 32 + ((((col >> 3)) ^ sw) << 3) + (col & 7)] = f2bf(p0);
+      pw[prow * 32 + ((((16 + col) >> 3) ^ sw) << 3) + (col & 7)] = f2bf(p1);
+    }
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[n][r] *= alpha[r];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bf16x8 pf = as_bf16x8(*reinterpret_cast<const uint4*>(pw + col * 32 + ((grp ^ ((col >> 2) & 3)) << 3)));
+#pragma unroll
+    for (int n = 0; n < 8; ++n) o[n] = mfma16x16x32(pf, as_bf16x8(vc[n]), o[n]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  // o[n][r] = row 4*grp + r, dim n*16 + col; rows >= G are padding
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 4 * grp + r;
+    if (row < G) {
+      const float inv = l[r] > 0.f ? 1.f / l[r] : 0.f;
+      bf16_t* op = out + ((size_t)b * hq + h * G + row) * HD + col;
+#pragma unroll
+      for (int n = 0; n < 8; ++n) op[n * 16] = f2bf(o[n][r] * inv);
+    }
+  }
+}
+
 extern "C" int ka_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache,
                                const int* block_tables, int max_blocks, const int* ctx_lens, int batch, int hq,
                                int hkv, int head_dim, int block_size, float scale, hipStream_t stream) {
   if (batch <= 0) return 0;
   if (head_dim != HD || block_size != KBS || hq % hkv != 0 || hq / hkv > 16) return (int)hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
+  // the wave kernel measured slower than the split kernel at serving context lengths
+  // (scripts/bench_decode_attn.py): opt-in only
+  static const int wave_min = getenv("KA_DECODE_WAVE_MIN") ? atoi(getenv("KA_DECODE_WAVE_MIN")) : (1 << 30);
+  if (batch * hkv >= wave_min) {
+    hipLaunchKernelGGL(paged_decode_wave_kernel, dim3((batch * hkv + 3) / 4), dim3(256), 0, stream,
+                       static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
+                       static_cast<const bf16_t*>(v_cache), block_tables, max_blocks, ctx_lens, batch, hq, hkv,
+                       scale_log2);
+    KA_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(paged_decode_kernel, dim3(hkv, batch), dim3(256), 0, stream, static_cast<bf16_t*>(out),
                      static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
                      static_cast<const bf16_t*>(v_cache), block_tables, max_blocks, ctx_lens, hq, hkv, scale_log2);

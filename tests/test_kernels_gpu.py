@@ -90,6 +90,26 @@ def test_paged_decode(hq, hkv, ctx_lens):
     close(ops.attention_decode(q, kc, vc, bt, ctx, scale), ref.attention_decode(q, kc, vc, bt, ctx, scale), atol=2e-2)
 
 
+def test_paged_decode_wave_kernel_large_batch():
+    """B * Hkv >= 512 selects the wave-per-(sequence, kv head) kernel: mixed lengths, padding rows
+    (ctx 0 -> zeros) and a long context walked by a single wave."""
+    import random
+    rng = random.Random(0)
+    S, hq, hkv = 80, 32, 8
+    ctx_lens = [rng.randint(1, 300) for _ in range(S)]
+    ctx_lens[5] = 0
+    ctx_lens[7] = 1000
+    nb = 2000
+    kc, vc = _cache(nb, hkv)
+    bt = _tables(S, ctx_lens, nb, 64)
+    q = torch.randn(S, hq, 128, device=DEV, dtype=BF)
+    ctx = torch.tensor(ctx_lens, dtype=torch.int32, device=DEV)
+    got = ops.attention_decode(q, kc, vc, bt, ctx, 128 ** -0.5)
+    want = ref.attention_decode(q, kc, vc, bt, ctx, 128 ** -0.5)
+    close(got, want, atol=2e-2)
+    assert got[5].abs().max().item() == 0
+
+
 def test_paged_decode_padding_rows_zero():
     kc, vc = _cache(8, 8)
     bt = torch.zeros(2, 4, dtype=torch.int32, device=DEV)
