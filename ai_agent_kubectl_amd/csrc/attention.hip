@@ -359,7 +359,7 @@ __device__ __forceinline__ void prefill_store_tile(PrefillSmem& s, const u32x4 (
   }
 }
 
-__global__ __launch_bounds__(256) void paged_prefill_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
+__global__ __launch_bounds__(256, 3) void paged_prefill_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
                                                             const bf16_t* __restrict__ k_cache,
                                                             const bf16_t* __restrict__ v_cache,
                                                             const int* __restrict__ block_tables, int max_blocks,
