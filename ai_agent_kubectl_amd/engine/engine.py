@@ -35,7 +35,9 @@ class LLMEngine:
         self.tokenizer = tokenizer
         self.bm = make_block_manager(runner.num_blocks, runner.block_size, enable_prefix_caching=prefix_caching)
         self.scheduler = Scheduler(self.bm, max_batch=max_batch, max_batched_tokens=max_batched_tokens,
-                                   max_model_len=max_model_len)
+                                   max_model_len=max_model_len,
+                                   gather_max_s=float(os.environ.get("KA_GATHER_MAX_MS", "5")) / 1000.0,
+                                   gather_quiet_s=float(os.environ.get("KA_GATHER_QUIET_MS", "1.5")) / 1000.0)
         self.metrics = metrics
         self._inbox: "queue.SimpleQueue" = queue.SimpleQueue()
         self._wake = threading.Event()
@@ -261,6 +263,11 @@ class LLMEngine:
                 self._wake.wait(timeout=0.05)
                 self._wake.clear()
                 self.idle_s += time.perf_counter() - t_idle
+            elif n == 0 and self.scheduler.gathering():   # let the arriving burst in (no busy spin)
+                t_idle = time.perf_counter()
+                self._wake.wait(timeout=self.scheduler.gather_quiet_s)
+                self._wake.clear()
+                self.idle_s += time.perf_counter() - t_idle
         if self._inflight is not None:   # stopping with a step in flight: finish it cleanly
             prev, handle = self._inflight
             self._inflight = None
@@ -277,11 +284,15 @@ class LLMEngine:
                 for p in prompt_ids_list]
         for s in seqs:
             self.scheduler.add(s)
-        while any(not s.finished for s in seqs):
-            batch = self.scheduler.schedule()
-            if not batch.seqs:
-                raise RuntimeError("scheduler produced an empty batch (out of KV blocks?)")
-            tokens = self.runner.execute(batch)
-            self._apply(batch, tokens)
-            self.scheduler.on_step_done(batch)
+        gather, self.scheduler.gather_max_s = self.scheduler.gather_max_s, 0.0   # everything is here
+        try:
+            while any(not s.finished for s in seqs):
+                batch = self.scheduler.schedule()
+                if not batch.seqs:
+                    raise RuntimeError("scheduler produced an empty batch (out of KV blocks?)")
+                tokens = self.runner.execute(batch)
+                self._apply(batch, tokens)
+                self.scheduler.on_step_done(batch)
+        finally:
+            self.scheduler.gather_max_s = gather
         return seqs

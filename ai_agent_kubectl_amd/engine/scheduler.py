@@ -40,7 +40,7 @@ class Scheduler:
     def __init__(self, block_manager: BlockManager, max_batch: int = 256, max_batched_tokens: int = 8192,
                  max_model_len: int = 4096, mix_decode_into_prefill: bool = True,
                  prefill_max_wait_s: Optional[float] = None, prefill_min_frac: Optional[float] = None,
-                 partial_block_reuse: bool = True):
+                 partial_block_reuse: bool = True, gather_max_s: float = 0.0, gather_quiet_s: float = 0.0015):
         # Prefill batching under continuous arrivals: a prefill step is an eager (non-graph) step,
         # so while sequences are decoding, new arrivals are admitted together — when at least
         # max(4, prefill_min_frac * running) are waiting or the oldest has waited
@@ -51,6 +51,12 @@ class Scheduler:
             prefill_min_frac = float(os.environ.get("KA_PREFILL_MIN_FRAC", "0.25"))
         self.prefill_max_wait_s = prefill_max_wait_s
         self.prefill_min_frac = prefill_min_frac
+        # idle engine + a burst still arriving (the replies of a finished wave turn into new
+        # requests over a few ms): gather while the newest arrival is younger than gather_quiet_s,
+        # for at most gather_max_s, so the burst is prefilled as one large step instead of a
+        # small, GEMM-inefficient first step followed by the rest
+        self.gather_max_s = gather_max_s
+        self.gather_quiet_s = gather_quiet_s
         self.bm = block_manager
         self.max_batch = max_batch
         self.max_batched_tokens = max_batched_tokens
@@ -106,11 +112,20 @@ class Scheduler:
             budget -= q
         return admitted
 
+    def gathering(self) -> bool:
+        """Idle engine, requests still streaming in: hold the admission for a moment."""
+        if self.running or not self.waiting or self.gather_max_s <= 0:
+            return False
+        now = time.perf_counter()
+        return (now - self.waiting[-1].t_arrival < self.gather_quiet_s
+                and now - self.waiting[0].t_arrival < self.gather_max_s
+                and len(self.waiting) < self.max_batch)
+
     def _should_prefill(self) -> bool:
         if not self.waiting:
             return False
         if not self.running:
-            return True
+            return not self.gathering()
         if len(self.running) >= self.max_batch:
             return False
         if len(self.waiting) >= max(4, int(self.prefill_min_frac * len(self.running))):

@@ -49,6 +49,7 @@ def main():
     eng.runner.capture_graphs()
     be = EngineLLM(eng, max_new_tokens=16, ignore_eos=True)
     params = SamplingParams(max_new_tokens=16, ignore_eos=True)
+    eng.scheduler.gather_max_s = 0.0
     for w in range(2):   # warm: publish the instruction blocks, exercise the plans
         eng.generate_blocking([be.prompt_ids(bench.make_query(0, w, i)) for i in range(C)], params,
                               forced_prefix=be._forced)

@@ -7,6 +7,7 @@ def run_staggered(eng, prompts, params, forced):
     seqs = []
     run_staggered.mixed = 0
     wait, eng.scheduler.prefill_max_wait_s = eng.scheduler.prefill_max_wait_s, 0.0
+    gather, eng.scheduler.gather_max_s = eng.scheduler.gather_max_s, 0.0
     try:
         pending = list(prompts)
         while pending or any(not s.finished for s in seqs):
@@ -20,4 +21,5 @@ def run_staggered(eng, prompts, params, forced):
             eng.scheduler.on_step_done(batch)
     finally:
         eng.scheduler.prefill_max_wait_s = wait
+        eng.scheduler.gather_max_s = gather
     return [s.output_ids for s in seqs]
