@@ -31,7 +31,21 @@ struct TileCfg {
   static_assert(BN * 8 % NT == 0 && BM * 8 % NT == 0, "tile pieces must divide the thread count");
 };
 
-template <int WN, int WM, int TN, int TM>
+// SWIGLU: X is the fused gate_up output GU [M, 2K] and the activation is computed while staging,
+// X[m][k] = bf16(silu(GU[m][k]) * GU[m][K + k]) — bit-identical to silu_mul_kernel, so the down
+// projection consumes the gate_up output directly (no SiLU kernel, no [M, K] round trip).
+__device__ __forceinline__ u32x4 swiglu8(u32x4 g, u32x4 u) {
+  u32x4 o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float g0 = lo_f(g[k]), g1 = hi_f(g[k]);
+    const float s0 = g0 / (1.f + __expf(-g0)), s1 = g1 / (1.f + __expf(-g1));
+    o[k] = pack2(s0 * lo_f(u[k]), s1 * hi_f(u[k]));
+  }
+  return o;
+}
+
+template <int WN, int WM, int TN, int TM, bool SWIGLU = false>
 __global__ __launch_bounds__(64 * WN * WM) void gemm_tile_kernel(const bf16_t* __restrict__ X,
                                                                  const bf16_t* __restrict__ W,
                                                                  bf16_t* __restrict__ Y, float* __restrict__ P, int M,
@@ -57,10 +71,11 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tile_kernel(const bf16_t* _
     wsrc[i] = W + (size_t)min(n0 + row, N - 1) * K + kb + ch * 8;
     wdst[i] = row * 8 + sw_slot(row, ch);
   }
+  const size_t ldx = SWIGLU ? 2 * (size_t)K : (size_t)K;
 #pragma unroll
   for (int i = 0; i < C::XP; ++i) {
     const int p = tid + i * C::NT, row = p >> 3, ch = p & 7;
-    xsrc[i] = X + (size_t)min(m0 + row, M - 1) * K + kb + ch * 8;
+    xsrc[i] = X + (size_t)min(m0 + row, M - 1) * ldx + kb + ch * 8;
     xdst[i] = row * 8 + sw_slot(row, ch);
   }
 
@@ -69,7 +84,14 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tile_kernel(const bf16_t* _
 #pragma unroll
     for (int i = 0; i < C::WP; ++i) wr[i] = *reinterpret_cast<const u32x4*>(wsrc[i] + t * 64);
 #pragma unroll
-    for (int i = 0; i < C::XP; ++i) xr[i] = *reinterpret_cast<const u32x4*>(xsrc[i] + t * 64);
+    for (int i = 0; i < C::XP; ++i) {
+      if constexpr (SWIGLU) {
+        xr[i] = swiglu8(*reinterpret_cast<const u32x4*>(xsrc[i] + t * 64),
+                        *reinterpret_cast<const u32x4*>(xsrc[i] + K + t * 64));
+      } else {
+        xr[i] = *reinterpret_cast<const u32x4*>(xsrc[i] + t * 64);
+      }
+    }
   };
   auto store = [&](int buf) {
 #pragma unroll
@@ -277,19 +299,19 @@ static void launch_wide(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, i
 
 extern "C" void ka_splitk_reduce_launch(bf16_t* Y, const float* P, int split, long mn, hipStream_t stream);
 
-template <int WN, int WM, int TN, int TM>
+template <int WN, int WM, int TN, int TM, bool SW = false>
 static void launch_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int split,
                         int kps, hipStream_t stream) {
   using C = TileCfg<WN, WM, TN, TM>;
   static bool lds_attr = false;   // > 64 KB of dynamic LDS must be opted into (160 KB per CU on gfx950)
   if (!lds_attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<WN, WM, TN, TM>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<WN, WM, TN, TM, SW>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
     lds_attr = true;
   }
   dim3 grid((N + C::BN - 1) / C::BN, (M + C::BM - 1) / C::BM, split);
-  hipLaunchKernelGGL((gemm_tile_kernel<WN, WM, TN, TM>), grid, dim3(C::NT), C::LDS_BYTES, stream, X, W, Y, P, M, N,
-                     K, kps);
+  hipLaunchKernelGGL((gemm_tile_kernel<WN, WM, TN, TM, SW>), grid, dim3(C::NT), C::LDS_BYTES, stream, X, W, Y, P, M,
+                     N, K, kps);
 }
 
 // Configurations (BN x BM, waves): 0 = 128x256 (2x4 waves, 64x64 per wave), 1 = 64x256 (1x4),
@@ -354,6 +376,28 @@ extern "C" int ka_gemm_tile(void* Y, const void* X, const void* W, void* workspa
     case 9: launch_wide<4, 2, 8>(x, w, y, p, M, N, K, split, kps, stream); break;
   }
   // Y == nullptr: leave the fp32 partials for a fused consumer (ka_rmsnorm_splitk)
+  if (split > 1 && y != nullptr) ka_splitk_reduce_launch(y, p, split, (long)M * N, stream);
+  KA_CHECK_LAUNCH();
+}
+
+// Y = swiglu(GU) * W^T with GU = [M, 2K] (gate | up); cfg 0-4 (the LDS-tiled variants).
+extern "C" int ka_gemm_tile_swiglu(void* Y, const void* GU, const void* W, void* workspace, int M, int N, int K,
+                                   int split, int cfg, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K % 64 != 0 || N % 16 != 0 || split < 1 || cfg < 0 || cfg > 4) return (int)hipErrorInvalidValue;
+  int kps = (K / split + 63) / 64 * 64;
+  split = (K + kps - 1) / kps;
+  auto* x = static_cast<const bf16_t*>(GU);
+  auto* w = static_cast<const bf16_t*>(W);
+  auto* y = static_cast<bf16_t*>(Y);
+  float* p = split > 1 ? static_cast<float*>(workspace) : nullptr;
+  switch (cfg) {
+    case 0: launch_tile<2, 4, 4, 4, true>(x, w, y, p, M, N, K, split, kps, stream); break;
+    case 1: launch_tile<1, 4, 4, 4, true>(x, w, y, p, M, N, K, split, kps, stream); break;
+    case 2: launch_tile<2, 2, 4, 4, true>(x, w, y, p, M, N, K, split, kps, stream); break;
+    case 3: launch_tile<2, 2, 4, 8, true>(x, w, y, p, M, N, K, split, kps, stream); break;
+    case 4: launch_tile<4, 2, 4, 4, true>(x, w, y, p, M, N, K, split, kps, stream); break;
+  }
   if (split > 1 && y != nullptr) ka_splitk_reduce_launch(y, p, split, (long)M * N, stream);
   KA_CHECK_LAUNCH();
 }

@@ -39,6 +39,7 @@ _SIGS = {
     "ka_rmsnorm_splitk": [P, P, P, I, P, I, I, F, P],
     "ka_kv_block_copy": [P, P, P, P, I, I, ctypes.c_long, ctypes.c_long, P],
     "ka_gemm_tile": [P, P, P, P, I, I, I, I, I, P],
+    "ka_gemm_tile_swiglu": [P, P, P, P, I, I, I, I, I, P],
     "ka_gemm_tile_bm": [I],
     "ka_gemm_tile_bn": [I],
     "ka_moe_align": [P, P, P, I, I, I, P],

@@ -263,6 +263,30 @@ def test_gemm_tile(M, N, K):
             close(got, want, atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("M", [48, 256, 300])
+def test_gemm_tile_swiglu_fused_is_exact(M):
+    """down(silu(gate) * up) with the activation computed in the GEMM's X staging is bit-identical to
+    SiLU·mul followed by the same tiled GEMM (same cfg / split-K)."""
+    I, N = 1024, 4096
+    gu = torch.randn(M, 2 * I, device=DEV, dtype=BF)
+    w = (torch.randn(N, I, device=DEV) * 0.02).to(BF)
+    h = ops.silu_mul(gu)
+    for cfg in range(5):
+        for split in (1, 4):
+            want = ops.linear_tile(h, w, cfg, split)
+            ops.GEMM_PLAN[(M, N, I)] = ("tile", split, cfg)
+            try:
+                got = ops.swiglu_linear(gu, w)
+                sk = ops.swiglu_linear(gu, w, defer_reduce=True)
+            finally:
+                ops.GEMM_PLAN.pop((M, N, I))
+            assert torch.equal(got, want), (cfg, split)
+            if split > 1:
+                assert isinstance(sk, ops.SplitK)
+                close(sk.resolve(), want, atol=2e-2)
+    close(want, ref.silu_mul(gu).float() @ w.float().t(), atol=3e-2, rtol=2e-2)
+
+
 def test_gemm_tile_autotune_plan_dispatch():
     from ai_agent_kubectl_amd.ops.autotune import tune_linear
     ws = [(torch.randn(6144, 4096, device=DEV) * 0.02).to(BF) for _ in range(3)]
