@@ -402,6 +402,34 @@ def test_native_tokenizer_matches_python():
         tok._native = saved
 
 
+def test_scheduler_gathers_a_streaming_burst_when_idle():
+    import time
+    bm = BlockManager(64, 16)
+    sch = Scheduler(bm, max_batch=8, max_batched_tokens=4096, gather_max_s=0.05, gather_quiet_s=0.01)
+    a = _seq(20)
+    sch.add(a)
+    assert sch.gathering() and sch.schedule().seqs == []        # newest arrival is fresh: hold
+    time.sleep(0.015)                                            # quiet gap passed
+    assert not sch.gathering()
+    b = sch.schedule()
+    assert b.prefill_seqs == [a]
+    # with sequences running, gathering never applies (the mixed-step policy decides)
+    sch.on_step_done(b)
+    sch.add(_seq(20))
+    assert not sch.gathering()
+    # a burst that keeps arriving is cut off at gather_max_s
+    sch2 = Scheduler(BlockManager(64, 16), max_batch=8, max_batched_tokens=4096, gather_max_s=0.02,
+                     gather_quiet_s=0.01)
+    first = _seq(10)
+    sch2.add(first)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.03:
+        if sch2.gathering():
+            sch2.add(_seq(10))
+        time.sleep(0.002)
+    assert not sch2.gathering() and len(sch2.schedule().prefill_seqs) >= 2
+
+
 def test_scheduler_batches_prefills_while_decoding():
     bm = BlockManager(64, 4, enable_prefix_caching=False)
     sch = Scheduler(bm, max_batch=16, max_batched_tokens=1000, prefill_max_wait_s=10.0)
