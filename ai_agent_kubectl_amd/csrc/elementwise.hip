@@ -150,16 +150,33 @@ extern "C" int ka_rmsnorm_splitk(void* out, void* residual, const void* P, int s
 
 // ------------------------------------------------------------------------------------------------
 // RoPE (neox / rotate-half pairs (i, i + D/2)) on q and k, q -> q_out [T, Hq, D], k and v -> paged cache.
+// With P != nullptr the qkv row is the bf16-rounded sum of `split` fp32 split-K partial slabs of the
+// QKV projection (bit-identical to splitk_reduce_kernel + this kernel, one launch and HBM pass fewer).
+__device__ __forceinline__ uint2 ld4(const bf16_t* row, const float* P, int split, size_t pstride, size_t off) {
+  if (P == nullptr) return *reinterpret_cast<const uint2*>(row + off);
+  f32x4 s = *reinterpret_cast<const f32x4*>(P + off);
+  for (int k = 1; k < split; ++k) s += *reinterpret_cast<const f32x4*>(P + k * pstride + off);
+  return make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
+}
+
+__device__ __forceinline__ uint4 ld8(const bf16_t* row, const float* P, int split, size_t pstride, size_t off) {
+  if (P == nullptr) return *reinterpret_cast<const uint4*>(row + off);
+  const uint2 a = ld4(row, P, split, pstride, off), b = ld4(row, P, split, pstride, off + 4);
+  return make_uint4(a.x, a.y, b.x, b.y);
+}
+
 __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_cache,
                                                       bf16_t* __restrict__ v_cache, const bf16_t* __restrict__ qkv,
                                                       const int* __restrict__ positions,
                                                       const float* __restrict__ cos_sin,
                                                       const int* __restrict__ slot_mapping, int hq, int hkv, int d,
-                                                      int bs) {
+                                                      int bs, const float* __restrict__ Pq, int split,
+                                                      size_t pstride) {
   const int t = blockIdx.x;
   const int half = d >> 1;
   const int qkv_stride = (hq + 2 * hkv) * d;
   const bf16_t* row = qkv + (size_t)t * qkv_stride;
+  const float* prow = Pq ? Pq + (size_t)t * qkv_stride : nullptr;
   const int pos = positions[t];
   const int slot = slot_mapping[t];
   const float* cs = cos_sin + (size_t)pos * d;
@@ -170,9 +187,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ q_out
   for (int it = threadIdx.x; it < n_rot; it += blockDim.x) {
     const int h = it / chunks;
     const int i = (it % chunks) * 4;
-    const bf16_t* src = row + h * d;  // q heads first, then k heads (contiguous in qkv)
-    uint2 a = *reinterpret_cast<const uint2*>(src + i);
-    uint2 b = *reinterpret_cast<const uint2*>(src + i + half);
+    // q heads first, then k heads (contiguous in qkv)
+    uint2 a = ld4(row, prow, split, pstride, (size_t)h * d + i);
+    uint2 b = ld4(row, prow, split, pstride, (size_t)h * d + i + half);
     float4 c = *reinterpret_cast<const float4*>(cs + i);
     float4 s = *reinterpret_cast<const float4*>(cs + half + i);
     float x1[4] = {lo_f(a.x), hi_f(a.x), lo_f(a.y), hi_f(a.y)};
@@ -198,11 +215,11 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ q_out
   }
   if (slot < 0) return;
   const int vchunks = d >> 3;
-  const bf16_t* vsrc = row + (hq + hkv) * d;
+  const size_t vbase = (size_t)(hq + hkv) * d;
   for (int it = threadIdx.x; it < hkv * vchunks; it += blockDim.x) {
     const int h = it / vchunks;
     const int i = (it % vchunks) * 8;
-    uint4 v = *reinterpret_cast<const uint4*>(vsrc + h * d + i);
+    uint4 v = ld8(row, prow, split, pstride, vbase + (size_t)h * d + i);
     bf16_t e[8] = {(bf16_t)v.x, (bf16_t)(v.x >> 16), (bf16_t)v.y, (bf16_t)(v.y >> 16),
                    (bf16_t)v.z, (bf16_t)(v.z >> 16), (bf16_t)v.w, (bf16_t)(v.w >> 16)};
     bf16_t* dst = v_cache + (((size_t)blk * hkv + h) * d + i) * bs + off;
@@ -218,21 +235,39 @@ extern "C" int ka_rope_kv(void* q_out, void* k_cache, void* v_cache, const void*
   if (d % 16 != 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(rope_kv_kernel, dim3(tokens), dim3(256), 0, stream, static_cast<bf16_t*>(q_out),
                      static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache),
-                     static_cast<const bf16_t*>(qkv), positions, cos_sin, slot_mapping, hq, hkv, d, bs);
+                     static_cast<const bf16_t*>(qkv), positions, cos_sin, slot_mapping, hq, hkv, d, bs, nullptr, 0,
+                     (size_t)0);
+  KA_CHECK_LAUNCH();
+}
+
+// rope_kv over the split-K partials P [split, tokens, (hq + 2 hkv) d] of the QKV projection
+extern "C" int ka_rope_kv_splitk(void* q_out, void* k_cache, void* v_cache, const void* P, int split,
+                                 const int* positions, const float* cos_sin, const int* slot_mapping, int tokens,
+                                 int hq, int hkv, int d, int bs, hipStream_t stream) {
+  if (tokens <= 0) return 0;
+  if (d % 16 != 0 || split < 1) return (int)hipErrorInvalidValue;
+  const size_t pstride = (size_t)tokens * (hq + 2 * hkv) * d;
+  hipLaunchKernelGGL(rope_kv_kernel, dim3(tokens), dim3(256), 0, stream, static_cast<bf16_t*>(q_out),
+                     static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache), nullptr, positions, cos_sin,
+                     slot_mapping, hq, hkv, d, bs, static_cast<const float*>(P), split, pstride);
   KA_CHECK_LAUNCH();
 }
 
 // ------------------------------------------------------------------------------------------------
 // out[t, :I] = silu(gu[t, :I]) * gu[t, I:2I]     (gate | up halves of the fused gate_up projection)
+// (P != nullptr: gu is the bf16-rounded sum of `split` fp32 split-K partials of the gate_up GEMM)
 __global__ __launch_bounds__(256) void silu_mul_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ gu,
-                                                       int inter, long total_vec) {
+                                                       int inter, long total_vec, const float* __restrict__ P,
+                                                       int split, size_t pstride) {
   const int vpr = inter >> 3;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total_vec; i += (long)gridDim.x * blockDim.x) {
     const long t = i / vpr;
     const int c = (int)(i % vpr) * 8;
-    const bf16_t* r = gu + t * 2 * (long)inter;
-    uint4 g = *reinterpret_cast<const uint4*>(r + c);
-    uint4 u = *reinterpret_cast<const uint4*>(r + inter + c);
+    const size_t roff = (size_t)t * 2 * (size_t)inter;
+    const bf16_t* r = gu ? gu + roff : nullptr;
+    const float* pr = P ? P + roff : nullptr;
+    uint4 g = ld8(r, pr, split, pstride, c);
+    uint4 u = ld8(r, pr, split, pstride, (size_t)inter + c);
     uint32_t gw[4] = {g.x, g.y, g.z, g.w}, uw[4] = {u.x, u.y, u.z, u.w}, o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -250,7 +285,18 @@ extern "C" int ka_silu_mul(void* out, const void* gu, int tokens, int inter, hip
   const long total = (long)tokens * (inter / 8);
   const int grid = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
   hipLaunchKernelGGL(silu_mul_kernel, dim3(grid), dim3(256), 0, stream, static_cast<bf16_t*>(out),
-                     static_cast<const bf16_t*>(gu), inter, total);
+                     static_cast<const bf16_t*>(gu), inter, total, nullptr, 0, (size_t)0);
+  KA_CHECK_LAUNCH();
+}
+
+extern "C" int ka_silu_mul_splitk(void* out, const void* P, int split, int tokens, int inter, hipStream_t stream) {
+  if (tokens <= 0) return 0;
+  if (inter % 8 != 0 || split < 1) return (int)hipErrorInvalidValue;
+  const long total = (long)tokens * (inter / 8);
+  const int grid = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  const size_t pstride = (size_t)tokens * 2 * inter;
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(grid), dim3(256), 0, stream, static_cast<bf16_t*>(out), nullptr, inter,
+                     total, static_cast<const float*>(P), split, pstride);
   KA_CHECK_LAUNCH();
 }
 

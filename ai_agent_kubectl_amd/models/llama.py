@@ -79,7 +79,9 @@ class LlamaModel:
                 x = ops.rmsnorm(h, L["ln1"], eps)
             else:
                 x = ops.rmsnorm(h, L["ln1"], eps, residual=residual)
-            qkv = ops.linear(x, L["wqkv"])
+            # column-parallel projections: no all-reduce before their consumer, so a split-K plan
+            # hands its fp32 partials to the RoPE / SiLU kernels, which reduce them on the fly
+            qkv = ops.linear(x, L["wqkv"], defer_reduce=True)
             q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, k_cache[li], v_cache[li],
                                   self.hq, self.hkv, self.D)
             if meta.is_decode:
@@ -106,7 +108,7 @@ class LlamaModel:
             if cfg.is_moe:
                 h = moe_forward(x, L, cfg, self.ep_rank, self.ep_size, meta.is_decode)
             else:
-                h = ops.linear(ops.silu_mul(ops.linear(x, L["w13"])), L["w2"], defer_reduce=fuse)
+                h = ops.linear(ops.silu_mul(ops.linear(x, L["w13"], defer_reduce=True)), L["w2"], defer_reduce=fuse)
             self.comm.all_reduce(h)
         x = ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
         return x.index_select(0, meta.logits_indices)

@@ -102,6 +102,16 @@ def kv_block_copy(k_cache: torch.Tensor, v_cache: torch.Tensor, src: torch.Tenso
 
 def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq: int, hkv: int, d: int,
                   q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """RoPE on q/k + paged KV append.  `qkv` may be a `SplitK` (the QKV projection's fp32 partials):
+    the reduction then happens inside this kernel (bit-identical to reduce-then-rope)."""
+    if isinstance(qkv, SplitK):
+        lib = require()
+        T = qkv.shape[0]
+        q_out = torch.empty((T, hq, d), dtype=k_cache.dtype, device=k_cache.device) if q_out is None else q_out
+        check(lib.ka_rope_kv_splitk(_p(q_out), _p(k_cache), _p(v_cache), _p(qkv.P), qkv.split, _p(positions),
+                                    _p(cos_sin), _p(slot_mapping), T, hq, hkv, d, k_cache.shape[2], _stream()),
+              "rope_kv_splitk")
+        return q_out
     if _ref(qkv):
         return ref.rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq, hkv, d)
     lib = require()
@@ -146,7 +156,14 @@ def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float,
     return out
 
 
-def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def silu_mul(gu, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(gate) * up of the fused gate_up output; `gu` may be a `SplitK` (reduction fused in)."""
+    if isinstance(gu, SplitK):
+        lib = require()
+        T, two_i = gu.shape
+        out = torch.empty((T, two_i // 2), dtype=torch.bfloat16, device=gu.P.device) if out is None else out
+        check(lib.ka_silu_mul_splitk(_p(out), _p(gu.P), gu.split, T, two_i // 2, _stream()), "silu_mul_splitk")
+        return out
     if _ref(gu):
         return ref.silu_mul(gu)
     lib = require()

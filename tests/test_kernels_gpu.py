@@ -226,6 +226,33 @@ def test_rmsnorm_fused_splitk_reduce(rows, hidden, split):
     close(r1, r2, atol=1e-2)
 
 
+def test_rope_and_silu_consume_splitk_partials_exactly():
+    """RoPE+KV append and SiLU·mul summing the fp32 split-K partials themselves give bit-identical
+    results to the reduce kernel followed by the bf16 op."""
+    T, hq, hkv, d, split = 37, 32, 8, 128, 4
+    P = torch.randn(split, T, (hq + 2 * hkv) * d, device=DEV)
+    red = ops.SplitK(P, split).resolve()                         # torch sum in the same order...
+    want_bf = P[0].clone()
+    for k in range(1, split):
+        want_bf += P[k]
+    red = want_bf.to(BF)                                         # ...exactly the reduce kernel's order
+    cs = ref.rope_cos_sin(4096, d, 5e5, device=DEV)
+    pos = torch.randint(0, 4000, (T,), dtype=torch.int32, device=DEV)
+    slots = torch.randperm(64 * 16, device=DEV)[:T].int()
+    kc1 = torch.zeros(64, hkv, 16, d, device=DEV, dtype=BF)
+    vc1 = torch.zeros(64, hkv, d, 16, device=DEV, dtype=BF)
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    q1 = ops.rope_kv_write(red, pos, cs, slots, kc1, vc1, hq, hkv, d)
+    q2 = ops.rope_kv_write(ops.SplitK(P, split), pos, cs, slots, kc2, vc2, hq, hkv, d)
+    assert torch.equal(q1, q2) and torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    I = 1024
+    G = torch.randn(split, T, 2 * I, device=DEV)
+    acc = G[0].clone()
+    for k in range(1, split):
+        acc += G[k]
+    assert torch.equal(ops.silu_mul(acc.to(BF)), ops.silu_mul(ops.SplitK(G, split)))
+
+
 def test_kv_block_copy():
     L, NB, hkv = 4, 40, 8
     kc = torch.randn(L, NB, hkv, 16, 128, device=DEV).to(BF)
