@@ -318,7 +318,15 @@ static void launch_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, i
 // 2 = 128x128 (2x2), 3 = 128x256 (2x2 waves, 64x128 per wave), 4 = 256x128 (4x2);
 // wide (W in VGPRs): 5 = 256x128 (4 waves x 64 rows), 6 = 128x128 (2 waves), 7 = 128x64 (2 waves),
 // 8 = 64x128 (1 wave x 64 rows), 9 = 128x128 (4 waves x 32 rows).
+extern "C" int ka_gemm_stream_bm(int cfg);
+extern "C" int ka_gemm_stream_bn(int cfg);
+extern "C" int ka_gemm_stream_launch(bf16_t* Y, const bf16_t* X, const bf16_t* W, float* P, int M, int N, int K,
+                                     int split, int kps, int cfg, hipStream_t stream);
+
 extern "C" int ka_gemm_tile_bm(int cfg) {
+  if (cfg == 15) return TileCfg<4, 2, 4, 8>::BM;
+  if (cfg == 16) return TileCfg<2, 4, 8, 4>::BM;
+  if (cfg >= 10) return ka_gemm_stream_bm(cfg);
   switch (cfg) {
     case 0: return TileCfg<2, 4, 4, 4>::BM;
     case 1: return TileCfg<1, 4, 4, 4>::BM;
@@ -335,6 +343,9 @@ extern "C" int ka_gemm_tile_bm(int cfg) {
 }
 
 extern "C" int ka_gemm_tile_bn(int cfg) {
+  if (cfg == 15) return TileCfg<4, 2, 4, 8>::BN;
+  if (cfg == 16) return TileCfg<2, 4, 8, 4>::BN;
+  if (cfg >= 10) return ka_gemm_stream_bn(cfg);
   switch (cfg) {
     case 0: return TileCfg<2, 4, 4, 4>::BN;
     case 1: return TileCfg<1, 4, 4, 4>::BN;
@@ -354,8 +365,9 @@ extern "C" int ka_gemm_tile_bn(int cfg) {
 extern "C" int ka_gemm_tile(void* Y, const void* X, const void* W, void* workspace, int M, int N, int K, int split,
                             int cfg, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (K % 64 != 0 || N % 16 != 0 || split < 1 || cfg < 0 || cfg > 9) return (int)hipErrorInvalidValue;
-  const int kq = cfg >= 5 ? 128 : 64;   // the wide kernels consume k in pairs of 64-steps
+  if (K % 32 != 0 || N % 16 != 0 || split < 1 || cfg < 0 || ka_gemm_tile_bm(cfg) < 0) return (int)hipErrorInvalidValue;
+  // k quantum: stream kernels (cfg >= 10) 32-deep stages, wide kernels pairs of 64-steps, tile 64
+  const int kq = cfg >= 15 ? 64 : cfg >= 10 ? 32 : cfg >= 5 ? 128 : 64;
   if (K % kq != 0) return (int)hipErrorInvalidValue;
   int kps = (K / split + kq - 1) / kq * kq;
   split = (K + kps - 1) / kps;
@@ -363,6 +375,12 @@ extern "C" int ka_gemm_tile(void* Y, const void* X, const void* W, void* workspa
   auto* w = static_cast<const bf16_t*>(W);
   auto* y = static_cast<bf16_t*>(Y);
   float* p = split > 1 ? static_cast<float*>(workspace) : nullptr;
+  if (cfg == 15) launch_tile<4, 2, 4, 8>(x, w, y, p, M, N, K, split, kps, stream);
+  if (cfg == 16) launch_tile<2, 4, 8, 4>(x, w, y, p, M, N, K, split, kps, stream);
+  if (cfg >= 10 && cfg < 15) {
+    const int rc = ka_gemm_stream_launch(y, x, w, p, M, N, K, split, kps, cfg, stream);
+    if (rc) return rc;
+  }
   switch (cfg) {
     case 0: launch_tile<2, 4, 4, 4>(x, w, y, p, M, N, K, split, kps, stream); break;
     case 1: launch_tile<1, 4, 4, 4>(x, w, y, p, M, N, K, split, kps, stream); break;

@@ -267,11 +267,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
     return y
 
 
-TILE_CFGS = tuple(range(10))   # csrc/gemm_tile.hip configurations (BN x BM tiles; >= 5: W in VGPRs)
+# csrc/gemm_tile.hip configurations (BN x BM tiles; 5-9: W in VGPRs; 10-14: csrc/gemm_stream.hip,
+# deep-prefetch LDS-DMA stages; 15-16: 256 x 256 register-staged tiles)
+TILE_CFGS = tuple(range(17))
 
 
 def tile_k_quantum(cfg: int) -> int:
-    return 128 if cfg >= 5 else 64
+    return 64 if cfg >= 15 else 32 if cfg >= 10 else 128 if cfg >= 5 else 64
 
 
 def swiglu_linear(gu: torch.Tensor, w: torch.Tensor, defer_reduce: bool = False):

@@ -92,18 +92,18 @@ def tune_linear(groups: Dict[Tuple[int, int], List[torch.Tensor]], Ms: Sequence[
 TUNE_CFGS = (0, 1, 2, 4, 9)
 
 
-def tile_candidates(M: int, N: int, K: int):
+def tile_candidates(M: int, N: int, K: int, cfgs: Sequence[int] = ()):
     """(cfg, split) pairs of the LDS-tiled kernel worth timing for this shape: tiles no taller than
     twice M, split-K so that the grid lands between ~1/2 and ~4 waves of workgroups on 256 CUs."""
     out = []
-    if M < 48 or K % 64 or N % 16:
+    if M < 48 or K % 32 or N % 16:
         return out
-    for cfg in TUNE_CFGS:
+    for cfg in cfgs or TUNE_CFGS:
         bn, bm = tile_shape(cfg)
         if bm > 2 * M and bm > 128:
             continue
         tiles = ((N + bn - 1) // bn) * ((M + bm - 1) // bm)
-        for split in (1, 2, 3, 4, 6, 8):
+        for split in (1, 2, 3, 4, 6, 8, 16):
             if K % (tile_k_quantum(cfg) * split) or K // split < 256:
                 continue
             if split > 1 and tiles * split > 1024:
