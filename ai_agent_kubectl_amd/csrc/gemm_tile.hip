@@ -45,7 +45,11 @@ __device__ __forceinline__ u32x4 swiglu8(u32x4 g, u32x4 u) {
   return o;
 }
 
-template <int WN, int WM, int TN, int TM, bool SWIGLU = false>
+// PF2: two register stages in flight (k-step t+2 is issued before computing t, t+1 is written to
+// LDS after it): hides about two loaded-HBM latencies instead of one; K per split must then be a
+// multiple of 128 (the loop is unrolled by two so hipcc counts vmcnt statically; loads past the
+// end are clamped to the last step and land in a buffer nobody reads again).
+template <int WN, int WM, int TN, int TM, bool SWIGLU = false, bool PF2 = false>
 __global__ __launch_bounds__(64 * WN * WM) void gemm_tile_kernel(const bf16_t* __restrict__ X,
                                                                  const bf16_t* __restrict__ W,
                                                                  bf16_t* __restrict__ Y, float* __restrict__ P, int M,
@@ -107,14 +111,7 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tile_kernel(const bf16_t* _
     for (int b = 0; b < TM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int r16 = lane & 15, grp = lane >> 4;
-  if (nk > 0) {
-    load(0);
-    store(0);
-  }
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nk) load(t + 1);
+  auto compute = [&](int buf) {
     const u32x4* wb = ws + buf * C::BN * 8;
     const u32x4* xb = xs + buf * C::BM * 8;
 #pragma unroll
@@ -136,8 +133,54 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tile_kernel(const bf16_t* _
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < nk) store(buf ^ 1);
+  };
+  if constexpr (PF2) {
+    static_assert(!SWIGLU, "PF2 variant is plain X staging only");
+    u32x4 wr2[C::WP], xr2[C::XP];
+    auto load2 = [&](u32x4 (&w)[C::WP], u32x4 (&x)[C::XP], int t) {
+      t = min(t, nk - 1);
+#pragma unroll
+      for (int i = 0; i < C::WP; ++i) w[i] = *reinterpret_cast<const u32x4*>(wsrc[i] + t * 64);
+#pragma unroll
+      for (int i = 0; i < C::XP; ++i) x[i] = *reinterpret_cast<const u32x4*>(xsrc[i] + t * 64);
+    };
+    auto store2 = [&](const u32x4 (&w)[C::WP], const u32x4 (&x)[C::XP], int buf) {
+#pragma unroll
+      for (int i = 0; i < C::WP; ++i) ws[buf * C::BN * 8 + wdst[i]] = w[i];
+#pragma unroll
+      for (int i = 0; i < C::XP; ++i) xs[buf * C::BM * 8 + xdst[i]] = x[i];
+    };
+    if (nk > 0) {
+      load2(wr, xr, 0);
+      load2(wr2, xr2, 1);
+      store2(wr, xr, 0);
+    }
     __syncthreads();
+    for (int t = 0; t < nk; t += 2) {   // nk is even
+      load2(wr, xr, t + 2);
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch above the MFMAs (hipcc sinks it otherwise)
+      compute(0);
+      store2(wr2, xr2, 1);
+      __syncthreads();
+      load2(wr2, xr2, t + 3);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(1);
+      store2(wr, xr, 0);
+      __syncthreads();
+    }
+  } else {
+    if (nk > 0) {
+      load(0);
+      store(0);
+    }
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      if (t + 1 < nk) load(t + 1);
+      compute(buf);
+      if (t + 1 < nk) store(buf ^ 1);
+      __syncthreads();
+    }
   }
 
   // epilogue: acc[i][j][r] = C[n = .. + 4*grp + r][m = .. + r16]  ->  Y[m][n .. n+3]
@@ -299,18 +342,18 @@ static void launch_wide(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, i
 
 extern "C" void ka_splitk_reduce_launch(bf16_t* Y, const float* P, int split, long mn, hipStream_t stream);
 
-template <int WN, int WM, int TN, int TM, bool SW = false>
+template <int WN, int WM, int TN, int TM, bool SW = false, bool PF2 = false>
 static void launch_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int split,
                         int kps, hipStream_t stream) {
   using C = TileCfg<WN, WM, TN, TM>;
   static bool lds_attr = false;   // > 64 KB of dynamic LDS must be opted into (160 KB per CU on gfx950)
   if (!lds_attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<WN, WM, TN, TM, SW>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<WN, WM, TN, TM, SW, PF2>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
     lds_attr = true;
   }
   dim3 grid((N + C::BN - 1) / C::BN, (M + C::BM - 1) / C::BM, split);
-  hipLaunchKernelGGL((gemm_tile_kernel<WN, WM, TN, TM, SW>), grid, dim3(C::NT), C::LDS_BYTES, stream, X, W, Y, P, M,
+  hipLaunchKernelGGL((gemm_tile_kernel<WN, WM, TN, TM, SW, PF2>), grid, dim3(C::NT), C::LDS_BYTES, stream, X, W, Y, P, M,
                      N, K, kps);
 }
 
@@ -323,7 +366,14 @@ extern "C" int ka_gemm_stream_bn(int cfg);
 extern "C" int ka_gemm_stream_launch(bf16_t* Y, const bf16_t* X, const bf16_t* W, float* P, int M, int N, int K,
                                      int split, int kps, int cfg, hipStream_t stream);
 
+// PF2 (two register stages in flight): 17 = 128x128 (2x2 waves), 18 = 128x256 (2x2, 64x128 per
+// wave), 19 = 128x256 (2x4 waves), 20 = 256x128 (4x2 waves).
+#define KA_PF2_CFGS(X) X(17, 2, 2, 4, 4) X(18, 2, 2, 4, 8) X(19, 2, 4, 4, 4) X(20, 4, 2, 4, 4)
+
 extern "C" int ka_gemm_tile_bm(int cfg) {
+#define X_(id, a, b, c, d) if (cfg == id) return TileCfg<a, b, c, d>::BM;
+  KA_PF2_CFGS(X_)
+#undef X_
   if (cfg == 15) return TileCfg<4, 2, 4, 8>::BM;
   if (cfg == 16) return TileCfg<2, 4, 8, 4>::BM;
   if (cfg >= 10) return ka_gemm_stream_bm(cfg);
@@ -343,6 +393,9 @@ extern "C" int ka_gemm_tile_bm(int cfg) {
 }
 
 extern "C" int ka_gemm_tile_bn(int cfg) {
+#define X_(id, a, b, c, d) if (cfg == id) return TileCfg<a, b, c, d>::BN;
+  KA_PF2_CFGS(X_)
+#undef X_
   if (cfg == 15) return TileCfg<4, 2, 4, 8>::BN;
   if (cfg == 16) return TileCfg<2, 4, 8, 4>::BN;
   if (cfg >= 10) return ka_gemm_stream_bn(cfg);
@@ -367,7 +420,7 @@ extern "C" int ka_gemm_tile(void* Y, const void* X, const void* W, void* workspa
   if (M <= 0 || N <= 0) return 0;
   if (K % 32 != 0 || N % 16 != 0 || split < 1 || cfg < 0 || ka_gemm_tile_bm(cfg) < 0) return (int)hipErrorInvalidValue;
   // k quantum: stream kernels (cfg >= 10) 32-deep stages, wide kernels pairs of 64-steps, tile 64
-  const int kq = cfg >= 15 ? 64 : cfg >= 10 ? 32 : cfg >= 5 ? 128 : 64;
+  const int kq = cfg >= 17 ? 128 : cfg >= 15 ? 64 : cfg >= 10 ? 32 : cfg >= 5 ? 128 : 64;
   if (K % kq != 0) return (int)hipErrorInvalidValue;
   int kps = (K / split + kq - 1) / kq * kq;
   split = (K + kps - 1) / kps;
@@ -375,6 +428,9 @@ extern "C" int ka_gemm_tile(void* Y, const void* X, const void* W, void* workspa
   auto* w = static_cast<const bf16_t*>(W);
   auto* y = static_cast<bf16_t*>(Y);
   float* p = split > 1 ? static_cast<float*>(workspace) : nullptr;
+#define X_(id, a, b, c, d) if (cfg == id) launch_tile<a, b, c, d, false, true>(x, w, y, p, M, N, K, split, kps, stream);
+  KA_PF2_CFGS(X_)
+#undef X_
   if (cfg == 15) launch_tile<4, 2, 4, 8>(x, w, y, p, M, N, K, split, kps, stream);
   if (cfg == 16) launch_tile<2, 4, 8, 4>(x, w, y, p, M, N, K, split, kps, stream);
   if (cfg >= 10 && cfg < 15) {

@@ -268,12 +268,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
 
 
 # csrc/gemm_tile.hip configurations (BN x BM tiles; 5-9: W in VGPRs; 10-14: csrc/gemm_stream.hip,
-# deep-prefetch LDS-DMA stages; 15-16: 256 x 256 register-staged tiles)
-TILE_CFGS = tuple(range(17))
+# deep-prefetch LDS-DMA stages; 15-16: 256 x 256 register-staged tiles; 17-20: two register stages
+# in flight)
+TILE_CFGS = tuple(range(21))
 
 
 def tile_k_quantum(cfg: int) -> int:
-    return 64 if cfg >= 15 else 32 if cfg >= 10 else 128 if cfg >= 5 else 64
+    return 128 if cfg >= 17 else 64 if cfg >= 15 else 32 if cfg >= 10 else 128 if cfg >= 5 else 64
 
 
 def swiglu_linear(gu: torch.Tensor, w: torch.Tensor, defer_reduce: bool = False):

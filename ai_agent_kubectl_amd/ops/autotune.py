@@ -88,8 +88,10 @@ def tune_linear(groups: Dict[Tuple[int, int], List[torch.Tensor]], Ms: Sequence[
 
 
 # configurations worth timing on MI355X (bench_gemm_tile.py: the W-in-VGPR variants 5-8 and the
-# 64x128-per-wave cfg 3 never made the top three for the Llama/Mixtral projection shapes)
-TUNE_CFGS = (0, 1, 2, 4, 9)
+# 64x128-per-wave cfg 3 never made the top three for the Llama/Mixtral projection shapes; the
+# LDS-DMA stream kernels 10-14 and 256x256 tiles 15-16 never beat the best of these, while the
+# two-stage-prefetch tiles 17/19/20 win QKV / O / down by 3-7 % — profiles/gemm_stream_vs_tile_*.txt)
+TUNE_CFGS = (0, 1, 2, 4, 9, 17, 19, 20)
 
 
 def tile_candidates(M: int, N: int, K: int, cfgs: Sequence[int] = ()):

@@ -28,12 +28,12 @@ def main():
             want = x.float() @ ws[0].float().t()
             tb = _time(lambda w: torch.nn.functional.linear(x, w), ws, reps=24)
             old, new = [], []
-            for cfg, sp in tile_candidates(M, N, K, cfgs=(0, 1, 2, 4, 9, 10, 11, 12, 13, 14, 15, 16)):
-                if cfg >= 10 and sp == 1:
+            for cfg, sp in tile_candidates(M, N, K, cfgs=(0, 1, 2, 3, 4, 9, 14, 15, 17, 18, 19, 20)):
+                if cfg >= 17 and sp == 1:
                     err = (ops.linear_tile(x, ws[0], cfg, sp).float() - want).abs().max().item()
                     assert err < 0.1, (cfg, err)
                 t = _time(lambda w: ops.linear_tile(x, w, cfg, sp, defer_reduce=True), ws, reps=24)
-                (new if cfg >= 10 else old).append((round(t, 1), cfg, sp))
+                (new if cfg >= 17 else old).append((round(t, 1), cfg, sp))
             old.sort()
             new.sort()
             fl = 2 * M * N * K
@@ -43,8 +43,8 @@ def main():
             tot["old"] += min(tb, bo)
             tot["new"] += min(tb, bo, bn)
             print(f"M={M:4d} {name:8s} N={N:6d} K={K:6d}  blas {tb:6.1f}us ({gb / tb * 1e3:5.2f} TB/s)  "
-                  f"tile {bo:6.1f}us  stream {bn:6.1f}us ({gb / bn * 1e3:5.2f} TB/s, {fl / bn / 1e6:5.0f} TF)  "
-                  f"stream top4={new[:4]}  tile top2={old[:2]}", flush=True)
+                  f"tile {bo:6.1f}us  pf2 {bn:6.1f}us ({gb / bn * 1e3:5.2f} TB/s, {fl / bn / 1e6:5.0f} TF)  "
+                  f"pf2 top4={new[:4]}  tile top2={old[:2]}", flush=True)
             del ws
         print(f"M={M} per-layer: blas {tot['blas']:.1f} us, best-of(blas,tile) {tot['old']:.1f} us, "
               f"best-of(all) {tot['new']:.1f} us", flush=True)
