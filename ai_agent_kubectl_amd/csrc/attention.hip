@@ -27,35 +27,135 @@
 #define KBS 16
 
 // ------------------------------------------------------------------------------------------------
+// Fused decode step (FUSED = true): the workgroup of (kv head h, sequence b) first does what
+// rope_kv_kernel would do for its slice of the QKV projection (reducing the split-K partials on the
+// fly when the projection left them): RoPE on its G query heads and its key head at position
+// positions[b], the new K/V appended at slot_mapping[b].  The rotated queries go to LDS (never to
+// HBM), the chunk loop runs over the ctx - 1 cached tokens, and the new token's score and value are
+// folded into the cross-wave merge straight from LDS — no read-back of the slot being written, one
+// kernel and one launch boundary less per layer.
+struct DecodeFuse {
+  const bf16_t* qkv;        // [B, (hq + 2 hkv) * 128] bf16, or nullptr when P is given
+  const float* P;           // [split, B, (hq + 2 hkv) * 128] fp32 split-K partials
+  int split;
+  size_t pstride;
+  const int* positions;
+  const float* cos_sin;     // [max_pos, 128]: cos | sin halves
+  const int* slot_mapping;
+  bf16_t* k_cache;
+  bf16_t* v_cache;
+};
+
+__device__ __forceinline__ uint2 dq_ld4(const DecodeFuse& f, size_t off) {
+  if (f.P == nullptr) return *reinterpret_cast<const uint2*>(f.qkv + off);
+  f32x4 s = *reinterpret_cast<const f32x4*>(f.P + off);
+  for (int k = 1; k < f.split; ++k) s += *reinterpret_cast<const f32x4*>(f.P + k * f.pstride + off);
+  return make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
+}
+
+template <bool FUSED>
 __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
                                                            const bf16_t* __restrict__ k_cache,
                                                            const bf16_t* __restrict__ v_cache,
                                                            const int* __restrict__ block_tables, int max_blocks,
                                                            const int* __restrict__ ctx_lens, int hq, int hkv,
-                                                           float scale_log2) {
+                                                           float scale_log2, DecodeFuse fz) {
   const int h = blockIdx.x, b = blockIdx.y;
   const int G = hq / hkv;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, grp = lane >> 4;
-  const int ctx = ctx_lens[b];
+  // fused: the chunk loop covers the cached tokens only; the new one is merged from LDS
+  const int ctx = ctx_lens[b] - (FUSED ? 1 : 0);
 
   __shared__ __attribute__((aligned(16))) float smem[4 * 16 * 2 + 4 * 16 * (HD + 4)];
   __shared__ __attribute__((aligned(16))) bf16_t p_lds[4][16 * 32];
+  // fused: new token's value and per-row score (the rotated q rows and k are staged in p_lds)
+  __shared__ __attribute__((aligned(16))) float new_lds[FUSED ? HD / 2 + 16 : 4];
   float* sm = smem;                 // [4][16]
   float* sl = smem + 64;            // [4][16]
   float* so = smem + 128;           // [4][16][HD+4]
+
+  if constexpr (FUSED) {
+    const int half = HD / 2;
+    const size_t stride = (size_t)(hq + 2 * hkv) * HD;
+    const size_t rowoff = (size_t)b * stride;
+    const float* cs = fz.cos_sin + (size_t)fz.positions[b] * HD;
+    const int slot = fz.slot_mapping[b];   // -1: padding row (no cache write, empty output)
+    const int blk = slot >= 0 ? slot / KBS : 0, off = slot >= 0 ? slot % KBS : 0;
+    // (G query heads + 1 key head) x 16 items of 4 rotary pairs
+    for (int it = threadIdx.x; it < (G + 1) * 16; it += 256) {
+      const int hh = it >> 4, i = (it & 15) * 4;
+      const size_t col0 = hh < G ? (size_t)(h * G + hh) * HD : (size_t)(hq + h) * HD;
+      const uint2 a = dq_ld4(fz, rowoff + col0 + i);
+      const uint2 c2 = dq_ld4(fz, rowoff + col0 + i + half);
+      const float4 c = *reinterpret_cast<const float4*>(cs + i);
+      const float4 sn = *reinterpret_cast<const float4*>(cs + half + i);
+      const float x1[4] = {lo_f(a.x), hi_f(a.x), lo_f(a.y), hi_f(a.y)};
+      const float x2[4] = {lo_f(c2.x), hi_f(c2.x), lo_f(c2.y), hi_f(c2.y)};
+      const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+      float o1[4], o2[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o1[k] = x1[k] * cc[k] - x2[k] * ss[k];
+        o2[k] = x2[k] * cc[k] + x1[k] * ss[k];
+      }
+      const uint2 r1 = make_uint2(pack2(o1[0], o1[1]), pack2(o1[2], o1[3]));
+      const uint2 r2 = make_uint2(pack2(o2[0], o2[1]), pack2(o2[2], o2[3]));
+      bf16_t* dl = &p_lds[0][0] + hh * HD;   // rows 0..G-1: q heads, row G: k
+      *reinterpret_cast<uint2*>(dl + i) = r1;
+      *reinterpret_cast<uint2*>(dl + i + half) = r2;
+      if (hh == G && slot >= 0) {
+        bf16_t* kd = fz.k_cache + (((size_t)blk * hkv + h) * KBS + off) * HD;
+        *reinterpret_cast<uint2*>(kd + i) = r1;
+        *reinterpret_cast<uint2*>(kd + i + half) = r2;
+      }
+    }
+    // value: 32 items of 4 dims -> LDS and the dim-major cache slot
+    if (threadIdx.x < HD / 4) {
+      const int i = threadIdx.x * 4;
+      const uint2 v = dq_ld4(fz, rowoff + (size_t)(hq + hkv + h) * HD + i);
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(new_lds) + i) = v;
+      if (slot >= 0) {
+      bf16_t* vd = fz.v_cache + (((size_t)blk * hkv + h) * HD + i) * KBS + off;
+      vd[0] = (bf16_t)v.x;
+      vd[KBS] = (bf16_t)(v.x >> 16);
+      vd[2 * KBS] = (bf16_t)v.y;
+      vd[3 * KBS] = (bf16_t)(v.y >> 16);
+      }
+    }
+    __syncthreads();
+  }
 
   bf16x8 qf[4];
   {
     const int row = col;
     if (row < G) {
-      const bf16_t* qp = q + ((size_t)b * hq + h * G + row) * HD + 8 * grp;
+      const bf16_t* qp = FUSED ? &p_lds[0][0] + row * HD + 8 * grp : q + ((size_t)b * hq + h * G + row) * HD + 8 * grp;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(*reinterpret_cast<const uint4*>(qp + 32 * ks));
     } else {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(make_uint4(0, 0, 0, 0));
     }
+  }
+  if constexpr (FUSED) {
+    // new token's score per query row (wave 0): lane (col = row, grp) holds dims 8*grp + 32*ks
+    if (wave == 0 && col < G) {
+      const bf16_t* kp = &p_lds[0][0] + G * HD + 8 * grp;
+      float dot = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const uint4 ka = *reinterpret_cast<const uint4*>(kp + 32 * ks);
+        const uint4 qa = __builtin_bit_cast(uint4, qf[ks]);
+        const uint32_t qw[4] = {qa.x, qa.y, qa.z, qa.w}, kw[4] = {ka.x, ka.y, ka.z, ka.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dot += lo_f(qw[k]) * lo_f(kw[k]) + hi_f(qw[k]) * hi_f(kw[k]);
+      }
+      dot += __shfl_xor(dot, 16, 64);
+      dot += __shfl_xor(dot, 32, 64);
+      if (grp == 0) new_lds[HD / 2 + col] = fz.slot_mapping[b] >= 0 ? dot * scale_log2 : -INFINITY;
+    }
+    __syncthreads();   // p_lds is the chunk loop's P scratch from here on
   }
   float m[4], l[4];
   f32x4 o[8];
@@ -146,6 +246,11 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
     float M = -INFINITY;
 #pragma unroll
     for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[w * 16 + row]);
+    float s_new = -INFINITY;
+    if constexpr (FUSED) {
+      s_new = new_lds[HD / 2 + row];
+      M = fmaxf(M, s_new);
+    }
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     float den = 0.f;
     if (M != -INFINITY) {
@@ -156,6 +261,17 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
         const float* src = so + (w * 16 + row) * (HD + 4) + d0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc[k] += e * src[k];
+      }
+      if constexpr (FUSED) {
+        const float e = exp2f(s_new - M);
+        den += e;
+        const uint4 va = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(new_lds) + d0);
+        const uint32_t vw[4] = {va.x, va.y, va.z, va.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          acc[2 * k] += e * lo_f(vw[k]);
+          acc[2 * k + 1] += e * hi_f(vw[k]);
+        }
       }
     }
     const float inv = den > 0.f ? 1.f / den : 0.f;
@@ -306,9 +422,31 @@ extern "C" int ka_paged_decode(void* out, const void* q, const void* k_cache, co
                        scale_log2);
     KA_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(paged_decode_kernel, dim3(hkv, batch), dim3(256), 0, stream, static_cast<bf16_t*>(out),
+  hipLaunchKernelGGL(paged_decode_kernel<false>, dim3(hkv, batch), dim3(256), 0, stream, static_cast<bf16_t*>(out),
                      static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
-                     static_cast<const bf16_t*>(v_cache), block_tables, max_blocks, ctx_lens, hq, hkv, scale_log2);
+                     static_cast<const bf16_t*>(v_cache), block_tables, max_blocks, ctx_lens, hq, hkv, scale_log2,
+                     DecodeFuse{});
+  KA_CHECK_LAUNCH();
+}
+
+// Fused RoPE + KV append + paged decode attention (one query token per sequence; every
+// slot_mapping entry must be a valid slot).  qkv: bf16 [B, (hq + 2 hkv) * 128], or P: fp32 split-K
+// partials [split, B, (hq + 2 hkv) * 128] (qkv ignored when P is non-null).  ctx_lens include the
+// new token.
+extern "C" int ka_paged_decode_rope(void* out, const void* qkv, const float* P, int split, void* k_cache,
+                                    void* v_cache, const int* positions, const float* cos_sin,
+                                    const int* slot_mapping, const int* block_tables, int max_blocks,
+                                    const int* ctx_lens, int batch, int hq, int hkv, int head_dim, int block_size,
+                                    float scale, hipStream_t stream) {
+  if (batch <= 0) return 0;
+  // the rotated q rows + k are staged in the 4 KB P scratch: G + 1 <= 16 rows of 128
+  if (head_dim != HD || block_size != KBS || hq % hkv != 0 || hq / hkv > 15) return (int)hipErrorInvalidValue;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  DecodeFuse fz{static_cast<const bf16_t*>(qkv), P, split, (size_t)batch * (hq + 2 * hkv) * HD, positions, cos_sin,
+                slot_mapping, static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache)};
+  hipLaunchKernelGGL(paged_decode_kernel<true>, dim3(hkv, batch), dim3(256), 0, stream, static_cast<bf16_t*>(out),
+                     nullptr, static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), block_tables,
+                     max_blocks, ctx_lens, hq, hkv, scale_log2, fz);
   KA_CHECK_LAUNCH();
 }
 

@@ -13,6 +13,7 @@ token count, so decode steps can be captured into hipGraphs by the runner.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -58,6 +59,7 @@ class LlamaModel:
         dev = weights["embed"].device
         self.device = dev
         self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, device=dev)
+        self.fuse_decode_rope = os.environ.get("KA_FUSE_DECODE_ROPE", "1") == "1"
         self.layers = [self._layer(i) for i in range(cfg.num_layers)]
 
     def _layer(self, i):
@@ -82,21 +84,15 @@ class LlamaModel:
             # column-parallel projections: no all-reduce before their consumer, so a split-K plan
             # hands its fp32 partials to the RoPE / SiLU kernels, which reduce them on the fly
             qkv = ops.linear(x, L["wqkv"], defer_reduce=True)
-            q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, k_cache[li], v_cache[li],
-                                  self.hq, self.hkv, self.D)
-            if meta.is_decode:
-                a = ops.attention_decode(q, k_cache[li], v_cache[li], meta.block_tables, meta.ctx_lens, self.scale)
-            elif meta.num_decode:
-                # mixed step: prompt rows through the varlen prefill kernel, the leading decode rows
-                # through the decode kernel (a 1-row query would waste a 64-row prefill tile)
-                nd = meta.num_decode
-                a = ops.attention_prefill(q, k_cache[li], v_cache[li], meta.block_tables[nd:], meta.q_starts[nd:],
-                                          meta.ctx_lens[nd:], meta.max_q_len, self.scale, out=torch.empty_like(q))
-                ops.attention_decode(q[:nd], k_cache[li], v_cache[li], meta.block_tables[:nd], meta.ctx_lens[:nd],
-                                     self.scale, out=a[:nd])
+            if meta.is_decode and self.fuse_decode_rope:
+                # RoPE + KV append + attention in one kernel (the rotated q never goes to HBM)
+                a = ops.decode_attention_rope(qkv, meta.positions, self.cos_sin, meta.slot_mapping, k_cache[li],
+                                              v_cache[li], meta.block_tables, meta.ctx_lens, self.hq, self.hkv,
+                                              self.D, self.scale)
             else:
-                a = ops.attention_prefill(q, k_cache[li], v_cache[li], meta.block_tables, meta.q_starts,
-                                          meta.ctx_lens, meta.max_q_len, self.scale)
+                q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, k_cache[li],
+                                      v_cache[li], self.hq, self.hkv, self.D)
+                a = self._attention(q, meta, k_cache[li], v_cache[li])
             if 0 < meta.num_tokens < T and not meta.is_decode:
                 a[meta.num_tokens:].zero_()   # padding rows: no sequence's attention writes them
             # TP = 1: the projections feeding a norm leave their split-K partials to the fused
@@ -112,6 +108,20 @@ class LlamaModel:
             self.comm.all_reduce(h)
         x = ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
         return x.index_select(0, meta.logits_indices)
+
+    def _attention(self, q, meta: AttnMeta, kc: torch.Tensor, vc: torch.Tensor) -> torch.Tensor:
+        if meta.is_decode:
+            return ops.attention_decode(q, kc, vc, meta.block_tables, meta.ctx_lens, self.scale)
+        if meta.num_decode:
+            # mixed step: prompt rows through the varlen prefill kernel, the leading decode rows
+            # through the decode kernel (a 1-row query would waste a 64-row prefill tile)
+            nd = meta.num_decode
+            a = ops.attention_prefill(q, kc, vc, meta.block_tables[nd:], meta.q_starts[nd:], meta.ctx_lens[nd:],
+                                      meta.max_q_len, self.scale, out=torch.empty_like(q))
+            ops.attention_decode(q[:nd], kc, vc, meta.block_tables[:nd], meta.ctx_lens[:nd], self.scale, out=a[:nd])
+            return a
+        return ops.attention_prefill(q, kc, vc, meta.block_tables, meta.q_starts, meta.ctx_lens, meta.max_q_len,
+                                     self.scale)
 
     def logits(self, hidden_last: torch.Tensor) -> torch.Tensor:
         """Vocab-parallel logits of this rank: [S, V / tp] (bf16)."""

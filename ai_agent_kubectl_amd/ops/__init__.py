@@ -156,6 +156,29 @@ def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float,
     return out
 
 
+def decode_attention_rope(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, block_tables, ctx_lens,
+                          hq: int, hkv: int, d: int, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One decode token per sequence: RoPE + paged-KV append + paged attention in ONE kernel
+    (attention.hip, paged_decode_kernel<true>): the rotated queries never leave the chip and the new
+    token is merged from LDS.  `qkv` may be a `SplitK` (the QKV projection's fp32 partials).
+    Equivalent to `attention_decode(rope_kv_write(qkv, ...), ...)` (the CPU path)."""
+    lead = qkv.P if isinstance(qkv, SplitK) else qkv
+    if _ref(lead) or d != 128 or k_cache.shape[2] != 16 or hq % hkv or hq // hkv > 15:
+        q = rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq, hkv, d)
+        return attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, out=out)
+    lib = require()
+    B = ctx_lens.shape[0]
+    out = torch.empty((B, hq, d), dtype=k_cache.dtype, device=k_cache.device) if out is None else out
+    if isinstance(qkv, SplitK):
+        src, P, split = None, _p(qkv.P), qkv.split
+    else:
+        src, P, split = _p(qkv), None, 1
+    check(lib.ka_paged_decode_rope(_p(out), src, P, split, _p(k_cache), _p(v_cache), _p(positions), _p(cos_sin),
+                                   _p(slot_mapping), _p(block_tables), block_tables.shape[1], _p(ctx_lens), B, hq,
+                                   hkv, d, k_cache.shape[2], float(scale), _stream()), "paged_decode_rope")
+    return out
+
+
 def silu_mul(gu, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """silu(gate) * up of the fused gate_up output; `gu` may be a `SplitK` (reduction fused in)."""
     if isinstance(gu, SplitK):

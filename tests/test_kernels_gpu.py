@@ -120,6 +120,43 @@ def test_paged_decode_padding_rows_zero():
     assert out[1].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (4, 1)])
+@pytest.mark.parametrize("split", [0, 1, 4])
+def test_decode_attention_rope_fused(hq, hkv, split):
+    """RoPE + KV append + paged decode in one kernel == rope_kv_write then attention_decode (fp32
+    torch references), on bf16 qkv and on split-K partials; cache contents identical to the
+    unfused kernels'; a padding row (slot -1, ctx 0) writes nothing and returns zeros."""
+    d, nb = 128, 400
+    ctx_lens = [1, 2, 17, 100, 129, 33, 0]
+    S = len(ctx_lens)
+    bt = _tables(S, ctx_lens, nb, 16)
+    ctx = torch.tensor(ctx_lens, dtype=torch.int32, device=DEV)
+    btc = bt.cpu()
+    slots = torch.tensor([int(btc[s, (c - 1) // 16]) * 16 + (c - 1) % 16 if c > 0 else -1
+                          for s, c in enumerate(ctx_lens)], dtype=torch.int32, device=DEV)
+    pos = (ctx - 1).clamp(min=0)
+    cs = ref.rope_cos_sin(4096, d, 5e5, device=DEV)
+    width = (hq + 2 * hkv) * d
+    if split:
+        qkv = ops.SplitK(torch.randn(split, S, width, device=DEV), split)
+        qkv_bf = qkv.resolve()
+        P0 = qkv.P[0].clone()
+        for k in range(1, split):
+            P0 += qkv.P[k]
+        qkv_bf = P0.to(BF)                                   # the kernels' summation order
+    else:
+        qkv = qkv_bf = torch.randn(S, width, device=DEV, dtype=BF)
+    k1, v1 = _cache(nb, hkv)
+    k2, v2 = k1.clone(), v1.clone()
+    scale = d ** -0.5
+    got = ops.decode_attention_rope(qkv, pos, cs, slots, k1, v1, bt, ctx, hq, hkv, d, scale)
+    q = ops.rope_kv_write(qkv_bf, pos, cs, slots, k2, v2, hq, hkv, d)
+    want = ref.attention_decode(q, k2, v2, bt, ctx, scale)
+    assert torch.equal(k1, k2) and torch.equal(v1, v2)
+    close(got, want, atol=2e-2)
+    assert got[-1].abs().max().item() == 0
+
+
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 8)])
 @pytest.mark.parametrize("qlens,ctxs", [([90], [90]), ([7, 1, 33, 20], [71, 130, 33, 84]), ([130, 1], [130, 5])])
 def test_paged_prefill(hq, hkv, qlens, ctxs):
