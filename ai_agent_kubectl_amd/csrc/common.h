@@ -20,17 +20,19 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 KA_DEV float bf2f(bf16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
 
-KA_DEV bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);  // quiet NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
-}
+// fp32 -> bf16 round-to-nearest-even (torch's rounding) in one instruction: gfx950's
+// v_cvt_pk_bf16_f32 (the bit-twiddling form costs ~6 VALU ops per value, which showed up in the
+// VALU-bound softmax / epilogue loops)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+KA_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 
 // two packed bf16 <-> two floats
 KA_DEV float lo_f(uint32_t w) { return __uint_as_float(w << 16); }
 KA_DEV float hi_f(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
-KA_DEV uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+KA_DEV uint32_t pack2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
+}
 
 template <typename T>
 KA_DEV T wave_sum(T v) {
