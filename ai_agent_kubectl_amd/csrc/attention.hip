@@ -779,6 +779,9 @@ __global__ __launch_bounds__(64 * NW, 2) void paged_prefill_chunk_kernel(
   }
 }
 
+static int g_prefill_chunk = -1;   // -1: from KA_PREFILL_ATTN_CHUNK at first use
+extern "C" void ka_set_prefill_attn_chunk(int on) { g_prefill_chunk = on ? 1 : 0; }
+
 extern "C" int ka_paged_prefill(void* out, const void* q, const void* k_cache, const void* v_cache,
                                 const int* block_tables, int max_blocks, const int* q_starts, const int* ctx_lens,
                                 int num_seqs, int max_q_len, int hq, int hkv, int head_dim, int block_size,
@@ -787,9 +790,12 @@ extern "C" int ka_paged_prefill(void* out, const void* q, const void* k_cache, c
   const int G = hkv > 0 ? hq / hkv : 0;
   if (head_dim != HD || block_size != KBS || hq % hkv != 0 || G > 64 || 64 % G != 0) return (int)hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
-  // chunk-resident kernel (default): 8 waves when a sequence's rows exceed 64 (serving shape)
-  static const bool chunk = !getenv("KA_PREFILL_ATTN_TILE") || atoi(getenv("KA_PREFILL_ATTN_TILE")) == 0;
-  if (chunk && G <= 16) {
+  // chunk-resident kernel: opt-in (KA_PREFILL_ATTN_CHUNK=1).  It wins the isolated microbenchmark
+  // (81 vs 96 us/layer, scripts/bench_prefill_attn.py) but loses inside the real 8k-token prefill
+  // step (137 vs 106 us/layer, scripts/phase_profile.py), where the tile kernel's load/compute
+  // overlap across 32-token tiles matters more than one DMA burst per chunk.
+  if (g_prefill_chunk < 0) g_prefill_chunk = getenv("KA_PREFILL_ATTN_CHUNK") && atoi(getenv("KA_PREFILL_ATTN_CHUNK")) == 1;
+  if (g_prefill_chunk == 1 && G <= 16) {
     const int nw = max_q_len * G > 64 ? 8 : 4;
     const int tpt = nw * 16 / G;
     const int qtiles = (max_q_len + tpt - 1) / tpt;

@@ -228,11 +228,106 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ q_out
   }
 }
 
+// Prefill-sized RoPE + KV append: one workgroup per window of 16 consecutive tokens.  The per-token
+// kernel above writes the dim-major V cache ([blk][h][d][16]) as isolated 2-byte stores, one per
+// (token, dim), each to its own 32-byte segment — the write path, not the math, bounded it (~3x the
+// q/k/v bytes at 6 TB/s).  Here each head's 16 x 128 V tile is loaded with 16-B loads, transposed
+// through LDS, and stored with lanes = the 16 tokens of one dim, so the 16 stores of a wave quarter
+// hit consecutive addresses whenever the tokens' slots are consecutive (one 32-B segment per dim for
+// a block-aligned window, two when it straddles a block boundary).
+__global__ __launch_bounds__(256) void rope_kv_window_kernel(bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_cache,
+                                                             bf16_t* __restrict__ v_cache,
+                                                             const bf16_t* __restrict__ qkv,
+                                                             const int* __restrict__ positions,
+                                                             const float* __restrict__ cos_sin,
+                                                             const int* __restrict__ slot_mapping, int tokens, int hq,
+                                                             int hkv, const float* __restrict__ Pq, int split,
+                                                             size_t pstride) {
+  constexpr int d = 128, half = 64, bs = 16, W = 16;
+  __shared__ bf16_t vt[d][W + 2];   // [dim][token] (+2 pad: the transposing writes spread over banks)
+  const int t0 = blockIdx.x * W;
+  const int nt = min(W, tokens - t0);
+  const int qkv_stride = (hq + 2 * hkv) * d;
+  // ---- q / k rotation: (hq + hkv) heads x 16 items of 4 rotary pairs per token ----
+  const int per_tok = (hq + hkv) * 16;
+  for (int it = threadIdx.x; it < nt * per_tok; it += 256) {
+    const int j = it / per_tok, r = it % per_tok;
+    const int t = t0 + j;
+    const int h = r >> 4, i = (r & 15) * 4;
+    const bf16_t* row = qkv + (size_t)t * qkv_stride;
+    const float* prow = Pq ? Pq + (size_t)t * qkv_stride : nullptr;
+    const int slot = slot_mapping[t];
+    if (h >= hq && slot < 0) continue;
+    const float* cs = cos_sin + (size_t)positions[t] * d;
+    const uint2 a = ld4(row, prow, split, pstride, (size_t)h * d + i);
+    const uint2 b = ld4(row, prow, split, pstride, (size_t)h * d + i + half);
+    const float4 c = *reinterpret_cast<const float4*>(cs + i);
+    const float4 sn = *reinterpret_cast<const float4*>(cs + half + i);
+    const float x1[4] = {lo_f(a.x), hi_f(a.x), lo_f(a.y), hi_f(a.y)};
+    const float x2[4] = {lo_f(b.x), hi_f(b.x), lo_f(b.y), hi_f(b.y)};
+    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+    float o1[4], o2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o1[k] = x1[k] * cc[k] - x2[k] * ss[k];
+      o2[k] = x2[k] * cc[k] + x1[k] * ss[k];
+    }
+    bf16_t* dst = h < hq ? q_out + ((size_t)t * hq + h) * d
+                         : k_cache + (((size_t)(slot / bs) * hkv + (h - hq)) * bs + slot % bs) * d;
+    *reinterpret_cast<uint2*>(dst + i) = make_uint2(pack2(o1[0], o1[1]), pack2(o1[2], o1[3]));
+    *reinterpret_cast<uint2*>(dst + i + half) = make_uint2(pack2(o2[0], o2[1]), pack2(o2[2], o2[3]));
+  }
+  // ---- V: per kv head, 16 tokens x 128 dims through LDS ----
+  const int lj = threadIdx.x & 15;                  // store phase: lane -> token
+  const int ls = slot_mapping[t0 + min(lj, nt - 1)];
+  const bool lvalid = lj < nt && ls >= 0;
+  const size_t vbase = (size_t)(hq + hkv) * d;
+  for (int h = 0; h < hkv; ++h) {
+    {   // load phase: thread -> (token, 8-dim chunk)
+      const int j = threadIdx.x >> 4, c = (threadIdx.x & 15) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (j < nt) {
+        const int t = t0 + j;
+        v = ld8(qkv + (size_t)t * qkv_stride, Pq ? Pq + (size_t)t * qkv_stride : nullptr, split, pstride,
+                vbase + (size_t)h * d + c);
+      }
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        vt[c + 2 * k][j] = (bf16_t)w[k];
+        vt[c + 2 * k + 1][j] = (bf16_t)(w[k] >> 16);
+      }
+    }
+    __syncthreads();
+    if (lvalid) {
+      bf16_t* dst = v_cache + ((size_t)(ls / bs) * hkv + h) * d * bs + ls % bs;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int dim = (threadIdx.x >> 4) + 16 * k;
+        dst[(size_t)dim * bs] = vt[dim][lj];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+static bool rope_window_ok(int tokens, int d, int bs) {
+  static const int min_tok = getenv("KA_ROPE_WINDOW_MIN") ? atoi(getenv("KA_ROPE_WINDOW_MIN")) : 64;
+  return tokens >= min_tok && d == 128 && bs == 16;
+}
+
 extern "C" int ka_rope_kv(void* q_out, void* k_cache, void* v_cache, const void* qkv, const int* positions,
                           const float* cos_sin, const int* slot_mapping, int tokens, int hq, int hkv, int d, int bs,
                           hipStream_t stream) {
   if (tokens <= 0) return 0;
   if (d % 16 != 0) return (int)hipErrorInvalidValue;
+  if (rope_window_ok(tokens, d, bs)) {
+    hipLaunchKernelGGL(rope_kv_window_kernel, dim3((tokens + 15) / 16), dim3(256), 0, stream,
+                       static_cast<bf16_t*>(q_out), static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache),
+                       static_cast<const bf16_t*>(qkv), positions, cos_sin, slot_mapping, tokens, hq, hkv, nullptr,
+                       0, (size_t)0);
+    KA_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(rope_kv_kernel, dim3(tokens), dim3(256), 0, stream, static_cast<bf16_t*>(q_out),
                      static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache),
                      static_cast<const bf16_t*>(qkv), positions, cos_sin, slot_mapping, hq, hkv, d, bs, nullptr, 0,
@@ -247,6 +342,13 @@ extern "C" int ka_rope_kv_splitk(void* q_out, void* k_cache, void* v_cache, cons
   if (tokens <= 0) return 0;
   if (d % 16 != 0 || split < 1) return (int)hipErrorInvalidValue;
   const size_t pstride = (size_t)tokens * (hq + 2 * hkv) * d;
+  if (rope_window_ok(tokens, d, bs)) {
+    hipLaunchKernelGGL(rope_kv_window_kernel, dim3((tokens + 15) / 16), dim3(256), 0, stream,
+                       static_cast<bf16_t*>(q_out), static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache),
+                       nullptr, positions, cos_sin, slot_mapping, tokens, hq, hkv, static_cast<const float*>(P),
+                       split, pstride);
+    KA_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(rope_kv_kernel, dim3(tokens), dim3(256), 0, stream, static_cast<bf16_t*>(q_out),
                      static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache), nullptr, positions, cos_sin,
                      slot_mapping, hq, hkv, d, bs, static_cast<const float*>(P), split, pstride);

@@ -140,6 +140,11 @@ def attention_prefill(q, k_cache, v_cache, block_tables, q_starts, ctx_lens, max
     return out
 
 
+def set_prefill_attention_chunk(on: bool) -> None:
+    """Select the chunk-resident prefill attention kernel (opt-in; default: the tile pipeline)."""
+    require().ka_set_prefill_attn_chunk(1 if on else 0)
+
+
 def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float,
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if _ref(q):

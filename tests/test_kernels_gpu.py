@@ -51,12 +51,19 @@ def _cache(nb, hkv, bs=16, d=128):
 
 
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1)])
-def test_rope_kv_write(hq, hkv):
-    T, d = 23, 128
+@pytest.mark.parametrize("T", [23, 301])
+def test_rope_kv_write(hq, hkv, T):
+    """T >= 64 takes the 16-token window kernel (V transposed through LDS)."""
+    d = 128
     qkv = torch.randn(T, (hq + 2 * hkv) * d, device=DEV, dtype=BF)
     cs = ref.rope_cos_sin(4096, d, 5e5, device=DEV)
     pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
-    slots = torch.randperm(64 * 16, device=DEV)[:T].to(torch.int32)
+    perm = torch.randperm(64 * 16)
+    if T > 64:   # unique slots with a run of 100 consecutive ones (straddling blocks) at rows 40..139
+        run = torch.arange(333, 433)
+        rest = perm[~torch.isin(perm, run)]
+        perm = torch.cat([rest[:40], run, rest[40:]])
+    slots = perm[:T].to(DEV, torch.int32)
     slots[3] = -1
     k1, v1 = _cache(64, hkv)
     k2, v2 = k1.clone(), v1.clone()
@@ -159,7 +166,10 @@ def test_decode_attention_rope_fused(hq, hkv, split):
 
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 8)])
 @pytest.mark.parametrize("qlens,ctxs", [([90], [90]), ([7, 1, 33, 20], [71, 130, 33, 84]), ([130, 1], [130, 5])])
-def test_paged_prefill(hq, hkv, qlens, ctxs):
+@pytest.mark.parametrize("chunk", [False, True])
+def test_paged_prefill(hq, hkv, qlens, ctxs, chunk):
+    """Both prefill attention kernels: the tile pipeline (default) and the chunk-resident one."""
+    ops.set_prefill_attention_chunk(chunk)
     S = len(qlens)
     kc, vc = _cache(200, hkv)
     bt = _tables(S, ctxs, 200, 16)
@@ -168,7 +178,10 @@ def test_paged_prefill(hq, hkv, qlens, ctxs):
     starts = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
     ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
     scale = 128 ** -0.5
-    got = ops.attention_prefill(q, kc, vc, bt, starts, ctx, max(qlens), scale)
+    try:
+        got = ops.attention_prefill(q, kc, vc, bt, starts, ctx, max(qlens), scale)
+    finally:
+        ops.set_prefill_attention_chunk(False)
     want = ref.attention_prefill(q, kc, vc, bt, starts, ctx, scale)
     close(got, want, atol=2e-2)
 
@@ -263,10 +276,11 @@ def test_rmsnorm_fused_splitk_reduce(rows, hidden, split):
     close(r1, r2, atol=1e-2)
 
 
-def test_rope_and_silu_consume_splitk_partials_exactly():
+@pytest.mark.parametrize("T", [37, 150])
+def test_rope_and_silu_consume_splitk_partials_exactly(T):
     """RoPE+KV append and SiLU·mul summing the fp32 split-K partials themselves give bit-identical
-    results to the reduce kernel followed by the bf16 op."""
-    T, hq, hkv, d, split = 37, 32, 8, 128, 4
+    results to the reduce kernel followed by the bf16 op (T = 150: the 16-token window kernel)."""
+    hq, hkv, d, split = 32, 8, 128, 4
     P = torch.randn(split, T, (hq + 2 * hkv) * d, device=DEV)
     red = ops.SplitK(P, split).resolve()                         # torch sum in the same order...
     want_bf = P[0].clone()
