@@ -36,7 +36,7 @@ class LLMEngine:
         self.bm = make_block_manager(runner.num_blocks, runner.block_size, enable_prefix_caching=prefix_caching)
         self.scheduler = Scheduler(self.bm, max_batch=max_batch, max_batched_tokens=max_batched_tokens,
                                    max_model_len=max_model_len,
-                                   gather_max_s=float(os.environ.get("KA_GATHER_MAX_MS", "5")) / 1000.0,
+                                   gather_max_s=float(os.environ.get("KA_GATHER_MAX_MS", "15")) / 1000.0,
                                    gather_quiet_s=float(os.environ.get("KA_GATHER_QUIET_MS", "1.5")) / 1000.0)
         self.metrics = metrics
         self._inbox: "queue.SimpleQueue" = queue.SimpleQueue()

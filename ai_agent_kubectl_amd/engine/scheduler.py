@@ -40,7 +40,8 @@ class Scheduler:
     def __init__(self, block_manager: BlockManager, max_batch: int = 256, max_batched_tokens: int = 8192,
                  max_model_len: int = 4096, mix_decode_into_prefill: bool = True,
                  prefill_max_wait_s: Optional[float] = None, prefill_min_frac: Optional[float] = None,
-                 partial_block_reuse: bool = True, gather_max_s: float = 0.0, gather_quiet_s: float = 0.0015):
+                 partial_block_reuse: bool = True, gather_max_s: float = 0.0, gather_quiet_s: float = 0.0015,
+                 hold_steps: Optional[int] = None, hold_max_s: Optional[float] = None):
         # Prefill batching under continuous arrivals: a prefill step is an eager (non-graph) step,
         # so while sequences are decoding, new arrivals are admitted together — when at least
         # max(4, prefill_min_frac * running) are waiting or the oldest has waited
@@ -57,6 +58,25 @@ class Scheduler:
         # small, GEMM-inefficient first step followed by the rest
         self.gather_max_s = gather_max_s
         self.gather_quiet_s = gather_quiet_s
+        self._idle_since = 0.0     # when the running set last became empty
+        self._drained = 0          # sequences that left in the step that emptied the running set
+        # after a large wave drains, its clients' next requests come back as a burst spread over
+        # the API process's turnaround (~10 ms for 256 requests): a longer quiet gap keeps them in
+        # one prefill; a lone request to an idle engine still waits only gather_quiet_s
+        self.burst_quiet_s = float(os.environ.get("KA_GATHER_BURST_QUIET_MS", "4")) / 1000.0
+        self.burst_min = int(os.environ.get("KA_GATHER_BURST_MIN", "32"))
+        # Wave merging: arrivals that find every running sequence within `hold_steps` decode steps
+        # of its token limit wait for that batch to drain (then gather with its clients' next
+        # requests) instead of starting a second, half-size prefill wave beside it.  Two offset
+        # waves cost a whole extra prefill step per cycle: at 256 requests of ~31 new tokens two
+        # ~4k-token steps take 2 x 58 ms against 96 ms for one 8k-token step
+        # (profiles/phase_profile_c256.txt).  Bounded by hold_max_s of waiting.
+        if hold_steps is None:
+            hold_steps = int(os.environ.get("KA_PREFILL_HOLD_STEPS", "8"))
+        if hold_max_s is None:
+            hold_max_s = float(os.environ.get("KA_PREFILL_HOLD_MAX_MS", "100")) / 1000.0
+        self.hold_steps = hold_steps
+        self.hold_max_s = hold_max_s
         self.bm = block_manager
         self.max_batch = max_batch
         self.max_batched_tokens = max_batched_tokens
@@ -113,13 +133,30 @@ class Scheduler:
         return admitted
 
     def gathering(self) -> bool:
-        """Idle engine, requests still streaming in: hold the admission for a moment."""
-        if self.running or not self.waiting or self.gather_max_s <= 0:
+        """Idle engine, requests still streaming in: hold the admission for a moment.  The window
+        opens at the later of the first waiting arrival and the moment the engine went idle (held
+        requests wait for the drained batch's clients to come back); it closes after a quiet gap of
+        gather_quiet_s once something has arrived since then, or after gather_max_s."""
+        if self.running or not self.waiting or self.gather_max_s <= 0 or len(self.waiting) >= self.max_batch:
             return False
         now = time.perf_counter()
-        return (now - self.waiting[-1].t_arrival < self.gather_quiet_s
-                and now - self.waiting[0].t_arrival < self.gather_max_s
-                and len(self.waiting) < self.max_batch)
+        if now - max(self.waiting[0].t_arrival, self._idle_since) >= self.gather_max_s:
+            return False
+        newest = self.waiting[-1].t_arrival
+        if newest < self._idle_since:
+            return True
+        quiet = self.gather_quiet_s
+        if self._drained >= self.burst_min and newest - self._idle_since < self.gather_max_s:
+            quiet = max(quiet, self.burst_quiet_s)
+        return now - newest < quiet
+
+    def _holding(self) -> bool:
+        if self.hold_steps <= 0 or len(self.running) + len(self.waiting) > self.max_batch:
+            return False
+        if time.perf_counter() - self.waiting[0].t_arrival >= self.hold_max_s:
+            return False
+        left = max(s.params.max_new_tokens - s.num_generated for s in self.running)
+        return left <= self.hold_steps
 
     def _should_prefill(self) -> bool:
         if not self.waiting:
@@ -127,6 +164,8 @@ class Scheduler:
         if not self.running:
             return not self.gathering()
         if len(self.running) >= self.max_batch:
+            return False
+        if self._holding():
             return False
         if len(self.waiting) >= max(4, int(self.prefill_min_frac * len(self.running))):
             return True
@@ -176,4 +215,8 @@ class Scheduler:
         for s in batch.prefill_seqs:
             if not s.finished:
                 self.running.append(s)
+        before = len(self.running)
         self.running = [s for s in self.running if not s.finished]
+        if not self.running and before:
+            self._idle_since = time.perf_counter()
+            self._drained = before

@@ -8,6 +8,7 @@ def run_staggered(eng, prompts, params, forced):
     run_staggered.mixed = 0
     wait, eng.scheduler.prefill_max_wait_s = eng.scheduler.prefill_max_wait_s, 0.0
     gather, eng.scheduler.gather_max_s = eng.scheduler.gather_max_s, 0.0
+    hold, eng.scheduler.hold_steps = eng.scheduler.hold_steps, 0
     try:
         pending = list(prompts)
         while pending or any(not s.finished for s in seqs):
@@ -22,4 +23,5 @@ def run_staggered(eng, prompts, params, forced):
     finally:
         eng.scheduler.prefill_max_wait_s = wait
         eng.scheduler.gather_max_s = gather
+        eng.scheduler.hold_steps = hold
     return [s.output_ids for s in seqs]

@@ -432,7 +432,7 @@ def test_scheduler_gathers_a_streaming_burst_when_idle():
 
 def test_scheduler_batches_prefills_while_decoding():
     bm = BlockManager(64, 4, enable_prefix_caching=False)
-    sch = Scheduler(bm, max_batch=16, max_batched_tokens=1000, prefill_max_wait_s=10.0)
+    sch = Scheduler(bm, max_batch=16, max_batched_tokens=1000, prefill_max_wait_s=10.0, hold_steps=0)
     first = _seq(8)
     sch.add(first)
     b = sch.schedule()
@@ -445,3 +445,49 @@ def test_scheduler_batches_prefills_while_decoding():
     sch.add(_seq(8))
     b = sch.schedule()
     assert len(b.prefill_seqs) == 4           # batch of 4 admitted together (+1 decode row mixed)
+
+
+def test_scheduler_holds_arrivals_until_the_running_wave_drains():
+    """Wave merging: arrivals that find every running sequence within hold_steps of its token
+    limit wait; once the wave drains, the gather window opens at the idle moment and keeps the
+    held requests until the drained wave's clients come back (or gather_max_s)."""
+    from ai_agent_kubectl_amd.engine.block_manager import BlockManager
+    from ai_agent_kubectl_amd.engine.scheduler import Scheduler
+    import time as _t
+    sch = Scheduler(BlockManager(256, 16), max_batch=8, max_batched_tokens=4096, gather_max_s=0.0,
+                    gather_quiet_s=0.01, hold_steps=4, hold_max_s=10.0, prefill_min_frac=0.0,
+                    prefill_max_wait_s=0.0)
+    p = SamplingParams(max_new_tokens=6, ignore_eos=True)
+    first = [Sequence(prompt_ids=list(range(i, i + 20)), params=p) for i in range(3)]
+    for s in first:
+        sch.add(s)
+    b = sch.schedule()
+    assert b.prefill_seqs == first
+    for s in first:
+        s.output_ids.append(1)
+    sch.on_step_done(b)
+    # far from the limit (5 tokens left > hold 4): an arrival is admitted as a mixed step
+    late = Sequence(prompt_ids=list(range(100, 120)), params=p)
+    sch.add(late)
+    assert sch.schedule().prefill_seqs == [late]
+    sch.running.append(late)
+    late.status = first[0].status
+    for s in first + [late]:
+        s.output_ids.extend([1] * 4)
+    # every running sequence within 4 tokens of its limit -> hold the next arrival
+    held = Sequence(prompt_ids=list(range(200, 220)), params=p)
+    sch.add(held)
+    b = sch.schedule()
+    assert b.is_decode and held in sch.waiting
+    # the wave drains: idle from now on; the held request alone does not end the gather window
+    sch.gather_max_s = 0.05
+    for s in first + [late]:
+        s.status = SeqStatus.FINISHED
+    sch.on_step_done(b)
+    assert not sch.running and sch.gathering()
+    comeback = Sequence(prompt_ids=list(range(300, 320)), params=p)
+    sch.add(comeback)
+    assert sch.gathering()                          # newest arrival is fresh
+    _t.sleep(0.02)
+    assert not sch.gathering()                      # quiet gap passed: admit both together
+    assert sch.schedule().prefill_seqs == [held, comeback]

@@ -111,6 +111,7 @@ def test_mixed_step_split_attention_hidden_matches_unsplit():
     sch, r = eng.scheduler, eng.runner
     sch.prefill_max_wait_s = 0.0
     sch.gather_max_s = 0.0
+    sch.hold_steps = 0
     with torch.inference_mode():
         first = [Sequence(prompt_ids=be.prompt_ids(q), params=params, forced_prefix=list(be._forced))
                  for q in QUERIES[:2]]
