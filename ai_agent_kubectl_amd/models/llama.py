@@ -8,7 +8,8 @@ forward pass of SURVEY.md §3.6 —
 
 Tensor parallelism is Megatron-style (column-parallel QKV / gate_up, row-parallel O / down,
 vocab-parallel LM head); Mixtral experts are sharded over the same group (EP = TP group) and
-combined by the all-reduce that follows the MoE block.  Every op is shape-static for a given
+combined by the all-reduce that follows the MoE block (decode) or by the all-to-all dispatch /
+combine of `moe_alltoall` (eager prefill, models/moe.py).  Every op is shape-static for a given
 token count, so decode steps can be captured into hipGraphs by the runner.
 """
 from __future__ import annotations
@@ -101,11 +102,13 @@ class LlamaModel:
             h = ops.linear(a.view(T, self.hq * self.D), L["wo"], defer_reduce=fuse)
             self.comm.all_reduce(h)
             x = ops.rmsnorm(h, L["ln2"], eps, residual=residual)
+            combined = False
             if cfg.is_moe:
-                h = moe_forward(x, L, cfg, self.ep_rank, self.ep_size, meta.is_decode)
+                h, combined = moe_forward(x, L, cfg, self.ep_rank, self.ep_size, meta.is_decode, self.comm)
             else:
                 h = ops.linear(ops.silu_mul(ops.linear(x, L["w13"], defer_reduce=True)), L["w2"], defer_reduce=fuse)
-            self.comm.all_reduce(h)
+            if not combined:
+                self.comm.all_reduce(h)
         x = ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
         return x.index_select(0, meta.logits_indices)
 

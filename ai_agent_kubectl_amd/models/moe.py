@@ -1,9 +1,20 @@
 """Mixtral sparse MoE block (K11 router + K12 expert GEMMs), expert-parallel.
 
-Each rank owns `E / ep` experts.  Token activations are replicated across the TP/EP group (the
-attention all-reduce already produced them), every rank computes the contribution of its own
-experts, and the block output is summed across ranks by the all-reduce the caller issues right
-after (`LlamaModel.forward`) — the EP combine costs no extra collective.
+Each rank owns `E / ep` experts.  Token activations arrive replicated across the TP/EP group (the
+attention all-reduce already produced them).  Two ways to combine the experts:
+
+* all-reduce combine (decode, graph-captured): every rank computes the contribution of its own
+  experts for every token and the block output is summed by the all-reduce the caller issues
+  right after (`LlamaModel.forward`).  Decode messages are a few KB-MB and latency-bound, and the
+  collective is shape-static, so it sits inside the decode hipGraphs;
+* all-to-all dispatch / combine (`moe_alltoall`, eager prefill when EP > 1 and
+  MOE_DISPATCH=a2a, the default): each rank routes only its 1/ep token shard, sends every
+  (token, slot) row to the rank owning its expert (A5 dispatch, `all_to_all_single` with exact
+  split sizes), runs its local experts on what it received, sends the rows back (A5 combine),
+  applies the router weights at the source and all-gathers the shards.  Per rank that moves
+  2·k·T·H/ep (dispatch + combine) + T·H·(ep-1)/ep (all-gather) instead of the ring all-reduce's
+  2·T·H·(ep-1)/ep, and the router / top-k work is divided by ep.  xGMI is point-to-point, so the
+  all-to-all uses every link at once rather than one ring neighbour.
 
 Execution shapes:
 * `moe_hip` (decode, T*k <= 512): device-side routing lists, grouped weight-streaming MFMA GEMMs
@@ -14,6 +25,8 @@ Execution shapes:
 * `moe_batched`: dense all-experts formulation, kept as a second reference.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn.functional as F
@@ -67,7 +80,70 @@ def moe_hip(x, L, cfg, ep_rank, ep_size):
     return ops.moe_experts(x, L["w13"], L["w2"], w, ids, ep_rank * el)
 
 
-def moe_forward(x, L, cfg, ep_rank, ep_size, is_decode: bool):
+def _local_experts(xr, er, L, e0):
+    """FFN_{er[r]}(xr[r]) for received rows whose expert id er[r] (global) is one of this rank's;
+    unweighted (the source applies the router weight).  [R, H] in xr's dtype."""
+    R = xr.shape[0]
+    if R == 0:
+        return xr.new_zeros((0, xr.shape[1]))
+    w13, w2 = L["w13"], L["w2"]
+    if xr.is_cuda and not ops._FORCE_REF and R <= MOE_HIP_MAX_ROWS:
+        ones = torch.ones((R, 1), dtype=torch.float32, device=xr.device)
+        return ops.moe_experts(xr, w13, w2, ones, er.view(R, 1).to(torch.int32), e0)
+    out = torch.empty_like(xr)
+    el = er.long() - e0
+    for e in range(w13.shape[0]):
+        rows = torch.nonzero(el == e, as_tuple=False).squeeze(1)
+        if rows.numel():
+            out.index_copy_(0, rows, F.linear(ops.silu_mul(F.linear(xr.index_select(0, rows), w13[e])), w2[e]))
+    return out
+
+
+def moe_alltoall(x, L, cfg, comm):
+    """Token-sharded MoE with all-to-all dispatch / combine (A5).  `x` [T, H] is replicated on every
+    rank of `comm`; returns the full MoE output [T, H], replicated (the caller must NOT all-reduce).
+    Split sizes are exchanged first (one small all-to-all + host read), so this is the eager path."""
+    p, r = comm.world_size, comm.rank
+    T, H = x.shape
+    k, E = cfg.top_k, cfg.num_experts
+    el = E // p
+    ts = -(-T // p)                                                  # tokens per shard (last may be short)
+    lo, hi = min(T, r * ts), min(T, (r + 1) * ts)
+    xs = x[lo:hi]
+    t_loc = hi - lo
+    w, ids = ops.moe_topk(ops.linear(xs, L["router"]), k) if t_loc else (
+        torch.zeros((0, k), dtype=torch.float32, device=x.device), torch.zeros((0, k), dtype=torch.int32,
+                                                                               device=x.device))
+    flat_ids = ids.reshape(-1).long()                                 # [t_loc * k]
+    dest = torch.div(flat_ids, el, rounding_mode="floor")
+    order = torch.argsort(dest, stable=True)                         # rows grouped by destination rank
+    tok = torch.div(order, k, rounding_mode="floor")
+    send_counts = torch.bincount(dest, minlength=p).to(torch.int64)
+    recv_counts = comm.all_to_all_single(send_counts)
+    sc, rc = send_counts.tolist(), recv_counts.tolist()              # host split sizes (eager path)
+    send_x = xs.index_select(0, tok)
+    send_e = flat_ids.index_select(0, order).to(torch.int32)
+    recv_x = comm.all_to_all_single(send_x, rc, sc)                  # A5 dispatch
+    recv_e = comm.all_to_all_single(send_e, rc, sc)
+    y = _local_experts(recv_x, recv_e, L, r * el)
+    back = comm.all_to_all_single(y, sc, rc)                         # A5 combine: rows return in `order`
+    contrib = back.float() * w.reshape(-1).index_select(0, order).unsqueeze(1)
+    out = torch.zeros((ts, H), dtype=torch.float32, device=x.device)
+    out.index_add_(0, tok, contrib)
+    full = comm.all_gather(out.to(x.dtype))                          # [p, ts, H]
+    return full.reshape(p * ts, H)[:T]
+
+
+def moe_dispatch_mode() -> str:
+    return os.environ.get("MOE_DISPATCH", "a2a")
+
+
+def moe_forward(x, L, cfg, ep_rank, ep_size, is_decode: bool, comm=None):
+    """Returns (out, combined): `combined` is True when the output is already summed over the EP
+    group (all-to-all path) and the caller's all-reduce must be skipped."""
+    if (comm is not None and ep_size > 1 and not is_decode and moe_dispatch_mode() == "a2a"
+            and not (x.is_cuda and torch.cuda.is_current_stream_capturing())):
+        return moe_alltoall(x, L, cfg, comm), True
     if x.is_cuda and not ops._FORCE_REF and x.shape[0] * cfg.top_k <= MOE_HIP_MAX_ROWS:
-        return moe_hip(x, L, cfg, ep_rank, ep_size)
-    return moe_grouped(x, L, cfg, ep_rank, ep_size)
+        return moe_hip(x, L, cfg, ep_rank, ep_size), False
+    return moe_grouped(x, L, cfg, ep_rank, ep_size), False

@@ -396,3 +396,23 @@ def test_moe_experts_vs_reference(T, e0, el):
                 a = (torch.nn.functional.silu(g[:I]) * g[I:]).to(BF).float()
                 want[t] += float(tw[t, j]) * (a @ w2[e].float().t())
     close(got, want, atol=5e-2, rtol=5e-2)
+
+
+@pytest.mark.parametrize("R", [1, 29, 200])
+def test_moe_local_experts_received_rows(R):
+    """Receive side of the A5 all-to-all (models/moe.py `_local_experts`): rows tagged with a global
+    expert id, unweighted FFN of this rank's experts through the HIP grouped GEMMs."""
+    from ai_agent_kubectl_amd.models.moe import _local_experts
+    H, I, el, e0 = 512, 384, 4, 4
+    x = torch.randn(R, H, device=DEV, dtype=BF)
+    L = {"w13": (torch.randn(el, 2 * I, H, device=DEV) * 0.05).to(BF),
+         "w2": (torch.randn(el, H, I, device=DEV) * 0.05).to(BF)}
+    er = torch.randint(e0, e0 + el, (R,), device=DEV, dtype=torch.int32)
+    got = _local_experts(x, er, L, e0)
+    want = torch.empty(R, H, device=DEV)
+    for r in range(R):
+        e = int(er[r]) - e0
+        g = x[r].float() @ L["w13"][e].float().t()
+        a = (torch.nn.functional.silu(g[:I]) * g[I:]).to(BF).float()
+        want[r] = a @ L["w2"][e].float().t()
+    close(got, want, atol=5e-2, rtol=5e-2)
