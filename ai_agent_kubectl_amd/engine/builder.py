@@ -95,7 +95,26 @@ def build_engine(opts: EngineOptions, comm=None, metrics=None) -> LLMEngine:
     eng = LLMEngine(runner, tok, max_batch=opts.max_batch, max_batched_tokens=opts.max_batched_tokens,
                     max_model_len=opts.max_model_len, prefix_caching=opts.prefix_caching, metrics=metrics)
     eng.options = opts
+    if comm is not None and opts.tp_size > 1:
+        _attach_liveness(eng, opts)
     eng.build_seconds = time.perf_counter() - t0
     logger.info("engine built: model=%s tp=%d blocks=%d (%.1f GiB KV) in %.1fs", cfg.name, opts.tp_size,
                 num_blocks, num_blocks * per_block / 2**30, eng.build_seconds)
     return eng
+
+
+def _attach_liveness(eng: LLMEngine, opts: EngineOptions) -> None:
+    """TP/EP > 1: workers beat into the rendezvous store, rank 0 watches (parallel/watchdog.py)."""
+    from ..parallel.watchdog import Heartbeat, Watchdog, default_store
+
+    store = default_store()
+    if store is None:
+        return
+    interval = float(os.environ.get("WORKER_HEARTBEAT_INTERVAL_S", "1"))
+    if opts.tp_rank != 0:
+        eng.heartbeat = Heartbeat(store, opts.tp_rank, interval).start()
+        return
+    eng.watchdog = Watchdog(store, range(1, opts.tp_size), eng.mark_unhealthy,
+                            hb_timeout=float(os.environ.get("WORKER_HEARTBEAT_TIMEOUT_S", "30")),
+                            step_timeout=float(os.environ.get("ENGINE_STEP_TIMEOUT_S", "120")),
+                            interval=interval, step_started=lambda: eng.step_t0)

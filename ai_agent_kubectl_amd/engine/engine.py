@@ -52,6 +52,13 @@ class LLMEngine:
         self._inflight = None
         self.chained_steps = 0
         self.idle_s = 0.0          # time the loop slept with no work (waiting for requests)
+        self.step_t0: Optional[float] = None   # perf_counter at the start of the running step
+        self.watchdog = None       # parallel/watchdog.py (TP/EP > 1, rank 0)
+
+    def mark_unhealthy(self, reason: str) -> None:
+        """Watchdog verdict (worker heartbeat lost / step stalled): new requests get 503."""
+        self.healthy = False
+        self.last_error = RuntimeError(reason)
 
     # ------------------------------------------------------------------------------------------
     def start(self) -> None:
@@ -63,8 +70,12 @@ class LLMEngine:
             self._stop.clear()
             self._thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
             self._thread.start()
+        if self.watchdog is not None and self.watchdog._thread is None:
+            self.watchdog.start()
 
     def shutdown(self) -> None:
+        if self.watchdog is not None:
+            self.watchdog.stop()
         self._stop.set()
         self._wake.set()
         if self._thread is not None:
@@ -247,11 +258,14 @@ class LLMEngine:
         tprof = self._torch_profile_hook()
         while not self._stop.is_set():
             try:
+                self.step_t0 = time.perf_counter()
                 n = self.step()
+                self.step_t0 = None
                 if tprof is not None:
                     tprof(n)
             except Exception as e:  # engine fault: fail in-flight requests, stay alive but unhealthy
                 logger.exception("engine step failed")
+                self.step_t0 = None
                 self.healthy = False
                 self.last_error = e
                 self._fail_all(e)
