@@ -54,6 +54,19 @@ class VirtualComm:
                 parent._bar.wait()
                 return out
 
+            def all_to_all_single(self, t, out_splits=None, in_splits=None):
+                w = parent.world_size
+                in_splits = list(in_splits) if in_splits is not None else [t.shape[0] // w] * w
+                parent._slots[rank] = (t, in_splits)
+                parent._bar.wait()
+                pieces = []
+                for j in range(w):
+                    tj, sj = parent._slots[j]
+                    off = sum(sj[:rank])
+                    pieces.append(tj[off:off + sj[rank]].clone())
+                parent._bar.wait()
+                return torch.cat(pieces)
+
             def broadcast(self, t, src=0):
                 return t
 
