@@ -54,6 +54,7 @@ class LLMEngine:
         self.idle_s = 0.0          # time the loop slept with no work (waiting for requests)
         self.step_t0: Optional[float] = None   # perf_counter at the start of the running step
         self.watchdog = None       # parallel/watchdog.py (TP/EP > 1, rank 0)
+        self._ar_bytes_seen = 0
 
     def mark_unhealthy(self, reason: str) -> None:
         """Watchdog verdict (worker heartbeat lost / step stalled): new requests get 503."""
@@ -202,6 +203,14 @@ class LLMEngine:
             m.llm_batch_size.set(len(batch.seqs))
             m.llm_queue_depth.set(len(self.scheduler.waiting))
             m.llm_kv_blocks_used.set(self.bm.num_used)
+            timer = getattr(self.runner.comm, "timer", None)
+            if timer is not None and hasattr(m, "rccl_allreduce"):
+                for sec in timer.drain():
+                    m.rccl_allreduce.observe(sec)
+                nbytes = self.runner.comm.allreduce_bytes
+                if nbytes > self._ar_bytes_seen:
+                    m.rccl_allreduce_bytes.inc(nbytes - self._ar_bytes_seen)
+                    self._ar_bytes_seen = nbytes
         return len(batch.seqs)
 
     def _fail_all(self, err: BaseException) -> None:

@@ -74,6 +74,12 @@ class ServiceMetrics:
         self.llm_queue_depth = Gauge("llm_queue_depth", "Requests waiting for the engine.", registry=r)
         self.llm_kv_blocks_used = Gauge("llm_kv_blocks_used", "Paged-KV blocks in use.", registry=r)
         self.llm_errors = Counter("llm_errors_total", "LLM failures by kind.", ("kind",), registry=r)
+        self.rccl_allreduce = Histogram("rccl_allreduce_seconds",
+                                        "Eager tensor-parallel all-reduce time (RCCL or one-shot IPC kernel).",
+                                        buckets=(1e-5, 2.5e-5, 5e-5, 1e-4, 2.5e-4, 5e-4, 1e-3, 2.5e-3, 5e-3, 1e-2,
+                                                 5e-2), registry=r)
+        self.rccl_allreduce_bytes = Counter("rccl_allreduce_bytes", "Bytes all-reduced across the TP group "
+                                            "(eager and graph-captured calls at capture time).", registry=r)
         self.execute_duration = Histogram("execute_duration_seconds", "kubectl subprocess wall time.",
                                           buckets=HIGHR_BUCKETS, registry=r)
         self.loop_lag = Histogram("event_loop_lag_seconds", "asyncio event-loop scheduling delay (50 ms probe).",

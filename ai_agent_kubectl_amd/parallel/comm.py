@@ -17,9 +17,54 @@ parallel/custom_allreduce.py) takes the small bf16 decode messages; RCCL keeps t
 """
 from __future__ import annotations
 
-from typing import Optional
+import os
+import time
+from typing import List, Optional
 
 import torch
+
+
+class CollectiveTimer:
+    """Wall time of eager all-reduces for the `rccl_allreduce_seconds` histogram.
+    Device tensors: a pair of timing events on the issuing stream, resolved later by `drain()`
+    once the end event has completed (no host sync on the hot path); host tensors (gloo): host
+    clock.  Collectives inside hipGraph capture are not timed (their replay has no per-node
+    events); decode all-reduces therefore show up only in eager / prefill steps."""
+
+    def __init__(self, max_pending: int = 4096):
+        self.pending: List = []
+        self.done: List[float] = []
+        self.max_pending = max_pending
+
+    def begin(self, t: torch.Tensor):
+        if t.is_cuda:
+            if torch.cuda.is_current_stream_capturing() or len(self.pending) >= self.max_pending:
+                return None
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def end(self, tok) -> None:
+        if tok is None:
+            return
+        if isinstance(tok, float):
+            self.done.append(time.perf_counter() - tok)
+            return
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.pending.append((tok, e))
+
+    def drain(self) -> List[float]:
+        keep = []
+        for a, b in self.pending:
+            if b.query():
+                self.done.append(a.elapsed_time(b) / 1e3)
+            else:
+                keep.append((a, b))
+        self.pending = keep
+        out, self.done = self.done, []
+        return out
 
 
 class LocalComm:
@@ -51,13 +96,22 @@ class TorchComm:
         self.world_size = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.custom_ar = None  # optional one-shot all-reduce (parallel/custom_allreduce.py)
+        self.allreduce_calls = 0
+        self.allreduce_bytes = 0
+        self.timer = CollectiveTimer() if os.environ.get("KA_TIME_COLLECTIVES", "1") == "1" else None
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.world_size == 1:
             return t
+        self.allreduce_calls += 1
+        self.allreduce_bytes += t.numel() * t.element_size()
+        tok = self.timer.begin(t) if self.timer is not None else None
         if self.custom_ar is not None and self.custom_ar.should_use(t):
-            return self.custom_ar.all_reduce(t)
-        self.dist.all_reduce(t, group=self.group)
+            self.custom_ar.all_reduce(t)
+        else:
+            self.dist.all_reduce(t, group=self.group)
+        if tok is not None:
+            self.timer.end(tok)
         return t
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:

@@ -58,3 +58,25 @@ def test_watchdog_thread_runs():
         time.sleep(0.02)
     wd.stop()
     assert fails and "rank 3" in fails[0]
+
+
+def test_collective_timer_host_path():
+    import torch
+    from ai_agent_kubectl_amd.parallel.comm import CollectiveTimer
+    t = CollectiveTimer()
+    tok = t.begin(torch.zeros(4))
+    time.sleep(0.01)
+    t.end(tok)
+    got = t.drain()
+    assert len(got) == 1 and got[0] >= 0.009
+    assert t.drain() == []
+
+
+def test_rccl_metrics_registered():
+    from ai_agent_kubectl_amd.metrics import ServiceMetrics
+    m = ServiceMetrics()
+    m.rccl_allreduce.observe(3e-5)
+    m.rccl_allreduce_bytes.inc(8192)
+    from prometheus_client import generate_latest
+    text = generate_latest(m.registry).decode()
+    assert "rccl_allreduce_seconds_bucket" in text and "rccl_allreduce_bytes_total 8192.0" in text
