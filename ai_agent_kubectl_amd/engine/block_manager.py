@@ -71,7 +71,7 @@ class BlockManager:
             h = self.block_hash[b]
             if h is not None and self.cached.get(h) == b:
                 del self.cached[h]
-            self.block_hash[b] = None
+            self._unhash(b)
             return b
         raise NoFreeBlocks()
 
@@ -87,12 +87,34 @@ class BlockManager:
             if self.block_hash[b] is not None and self.cached.get(self.block_hash[b]) == b:
                 self.evictable[b] = None
             else:
-                self.block_hash[b] = None
+                self._unhash(b)
                 self.free.append(b)
+
+    def _unhash(self, b: int) -> None:
+        """Drop b's prefix-cache identity and its entry in the sibling index (so the index keeps
+        one key per parent with a live published child, however many prompts pass through)."""
+        if self.block_hash[b] is None:
+            return
+        self.block_hash[b] = None
+        par = self.parent_of[b]
+        kids = self.children.get(par)
+        if kids is not None:
+            try:
+                kids.remove(b)
+            except ValueError:
+                pass   # already pushed out of the 4-deep deque
+            if not kids:
+                del self.children[par]
+        self.parent_of[b] = None
+        self.block_toks[b] = None
 
     # ------------------------------------------------------------------------------------------
     def ref_count(self, b: int) -> int:
         return self.ref[b]
+
+    @property
+    def num_index_keys(self) -> int:
+        return len(self.children)
 
     def blocks_needed(self, num_tokens: int) -> int:
         return (num_tokens + self.block_size - 1) // self.block_size
@@ -184,7 +206,9 @@ class BlockManager:
         self._release(b)
 
     def ensure_capacity(self, table: List[int], num_tokens: int) -> None:
-        """Grow a table so that it can hold `num_tokens` tokens (decode appends)."""
+        """Grow a table so that it can hold `num_tokens` tokens (decode appends); all or nothing."""
+        if self.blocks_needed(num_tokens) - len(table) > self.num_free:
+            raise NoFreeBlocks()
         while len(table) * self.block_size < num_tokens:
             b = self._pop_free()
             self._acquire(b)
@@ -197,7 +221,7 @@ class BlockManager:
 
     def reset_prefix_cache(self) -> None:
         for b in list(self.evictable):
-            self.block_hash[b] = None
+            self._unhash(b)
             self.free.append(b)
         self.evictable.clear()
         self.cached = {h: b for h, b in self.cached.items() if self.ref[b] > 0}

@@ -72,6 +72,10 @@ class NativeBlockManager:
     def ref_count(self, b: int) -> int:
         return self._m.ref(b)
 
+    @property
+    def num_index_keys(self) -> int:
+        return self._m.num_index_keys()
+
     def blocks_needed(self, n: int) -> int:
         return (n + self.block_size - 1) // self.block_size
 
