@@ -96,6 +96,10 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> 
     from ..engine.safe_decode import forced_prefix
     from ..engine.sequence import SamplingParams
 
+    cpus = []
+    if device.startswith("cuda"):
+        from ..utils.runtime import pin_to_device_numa
+        cpus = pin_to_device_numa(int(device.split(":")[1]) if ":" in device else 0)
     try:
         s = Settings(**settings_dict)
         opts = EngineOptions.from_settings(s)
@@ -109,7 +113,7 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> 
         eng.start()
         params = SamplingParams(max_new_tokens=s.MAX_NEW_TOKENS, ignore_eos=s.IGNORE_EOS, safe_decode=s.SAFE_DECODE)
         forced = forced_prefix(eng.tokenizer) if s.SAFE_DECODE else []
-        resp_q.put(("ready", idx, None))
+        resp_q.put(("ready", idx, cpus))
     except Exception as e:  # pragma: no cover - reported to the router
         resp_q.put(("dead", idx, repr(e)))
         return
@@ -188,6 +192,7 @@ class _Replica:
     up: bool = False
     outbox: list = dataclasses.field(default_factory=list)
     flush_scheduled: bool = False
+    cpus: list = dataclasses.field(default_factory=list)   # NUMA-local CPUs the replica pinned to
 
 
 class DPRouterLLM(LLMBackend):
@@ -241,6 +246,12 @@ class DPRouterLLM(LLMBackend):
                 continue
             if kind == "ready":
                 self.replicas[a].up = True
+                self.replicas[a].cpus = list(b or [])
+                if len(self.replicas) == 1 and self.replicas[a].cpus:
+                    # one replica (a bench rank, or DP=1 serving): the API process joins its
+                    # engine on the GPU's NUMA node
+                    from ..utils.runtime import pin_process
+                    pin_process(self.replicas[a].cpus)
                 self._n_ready += 1
                 if self._n_ready == len(self.replicas):
                     self._ready.set()

@@ -215,3 +215,16 @@ def test_openai_backend_without_key_is_degraded_mode():
     app = create_app(Settings(LLM_BACKEND="openai", RATE_LIMIT="100/minute"))
     r = TestClient(app).post("/kubectl-command", json={"query": "list pods"})
     assert (r.status_code, r.text) == (503, '{"detail":"LLM Chain not initialized"}')
+
+
+def test_cpulist_parse_and_pin_noop():
+    import os
+
+    from ai_agent_kubectl_amd.utils.runtime import _parse_cpulist, pin_process
+    assert _parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    assert _parse_cpulist("") == []
+    before = os.sched_getaffinity(0)
+    pin_process(sorted(before))          # pinning to the current mask is a no-op for every thread
+    assert os.sched_getaffinity(0) == before
+    pin_process([])
+    assert os.sched_getaffinity(0) == before
