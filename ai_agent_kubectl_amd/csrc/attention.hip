@@ -75,6 +75,37 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
   float* sl = smem + 64;            // [4][16]
   float* so = smem + 128;           // [4][16][HD+4]
 
+  // The wave's first 32-token chunk of K and V is fetched before anything else: those loads
+  // depend only on the block table, so their HBM latency overlaps the fused prologue's (split-K
+  // partial loads, RoPE, cache append) instead of following it.  At the serving shape (context
+  // <= 128 tokens, one chunk per wave) that is the whole chunk loop's memory traffic.
+  const int* bt = block_tables + (size_t)b * max_blocks;
+  const int nchunks = (ctx + 31) >> 5;
+  const size_t head_stride = (size_t)KBS * HD;  // elements per (block, head)
+  uint4 kr[2][4], vr[8];
+  auto load_k = [&](int c) {
+    const int t0 = c * 32;
+    const int blk0 = bt[2 * c];
+    const int blk1 = (t0 + 16 < ctx) ? bt[2 * c + 1] : blk0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bf16_t* kp = k_cache + ((size_t)(j ? blk1 : blk0) * hkv + h) * head_stride + col * HD + 8 * grp;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) kr[j][ks] = *reinterpret_cast<const uint4*>(kp + 32 * ks);
+    }
+  };
+  auto load_v = [&](int c) {
+    const int t0 = c * 32;
+    const int blk = (grp >> 1) ? ((t0 + 16 < ctx) ? bt[2 * c + 1] : bt[2 * c]) : bt[2 * c];
+    const bf16_t* vp = v_cache + ((size_t)blk * hkv + h) * head_stride + col * KBS + 8 * (grp & 1);
+#pragma unroll
+    for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(vp + (size_t)n * 16 * KBS);
+  };
+  if (wave < nchunks) {
+    load_k(wave);
+    if constexpr (!FUSED) load_v(wave);   // fused: V after the prologue (128-VGPR budget)
+  }
+
   if constexpr (FUSED) {
     const int half = HD / 2;
     const size_t stride = (size_t)(hq + 2 * hkv) * HD;
@@ -126,6 +157,9 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
     __syncthreads();
   }
 
+  if constexpr (FUSED) {
+    if (wave < nchunks) load_v(wave);
+  }
   bf16x8 qf[4];
   {
     const int row = col;
@@ -167,36 +201,21 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
 #pragma unroll
   for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int* bt = block_tables + (size_t)b * max_blocks;
-  const int nchunks = (ctx + 31) >> 5;
-  const size_t head_stride = (size_t)KBS * HD;  // elements per (block, head)
   bf16_t* pw = p_lds[wave];
   for (int c = wave; c < nchunks; c += 4) {
     const int t0 = c * 32;
-    const int blk0 = bt[2 * c];
-    const int blk1 = (t0 + 16 < ctx) ? bt[2 * c + 1] : blk0;
+    if (c != wave) load_k(c);   // later chunks (contexts > 128 tokens): fetched in the loop
     // ---- S = Q K^T for the two 16-token halves ----
     f32x4 s[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int blk = j ? blk1 : blk0;
-      const bf16_t* kp = k_cache + ((size_t)blk * hkv + h) * head_stride + col * HD + 8 * grp;
-      uint4 kr[4];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) kr[ks] = *reinterpret_cast<const uint4*>(kp + 32 * ks);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) acc = mfma16x16x32(qf[ks], as_bf16x8(kr[ks]), acc);
+      for (int ks = 0; ks < 4; ++ks) acc = mfma16x16x32(qf[ks], as_bf16x8(kr[j][ks]), acc);
       s[j] = acc;
     }
     // ---- V fragments (issued before the softmax so their latency hides under it) ----
-    uint4 vr[8];
-    {
-      const int blk = (grp >> 1) ? blk1 : blk0;
-      const bf16_t* vp = v_cache + ((size_t)blk * hkv + h) * head_stride + col * KBS + 8 * (grp & 1);
-#pragma unroll
-      for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(vp + (size_t)n * 16 * KBS);
-    }
+    if (c != wave) load_v(c);
     // ---- online softmax over this chunk ----
     float alpha[4];
 #pragma unroll

@@ -16,7 +16,8 @@ import threading
 from typing import Optional
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libkagent_hip.so")
+# KA_HIP_LIB: load another build of the same library (A/B kernel experiments, scripts/)
+LIB_PATH = os.environ.get("KA_HIP_LIB") or os.path.join(LIB_DIR, "libkagent_hip.so")
 
 _lock = threading.Lock()
 _lib: Optional[ctypes.CDLL] = None
