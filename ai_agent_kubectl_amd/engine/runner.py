@@ -245,22 +245,39 @@ class ModelRunner:
         mask = buf[o:o + S]; o += S
         lidx = buf[o:o + S]; o += S
         bt = buf[o:o + S * mb].reshape(S, mb)
-        t = 0
+        # one Python pass collects per-sequence scalars, token slices and tables; the per-token
+        # arrays are then built with a handful of vectorised numpy ops (was ~10 numpy calls per
+        # sequence: ~2.7 ms of GPU-idle host time for a 256-request prefill)
+        nqs = np.asarray(batch.num_query, dtype=np.int64)
+        tot = np.empty(S, dtype=np.int64)
+        toks: list = []
         for i, (s, nq) in enumerate(zip(batch.seqs, batch.num_query)):
-            q_starts[i] = t
-            start = s.total_len - nq
-            toks = s.all_ids[start:s.total_len]
-            ids[t:t + nq] = toks
-            p = np.arange(start, s.total_len, dtype=np.int32)
-            pos[t:t + nq] = p
-            tbl = np.asarray(s.block_table, dtype=np.int32)
-            slots[t:t + nq] = tbl[p // self.block_size] * self.block_size + p % self.block_size
-            ctx[i] = s.total_len
-            mask[i] = mask_index_for(s.num_generated, s.params.safe_decode)
+            n = s.total_len
+            tot[i] = n
+            ng = len(s.output_ids) - s.n_forced
+            lp = len(s.prompt_ids)
+            start = n - nq
+            if start >= lp:                      # decode row (mixed step): generated tokens only
+                toks.extend(s.output_ids[s.n_forced + start - lp:s.n_forced + n - lp])
+            else:
+                toks.extend(s.prompt_ids[start:])
+                if ng:
+                    toks.extend(s.output_ids[s.n_forced:])
+            tbl = s.block_table
             bt[i, :len(tbl)] = tbl
-            t += nq
-            lidx[i] = t - 1
-        q_starts[S] = t
+            mask[i] = mask_index_for(ng, s.params.safe_decode)
+        n_real = int(nqs.sum())
+        ends = np.cumsum(nqs)
+        q_starts[0] = 0
+        q_starts[1:] = ends
+        ctx[:] = tot
+        lidx[:] = ends - 1
+        ids[:n_real] = toks
+        seq_of = np.repeat(np.arange(S), nqs)
+        p = np.arange(n_real, dtype=np.int64) - np.repeat(ends - nqs, nqs) + np.repeat(tot - nqs, nqs)
+        pos[:n_real] = p
+        bs = self.block_size
+        slots[:n_real] = bt[seq_of, p // bs] * bs + p % bs
         return buf
 
     def _run_prefill(self, buf: torch.Tensor, T: int, S: int, max_q: int, nc: int = 0, nd: int = 0,

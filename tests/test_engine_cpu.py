@@ -491,3 +491,60 @@ def test_scheduler_holds_arrivals_until_the_running_wave_drains():
     _t.sleep(0.02)
     assert not sch.gathering()                      # quiet gap passed: admit both together
     assert sch.schedule().prefill_seqs == [held, comeback]
+
+
+def test_pack_prefill_matches_per_sequence_reference():
+    """runner._pack_prefill (vectorised) against a per-sequence construction from first principles,
+    on a mixed batch: fresh prompts, a prefix-cached prompt and decode rows, with padding."""
+    import numpy as np
+
+    from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine
+    from ai_agent_kubectl_amd.engine.safe_decode import forced_prefix, mask_index_for
+    from ai_agent_kubectl_amd.engine.scheduler import Batch
+    from ai_agent_kubectl_amd.engine.sequence import SamplingParams, Sequence
+
+    eng = build_engine(EngineOptions(model="tiny-llama", device="cpu", max_batch=16, kv_cache_tokens=4096,
+                                     max_model_len=512, use_graphs=False))
+    tok = eng.tokenizer
+    forced = forced_prefix(tok)
+    params = SamplingParams(max_new_tokens=6, ignore_eos=True)
+    prompts = [tok.encode(f"query number {i} " * (i + 3)) for i in range(5)]
+    seqs = [Sequence(prompt_ids=p, params=params, forced_prefix=list(forced)) for p in prompts]
+    eng.generate_blocking([prompts[0]], params, forced_prefix=forced)     # warm the prefix cache
+    for s in seqs[:2]:                                                   # two sequences already decoding
+        eng.scheduler.add(s)
+    b0 = eng.scheduler.schedule()
+    eng._apply(b0, eng.runner.execute(b0))
+    eng.scheduler.on_step_done(b0)
+    for s in seqs[:2]:
+        eng.bm.ensure_capacity(s.block_table, s.total_len)
+    for s in seqs[2:]:
+        eng.scheduler.add(s)
+        t, cached, hashes = eng.bm.allocate_prompt(s.all_ids)
+        s.block_table, s.block_hashes, s.num_computed = t, hashes, cached
+    rows = [(s, 1) for s in seqs[:2]] + [(s, s.total_len - s.num_computed) for s in seqs[2:]]
+    batch = Batch([r[0] for r in rows], [r[1] for r in rows], is_decode=False)
+    batch.prefill_seqs = list(seqs[2:])
+    buf = eng.runner._pack_prefill(batch, pad=True)
+
+    T = eng.runner.padded_tokens(batch.num_tokens)
+    S, mb, bs = len(rows), eng.runner.max_blocks, eng.runner.block_size
+    ids, pos, slots = buf[:T], buf[T:2 * T], buf[2 * T:3 * T]
+    o = 3 * T
+    q_starts = buf[o:o + S + 1]; o += S + 1
+    ctx = buf[o:o + S]; o += S
+    mask = buf[o:o + S]; o += S
+    lidx = buf[o:o + S]; o += S
+    bt = buf[o:o + S * mb].reshape(S, mb)
+    t = 0
+    for i, (s, nq) in enumerate(rows):
+        start = s.total_len - nq
+        assert q_starts[i] == t and ctx[i] == s.total_len and lidx[i] == t + nq - 1
+        assert list(ids[t:t + nq]) == s.all_ids[start:s.total_len]
+        assert list(pos[t:t + nq]) == list(range(start, s.total_len))
+        want = [s.block_table[p // bs] * bs + p % bs for p in range(start, s.total_len)]
+        assert list(slots[t:t + nq]) == want
+        assert list(bt[i, :len(s.block_table)]) == s.block_table
+        assert mask[i] == mask_index_for(s.num_generated, s.params.safe_decode)
+        t += nq
+    assert q_starts[S] == t and np.all(slots[t:] == -1)
