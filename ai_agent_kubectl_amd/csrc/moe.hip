@@ -32,17 +32,20 @@ __global__ __launch_bounds__(256) void moe_align_kernel(int* __restrict__ counts
 }
 
 template <int MT>
-__global__ __launch_bounds__(256) void moe_gemm_kernel(bf16_t* __restrict__ Y, const bf16_t* __restrict__ A,
-                                                       const bf16_t* __restrict__ W, const int* __restrict__ counts,
-                                                       const int* __restrict__ lists, int list_stride, int N, int K,
-                                                       int src_div) {
+__global__ __launch_bounds__(256) void moe_gemm_kernel(bf16_t* __restrict__ Y, float* __restrict__ P,
+                                                       const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                       const int* __restrict__ counts, const int* __restrict__ lists,
+                                                       int list_stride, int N, int K, int src_div, int n_rchunks,
+                                                       int kps, int R) {
   constexpr int ROWS = MT * 16;
   constexpr int PIECES = ROWS * 8;
   constexpr int XR = (PIECES + 255) / 256;
   __shared__ __attribute__((aligned(16))) u32x4 xs[ROWS * 8];
   const int e = blockIdx.y;
   const int count = counts[e];
-  const int r0 = blockIdx.z * ROWS;
+  const int ks = blockIdx.z / n_rchunks;             // split-K slice (P != nullptr when > 1 slices)
+  const int r0 = (blockIdx.z % n_rchunks) * ROWS;
+  const int kb = ks * kps;
   if (r0 >= count) return;
   const int nrows = min(ROWS, count - r0);
   const int* list = lists + (size_t)e * list_stride + r0;
@@ -52,8 +55,8 @@ __global__ __launch_bounds__(256) void moe_gemm_kernel(bf16_t* __restrict__ Y, c
   const int col = lane & 15, grp = lane >> 4;
   const int n0 = blockIdx.x * 64;
   const int wn = min(n0 + wave * 16 + col, N - 1);
-  const bf16_t* wp = We + (size_t)wn * K + 8 * grp;
-  const int nchunks = K >> 6;
+  const bf16_t* wp = We + (size_t)wn * K + kb + 8 * grp;
+  const int nchunks = min(kps, K - kb) >> 6;
 
   // per-thread source rows of the X staging pieces (fixed over the K loop)
   int srow[XR];
@@ -72,7 +75,7 @@ __global__ __launch_bounds__(256) void moe_gemm_kernel(bf16_t* __restrict__ Y, c
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
       const int p = tid + 256 * i;
-      xr[i] = *reinterpret_cast<const u32x4*>(A + (size_t)srow[i] * K + c * 64 + (p & 7) * 8);
+      xr[i] = *reinterpret_cast<const u32x4*>(A + (size_t)srow[i] * K + kb + c * 64 + (p & 7) * 8);
     }
   };
   auto store_x = [&]() {
@@ -130,16 +133,22 @@ __global__ __launch_bounds__(256) void moe_gemm_kernel(bf16_t* __restrict__ Y, c
   for (int mt = 0; mt < MT; ++mt) {
     const int m = mt * 16 + col;
     if (m < nrows) {
-      bf16_t* dst = Y + (size_t)list[m] * N + nb;
-      *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc[mt][0], acc[mt][1]), pack2(acc[mt][2], acc[mt][3]));
+      if (P != nullptr) {
+        *reinterpret_cast<f32x4*>(P + ((size_t)ks * R + list[m]) * N + nb) = acc[mt];
+      } else {
+        bf16_t* dst = Y + (size_t)list[m] * N + nb;
+        *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc[mt][0], acc[mt][1]), pack2(acc[mt][2], acc[mt][3]));
+      }
     }
   }
 }
 
 __global__ __launch_bounds__(256) void moe_combine_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ Y,
+                                                          const float* __restrict__ P, int split,
                                                           const float* __restrict__ topk_w,
                                                           const int* __restrict__ topk_ids, int k, int H, int e0,
                                                           int el) {
+  const size_t pstride = (size_t)gridDim.x * k * H;   // one split-K slice of P: [T * k, H]
   const int t = blockIdx.x;
   for (int c = threadIdx.x * 8; c < H; c += blockDim.x * 8) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -147,6 +156,20 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(bf16_t* __restrict__ o
       const int e = topk_ids[t * k + j] - e0;
       if (e < 0 || e >= el) continue;
       const float w = topk_w[t * k + j];
+      if (P != nullptr) {   // the expert GEMM's split-K slices: reduce them here (fp32, no bf16 round)
+        const float* pr = P + ((size_t)t * k + j) * H + c;
+        f32x4 y0 = *reinterpret_cast<const f32x4*>(pr), y1 = *reinterpret_cast<const f32x4*>(pr + 4);
+        for (int s2 = 1; s2 < split; ++s2) {
+          y0 += *reinterpret_cast<const f32x4*>(pr + s2 * pstride);
+          y1 += *reinterpret_cast<const f32x4*>(pr + s2 * pstride + 4);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[q] += w * y0[q];
+          acc[4 + q] += w * y1[q];
+        }
+        continue;
+      }
       const uint4 y = *reinterpret_cast<const uint4*>(Y + ((size_t)t * k + j) * H + c);
       const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
@@ -161,10 +184,13 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(bf16_t* __restrict__ o
 }
 
 template <int MT>
-static void launch_gemm(bf16_t* Y, const bf16_t* A, const bf16_t* W, const int* counts, const int* lists, int stride,
-                        int el, int N, int K, int src_div, int max_rows, hipStream_t s) {
-  dim3 grid((N + 63) / 64, el, (max_rows + MT * 16 - 1) / (MT * 16));
-  hipLaunchKernelGGL(moe_gemm_kernel<MT>, grid, dim3(256), 0, s, Y, A, W, counts, lists, stride, N, K, src_div);
+static void launch_gemm(bf16_t* Y, float* P, const bf16_t* A, const bf16_t* W, const int* counts, const int* lists,
+                        int stride, int el, int N, int K, int src_div, int max_rows, int split, int kps,
+                        hipStream_t s) {
+  const int n_rchunks = (max_rows + MT * 16 - 1) / (MT * 16);
+  dim3 grid((N + 63) / 64, el, n_rchunks * split);
+  hipLaunchKernelGGL(moe_gemm_kernel<MT>, grid, dim3(256), 0, s, Y, P, A, W, counts, lists, stride, N, K, src_div,
+                     n_rchunks, kps, max_rows);
 }
 
 extern "C" int ka_moe_align(int* counts, int* lists, const int* topk_ids, int rows, int e0, int el, hipStream_t s) {
@@ -174,27 +200,36 @@ extern "C" int ka_moe_align(int* counts, int* lists, const int* topk_ids, int ro
   KA_CHECK_LAUNCH();
 }
 
-// Y [rows_total, N] (rows_total = T*k), A [T or T*k, K], W [el, N, K]; max_rows = T*k (worst case per expert)
+// Y [rows_total, N] (rows_total = T*k), A [T or T*k, K], W [el, N, K]; max_rows = T*k (worst case per expert).
+// split > 1: K is cut into `split` slices of a multiple of 64 and every slice writes fp32 partials
+// P [split, max_rows, N] (Y unused) for a consumer that reduces them (silu_mul_splitk after the
+// w13 GEMM, moe_combine after w2).  At decode row counts only a couple of experts are active, so
+// without a K split the w2 GEMM (N = 4096) would put ~128 workgroups on 256 CUs, each streaming
+// 1.8 MB of weights through a latency-bound register ring.
 extern "C" int ka_moe_gemm(void* Y, const void* A, const void* W, const int* counts, const int* lists, int list_stride,
-                           int el, int N, int K, int src_div, int max_rows, hipStream_t s) {
+                           int el, int N, int K, int src_div, int max_rows, int split, void* P, hipStream_t s) {
   if (max_rows <= 0) return 0;
-  if (K % 64 != 0 || N % 4 != 0) return (int)hipErrorInvalidValue;
+  if (K % 64 != 0 || N % 4 != 0 || split < 1 || (split > 1 && P == nullptr)) return (int)hipErrorInvalidValue;
+  const int kps = (K / 64 + split - 1) / split * 64;
+  if ((K + kps - 1) / kps != split) return (int)hipErrorInvalidValue;   // every slice non-empty
   auto* y = static_cast<bf16_t*>(Y);
+  auto* p = split > 1 ? static_cast<float*>(P) : nullptr;
   auto* a = static_cast<const bf16_t*>(A);
   auto* w = static_cast<const bf16_t*>(W);
   const int mt = (max_rows + 15) / 16;  // rows per expert never exceed max_rows
-  if (mt <= 1) launch_gemm<1>(y, a, w, counts, lists, list_stride, el, N, K, src_div, max_rows, s);
-  else if (mt <= 2) launch_gemm<2>(y, a, w, counts, lists, list_stride, el, N, K, src_div, max_rows, s);
-  else if (mt <= 4) launch_gemm<4>(y, a, w, counts, lists, list_stride, el, N, K, src_div, max_rows, s);
-  else launch_gemm<8>(y, a, w, counts, lists, list_stride, el, N, K, src_div, max_rows, s);
+  if (mt <= 1) launch_gemm<1>(y, p, a, w, counts, lists, list_stride, el, N, K, src_div, max_rows, split, kps, s);
+  else if (mt <= 2) launch_gemm<2>(y, p, a, w, counts, lists, list_stride, el, N, K, src_div, max_rows, split, kps, s);
+  else if (mt <= 4) launch_gemm<4>(y, p, a, w, counts, lists, list_stride, el, N, K, src_div, max_rows, split, kps, s);
+  else launch_gemm<8>(y, p, a, w, counts, lists, list_stride, el, N, K, src_div, max_rows, split, kps, s);
   KA_CHECK_LAUNCH();
 }
 
-extern "C" int ka_moe_combine(void* out, const void* Y, const float* topk_w, const int* topk_ids, int T, int k, int H,
-                              int e0, int el, hipStream_t s) {
+// P != nullptr: read the w2 GEMM's split-K partials P [split, T*k, H] (fp32) instead of Y.
+extern "C" int ka_moe_combine(void* out, const void* Y, const float* P, int split, const float* topk_w,
+                              const int* topk_ids, int T, int k, int H, int e0, int el, hipStream_t s) {
   if (T <= 0) return 0;
-  if (H % 8 != 0) return (int)hipErrorInvalidValue;
+  if (H % 8 != 0 || split < 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, s, static_cast<bf16_t*>(out),
-                     static_cast<const bf16_t*>(Y), topk_w, topk_ids, k, H, e0, el);
+                     static_cast<const bf16_t*>(Y), P, split, topk_w, topk_ids, k, H, e0, el);
   KA_CHECK_LAUNCH();
 }

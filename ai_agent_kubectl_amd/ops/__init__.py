@@ -359,6 +359,22 @@ def linear_tile(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, defe
 
 
 # ---- Mixtral MoE (K12): device-side routing lists + grouped weight-streaming GEMM + combine ----
+def moe_split(rows: int, n_experts_local: int, N: int, K: int, target_wgs: int = 0) -> int:
+    """Split-K factor for the grouped expert GEMM: at decode row counts only min(El, rows) experts
+    are active, so (N / 64 column tiles) x (active experts) workgroups can leave most CUs idle
+    (w2 at batch 1: 128 on 256 CUs).  Split K until ~target_wgs workgroups stream weights; the
+    default target per row count is the best of a 1024/2048/4096/8192 sweep at the Mixtral-8x7B
+    geometry (profiles/moe_split_sweep.txt: T=1 block 304 -> 161 us)."""
+    if target_wgs <= 0:
+        target_wgs = 4096 if rows <= 2 else 2048 if rows >= 256 else 1024
+    active = max(1, min(n_experts_local, rows))
+    wgs = (N + 63) // 64 * active * ((rows + 127) // 128)
+    split = 1
+    while split < 16 and wgs * split * 2 <= target_wgs and K % (64 * split * 2) == 0:
+        split *= 2
+    return split
+
+
 def moe_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
                 topk_ids: torch.Tensor, e0: int) -> torch.Tensor:
     """sum_j topk_w[t,j] * FFN_{e(t,j)}(x[t]) over this rank's experts [e0, e0 + El); [T, H] bf16."""
@@ -372,14 +388,32 @@ def moe_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: to
     lists = torch.empty((El, R), dtype=torch.int32, device=dev)
     st = _stream()
     check(lib.ka_moe_align(_p(counts), _p(lists), _p(topk_ids), R, e0, El, st), "moe_align")
-    y1 = torch.empty((R, two_i), dtype=x.dtype, device=dev)
-    check(lib.ka_moe_gemm(_p(y1), _p(x), _p(w13), _p(counts), _p(lists), R, El, two_i, H, k, R, st), "moe_gemm1")
-    act = silu_mul(y1)
-    y2 = torch.empty((R, H), dtype=x.dtype, device=dev)
-    check(lib.ka_moe_gemm(_p(y2), _p(act), _p(w2), _p(counts), _p(lists), R, El, H, two_i // 2, 1, R, st),
-          "moe_gemm2")
+    s1 = moe_split(R, El, two_i, H)
+    if s1 > 1:   # fp32 partials; silu_mul_splitk reduces them
+        p1 = torch.empty((s1, R, two_i), dtype=torch.float32, device=dev)
+        check(lib.ka_moe_gemm(None, _p(x), _p(w13), _p(counts), _p(lists), R, El, two_i, H, k, R, s1, _p(p1), st),
+              "moe_gemm1")
+        act = silu_mul(SplitK(p1, s1))
+    else:
+        y1 = torch.empty((R, two_i), dtype=x.dtype, device=dev)
+        check(lib.ka_moe_gemm(_p(y1), _p(x), _p(w13), _p(counts), _p(lists), R, El, two_i, H, k, R, 1, None, st),
+              "moe_gemm1")
+        act = silu_mul(y1)
+    I = two_i // 2
+    s2 = moe_split(R, El, H, I)
     out = torch.empty((T, H), dtype=x.dtype, device=dev)
-    check(lib.ka_moe_combine(_p(out), _p(y2), _p(topk_w), _p(topk_ids), T, k, H, e0, El, st), "moe_combine")
+    if s2 > 1:
+        p2 = torch.empty((s2, R, H), dtype=torch.float32, device=dev)
+        check(lib.ka_moe_gemm(None, _p(act), _p(w2), _p(counts), _p(lists), R, El, H, I, 1, R, s2, _p(p2), st),
+              "moe_gemm2")
+        check(lib.ka_moe_combine(_p(out), None, _p(p2), s2, _p(topk_w), _p(topk_ids), T, k, H, e0, El, st),
+              "moe_combine")
+    else:
+        y2 = torch.empty((R, H), dtype=x.dtype, device=dev)
+        check(lib.ka_moe_gemm(_p(y2), _p(act), _p(w2), _p(counts), _p(lists), R, El, H, I, 1, R, 1, None, st),
+              "moe_gemm2")
+        check(lib.ka_moe_combine(_p(out), _p(y2), None, 1, _p(topk_w), _p(topk_ids), T, k, H, e0, El, st),
+              "moe_combine")
     return out
 
 

@@ -48,8 +48,8 @@ _SIGS = {
     "ka_gemm_tile_bm": [I],
     "ka_gemm_tile_bn": [I],
     "ka_moe_align": [P, P, P, I, I, I, P],
-    "ka_moe_gemm": [P, P, P, P, P, I, I, I, I, I, I, P],
-    "ka_moe_combine": [P, P, P, P, I, I, I, I, I, P],
+    "ka_moe_gemm": [P, P, P, P, P, I, I, I, I, I, I, I, P, P],
+    "ka_moe_combine": [P, P, P, I, P, P, I, I, I, I, I, P],
     "ka_allreduce_oneshot": [P, P, P, P, P, P, P, I, I, I, I, I, P],
     "ka_ar_alloc": [P, ctypes.c_size_t],
     "ka_ar_free": [P],
