@@ -7,20 +7,28 @@
 // after an all-gather (ops/__init__.py: tp_argmax).  temperature=0 in the reference (app.py:109).
 #include "common.h"
 
+// Small batches: the row is cut into gridDim.y slices (one workgroup each, partial (max, idx) to
+// part_val / part_idx [rows][slices]) and argmax_finish_kernel picks the winner per row — one
+// workgroup per 128k-entry row would leave the chip idle for ~30 us at batch 1.
 template <int NT>
 __global__ __launch_bounds__(NT) void masked_argmax_kernel(int* __restrict__ out_idx, float* __restrict__ out_val,
                                                            const bf16_t* __restrict__ logits,
                                                            const uint32_t* __restrict__ mask_bits,
                                                            const int* __restrict__ mask_idx, int vocab,
-                                                           int mask_words, int vocab_offset) {
+                                                           int mask_words, int vocab_offset,
+                                                           float* __restrict__ part_val,
+                                                           int* __restrict__ part_idx) {
   const int row = blockIdx.x;
   const bf16_t* lr = logits + (size_t)row * vocab;
   const int mi = mask_idx ? mask_idx[row] : -1;
   const uint32_t* mrow = mi >= 0 ? mask_bits + (size_t)mi * mask_words : nullptr;
   float best = -INFINITY;
   int bidx = 0x7fffffff;
-  const int nvec = vocab >> 3;
-  for (int v = threadIdx.x; v < nvec; v += NT) {
+  const int nvec_all = vocab >> 3;
+  const int per = (nvec_all + gridDim.y - 1) / gridDim.y;
+  const int v0 = blockIdx.y * per;
+  const int nvec = min(nvec_all, v0 + per);
+  for (int v = v0 + threadIdx.x; v < nvec; v += NT) {
     const int base = v << 3;
     uint32_t bits = 0xffu;
     if (mrow) {
@@ -63,19 +71,70 @@ __global__ __launch_bounds__(NT) void masked_argmax_kernel(int* __restrict__ out
         b = sb[i];
         bi = si[i];
       }
+    if (part_val != nullptr) {   // sliced row: the finish kernel decides
+      part_val[row * gridDim.y + blockIdx.y] = b;
+      part_idx[row * gridDim.y + blockIdx.y] = bi;
+      return;
+    }
     if (bi == 0x7fffffff) bi = 0;  // fully masked row (cannot happen with a valid mask): token 0
     out_idx[row] = bi + vocab_offset;
     if (out_val) out_val[row] = b;
   }
 }
 
+__global__ __launch_bounds__(64) void argmax_finish_kernel(int* __restrict__ out_idx, float* __restrict__ out_val,
+                                                           const float* __restrict__ part_val,
+                                                           const int* __restrict__ part_idx, int slices,
+                                                           int vocab_offset) {
+  const int row = blockIdx.x;
+  float best = -INFINITY;
+  int bidx = 0x7fffffff;
+  for (int i = threadIdx.x; i < slices; i += 64) {   // slices in index order: '>' keeps the lowest index
+    const float v = part_val[row * slices + i];
+    const int ix = part_idx[row * slices + i];
+    if (v > best || (v == best && ix < bidx)) {
+      best = v;
+      bidx = ix;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bidx, o, 64);
+    if (ob > best || (ob == best && oi < bidx)) {
+      best = ob;
+      bidx = oi;
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (bidx == 0x7fffffff) bidx = 0;
+    out_idx[row] = bidx + vocab_offset;
+    if (out_val) out_val[row] = best;
+  }
+}
+
+// slices > 1 needs a workspace of rows * slices floats + rows * slices ints (ka_argmax_slices).
+extern "C" int ka_argmax_slices(int rows, int vocab) {
+  if (rows >= 128) return 1;
+  int s = 1;
+  while (s < 64 && rows * s * 2 <= 512 && vocab / (s * 2) >= 4096) s *= 2;
+  return s;
+}
+
 extern "C" int ka_masked_argmax(int* out_idx, float* out_val, const void* logits, const uint32_t* mask_bits,
                                 const int* mask_idx, int rows, int vocab, int mask_words, int vocab_offset,
-                                hipStream_t stream) {
+                                void* workspace, int slices, hipStream_t stream) {
   if (rows <= 0) return 0;
-  if (vocab % 8 != 0 || vocab_offset % 8 != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL((masked_argmax_kernel<512>), dim3(rows), dim3(512), 0, stream, out_idx, out_val,
-                     static_cast<const bf16_t*>(logits), mask_bits, mask_idx, vocab, mask_words, vocab_offset);
+  if (vocab % 8 != 0 || vocab_offset % 8 != 0 || slices < 1 || (slices > 1 && workspace == nullptr))
+    return (int)hipErrorInvalidValue;
+  float* pv = slices > 1 ? static_cast<float*>(workspace) : nullptr;
+  int* pi = slices > 1 ? reinterpret_cast<int*>(pv + (size_t)rows * slices) : nullptr;
+  hipLaunchKernelGGL((masked_argmax_kernel<512>), dim3(rows, slices), dim3(512), 0, stream, out_idx, out_val,
+                     static_cast<const bf16_t*>(logits), mask_bits, mask_idx, vocab, mask_words, vocab_offset, pv,
+                     pi);
+  if (slices > 1)
+    hipLaunchKernelGGL(argmax_finish_kernel, dim3(rows), dim3(64), 0, stream, out_idx, out_val, pv, pi, slices,
+                       vocab_offset);
   KA_CHECK_LAUNCH();
 }
 

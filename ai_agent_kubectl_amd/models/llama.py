@@ -109,8 +109,14 @@ class LlamaModel:
                 h = ops.linear(ops.silu_mul(ops.linear(x, L["w13"], defer_reduce=True)), L["w2"], defer_reduce=fuse)
             if not combined:
                 self.comm.all_reduce(h)
-        x = ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
-        return x.index_select(0, meta.logits_indices)
+        if meta.is_decode:   # every row is its sequence's last token (logits_indices = arange)
+            return ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
+        if isinstance(h, ops.SplitK):
+            x = ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
+            return x.index_select(0, meta.logits_indices)
+        # prefill: only the sequences' last rows are sampled, so only they are normed
+        idx = meta.logits_indices
+        return ops.rmsnorm(h.index_select(0, idx), self.W["norm"], eps, residual=residual.index_select(0, idx))
 
     def _attention(self, q, meta: AttnMeta, kc: torch.Tensor, vc: torch.Tensor) -> torch.Tensor:
         if meta.is_decode:

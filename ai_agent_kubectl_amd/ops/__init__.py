@@ -224,9 +224,11 @@ def masked_argmax(logits: torch.Tensor, mask_bits: Optional[torch.Tensor], mask_
     out_idx = torch.empty(B, dtype=torch.int32, device=logits.device) if out_idx is None else out_idx
     out_val = torch.empty(B, dtype=torch.float32, device=logits.device) if out_val is None else out_val
     words = mask_bits.shape[1] if mask_bits is not None else 0
+    slices = lib.ka_argmax_slices(B, V)   # small batches: the row is split over workgroups
+    ws = torch.empty(2 * B * slices, dtype=torch.float32, device=logits.device) if slices > 1 else None
     check(lib.ka_masked_argmax(_p(out_idx), _p(out_val), _p(logits), _p(mask_bits),
                                _p(mask_idx) if mask_bits is not None else None, B, V, words, int(vocab_offset),
-                               _stream()), "masked_argmax")
+                               _p(ws), slices, _stream()), "masked_argmax")
     return out_idx, out_val
 
 

@@ -32,7 +32,8 @@ _SIGS = {
     "ka_rope_kv": [P, P, P, P, P, P, P, I, I, I, I, I, P],
     "ka_silu_mul": [P, P, I, I, P],
     "ka_embedding": [P, P, P, I, I, I, I, P],
-    "ka_masked_argmax": [P, P, P, P, P, I, I, I, I, P],
+    "ka_masked_argmax": [P, P, P, P, P, I, I, I, I, P, I, P],
+    "ka_argmax_slices": [I, I],
     "ka_moe_topk": [P, P, P, I, I, I, P],
     "ka_paged_decode": [P, P, P, P, P, I, P, I, I, I, I, I, F, P],
     "ka_set_prefill_attn_chunk": [I],

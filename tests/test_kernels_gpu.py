@@ -229,19 +229,32 @@ def test_silu_mul_and_embedding():
     assert torch.equal(ops.embedding(ids, table), ref.embedding(ids, table))
 
 
+@pytest.mark.parametrize("B", [1, 9, 200])
 @pytest.mark.parametrize("V,off", [(128256, 0), (16032, 16032 * 3), (32000, 0)])
-def test_masked_argmax(V, off):
+def test_masked_argmax(V, off, B):
+    """B < 128 takes the sliced two-stage path (ka_argmax_slices), B = 200 one workgroup per row."""
     import numpy as np
-    B = 9
     logits = torch.randn(B, V, device=DEV, dtype=BF)
     words = (V + off + 31) // 32
     bits = torch.from_numpy(np.random.RandomState(0).randint(0, 2**32, size=(2, words), dtype=np.uint64)
                             .astype(np.uint32).view(np.int32)).to(DEV)
-    midx = torch.tensor([0, 1, -1, 0, 1, -1, 0, 0, 1], dtype=torch.int32, device=DEV)
+    midx = torch.tensor([0, 1, -1, 0, 1, -1, 0, 0, 1] * (B // 9 + 1), dtype=torch.int32, device=DEV)[:B]
     i1, v1 = ops.masked_argmax(logits, bits, midx, vocab_offset=off)
     i2, v2 = ref.masked_argmax(logits.cpu(), bits.cpu(), midx.cpu(), vocab_offset=off)
     assert torch.equal(i1.cpu(), i2.cpu())
     close(v1, v2, atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("B", [1, 3, 130])
+def test_masked_argmax_ties_lowest_index(B):
+    """Equal maxima in different workgroup slices: the lowest token id wins (torch.argmax rule)."""
+    V = 128256
+    logits = torch.zeros(B, V, device=DEV, dtype=BF)
+    for i, pos in enumerate((100000, 70000, 9000)):
+        logits[:, pos] = 5.0
+    logits[0, 127000] = 5.0
+    idx, val = ops.masked_argmax(logits, None, None)
+    assert idx.cpu().tolist() == [9000] * B and val.cpu().tolist() == [5.0] * B
 
 
 def test_moe_topk():
