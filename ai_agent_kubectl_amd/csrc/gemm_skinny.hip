@@ -147,6 +147,99 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
   }
 }
 
+// M <= GEMV_MAX_M ("GEMV") variant.  With one MFMA row tile the X operand is tiny, so instead of
+// re-staging it through LDS every 64-k chunk (two barriers per chunk, an L2 round trip exposed per
+// chunk) the workgroup stages its whole K slice of X once (M rows x kps, 16-B pieces XOR-swizzled by
+// row) and the k loop only streams W: RING chunks per wave in flight in a register ring, no
+// barriers (guide §5 table, 'GEMV / M <= 16' row: straight to VGPRs, deep unroll, late vmcnt).  The
+// ring's first loads are issued before the X staging so their HBM latency overlaps it.  Loads past
+// the slice end are clamped to its last chunk (L2 re-reads) so every wait count stays static.
+template <int RING>
+__global__ __launch_bounds__(256) void gemv_ring_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                        bf16_t* __restrict__ Y, float* __restrict__ P, int M, int N,
+                                                        int K, int kps) {
+  extern __shared__ __attribute__((aligned(16))) uint4 xsd[];   // [M][klen / 8] pieces
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int n0 = blockIdx.x * NW;
+  const int split = blockIdx.y;
+  const int k_begin = split * kps;
+  const int klen = min(K, k_begin + kps) - k_begin;
+  const int nchunks = klen >> 6;
+  const int pr = klen >> 3;
+
+  const int wn = min(n0 + wave * 16 + col, N - 1);
+  const bf16_t* wp = W + (size_t)wn * K + k_begin + 8 * grp;
+  uint4 w[RING][2];
+#pragma unroll
+  for (int r = 0; r < RING; ++r) {
+    const int c = min(r, nchunks - 1);
+    w[r][0] = *reinterpret_cast<const uint4*>(wp + c * 64);
+    w[r][1] = *reinterpret_cast<const uint4*>(wp + c * 64 + 32);
+  }
+  for (int p = tid; p < M * pr; p += 256) {
+    const int row = p / pr, pc = p - row * pr;
+    xsd[row * pr + (pc ^ (row & 7))] = *reinterpret_cast<const uint4*>(X + (size_t)row * K + k_begin + pc * 8);
+  }
+  __syncthreads();
+
+  const int xrow = min(col, M - 1);
+  const uint4* xr = xsd + xrow * pr;
+  const int sw = xrow & 7;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < nchunks; c0 += RING) {
+#pragma unroll
+    for (int r = 0; r < RING; ++r) {
+      const int c = c0 + r;
+      if (c < nchunks) {
+        acc = mfma16x16x32(as_bf16x8(w[r][0]), as_bf16x8(xr[(c * 8 + grp) ^ sw]), acc);
+        acc = mfma16x16x32(as_bf16x8(w[r][1]), as_bf16x8(xr[(c * 8 + 4 + grp) ^ sw]), acc);
+      }
+      const int cn = min(c + RING, nchunks - 1);
+      w[r][0] = *reinterpret_cast<const uint4*>(wp + cn * 64);
+      w[r][1] = *reinterpret_cast<const uint4*>(wp + cn * 64 + 32);
+    }
+  }
+
+  const int nb = n0 + wave * 16 + 4 * grp;
+  const int m = col;
+  if (nb >= N || m >= M) return;
+  if (P) {
+    float* dst = P + ((size_t)split * M + m) * N + nb;
+    if (nb + 3 < N) {
+      *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (nb + r < N) dst[r] = acc[r];
+    }
+  } else {
+    bf16_t* dst = Y + (size_t)m * N + nb;
+    if (nb + 3 < N) {
+      *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]));
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (nb + r < N) dst[r] = f2bf(acc[r]);
+    }
+  }
+}
+
+// KA_GEMV_RING: ring depth 4 (default) or 8, 0 disables the variant (A/B runs).  Measured on
+// MI355X against the staged kernel (profiles/gemv_ring_ab.txt): ring 4 wins O / gate_up at
+// M = 1..4 by 3-10 %, ring 8 is no better, and at M = 16 the staged kernel is faster (QKV 14.5
+// vs 17.9 us), so the variant serves M <= GEMV_MAX_M.
+#define GEMV_MAX_M 4
+static int gemv_ring_depth() {
+  static int ring = -1;
+  if (ring < 0) {
+    const char* e = getenv("KA_GEMV_RING");
+    ring = e ? atoi(e) : 4;
+    if (ring != 0 && ring != 8) ring = 4;
+  }
+  return ring;
+}
+
 // Y[m, n] = bf16(sum_s P[s, m, n])
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(bf16_t* __restrict__ Y, const float* __restrict__ P,
                                                             int split, long mn) {
@@ -189,7 +282,15 @@ extern "C" int ka_gemm_skinny(void* Y, const void* X, const void* W, void* works
   auto* y = static_cast<bf16_t*>(Y);
   float* p = split > 1 ? static_cast<float*>(workspace) : nullptr;
   const int mt = (M + 15) / 16;
-  if (mt <= 1) launch_mt<1>(x, w, y, p, M, N, K, split, kps, stream);
+  const size_t gemv_lds = (size_t)M * kps * 2;
+  const int ring = gemv_ring_depth();
+  if (M <= GEMV_MAX_M && ring > 0 && gemv_lds <= 65536) {
+    dim3 grid((N + NW - 1) / NW, split);
+    if (ring == 4)
+      hipLaunchKernelGGL(gemv_ring_kernel<4>, grid, dim3(256), gemv_lds, stream, x, w, y, p, M, N, K, kps);
+    else
+      hipLaunchKernelGGL(gemv_ring_kernel<8>, grid, dim3(256), gemv_lds, stream, x, w, y, p, M, N, K, kps);
+  } else if (mt <= 1) launch_mt<1>(x, w, y, p, M, N, K, split, kps, stream);
   else if (mt <= 2) launch_mt<2>(x, w, y, p, M, N, K, split, kps, stream);
   else if (mt <= 4) launch_mt<4>(x, w, y, p, M, N, K, split, kps, stream);
   else if (mt <= 6) launch_mt<6>(x, w, y, p, M, N, K, split, kps, stream);

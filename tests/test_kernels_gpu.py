@@ -265,7 +265,7 @@ def test_moe_topk():
     close(w1.sort(1).values, w2.sort(1).values, atol=1e-5)
 
 
-@pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 128, 200, 256])
+@pytest.mark.parametrize("M", [1, 4, 5, 16, 33, 64, 128, 200, 256])
 @pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (16032, 4096), (1000, 512)])
 def test_gemm_skinny(M, N, K):
     x = torch.randn(M, K, device=DEV, dtype=BF)
