@@ -20,8 +20,9 @@ Execution shapes:
 * `moe_hip` (decode, T*k <= 512): device-side routing lists, grouped weight-streaming MFMA GEMMs
   over only the routed rows and a weighted combine (csrc/moe.hip) — shape-static, captured in
   the decode hipGraphs, every local expert's weights streamed once per step;
-* `moe_grouped` (prefill / CPU reference): tokens bucketed by expert on the host, hipBLASLt GEMMs
-  per expert (ragged, eager);
+* `moe_sorted` (prefill / CPU): rows sorted by expert on the device, one host read of the counts
+  per layer, hipBLASLt GEMMs per contiguous expert segment (ragged, eager);
+* `moe_grouped`: per-expert nonzero() bucketing (one host sync per expert), kept as a reference;
 * `moe_batched`: dense all-experts formulation, kept as a second reference.
 """
 from __future__ import annotations
@@ -69,6 +70,38 @@ def moe_grouped(x, L, cfg, ep_rank, ep_size):
     return out.to(x.dtype)
 
 
+def moe_sorted(x, L, cfg, ep_rank, ep_size):
+    """Prefill-sized MoE: (token, slot) rows sorted by local expert on the device, ONE host read
+    of the per-expert counts per layer (hipBLASLt needs host shapes), then one contiguous segment
+    per expert through hipBLASLt and a weighted index_add combine.  `moe_grouped` reads a nonzero()
+    per expert instead — E host syncs per layer, each draining the GPU queue."""
+    logits = F.linear(x, L["router"])
+    w, ids = ops.moe_topk(logits, cfg.top_k)                        # [T, k] f32 / int32
+    T, H = x.shape
+    k = cfg.top_k
+    w13, w2 = L["w13"], L["w2"]
+    el = w13.shape[0]
+    flat = ids.reshape(-1).long() - ep_rank * el                    # local expert id per (token, slot)
+    key = torch.where((flat >= 0) & (flat < el), flat, torch.full_like(flat, el))   # others sort last
+    order = torch.argsort(key, stable=True)
+    counts = torch.bincount(key, minlength=el + 1)[:el].tolist()    # the layer's one host sync
+    n = sum(counts)
+    out = torch.zeros((T, H), dtype=torch.float32, device=x.device)
+    if n == 0:
+        return out.to(x.dtype)
+    rows = order[:n]
+    tok = torch.div(rows, k, rounding_mode="floor")
+    xs = x.index_select(0, tok)
+    ys = torch.empty_like(xs)
+    off = 0
+    for e, c in enumerate(counts):
+        if c:
+            ys[off:off + c] = F.linear(ops.silu_mul(F.linear(xs[off:off + c], w13[e])), w2[e])
+            off += c
+    out.index_add_(0, tok, ys.float() * w.reshape(-1).index_select(0, rows).unsqueeze(1))
+    return out.to(x.dtype)
+
+
 MOE_HIP_MAX_ROWS = 512   # T * top_k handled by the HIP grouped kernel (decode buckets); larger -> grouped hipBLASLt
 
 
@@ -92,10 +125,16 @@ def _local_experts(xr, er, L, e0):
         return ops.moe_experts(xr, w13, w2, ones, er.view(R, 1).to(torch.int32), e0)
     out = torch.empty_like(xr)
     el = er.long() - e0
-    for e in range(w13.shape[0]):
-        rows = torch.nonzero(el == e, as_tuple=False).squeeze(1)
-        if rows.numel():
-            out.index_copy_(0, rows, F.linear(ops.silu_mul(F.linear(xr.index_select(0, rows), w13[e])), w2[e]))
+    order = torch.argsort(el, stable=True)
+    counts = torch.bincount(el, minlength=w13.shape[0]).tolist()   # one host sync (hipBLASLt shapes)
+    xs = xr.index_select(0, order)
+    ys = torch.empty_like(xs)
+    off = 0
+    for e, c in enumerate(counts):
+        if c:
+            ys[off:off + c] = F.linear(ops.silu_mul(F.linear(xs[off:off + c], w13[e])), w2[e])
+            off += c
+    out.index_copy_(0, order, ys)
     return out
 
 
@@ -146,4 +185,4 @@ def moe_forward(x, L, cfg, ep_rank, ep_size, is_decode: bool, comm=None):
         return moe_alltoall(x, L, cfg, comm), True
     if x.is_cuda and not ops._FORCE_REF and x.shape[0] * cfg.top_k <= MOE_HIP_MAX_ROWS:
         return moe_hip(x, L, cfg, ep_rank, ep_size), False
-    return moe_grouped(x, L, cfg, ep_rank, ep_size), False
+    return moe_sorted(x, L, cfg, ep_rank, ep_size), False

@@ -548,3 +548,25 @@ def test_pack_prefill_matches_per_sequence_reference():
         assert mask[i] == mask_index_for(s.num_generated, s.params.safe_decode)
         t += nq
     assert q_starts[S] == t and np.all(slots[t:] == -1)
+
+
+def test_moe_sorted_matches_grouped_and_batched():
+    """Prefill MoE path (one host sync per layer) == per-expert bucketing == dense formulation,
+    for the full expert set and for an EP shard."""
+    import torch
+
+    from ai_agent_kubectl_amd.models.config import get_config
+    from ai_agent_kubectl_amd.models.moe import moe_batched, moe_grouped, moe_sorted
+    cfg = get_config("tiny-mixtral")
+    torch.manual_seed(0)
+    T, H, I, E = 37, cfg.hidden, cfg.intermediate, cfg.num_experts
+    x = torch.randn(T, H)
+    for ep_rank, ep_size in ((0, 1), (1, 2)):
+        el = E // ep_size
+        L = {"router": torch.randn(E, H) * 0.1, "w13": torch.randn(el, 2 * I, H) * 0.05,
+             "w2": torch.randn(el, H, I) * 0.05}
+        a = moe_sorted(x, L, cfg, ep_rank, ep_size)
+        b = moe_grouped(x, L, cfg, ep_rank, ep_size)
+        c = moe_batched(x, L, cfg, ep_rank, ep_size)
+        torch.testing.assert_close(a, b, atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(a, c, atol=1e-4, rtol=1e-4)
