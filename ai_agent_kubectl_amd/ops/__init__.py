@@ -8,7 +8,8 @@ hand-written kernel wins (decode GEMV, MoE grouped GEMM).
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple, NamedTuple
+import os
+from typing import NamedTuple, Optional, Tuple
 
 import torch
 
@@ -245,7 +246,7 @@ def moe_topk(router_logits: torch.Tensor, k: int):
 
 # ---- decode GEMM (K13): hand-written weight-streaming split-K MFMA kernel for M <= 256 ----
 SKINNY_MAX_M = 256
-SKINNY_TARGET_WGS = int(__import__("os").environ.get("KA_SKINNY_WGS", "512"))
+SKINNY_TARGET_WGS = int(os.environ.get("KA_SKINNY_WGS", "512"))
 
 
 def skinny_split(M: int, N: int, K: int, target_wgs: int = 0) -> int:

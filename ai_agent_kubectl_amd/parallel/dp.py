@@ -121,7 +121,7 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> 
     # completions are batched: the engine thread appends, and one message per engine step carries
     # all of them back (a wave of 256 finishing together = 1 pickle + 1 pipe write, not 256)
     done_buf = []
-    done_lock = __import__("threading").Lock()
+    done_lock = threading.Lock()
 
     def done(seq, rid):
         err = repr(seq.error) if seq.error is not None else None
