@@ -71,3 +71,17 @@ KA_DEV f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
 KA_DEV bf16x8 as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
 
 #define KA_CHECK_LAUNCH() return (int)hipGetLastError()
+
+// X[m][k] = bf16(silu(GU[m][k]) * GU[m][K + k]) for 8 bf16 lanes — bit-identical to silu_mul_kernel
+// (elementwise.hip), so GEMMs that compute the activation while staging their X operand (gemm_tile
+// SWIGLU, gemv_ring SWIGLU) match the unfused SiLU kernel + GEMM exactly.
+KA_DEV u32x4 swiglu8(u32x4 g, u32x4 u) {
+  u32x4 o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float g0 = lo_f(g[k]), g1 = hi_f(g[k]);
+    const float s0 = g0 / (1.f + __expf(-g0)), s1 = g1 / (1.f + __expf(-g1));
+    o[k] = pack2(s0 * lo_f(u[k]), s1 * hi_f(u[k]));
+  }
+  return o;
+}

@@ -154,7 +154,9 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
 // barriers (guide §5 table, 'GEMV / M <= 16' row: straight to VGPRs, deep unroll, late vmcnt).  The
 // ring's first loads are issued before the X staging so their HBM latency overlaps it.  Loads past
 // the slice end are clamped to its last chunk (L2 re-reads) so every wait count stays static.
-template <int RING>
+// SWIGLU: X is the gate_up output GU [M, 2K] and the staged operand is swiglu8(gate, up) — the
+// down projection of a batch-1..4 decode step without the SiLU kernel (bit-identical result).
+template <int RING, bool SWIGLU = false>
 __global__ __launch_bounds__(256) void gemv_ring_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                         bf16_t* __restrict__ Y, float* __restrict__ P, int M, int N,
                                                         int K, int kps) {
@@ -179,7 +181,13 @@ __global__ __launch_bounds__(256) void gemv_ring_kernel(const bf16_t* __restrict
   }
   for (int p = tid; p < M * pr; p += 256) {
     const int row = p / pr, pc = p - row * pr;
-    xsd[row * pr + (pc ^ (row & 7))] = *reinterpret_cast<const uint4*>(X + (size_t)row * K + k_begin + pc * 8);
+    if constexpr (SWIGLU) {
+      const bf16_t* g = X + (size_t)row * 2 * K + k_begin + pc * 8;
+      const u32x4 v = swiglu8(*reinterpret_cast<const u32x4*>(g), *reinterpret_cast<const u32x4*>(g + K));
+      xsd[row * pr + (pc ^ (row & 7))] = __builtin_bit_cast(uint4, v);
+    } else {
+      xsd[row * pr + (pc ^ (row & 7))] = *reinterpret_cast<const uint4*>(X + (size_t)row * K + k_begin + pc * 8);
+    }
   }
   __syncthreads();
 
@@ -298,6 +306,27 @@ extern "C" int ka_gemm_skinny(void* Y, const void* X, const void* W, void* works
   else if (mt <= 12) launch_mt<12>(x, w, y, p, M, N, K, split, kps, stream);
   else launch_mt<16>(x, w, y, p, M, N, K, split, kps, stream);
   // Y == nullptr: leave the fp32 partials for a fused consumer (ka_rmsnorm_splitk)
+  if (split > 1 && y != nullptr) ka_splitk_reduce_launch(y, p, split, (long)M * N, stream);
+  KA_CHECK_LAUNCH();
+}
+
+// Y = swiglu(GU) * W^T for M <= GEMV_MAX_M (GU = [M, 2K] gate | up): the batch-1..4 down projection
+// with the SiLU*mul computed while staging X.  split > 1 needs the split * M * N float workspace;
+// Y == nullptr leaves the partials for a fused consumer.  Returns hipErrorInvalidValue for shapes
+// this path does not take (the caller then runs silu_mul + linear).
+extern "C" int ka_gemv_swiglu(void* Y, const void* GU, const void* W, void* workspace, int M, int N, int K,
+                              int split, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > GEMV_MAX_M || K % 64 != 0 || N % 4 != 0 || split < 1) return (int)hipErrorInvalidValue;
+  int kps = (K / split + 63) / 64 * 64;
+  split = (K + kps - 1) / kps;
+  const size_t lds = (size_t)M * kps * 2;
+  if (lds > 65536) return (int)hipErrorInvalidValue;
+  auto* y = static_cast<bf16_t*>(Y);
+  float* p = split > 1 ? static_cast<float*>(workspace) : nullptr;
+  dim3 grid((N + NW - 1) / NW, split);
+  hipLaunchKernelGGL((gemv_ring_kernel<4, true>), grid, dim3(256), lds, stream, static_cast<const bf16_t*>(GU),
+                     static_cast<const bf16_t*>(W), y, p, M, N, K, kps);
   if (split > 1 && y != nullptr) ka_splitk_reduce_launch(y, p, split, (long)M * N, stream);
   KA_CHECK_LAUNCH();
 }

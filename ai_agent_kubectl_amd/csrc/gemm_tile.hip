@@ -31,19 +31,8 @@ struct TileCfg {
   static_assert(BN * 8 % NT == 0 && BM * 8 % NT == 0, "tile pieces must divide the thread count");
 };
 
-// SWIGLU: X is the fused gate_up output GU [M, 2K] and the activation is computed while staging,
-// X[m][k] = bf16(silu(GU[m][k]) * GU[m][K + k]) — bit-identical to silu_mul_kernel, so the down
-// projection consumes the gate_up output directly (no SiLU kernel, no [M, K] round trip).
-__device__ __forceinline__ u32x4 swiglu8(u32x4 g, u32x4 u) {
-  u32x4 o;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float g0 = lo_f(g[k]), g1 = hi_f(g[k]);
-    const float s0 = g0 / (1.f + __expf(-g0)), s1 = g1 / (1.f + __expf(-g1));
-    o[k] = pack2(s0 * lo_f(u[k]), s1 * hi_f(u[k]));
-  }
-  return o;
-}
+// SWIGLU: X is the fused gate_up output GU [M, 2K] and the activation is computed while staging
+// (swiglu8, common.h) — the down projection consumes the gate_up output directly.
 
 // PF2: two register stages in flight (k-step t+2 is issued before computing t, t+1 is written to
 // LDS after it): hides about two loaded-HBM latencies instead of one; K per split must then be a
@@ -348,7 +337,7 @@ static void launch_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, i
   using C = TileCfg<WN, WM, TN, TM>;
   static bool lds_attr = false;   // > 64 KB of dynamic LDS must be opted into (160 KB per CU on gfx950)
   if (!lds_attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<WN, WM, TN, TM, SW, PF2>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<WN, WM, TN, TM, SW, PF2>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
     lds_attr = true;
   }

@@ -106,7 +106,9 @@ class LlamaModel:
             if cfg.is_moe:
                 h, combined = moe_forward(x, L, cfg, self.ep_rank, self.ep_size, meta.is_decode, self.comm)
             else:
-                h = ops.linear(ops.silu_mul(ops.linear(x, L["w13"], defer_reduce=True)), L["w2"], defer_reduce=fuse)
+                # batch <= 4: SiLU·mul computed inside the down GEMV's X staging (ops.swiglu_linear)
+                h = ops.swiglu_linear(ops.linear(x, L["w13"], defer_reduce=True), L["w2"], defer_reduce=fuse,
+                                      tile_fused=False)
             if not combined:
                 self.comm.all_reduce(h)
         if meta.is_decode:   # every row is its sequence's last token (logits_indices = arange)

@@ -308,16 +308,40 @@ def tile_k_quantum(cfg: int) -> int:
     return 128 if cfg >= 17 else 64 if cfg >= 15 else 32 if cfg >= 10 else 128 if cfg >= 5 else 64
 
 
-def swiglu_linear(gu: torch.Tensor, w: torch.Tensor, defer_reduce: bool = False):
+GEMV_SWIGLU_MAX_M = 4   # csrc/gemm_skinny.hip GEMV_MAX_M
+
+
+def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, tile_fused: bool = True):
     """y = (silu(gu[:, :I]) * gu[:, I:]) @ w.T — the MLP down projection fed directly by the fused
-    gate_up output.  When the autotuned plan for (M, N, I) is the LDS-tiled kernel the activation is
-    computed inside its X staging (ka_gemm_tile_swiglu, bit-identical); otherwise SiLU·mul then
-    `linear`.  Not used by the model: measured 138 us vs 47 + 6 us unfused at M=256 (Llama-3-8B
-    down), because every one of the N/BN column tiles re-stages X and so recomputes the activation."""
+    gate_up output (a bf16 tensor; a `SplitK` goes through silu_mul's fused reduce).
+
+    * M <= 4 (batch-1..4 decode, the model's path): the GEMV computes the activation while staging
+      its X slice once per workgroup (ka_gemv_swiglu, bit-identical to SiLU·mul + GEMV): one kernel
+      and one launch boundary less per layer;
+    * tile_fused and the autotuned plan for (M, N, I) is an LDS-tiled kernel: the activation is
+      computed inside its X staging (ka_gemm_tile_swiglu).  The model passes tile_fused=False:
+      measured 138 us vs 47 + 6 us unfused at M=256 (Llama-3-8B down), because every one of the
+      N/BN column tiles re-stages X and so recomputes the activation;
+    * otherwise SiLU·mul then `linear`."""
+    if isinstance(gu, SplitK) or _ref(gu) or not gu.is_contiguous():
+        return linear(silu_mul(gu), w, defer_reduce=defer_reduce)
     M, I2 = gu.shape
     I = I2 // 2
     N = w.shape[0]
-    if not _ref(gu) and gu.is_contiguous():
+    if M <= GEMV_SWIGLU_MAX_M and I % 64 == 0 and N % 4 == 0:
+        lib = require()
+        split = skinny_split(M, N, I, 256)
+        kps = ((I // split + 63) // 64) * 64
+        split = (I + kps - 1) // kps
+        if M * kps * 2 <= 65536:
+            ws = torch.empty((split, M, N), dtype=torch.float32, device=gu.device) if split > 1 else None
+            if defer_reduce and split > 1:
+                check(lib.ka_gemv_swiglu(None, _p(gu), _p(w), _p(ws), M, N, I, split, _stream()), "gemv_swiglu")
+                return SplitK(ws, split)
+            y = torch.empty((M, N), dtype=gu.dtype, device=gu.device)
+            check(lib.ka_gemv_swiglu(_p(y), _p(gu), _p(w), _p(ws), M, N, I, split, _stream()), "gemv_swiglu")
+            return y
+    if tile_fused:
         plan = GEMM_PLAN.get((M, N, I))
         if plan is not None and plan[0] == "tile" and plan[2] <= 4 and I % 64 == 0 and N % 16 == 0:
             cfg, split = plan[2], plan[1]

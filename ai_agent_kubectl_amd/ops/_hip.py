@@ -40,6 +40,7 @@ _SIGS = {
     "ka_paged_decode_rope": [P, P, P, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, P],
     "ka_paged_prefill": [P, P, P, P, P, I, P, P, I, I, I, I, I, I, F, P],
     "ka_gemm_skinny": [P, P, P, P, I, I, I, I, P],
+    "ka_gemv_swiglu": [P, P, P, P, I, I, I, I, P],
     "ka_rmsnorm_splitk": [P, P, P, I, P, I, I, F, P],
     "ka_rope_kv_splitk": [P, P, P, P, I, P, P, P, I, I, I, I, I, P],
     "ka_silu_mul_splitk": [P, P, I, I, I, P],

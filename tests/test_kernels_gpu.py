@@ -458,3 +458,22 @@ def test_moe_experts_split_k_mixtral_geometry(T):
             want[t] += float(tw[t, j]) * (a @ w2[e].float().t())
     close(got, want, atol=3e-2, rtol=3e-2)
     close(got, unsplit, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("N,I", [(4096, 14336), (1000, 512)])
+def test_gemv_swiglu_fused_is_exact(M, N, I):
+    """Batch-1..4 down projection with SiLU·mul computed in the GEMV's X staging == SiLU·mul kernel
+    then the same GEMV at the same split (bitwise), and close to the fp32 reference."""
+    gu = torch.randn(M, 2 * I, device=DEV, dtype=BF)
+    w = (torch.randn(N, I, device=DEV) * 0.02).to(BF)
+    split = ops.skinny_split(M, N, I, 256)
+    got = ops.swiglu_linear(gu, w, tile_fused=False)
+    want = ops.linear(ops.silu_mul(gu), w, split=split)
+    assert torch.equal(got, want)
+    parts = ops.swiglu_linear(gu, w, defer_reduce=True, tile_fused=False)
+    if isinstance(parts, ops.SplitK):
+        close(parts.resolve(), want, atol=1e-2, rtol=1e-2)
+    g = gu.float()
+    a = (torch.nn.functional.silu(g[:, :I]) * g[:, I:]).to(BF).float()
+    close(got, a @ w.float().t(), atol=3e-2, rtol=2e-2)
