@@ -21,8 +21,9 @@ DP replicas) without duplicate-registration errors.
 """
 from __future__ import annotations
 
+import bisect
 import time
-from typing import Callable, Optional
+from typing import Callable, List, Optional
 
 from prometheus_client import (CollectorRegistry, Counter, GCCollector, Gauge, Histogram,
                                PlatformCollector, ProcessCollector, Summary, generate_latest)
@@ -85,7 +86,11 @@ class ServiceMetrics:
         self.loop_lag = Histogram("event_loop_lag_seconds", "asyncio event-loop scheduling delay (50 ms probe).",
                                   buckets=(0.001, 0.002, 0.005, 0.01, 0.02, 0.05, 0.1, 0.2, 0.5, 1.0), registry=r)
 
+        self.flush_hooks: List[Callable[[], None]] = []   # pending HTTP observations (PrometheusMiddleware)
+
     def render(self) -> bytes:
+        for flush in self.flush_hooks:
+            flush()
         return generate_latest(self.registry)
 
 
@@ -130,6 +135,8 @@ class PrometheusMiddleware:
         self.metrics = metrics
         self.routes = routes
         self._children = {}
+        self._pending: list = []
+        metrics.flush_hooks.append(self.flush)
 
     async def __call__(self, scope, receive, send):
         if scope["type"] != "http":
@@ -170,8 +177,49 @@ class PrometheusMiddleware:
                             m.response_size.labels(handler), m.latency_lowr.labels(method, handler))
                 if len(self._children) < 4096:
                     self._children[key] = children
-            children[0].inc()
-            children[1].observe(req_len)
-            children[2].observe(resp_len[0])
-            self.metrics.latency_highr.observe(dur)
-            children[3].observe(dur)
+            # recorded now, applied in bulk (every FLUSH_EVERY requests and before every /metrics
+            # render): a request then costs one list append instead of a dozen lock-protected
+            # counter / summary / histogram updates on the event loop
+            self._pending.append((children, req_len, resp_len[0], dur))
+            if len(self._pending) >= self.FLUSH_EVERY:
+                self.flush()
+
+    FLUSH_EVERY = 256
+
+    def flush(self) -> None:
+        """Apply the pending observations: per labelled child one count / sum increment and one
+        increment per touched histogram bucket (the same values prometheus_client's observe()
+        would have produced one by one; bucket = first upper bound >= the value)."""
+        pend, self._pending = self._pending, []
+        if not pend:
+            return
+        agg = {}
+        hr = self.metrics.latency_highr
+        hr_bounds = hr._upper_bounds
+        hr_counts = [0] * len(hr_bounds)
+        hr_sum = 0.0
+        for children, req_len, resp_len, dur in pend:
+            a = agg.get(id(children))
+            if a is None:
+                a = agg[id(children)] = [children, 0, 0.0, 0.0, 0.0, [0] * len(children[3]._upper_bounds)]
+            a[1] += 1
+            a[2] += req_len
+            a[3] += resp_len
+            a[4] += dur
+            a[5][bisect.bisect_left(children[3]._upper_bounds, dur)] += 1
+            hr_counts[bisect.bisect_left(hr_bounds, dur)] += 1
+            hr_sum += dur
+        for children, n, req_sum, resp_sum, dur_sum, counts in agg.values():
+            children[0]._value.inc(n)
+            for summ, total in ((children[1], req_sum), (children[2], resp_sum)):
+                summ._count.inc(n)
+                summ._sum.inc(total)
+            lowr = children[3]
+            lowr._sum.inc(dur_sum)
+            for i, c in enumerate(counts):
+                if c:
+                    lowr._buckets[i].inc(c)
+        hr._sum.inc(hr_sum)
+        for i, c in enumerate(hr_counts):
+            if c:
+                hr._buckets[i].inc(c)

@@ -255,3 +255,39 @@ def test_fault_injection_and_ready():
     assert c.get("/ready").status_code == 200
     s = Settings(RATE_LIMIT="100/minute")
     assert TestClient(create_app(s, backend=None)).get("/ready").status_code == 503
+
+
+def test_metrics_batched_updates_match_per_request_observe():
+    """HTTP metrics are applied in bulk (every 256 requests and before every /metrics render): the
+    scraped counts, sums and histogram buckets equal what per-request observe() calls give."""
+    from prometheus_client import CollectorRegistry, Histogram
+
+    from ai_agent_kubectl_amd.metrics import HIGHR_BUCKETS, LOWR_BUCKETS
+    c, _ = make()
+    n = 300   # crosses the 256-request flush boundary
+    for i in range(n):
+        assert c.post("/kubectl-command", json={"query": f"list pods {i % 7}"}, headers=H).status_code == 200
+    app = c.app
+    mw = app.middleware_stack
+    while mw is not None and not hasattr(mw, "flush"):
+        mw = getattr(mw, "app", None)
+    assert mw is not None
+    durs = [d for (_, _, _, d) in mw._pending]
+    assert 0 < len(durs) < 256          # the last requests are still pending before the scrape
+    text = c.get("/metrics").text
+    assert re.search(r'http_requests_total\{handler="/kubectl-command",method="POST",status="2xx"\} 300\.0', text)
+    assert re.search(r'http_request_size_bytes_count\{handler="/kubectl-command"\} 300\.0', text)
+    assert re.search(r'http_request_duration_seconds_count\{handler="/kubectl-command",method="POST"\} 300\.0', text)
+    assert re.search(r'http_request_duration_highr_seconds_count (\d+)\.0', text)
+    # bucket placement: first upper bound >= value, exactly as Histogram.observe
+    reg = CollectorRegistry()
+    h = Histogram("x", "x", buckets=HIGHR_BUCKETS, registry=reg)
+    lo = Histogram("y", "y", buckets=LOWR_BUCKETS, registry=reg)
+    for v in (0.0, 0.01, 0.0100001, 0.5, 59.9, 60.0, 61.0):
+        h.observe(v)
+        lo.observe(v)
+    import bisect
+    got = [0] * len(h._upper_bounds)
+    for v in (0.0, 0.01, 0.0100001, 0.5, 59.9, 60.0, 61.0):
+        got[bisect.bisect_left(h._upper_bounds, v)] += 1
+    assert got == [b.get() for b in h._buckets]
