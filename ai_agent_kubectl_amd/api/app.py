@@ -67,6 +67,22 @@ def _command_body(command: str, from_cache: bool, execution_data: Dict[str, Any]
     }
 
 
+_STR = json.JSONEncoder(ensure_ascii=False).encode   # the str encoding json.dumps(ensure_ascii=False) uses
+
+
+def _generated_json(command: str, from_cache: bool, start: str, end: str) -> bytes:
+    """Byte-for-byte `_json(_command_body(command, from_cache, <synthetic metadata>))` for the
+    /kubectl-command success reply (app.py:333-346: duration 0.0, success true, no execution
+    fields), assembled from a fixed template: the reply of every generated or cached command
+    skips the generic dict walk of json.dumps (tests/test_api_golden.py checks the equality)."""
+    return (b'{"kubectl_command":' + _STR(command).encode("utf-8")
+            + (b',"execution_result":null,"execution_error":null,"from_cache":true,"metadata":{"start_time":'
+               if from_cache else
+               b',"execution_result":null,"execution_error":null,"from_cache":false,"metadata":{"start_time":')
+            + _STR(start).encode("utf-8") + b',"end_time":' + _STR(end).encode("utf-8")
+            + b',"duration_ms":0.0,"success":true,"error_type":null,"error_code":null}}')
+
+
 async def _lag_probe(metrics, period: float = 0.05) -> None:
     """Observe how late the event loop wakes a 50 ms sleeper (GIL / blocking-call diagnostics)."""
     loop = asyncio.get_running_loop()
@@ -318,9 +334,8 @@ def create_app(settings: Optional[Settings] = None, backend: Any = _UNSET,
             raise HTTPException(status_code=status.HTTP_500_INTERNAL_SERVER_ERROR,
                                 detail="Internal server error processing request")
         now = utcnow_iso()
-        execution_data = {"metadata": {"start_time": now, "end_time": utcnow_iso(), "duration_ms": 0.0,
-                                       "success": True}}
-        return _json(_command_body(command, from_cache, execution_data))
+        return Response(content=_generated_json(command, from_cache, now, utcnow_iso()), status_code=200,
+                        media_type="application/json")
 
     async def execute(command: str, scope) -> Response:
         """POST /execute after auth + body validation (app.py:369-389)."""

@@ -291,3 +291,15 @@ def test_metrics_batched_updates_match_per_request_observe():
     for v in (0.0, 0.01, 0.0100001, 0.5, 59.9, 60.0, 61.0):
         got[bisect.bisect_left(h._upper_bounds, v)] += 1
     assert got == [b.get() for b in h._buckets]
+
+
+def test_generated_reply_template_is_byte_identical():
+    """The /kubectl-command success reply template == the generic json.dumps path, byte for byte."""
+    from ai_agent_kubectl_amd.api.app import _command_body, _generated_json, _json
+    for cmd in ["kubectl get pods", 'kubectl get pods -l "app=x"', "kubectl get pods -o jsonpath='{.items}'",
+                "kubectl get ns \\\\ x", "kubectl describe pod ünïcødé-π", "kubectl get pods\\n--all", "kubectl   x"]:
+        for hit in (False, True):
+            md = {"metadata": {"start_time": "2026-10-16T12:00:00.123456", "end_time": "2026-10-16T12:00:00.123999",
+                               "duration_ms": 0.0, "success": True}}
+            assert _generated_json(cmd, hit, md["metadata"]["start_time"], md["metadata"]["end_time"]) == \
+                _json(_command_body(cmd, hit, md)).body
