@@ -22,15 +22,21 @@ import asyncio
 import datetime
 import logging
 import shlex
+import sys
 import time
 from typing import Any, Dict, List
 
 logger = logging.getLogger("app")
 
 
-def utcnow_iso() -> str:
-    """`datetime.datetime.utcnow().isoformat()` (naive, no `Z`; quirk Q7) without the deprecation."""
-    return datetime.datetime.now(datetime.timezone.utc).replace(tzinfo=None).isoformat()
+if sys.version_info < (3, 12):
+    def utcnow_iso() -> str:
+        """`datetime.datetime.utcnow().isoformat()` (naive, no `Z`; quirk Q7) — twice per request."""
+        return datetime.datetime.utcnow().isoformat()
+else:  # utcnow() is deprecated from 3.12: same value through an aware datetime
+    def utcnow_iso() -> str:
+        """`datetime.datetime.utcnow().isoformat()` (naive, no `Z`; quirk Q7) without the deprecation."""
+        return datetime.datetime.now(datetime.timezone.utc).replace(tzinfo=None).isoformat()
 
 
 def parse_kubectl_output(stdout: str) -> Dict[str, Any]:
