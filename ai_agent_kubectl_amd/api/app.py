@@ -225,7 +225,7 @@ class KubectlService:
                 if timer is not None:
                     timer.cancel()
             self.metrics.llm_latency.observe(loop.time() - t0)
-            logger.info(f"LLM generated command for query '{query}': {command}")
+            logger.info("LLM generated command for query '%s': %s", query, command)
             return command
         except asyncio.TimeoutError:
             self.metrics.llm_errors.labels("timeout").inc()
@@ -310,23 +310,23 @@ def create_app(settings: Optional[Settings] = None, backend: Any = _UNSET,
         """POST /kubectl-command after auth + body validation (app.py:299-346); shared by the
         FastAPI route and the fast path."""
         svc.limiter.check(client_address(scope), "%s.get_kubectl_command" % __name__, svc.route_limits)
-        logger.info(f"Received query: '{query}'")
+        logger.info("Received query: '%s'", query)
         sanitized_query = safety.sanitize_query(query)
         from_cache = False
         try:
             cached = svc.cache.get(sanitized_query)
             if cached is not None:
-                logger.info(f"Cache hit for query: {sanitized_query}")
+                logger.info("Cache hit for query: %s", sanitized_query)
                 svc.metrics.cache_hits.inc()
                 command = cached
                 from_cache = True
             else:
-                logger.info(f"Cache miss for query: {sanitized_query}")
+                logger.info("Cache miss for query: %s", sanitized_query)
                 svc.metrics.cache_misses.inc()
-                logger.debug(f"Calling LLM for query: {sanitized_query}")
+                logger.debug("Calling LLM for query: %s", sanitized_query)
                 command = await svc.run_llm(sanitized_query)
                 svc.cache[sanitized_query] = command
-                logger.debug(f"Stored result in cache for query: {sanitized_query}")
+                logger.debug("Stored result in cache for query: %s", sanitized_query)
         except HTTPException:
             raise
         except Exception as e:
@@ -340,7 +340,7 @@ def create_app(settings: Optional[Settings] = None, backend: Any = _UNSET,
     async def execute(command: str, scope) -> Response:
         """POST /execute after auth + body validation (app.py:369-389)."""
         svc.limiter.check(client_address(scope), "%s.execute_kubectl_command" % __name__, svc.route_limits)
-        logger.info(f"Received execute request for command: '{command}'")
+        logger.info("Received execute request for command: '%s'", command)
         if not safety.is_safe_kubectl_command(command):
             raise HTTPException(status_code=status.HTTP_400_BAD_REQUEST, detail="Command failed safety checks")
         execution_data = await execute_command_async(
