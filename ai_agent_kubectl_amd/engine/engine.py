@@ -51,6 +51,7 @@ class LLMEngine:
         self.overlap = os.environ.get("KA_OVERLAP", "1") == "1"
         self._inflight = None
         self.chained_steps = 0
+        self.prefill_chains = 0    # decode steps queued behind a prefill before its readback
         self.idle_s = 0.0          # time the loop slept with no work (waiting for requests)
         self.step_t0: Optional[float] = None   # perf_counter at the start of the running step
         self.watchdog = None       # parallel/watchdog.py (TP/EP > 1, rank 0)
@@ -196,6 +197,19 @@ class LLMEngine:
                 return 0
             if self.overlap and batch.is_decode and self.runner.can_overlap(len(batch.seqs)):
                 self._inflight = (batch, self.runner.launch_decode_async(batch))
+                return len(batch.seqs)
+            if (self.overlap and not batch.is_decode and len(batch.prefill_seqs) == len(batch.seqs)
+                    and self.runner.can_overlap(len(batch.seqs))):
+                # a pure prefill step: queue the first decode step of the same rows behind it
+                # (input ids copied on the device from the prefill's samples) before reading the
+                # prefill back, so the GPU does not idle while the host applies ~256 prompts
+                ph = self.runner.launch_prefill_async(batch)
+                nxt = self._chain(batch)
+                nh = self.runner.launch_decode_async(nxt, chained=True) if nxt is not None else None
+                self.chained_steps += nxt is not None
+                self.prefill_chains += nxt is not None
+                self._finish_step(batch, self.runner.collect(ph))
+                self._inflight = (nxt, nh) if nxt is not None else None
                 return len(batch.seqs)
             self._finish_step(batch, self.runner.execute(batch))
         m = self.metrics

@@ -199,7 +199,36 @@ class ModelRunner:
             ev.record()
         return (ev, ho, B, t0)
 
+    @torch.inference_mode()
+    def launch_prefill_async(self, batch: Batch):
+        """Queue a prefill step without waiting for its tokens (TP = 1, every row a prompt, at most
+        `bmax` sequences): the sampled tokens are also left in `d_out`, in batch row order, so the
+        first decode step can be queued right behind it (`launch_decode_async(chained=True)`)
+        while the host applies this step's results.  Returns a handle for `collect`."""
+        t0 = time.perf_counter()
+        host = self._pack_prefill(batch, pad=True)
+        T, S, max_q, nc = self.padded_tokens(batch.num_tokens), len(batch.seqs), max(batch.num_query), len(batch.copies)
+        buf = torch.from_numpy(host).to(self.device, non_blocking=False)
+        tok = self._run_prefill(buf, T, S, max_q, nc, 0, batch.num_tokens)
+        self.d_out[:S].copy_(tok)
+        self.h_out[:S].copy_(tok, non_blocking=True)
+        ev = None
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+        return (ev, self.h_out, S, t0, T)
+
     def collect(self, handle) -> List[int]:
+        if len(handle) == 5:   # prefill handle (launch_prefill_async)
+            ev, ho, S, t0, T = handle
+            if ev is not None:
+                ev.synchronize()
+            now = time.perf_counter()
+            self.stats["prefill_steps"] += 1
+            self.stats["prefill_tokens"] += T
+            self.stats["prefill_ms"] += (now - t0) * 1e3
+            self._last_collect = now
+            return ho[:S].tolist()
         ev, ho, B, t0 = handle
         if ev is not None:
             ev.synchronize()

@@ -288,6 +288,7 @@ def test_overlapped_decode_matches_sync(tiny_engine):
         assert seqs[2].finish_reason == "abort"
     eng.overlap = True
     assert eng.chained_steps > 0
+    assert eng.prefill_chains > 0      # first decode queued behind the prefill before its readback
     assert outs[(True, True)] == outs[(False, True)]
     assert outs[(True, False)] == outs[(False, False)]
     assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
