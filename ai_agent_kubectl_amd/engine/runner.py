@@ -16,7 +16,7 @@ from __future__ import annotations
 import bisect
 import os
 import time
-from typing import Dict, List, Optional
+from typing import Dict, List, NamedTuple, Optional
 
 import numpy as np
 import torch
@@ -31,6 +31,15 @@ from .scheduler import Batch
 KIND_STOP, KIND_DECODE, KIND_PREFILL = 0, 1, 2
 HDR = 8
 
+
+
+class StepHandle(NamedTuple):
+    """A step queued on the device and not yet read back (`collect`)."""
+    event: Optional["torch.cuda.Event"]   # recorded after the step's token readback copy
+    host_out: torch.Tensor                # pinned host buffer the sampled tokens land in
+    rows: int
+    t0: float                             # perf_counter at launch
+    prefill_tokens: int = 0               # > 0: a prefill step (launch_prefill_async)
 
 class ModelRunner:
     def __init__(self, cfg: ModelConfig, weights: Dict[str, torch.Tensor], device: torch.device,
@@ -197,7 +206,7 @@ class ModelRunner:
         if self.device.type == "cuda":
             ev = torch.cuda.Event()
             ev.record()
-        return (ev, ho, B, t0)
+        return StepHandle(ev, ho, B, t0)
 
     @torch.inference_mode()
     def launch_prefill_async(self, batch: Batch):
@@ -216,20 +225,19 @@ class ModelRunner:
         if self.device.type == "cuda":
             ev = torch.cuda.Event()
             ev.record()
-        return (ev, self.h_out, S, t0, T)
+        return StepHandle(ev, self.h_out, S, t0, prefill_tokens=T)
 
-    def collect(self, handle) -> List[int]:
-        if len(handle) == 5:   # prefill handle (launch_prefill_async)
-            ev, ho, S, t0, T = handle
+    def collect(self, handle: "StepHandle") -> List[int]:
+        ev, ho, B, t0 = handle.event, handle.host_out, handle.rows, handle.t0
+        if handle.prefill_tokens:   # launch_prefill_async
             if ev is not None:
                 ev.synchronize()
             now = time.perf_counter()
             self.stats["prefill_steps"] += 1
-            self.stats["prefill_tokens"] += T
+            self.stats["prefill_tokens"] += handle.prefill_tokens
             self.stats["prefill_ms"] += (now - t0) * 1e3
             self._last_collect = now
-            return ho[:S].tolist()
-        ev, ho, B, t0 = handle
+            return ho[:B].tolist()
         if ev is not None:
             ev.synchronize()
         now = time.perf_counter()
