@@ -16,10 +16,23 @@
 // and optionally with the split-K reduction of the GEMM that produced x: x = bf16(sum_k P[k]) where P
 // holds `split` fp32 partial slabs of [rows, hidden] (gemm_skinny / gemm_tile with no output), so
 // the projection's reduce kernel and its bf16 round trip through HBM disappear.
-template <int NT, int MAXV>
+// PT: element type of the split-K slices P (float, or bf16_t from gemm_tile's p_bf16 mode).
+template <typename PT>
+KA_DEV void ld_part8(const PT* p, f32x4& s0, f32x4& s1) {
+  if constexpr (sizeof(PT) == 4) {
+    s0 = *reinterpret_cast<const f32x4*>(p);
+    s1 = *reinterpret_cast<const f32x4*>(p + 4);
+  } else {
+    const uint4 q = *reinterpret_cast<const uint4*>(p);
+    s0 = f32x4{lo_f(q.x), hi_f(q.x), lo_f(q.y), hi_f(q.y)};
+    s1 = f32x4{lo_f(q.z), hi_f(q.z), lo_f(q.w), hi_f(q.w)};
+  }
+}
+
+template <int NT, int MAXV, typename PT = float>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16_t* __restrict__ out, bf16_t* __restrict__ residual,
                                                      const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
-                                                     int hidden, float eps, const float* __restrict__ P, int split,
+                                                     int hidden, float eps, const PT* __restrict__ P, int split,
                                                      size_t pstride) {
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
@@ -33,12 +46,15 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16_t* __restrict__ out, b
     if (idx < nvec) {
       uint4 a;
       if (P != nullptr) {
-        const float* pr = P + (size_t)row * hidden + idx * 8;
-        f32x4 s0 = *reinterpret_cast<const f32x4*>(pr), s1 = *reinterpret_cast<const f32x4*>(pr + 4);
+        const PT* pr = P + (size_t)row * hidden + idx * 8;
+        f32x4 s0, s1;
+        ld_part8(pr, s0, s1);
 #pragma unroll 4
         for (int k = 1; k < split; ++k) {
-          s0 += *reinterpret_cast<const f32x4*>(pr + k * pstride);
-          s1 += *reinterpret_cast<const f32x4*>(pr + k * pstride + 4);
+          f32x4 t0, t1;
+          ld_part8(pr + k * pstride, t0, t1);
+          s0 += t0;
+          s1 += t1;
         }
         a = make_uint4(pack2(s0[0], s0[1]), pack2(s0[2], s0[3]), pack2(s1[0], s1[1]), pack2(s1[2], s1[3]));
       } else {
@@ -122,29 +138,34 @@ extern "C" int ka_rmsnorm(void* out, void* residual, const void* x, const void* 
   KA_CHECK_LAUNCH();
 }
 
-// out = rmsnorm(bf16(sum_k P[k]) (+ residual)) * w; P = split fp32 slabs of [rows, hidden]
-extern "C" int ka_rmsnorm_splitk(void* out, void* residual, const void* P, int split, const void* w, int rows,
-                                 int hidden, float eps, hipStream_t stream) {
-  if (rows <= 0) return 0;
-  if (hidden % 8 != 0 || hidden > 256 * 8 * 4 || split < 1) return (int)hipErrorInvalidValue;
+template <typename PT>
+static void launch_rmsnorm_splitk(bf16_t* o, bf16_t* r, const PT* p, int split, const bf16_t* wi, int rows, int hidden,
+                                  float eps, hipStream_t stream) {
   const int nvec = hidden / 8;
-  auto* o = static_cast<bf16_t*>(out);
-  auto* r = static_cast<bf16_t*>(residual);
-  auto* p = static_cast<const float*>(P);
-  auto* wi = static_cast<const bf16_t*>(w);
   const size_t ps = (size_t)rows * hidden;
   if (nvec <= 256)
-    hipLaunchKernelGGL((rmsnorm_kernel<256, 1>), dim3(rows), dim3(256), 0, stream, o, r, nullptr, wi, hidden, eps,
+    hipLaunchKernelGGL((rmsnorm_kernel<256, 1, PT>), dim3(rows), dim3(256), 0, stream, o, r, nullptr, wi, hidden, eps,
                        p, split, ps);
   else if (nvec <= 512)   // the split slabs are read once: 8 waves per row keep more loads in flight
-    hipLaunchKernelGGL((rmsnorm_kernel<512, 1>), dim3(rows), dim3(512), 0, stream, o, r, nullptr, wi, hidden, eps,
-                       p, split, ps);
-  else if (nvec <= 512)
-    hipLaunchKernelGGL((rmsnorm_kernel<256, 2>), dim3(rows), dim3(256), 0, stream, o, r, nullptr, wi, hidden, eps,
+    hipLaunchKernelGGL((rmsnorm_kernel<512, 1, PT>), dim3(rows), dim3(512), 0, stream, o, r, nullptr, wi, hidden, eps,
                        p, split, ps);
   else
-    hipLaunchKernelGGL((rmsnorm_kernel<256, 4>), dim3(rows), dim3(256), 0, stream, o, r, nullptr, wi, hidden, eps,
+    hipLaunchKernelGGL((rmsnorm_kernel<256, 4, PT>), dim3(rows), dim3(256), 0, stream, o, r, nullptr, wi, hidden, eps,
                        p, split, ps);
+}
+
+// out = rmsnorm(bf16(sum_k P[k]) (+ residual)) * w; P = split slabs of [rows, hidden], fp32 or (p_bf16) bf16
+extern "C" int ka_rmsnorm_splitk(void* out, void* residual, const void* P, int split, int p_bf16, const void* w,
+                                 int rows, int hidden, float eps, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (hidden % 8 != 0 || hidden > 256 * 8 * 4 || split < 1) return (int)hipErrorInvalidValue;
+  auto* o = static_cast<bf16_t*>(out);
+  auto* r = static_cast<bf16_t*>(residual);
+  auto* wi = static_cast<const bf16_t*>(w);
+  if (p_bf16)
+    launch_rmsnorm_splitk(o, r, static_cast<const bf16_t*>(P), split, wi, rows, hidden, eps, stream);
+  else
+    launch_rmsnorm_splitk(o, r, static_cast<const float*>(P), split, wi, rows, hidden, eps, stream);
   KA_CHECK_LAUNCH();
 }
 

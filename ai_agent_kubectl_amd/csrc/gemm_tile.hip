@@ -38,11 +38,13 @@ struct TileCfg {
 // LDS after it): hides about two loaded-HBM latencies instead of one; K per split must then be a
 // multiple of 128 (the loop is unrolled by two so hipcc counts vmcnt statically; loads past the
 // end are clamped to the last step and land in a buffer nobody reads again).
+// pbf16: the split-K slices P are stored as bf16 (half the slab traffic; the consumer — RMSNorm or
+// the fused decode attention — sums them in fp32, like a bf16 tensor-parallel all-reduce would).
 template <int WN, int WM, int TN, int TM, bool SWIGLU = false, bool PF2 = false>
 __global__ __launch_bounds__(64 * WN * WM) void gemm_tile_kernel(const bf16_t* __restrict__ X,
                                                                  const bf16_t* __restrict__ W,
                                                                  bf16_t* __restrict__ Y, float* __restrict__ P, int M,
-                                                                 int N, int K, int kps) {
+                                                                 int N, int K, int kps, int pbf16) {
   using C = TileCfg<WN, WM, TN, TM>;
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];   // [2][BN*8] W then [2][BM*8] X
   u32x4* ws = lds;
@@ -184,6 +186,9 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tile_kernel(const bf16_t* _
       const f32x4 v = acc[i][j];
       if (P == nullptr) {
         *reinterpret_cast<uint2*>(Y + (size_t)m * N + n) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      } else if (pbf16) {
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(P) + ((size_t)blockIdx.z * M + m) * N + n) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       } else {
         *reinterpret_cast<f32x4*>(P + ((size_t)blockIdx.z * M + m) * N + n) = v;
       }
@@ -333,7 +338,7 @@ extern "C" void ka_splitk_reduce_launch(bf16_t* Y, const float* P, int split, lo
 
 template <int WN, int WM, int TN, int TM, bool SW = false, bool PF2 = false>
 static void launch_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int split,
-                        int kps, hipStream_t stream) {
+                        int kps, hipStream_t stream, int pbf16 = 0) {
   using C = TileCfg<WN, WM, TN, TM>;
   static bool lds_attr = false;   // > 64 KB of dynamic LDS must be opted into (160 KB per CU on gfx950)
   if (!lds_attr) {
@@ -343,7 +348,7 @@ static void launch_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, i
   }
   dim3 grid((N + C::BN - 1) / C::BN, (M + C::BM - 1) / C::BM, split);
   hipLaunchKernelGGL((gemm_tile_kernel<WN, WM, TN, TM, SW, PF2>), grid, dim3(C::NT), C::LDS_BYTES, stream, X, W, Y, P, M,
-                     N, K, kps);
+                     N, K, kps, pbf16);
 }
 
 // Configurations (BN x BM, waves): 0 = 128x256 (2x4 waves, 64x64 per wave), 1 = 64x256 (1x4),
@@ -404,10 +409,12 @@ extern "C" int ka_gemm_tile_bn(int cfg) {
 }
 
 // split > 1 requires a workspace of split * M * N floats (the reduce kernel then writes Y).
+// p_bf16 (Y == nullptr, LDS-tiled configurations 0-4 and 15-20 only): the slices are bf16.
 extern "C" int ka_gemm_tile(void* Y, const void* X, const void* W, void* workspace, int M, int N, int K, int split,
-                            int cfg, hipStream_t stream) {
+                            int cfg, int p_bf16, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 32 != 0 || N % 16 != 0 || split < 1 || cfg < 0 || ka_gemm_tile_bm(cfg) < 0) return (int)hipErrorInvalidValue;
+  if (p_bf16 && (Y != nullptr || (cfg >= 5 && cfg < 15))) return (int)hipErrorInvalidValue;
   // k quantum: stream kernels (cfg >= 10) 32-deep stages, wide kernels pairs of 64-steps, tile 64
   const int kq = cfg >= 17 ? 128 : cfg >= 15 ? 64 : cfg >= 10 ? 32 : cfg >= 5 ? 128 : 64;
   if (K % kq != 0) return (int)hipErrorInvalidValue;
@@ -417,21 +424,23 @@ extern "C" int ka_gemm_tile(void* Y, const void* X, const void* W, void* workspa
   auto* w = static_cast<const bf16_t*>(W);
   auto* y = static_cast<bf16_t*>(Y);
   float* p = split > 1 ? static_cast<float*>(workspace) : nullptr;
-#define X_(id, a, b, c, d) if (cfg == id) launch_tile<a, b, c, d, false, true>(x, w, y, p, M, N, K, split, kps, stream);
+  const int pb = split > 1 ? p_bf16 : 0;
+#define X_(id, a, b, c, d) \
+  if (cfg == id) launch_tile<a, b, c, d, false, true>(x, w, y, p, M, N, K, split, kps, stream, pb);
   KA_PF2_CFGS(X_)
 #undef X_
-  if (cfg == 15) launch_tile<4, 2, 4, 8>(x, w, y, p, M, N, K, split, kps, stream);
-  if (cfg == 16) launch_tile<2, 4, 8, 4>(x, w, y, p, M, N, K, split, kps, stream);
+  if (cfg == 15) launch_tile<4, 2, 4, 8>(x, w, y, p, M, N, K, split, kps, stream, pb);
+  if (cfg == 16) launch_tile<2, 4, 8, 4>(x, w, y, p, M, N, K, split, kps, stream, pb);
   if (cfg >= 10 && cfg < 15) {
     const int rc = ka_gemm_stream_launch(y, x, w, p, M, N, K, split, kps, cfg, stream);
     if (rc) return rc;
   }
   switch (cfg) {
-    case 0: launch_tile<2, 4, 4, 4>(x, w, y, p, M, N, K, split, kps, stream); break;
-    case 1: launch_tile<1, 4, 4, 4>(x, w, y, p, M, N, K, split, kps, stream); break;
-    case 2: launch_tile<2, 2, 4, 4>(x, w, y, p, M, N, K, split, kps, stream); break;
-    case 3: launch_tile<2, 2, 4, 8>(x, w, y, p, M, N, K, split, kps, stream); break;
-    case 4: launch_tile<4, 2, 4, 4>(x, w, y, p, M, N, K, split, kps, stream); break;
+    case 0: launch_tile<2, 4, 4, 4>(x, w, y, p, M, N, K, split, kps, stream, pb); break;
+    case 1: launch_tile<1, 4, 4, 4>(x, w, y, p, M, N, K, split, kps, stream, pb); break;
+    case 2: launch_tile<2, 2, 4, 4>(x, w, y, p, M, N, K, split, kps, stream, pb); break;
+    case 3: launch_tile<2, 2, 4, 8>(x, w, y, p, M, N, K, split, kps, stream, pb); break;
+    case 4: launch_tile<4, 2, 4, 4>(x, w, y, p, M, N, K, split, kps, stream, pb); break;
     case 5: launch_wide<4, 4, 8>(x, w, y, p, M, N, K, split, kps, stream); break;
     case 6: launch_wide<2, 4, 8>(x, w, y, p, M, N, K, split, kps, stream); break;
     case 7: launch_wide<2, 4, 4>(x, w, y, p, M, N, K, split, kps, stream); break;

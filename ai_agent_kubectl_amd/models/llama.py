@@ -61,6 +61,9 @@ class LlamaModel:
         self.device = dev
         self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, device=dev)
         self.fuse_decode_rope = os.environ.get("KA_FUSE_DECODE_ROPE", "1") == "1"
+        # split-K partials of the norm-feeding projections (o_proj, down) stored as bf16: half the
+        # slab traffic; the fused reduce + RMSNorm still accumulates them in fp32
+        self.bf16_partials = os.environ.get("KA_BF16_PARTIALS", "1") == "1"
         self.layers = [self._layer(i) for i in range(cfg.num_layers)]
 
     def _layer(self, i):
@@ -99,7 +102,7 @@ class LlamaModel:
             # TP = 1: the projections feeding a norm leave their split-K partials to the fused
             # reduce + residual + RMSNorm kernel (ops.SplitK); with TP the all-reduce needs bf16
             fuse = self._local_comm
-            h = ops.linear(a.view(T, self.hq * self.D), L["wo"], defer_reduce=fuse)
+            h = ops.linear(a.view(T, self.hq * self.D), L["wo"], defer_reduce=fuse, bf16_partials=self.bf16_partials)
             self.comm.all_reduce(h)
             x = ops.rmsnorm(h, L["ln2"], eps, residual=residual)
             combined = False
@@ -108,7 +111,7 @@ class LlamaModel:
             else:
                 # batch <= 4: SiLU·mul computed inside the down GEMV's X staging (ops.swiglu_linear)
                 h = ops.swiglu_linear(ops.linear(x, L["w13"], defer_reduce=True), L["w2"], defer_reduce=fuse,
-                                      tile_fused=False)
+                                      tile_fused=False, bf16_partials=self.bf16_partials)
             if not combined:
                 self.comm.all_reduce(h)
         if meta.is_decode:   # every row is its sequence's last token (logits_indices = arange)

@@ -53,17 +53,28 @@ def _stream() -> int:
 
 
 class SplitK(NamedTuple):
-    """fp32 split-K partials of a projection whose reduction is deferred to the consumer (rmsnorm)."""
-    P: torch.Tensor          # [split, M, N] fp32
+    """Split-K partials of a projection whose reduction is deferred to the consumer (rmsnorm).
+    P is fp32, or bf16 when the producer was asked for `bf16_partials` (only rmsnorm reads those)."""
+    P: torch.Tensor          # [split, M, N] fp32 | bf16
     split: int
+
+    @property
+    def is_bf16(self) -> bool:
+        return self.P.dtype == torch.bfloat16
 
     @property
     def shape(self):
         return self.P.shape[1:]
 
+    def fp32(self) -> "SplitK":
+        """The fp32 partials a consumer without a bf16 path (RoPE, attention, SiLU) needs."""
+        if self.is_bf16:
+            raise TypeError("bf16 split-K partials are only consumed by rmsnorm")
+        return self
+
     def resolve(self) -> torch.Tensor:
         """bf16 [M, N] (for consumers without a fused path)."""
-        return self.P.sum(0).to(torch.bfloat16)
+        return self.P.float().sum(0).to(torch.bfloat16)
 
 
 def rmsnorm(x, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
@@ -74,8 +85,8 @@ def rmsnorm(x, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = N
         lib = require()
         rows, hidden = x.shape
         out = torch.empty((rows, hidden), dtype=w.dtype, device=w.device) if out is None else out
-        check(lib.ka_rmsnorm_splitk(_p(out), _p(residual), _p(x.P), x.split, _p(w), rows, hidden, float(eps),
-                                    _stream()), "rmsnorm_splitk")
+        check(lib.ka_rmsnorm_splitk(_p(out), _p(residual), _p(x.P), x.split, int(x.is_bf16), _p(w), rows, hidden,
+                                    float(eps), _stream()), "rmsnorm_splitk")
         return out
     if _ref(x):
         return ref.rmsnorm(x, w, eps, residual)
@@ -107,6 +118,7 @@ def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq: i
     the reduction then happens inside this kernel (bit-identical to reduce-then-rope)."""
     if isinstance(qkv, SplitK):
         lib = require()
+        qkv = qkv.fp32()
         T = qkv.shape[0]
         q_out = torch.empty((T, hq, d), dtype=k_cache.dtype, device=k_cache.device) if q_out is None else q_out
         check(lib.ka_rope_kv_splitk(_p(q_out), _p(k_cache), _p(v_cache), _p(qkv.P), qkv.split, _p(positions),
@@ -176,7 +188,7 @@ def decode_attention_rope(qkv, positions, cos_sin, slot_mapping, k_cache, v_cach
     B = ctx_lens.shape[0]
     out = torch.empty((B, hq, d), dtype=k_cache.dtype, device=k_cache.device) if out is None else out
     if isinstance(qkv, SplitK):
-        src, P, split = None, _p(qkv.P), qkv.split
+        src, P, split = None, _p(qkv.fp32().P), qkv.split
     else:
         src, P, split = _p(qkv), None, 1
     check(lib.ka_paged_decode_rope(_p(out), src, P, split, _p(k_cache), _p(v_cache), _p(positions), _p(cos_sin),
@@ -189,6 +201,7 @@ def silu_mul(gu, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """silu(gate) * up of the fused gate_up output; `gu` may be a `SplitK` (reduction fused in)."""
     if isinstance(gu, SplitK):
         lib = require()
+        gu = gu.fp32()
         T, two_i = gu.shape
         out = torch.empty((T, two_i // 2), dtype=torch.bfloat16, device=gu.P.device) if out is None else out
         check(lib.ka_silu_mul_splitk(_p(out), _p(gu.P), gu.split, T, two_i // 2, _stream()), "silu_mul_splitk")
@@ -262,12 +275,15 @@ GEMM_PLAN: dict = {}
 TILE_MAX_M = 512
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool = False):
+def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool = False,
+           bf16_partials: bool = False):
     """y = x @ w.T (w is [out, in]).  Decode-sized M goes to the hand-written weight-streaming
     kernel (M <= 256), the LDS-tiled MFMA kernel (M <= 512) or hipBLASLt, whichever the autotuned
     plan measured fastest for this (M, N, K); other shapes (prefill) go to hipBLASLt via F.linear.
     defer_reduce: when the chosen kernel splits K, return its fp32 partials as a `SplitK` for a
-    consumer that fuses the reduction (rmsnorm) instead of running the reduce kernel."""
+    consumer that fuses the reduction (rmsnorm) instead of running the reduce kernel.
+    bf16_partials: with defer_reduce, an LDS-tiled plan stores those partials as bf16 (half the
+    slab write + read; the rmsnorm consumer still sums them in fp32) — for rmsnorm consumers only."""
     M, K = x.shape
     N = w.shape[0]
     if _ref(x) or M > TILE_MAX_M or K % 64 != 0 or N % 4 != 0 or not x.is_contiguous():
@@ -280,7 +296,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
         elif plan[0] == "blas":
             return torch.nn.functional.linear(x, w)
         elif plan[0] == "tile":
-            return linear_tile(x, w, plan[2], plan[1], defer_reduce)
+            return linear_tile(x, w, plan[2], plan[1], defer_reduce, bf16_partials)
         else:
             split = plan[1]
     if M > SKINNY_MAX_M:
@@ -311,7 +327,8 @@ def tile_k_quantum(cfg: int) -> int:
 GEMV_SWIGLU_MAX_M = 4   # csrc/gemm_skinny.hip GEMV_MAX_M
 
 
-def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, tile_fused: bool = True):
+def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, tile_fused: bool = True,
+                  bf16_partials: bool = False):
     """y = (silu(gu[:, :I]) * gu[:, I:]) @ w.T — the MLP down projection fed directly by the fused
     gate_up output (a bf16 tensor; a `SplitK` goes through silu_mul's fused reduce).
 
@@ -324,7 +341,7 @@ def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, tile_fused: b
       N/BN column tiles re-stages X and so recomputes the activation;
     * otherwise SiLU·mul then `linear`."""
     if isinstance(gu, SplitK) or _ref(gu) or not gu.is_contiguous():
-        return linear(silu_mul(gu), w, defer_reduce=defer_reduce)
+        return linear(silu_mul(gu), w, defer_reduce=defer_reduce, bf16_partials=bf16_partials)
     M, I2 = gu.shape
     I = I2 // 2
     N = w.shape[0]
@@ -357,7 +374,7 @@ def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, tile_fused: b
             check(lib.ka_gemm_tile_swiglu(_p(y), _p(gu), _p(w), _p(ws), M, N, I, split, cfg, _stream()),
                   "gemm_tile_swiglu")
             return y
-    return linear(silu_mul(gu), w, defer_reduce=defer_reduce)
+    return linear(silu_mul(gu), w, defer_reduce=defer_reduce, bf16_partials=bf16_partials)
 
 
 def tile_shape(cfg: int):
@@ -366,8 +383,10 @@ def tile_shape(cfg: int):
     return lib.ka_gemm_tile_bn(cfg), lib.ka_gemm_tile_bm(cfg)
 
 
-def linear_tile(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, defer_reduce: bool = False):
-    """y = x @ w.T through the LDS-tiled MFMA kernel (csrc/gemm_tile.hip), split-K `split`."""
+def linear_tile(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, defer_reduce: bool = False,
+                bf16_partials: bool = False):
+    """y = x @ w.T through the LDS-tiled MFMA kernel (csrc/gemm_tile.hip), split-K `split`.
+    bf16_partials (with defer_reduce; configurations 0-4 and 15-20): bf16 split-K slices."""
     M, K = x.shape
     N = w.shape[0]
     kq = tile_k_quantum(cfg)
@@ -376,12 +395,14 @@ def linear_tile(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, defe
     lib = require()
     kps = ((K // split + kq - 1) // kq) * kq
     split = (K + kps - 1) // kps
-    ws = torch.empty((split, M, N), dtype=torch.float32, device=x.device) if split > 1 else None
+    pb = int(defer_reduce and split > 1 and bf16_partials and not 5 <= cfg < 15)
+    ws = (torch.empty((split, M, N), dtype=torch.bfloat16 if pb else torch.float32, device=x.device)
+          if split > 1 else None)
     if defer_reduce and split > 1:
-        check(lib.ka_gemm_tile(None, _p(x), _p(w), _p(ws), M, N, K, split, cfg, _stream()), "gemm_tile")
+        check(lib.ka_gemm_tile(None, _p(x), _p(w), _p(ws), M, N, K, split, cfg, pb, _stream()), "gemm_tile")
         return SplitK(ws, split)
     y = torch.empty((M, N), dtype=x.dtype, device=x.device)
-    check(lib.ka_gemm_tile(_p(y), _p(x), _p(w), _p(ws), M, N, K, split, cfg, _stream()), "gemm_tile")
+    check(lib.ka_gemm_tile(_p(y), _p(x), _p(w), _p(ws), M, N, K, split, cfg, 0, _stream()), "gemm_tile")
     return y
 
 

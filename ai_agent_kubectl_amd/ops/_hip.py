@@ -41,11 +41,11 @@ _SIGS = {
     "ka_paged_prefill": [P, P, P, P, P, I, P, P, I, I, I, I, I, I, F, P],
     "ka_gemm_skinny": [P, P, P, P, I, I, I, I, P],
     "ka_gemv_swiglu": [P, P, P, P, I, I, I, I, P],
-    "ka_rmsnorm_splitk": [P, P, P, I, P, I, I, F, P],
+    "ka_rmsnorm_splitk": [P, P, P, I, I, P, I, I, F, P],
     "ka_rope_kv_splitk": [P, P, P, P, I, P, P, P, I, I, I, I, I, P],
     "ka_silu_mul_splitk": [P, P, I, I, I, P],
     "ka_kv_block_copy": [P, P, P, P, I, I, ctypes.c_long, ctypes.c_long, P],
-    "ka_gemm_tile": [P, P, P, P, I, I, I, I, I, P],
+    "ka_gemm_tile": [P, P, P, P, I, I, I, I, I, I, P],
     "ka_gemm_tile_swiglu": [P, P, P, P, I, I, I, I, I, P],
     "ka_gemm_tile_bm": [I],
     "ka_gemm_tile_bn": [I],

@@ -341,6 +341,28 @@ def test_linear_defer_reduce_roundtrip():
     close(sk2.resolve(), x.float() @ w.float().t(), atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("cfg", [0, 2, 4, 15, 17])
+def test_gemm_tile_bf16_partials_into_rmsnorm(cfg):
+    """bf16 split-K slices (o_proj / down at decode) -> fused reduce + residual + RMSNorm matches the
+    fp32 reference of the whole chain, and the slices themselves are bf16(fp32 slices)."""
+    M, N, K = 256, 4096, 4096
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(BF)
+    sk32 = ops.linear_tile(x, w, cfg, 4, defer_reduce=True)
+    sk16 = ops.linear_tile(x, w, cfg, 4, defer_reduce=True, bf16_partials=True)
+    assert sk16.is_bf16 and not sk32.is_bf16 and sk16.split == sk32.split
+    assert torch.equal(sk16.P, sk32.P.to(BF))
+    with pytest.raises(TypeError):
+        ops.silu_mul(sk16)
+    g = (torch.rand(N, device=DEV) + 0.5).to(BF)
+    res0 = torch.randn(M, N, device=DEV).to(BF)
+    r1, r2 = res0.clone(), res0.clone()
+    got = ops.rmsnorm(sk16, g, 1e-5, residual=r1)
+    want = ref.rmsnorm((x.float() @ w.float().t()).to(BF), g, 1e-5, r2)
+    close(got, want, atol=5e-2, rtol=3e-2)
+    close(r1, r2, atol=3e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("M", [48, 128, 200, 256, 384, 512])
 @pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1040, 512)])
 def test_gemm_tile(M, N, K):
