@@ -113,14 +113,18 @@ class ModelRunner:
             return {}
         from ..ops.autotune import tune_linear
         groups = {}
+        norm_fed = set()
+        local = getattr(self.model, "_local_comm", False)
         for L in self.model.layers:
             for k in ("wqkv", "wo", "w13", "w2"):
                 w = L.get(k)
                 if w is not None and w.dim() == 2:
                     groups.setdefault(tuple(w.shape), []).append(w)
+                    if local and k in ("wo", "w2"):   # llama.py defers their split-K reduce into the norm
+                        norm_fed.add(tuple(w.shape))
         lm = self.model.W["lm_head"]
         groups.setdefault(tuple(lm.shape), []).append(lm)
-        return tune_linear(groups, self.buckets)
+        return tune_linear(groups, self.buckets, norm_fed, getattr(self.model, "bf16_partials", False))
 
     @torch.inference_mode()
     def capture_graphs(self, autotune: bool = True) -> float:

@@ -13,8 +13,8 @@ from typing import Dict, List, Sequence, Tuple
 
 import torch
 
-from . import (GEMM_PLAN, SKINNY_MAX_M, TILE_CFGS, TILE_MAX_M, linear, linear_tile, skinny_split, tile_k_quantum,
-               tile_shape)
+from . import (GEMM_PLAN, SKINNY_MAX_M, TILE_CFGS, TILE_MAX_M, linear, linear_tile, rmsnorm, skinny_split,
+               tile_k_quantum, tile_shape)
 
 logger = logging.getLogger("app.engine")
 
@@ -77,11 +77,16 @@ def _tunableop_end() -> None:
 
 
 @torch.inference_mode()
-def tune_linear(groups: Dict[Tuple[int, int], List[torch.Tensor]], Ms: Sequence[int]) -> Dict:
-    """groups: (N, K) -> list of weight tensors of that shape (one per layer)."""
+def tune_linear(groups: Dict[Tuple[int, int], List[torch.Tensor]], Ms: Sequence[int],
+                norm_fed: Sequence[Tuple[int, int]] = (), bf16_partials: bool = True) -> Dict:
+    """groups: (N, K) -> list of weight tensors of that shape (one per layer).
+    norm_fed: shapes whose output goes straight into the fused residual + RMSNorm (o_proj and down
+    at TP = 1).  Their candidates are timed together with that norm, split-K ones with the
+    reduction deferred into it (as the model runs them), so a split plan is not charged for a
+    reduce kernel the model never launches."""
     tunable = _tunableop_begin()
     try:
-        return _tune(groups, Ms)
+        return _tune(groups, Ms, set(norm_fed), bf16_partials)
     finally:
         if tunable:
             _tunableop_end()
@@ -116,27 +121,33 @@ def tile_candidates(M: int, N: int, K: int, cfgs: Sequence[int] = ()):
     return out
 
 
-def _tune(groups, Ms) -> Dict:
+def _tune(groups, Ms, norm_fed=frozenset(), bf16_partials: bool = True) -> Dict:
     report = {}
     for (N, K), ws in groups.items():
         ws = ws[: max(2, min(len(ws), 16))]
+        fed = (N, K) in norm_fed
+        dev, dt = ws[0].device, ws[0].dtype
+        g = torch.ones(N, device=dev, dtype=dt)
         for M in sorted(set(int(m) for m in Ms if m <= TILE_MAX_M)):
-            x = torch.randn(M, K, device=ws[0].device, dtype=ws[0].dtype)
+            x = torch.randn(M, K, device=dev, dtype=dt)
+            res = torch.zeros(M, N, device=dev, dtype=dt)
+            norm = (lambda h: rmsnorm(h, g, 1e-5, residual=res)) if fed else (lambda h: h)
             GEMM_PLAN.pop((M, N, K), None)
-            t_blas = _time(lambda w: torch.nn.functional.linear(x, w), ws)
+            t_blas = _time(lambda w: norm(torch.nn.functional.linear(x, w)), ws)
             best = ("blas", 0, 0, t_blas)
             if M <= SKINNY_MAX_M and K % 64 == 0 and N % 4 == 0:
                 cands = sorted({skinny_split(M, N, K, t) for t in (256, 512, 1024, 2048)})
                 for sp in cands:
-                    t = _time(lambda w: linear(x, w, split=sp), ws)
+                    t = _time(lambda w: norm(linear(x, w, split=sp, defer_reduce=fed)), ws)
                     if t < best[3]:
                         best = ("skinny", sp, 0, t)
             for cfg, sp in tile_candidates(M, N, K):
-                t = _time(lambda w: linear_tile(x, w, cfg, sp), ws)
+                t = _time(lambda w: norm(linear_tile(x, w, cfg, sp, defer_reduce=fed, bf16_partials=bf16_partials)),
+                          ws)
                 if t < best[3]:
                     best = ("tile", sp, cfg, t)
             GEMM_PLAN[(M, N, K)] = (best[0], best[1], best[2])
             report[(M, N, K)] = {"choice": best[0], "split": best[1], "cfg": best[2], "us": round(best[3], 1),
-                                 "blas_us": round(t_blas, 1)}
+                                 "blas_us": round(t_blas, 1), "with_norm": fed}
     logger.info("gemm plan: %s", report)
     return report
