@@ -1,16 +1,21 @@
-import sys, torch
-sys.path.insert(0, "/root/repo")
-from ai_agent_kubectl_amd.ops.autotune import tune_linear
-from ai_agent_kubectl_amd.ops.autotune import _time
-from ai_agent_kubectl_amd import ops
+"""Print the decode GEMM plan the engine's autotune picks for the Llama-3-8B projection shapes.
+
+Usage (GPU): python scripts/autotune_report.py [M ...]   (default: 128 256)
+O / down are tuned as the model runs them at TP = 1: together with the fused reduce + RMSNorm.
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from ai_agent_kubectl_amd.ops.autotune import tune_linear  # noqa: E402
+
+Ms = [int(a) for a in sys.argv[1:]] or [128, 256]
 shapes = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
 groups = {s: [(torch.randn(*s, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(16)] for s in shapes}
-rep = tune_linear(groups, [1, 2, 8])
-for k, v in sorted(rep.items()):
-    print(k, v)
-# detail for O at M=1
-x = torch.randn(1, 4096, device="cuda", dtype=torch.bfloat16)
-ws = groups[(4096, 4096)]
-for sp in (1, 2, 4, 8, 16):
-    print("skinny O split", sp, round(_time(lambda w: ops.linear(x, w, split=sp), ws), 1))
-print("blas O", round(_time(lambda w: torch.nn.functional.linear(x, w), ws), 1))
+for fed in ((), ((4096, 4096), (4096, 14336))):
+    rep = tune_linear(groups, Ms, norm_fed=fed, bf16_partials=True)
+    print("norm-fed O/down" if fed else "plain (reduce kernel charged)")
+    for k, v in sorted(rep.items()):
+        print(" ", k, v)
