@@ -36,8 +36,9 @@
 // kernel and one launch boundary less per layer.
 struct DecodeFuse {
   const bf16_t* qkv;        // [B, (hq + 2 hkv) * 128] bf16, or nullptr when P is given
-  const float* P;           // [split, B, (hq + 2 hkv) * 128] fp32 split-K partials
+  const float* P;           // [split, B, (hq + 2 hkv) * 128] fp32 (or, pbf16, bf16) split-K partials
   int split;
+  int pbf16;
   size_t pstride;
   const int* positions;
   const float* cos_sin;     // [max_pos, 128]: cos | sin halves
@@ -48,6 +49,16 @@ struct DecodeFuse {
 
 __device__ __forceinline__ uint2 dq_ld4(const DecodeFuse& f, size_t off) {
   if (f.P == nullptr) return *reinterpret_cast<const uint2*>(f.qkv + off);
+  if (f.pbf16) {   // bf16 slices (gemm_tile p_bf16): summed in fp32
+    const bf16_t* pb = reinterpret_cast<const bf16_t*>(f.P);
+    uint2 q = *reinterpret_cast<const uint2*>(pb + off);
+    f32x4 s = f32x4{lo_f(q.x), hi_f(q.x), lo_f(q.y), hi_f(q.y)};
+    for (int k = 1; k < f.split; ++k) {
+      q = *reinterpret_cast<const uint2*>(pb + k * f.pstride + off);
+      s += f32x4{lo_f(q.x), hi_f(q.x), lo_f(q.y), hi_f(q.y)};
+    }
+    return make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
+  }
   f32x4 s = *reinterpret_cast<const f32x4*>(f.P + off);
   for (int k = 1; k < f.split; ++k) s += *reinterpret_cast<const f32x4*>(f.P + k * f.pstride + off);
   return make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
@@ -450,9 +461,9 @@ extern "C" int ka_paged_decode(void* out, const void* q, const void* k_cache, co
 
 // Fused RoPE + KV append + paged decode attention (one query token per sequence; every
 // slot_mapping entry must be a valid slot).  qkv: bf16 [B, (hq + 2 hkv) * 128], or P: fp32 split-K
-// partials [split, B, (hq + 2 hkv) * 128] (qkv ignored when P is non-null).  ctx_lens include the
-// new token.
-extern "C" int ka_paged_decode_rope(void* out, const void* qkv, const float* P, int split, void* k_cache,
+// partials [split, B, (hq + 2 hkv) * 128], bf16 when p_bf16 (qkv ignored when P is non-null).
+// ctx_lens include the new token.
+extern "C" int ka_paged_decode_rope(void* out, const void* qkv, const float* P, int split, int p_bf16, void* k_cache,
                                     void* v_cache, const int* positions, const float* cos_sin,
                                     const int* slot_mapping, const int* block_tables, int max_blocks,
                                     const int* ctx_lens, int batch, int hq, int hkv, int head_dim, int block_size,
@@ -461,8 +472,8 @@ extern "C" int ka_paged_decode_rope(void* out, const void* qkv, const float* P, 
   // the rotated q rows + k are staged in the 4 KB P scratch: G + 1 <= 16 rows of 128
   if (head_dim != HD || block_size != KBS || hq % hkv != 0 || hq / hkv > 15) return (int)hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
-  DecodeFuse fz{static_cast<const bf16_t*>(qkv), P, split, (size_t)batch * (hq + 2 * hkv) * HD, positions, cos_sin,
-                slot_mapping, static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache)};
+  DecodeFuse fz{static_cast<const bf16_t*>(qkv), P, split, p_bf16, (size_t)batch * (hq + 2 * hkv) * HD, positions,
+                cos_sin, slot_mapping, static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache)};
   hipLaunchKernelGGL(paged_decode_kernel<true>, dim3(hkv, batch), dim3(256), 0, stream, static_cast<bf16_t*>(out),
                      nullptr, static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), block_tables,
                      max_blocks, ctx_lens, hq, hkv, scale_log2, fz);

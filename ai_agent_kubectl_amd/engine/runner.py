@@ -122,6 +122,9 @@ class ModelRunner:
                     groups.setdefault(tuple(w.shape), []).append(w)
                     if local and k in ("wo", "w2"):   # llama.py defers their split-K reduce into the norm
                         norm_fed.add(tuple(w.shape))
+                    # not QKV: timed with a norm standing in for the fused decode attention, its
+                    # split-K plan won (25.8 vs 26.9 us at M = 256) but the attention prologue that
+                    # reduces the partials grew 24.1 -> 29.7 us (profiles/phase_profile_c256_qkv_proxy_negative.txt)
         lm = self.model.W["lm_head"]
         groups.setdefault(tuple(lm.shape), []).append(lm)
         return tune_linear(groups, self.buckets, norm_fed, getattr(self.model, "bf16_partials", False))

@@ -87,8 +87,10 @@ class LlamaModel:
                 x = ops.rmsnorm(h, L["ln1"], eps, residual=residual)
             # column-parallel projections: no all-reduce before their consumer, so a split-K plan
             # hands its fp32 partials to the RoPE / SiLU kernels, which reduce them on the fly
-            qkv = ops.linear(x, L["wqkv"], defer_reduce=True)
-            if meta.is_decode and self.fuse_decode_rope:
+            fused = meta.is_decode and self.fuse_decode_rope
+            # the fused decode attention reduces bf16 partials too; rope_kv_write needs fp32 ones
+            qkv = ops.linear(x, L["wqkv"], defer_reduce=True, bf16_partials=fused and self.bf16_partials)
+            if fused:
                 # RoPE + KV append + attention in one kernel (the rotated q never goes to HBM)
                 a = ops.decode_attention_rope(qkv, meta.positions, self.cos_sin, meta.slot_mapping, k_cache[li],
                                               v_cache[li], meta.block_tables, meta.ctx_lens, self.hq, self.hkv,

@@ -54,7 +54,8 @@ def _stream() -> int:
 
 class SplitK(NamedTuple):
     """Split-K partials of a projection whose reduction is deferred to the consumer (rmsnorm).
-    P is fp32, or bf16 when the producer was asked for `bf16_partials` (only rmsnorm reads those)."""
+    P is fp32, or bf16 when the producer was asked for `bf16_partials` (only rmsnorm and the fused
+    decode attention read those)."""
     P: torch.Tensor          # [split, M, N] fp32 | bf16
     split: int
 
@@ -69,7 +70,7 @@ class SplitK(NamedTuple):
     def fp32(self) -> "SplitK":
         """The fp32 partials a consumer without a bf16 path (RoPE, attention, SiLU) needs."""
         if self.is_bf16:
-            raise TypeError("bf16 split-K partials are only consumed by rmsnorm")
+            raise TypeError("bf16 split-K partials are only consumed by rmsnorm and decode_attention_rope")
         return self
 
     def resolve(self) -> torch.Tensor:
@@ -178,20 +179,22 @@ def decode_attention_rope(qkv, positions, cos_sin, slot_mapping, k_cache, v_cach
                           hq: int, hkv: int, d: int, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """One decode token per sequence: RoPE + paged-KV append + paged attention in ONE kernel
     (attention.hip, paged_decode_kernel<true>): the rotated queries never leave the chip and the new
-    token is merged from LDS.  `qkv` may be a `SplitK` (the QKV projection's fp32 partials).
+    token is merged from LDS.  `qkv` may be a `SplitK` (the QKV projection's fp32 or bf16 partials).
     Equivalent to `attention_decode(rope_kv_write(qkv, ...), ...)` (the CPU path)."""
     lead = qkv.P if isinstance(qkv, SplitK) else qkv
     if _ref(lead) or d != 128 or k_cache.shape[2] != 16 or hq % hkv or hq // hkv > 15:
+        if isinstance(qkv, SplitK) and qkv.is_bf16:
+            qkv = qkv.resolve()
         q = rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq, hkv, d)
         return attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, out=out)
     lib = require()
     B = ctx_lens.shape[0]
     out = torch.empty((B, hq, d), dtype=k_cache.dtype, device=k_cache.device) if out is None else out
-    if isinstance(qkv, SplitK):
-        src, P, split = None, _p(qkv.fp32().P), qkv.split
+    if isinstance(qkv, SplitK):   # fp32 or bf16 partials: the prologue reduces either
+        src, P, split, pb = None, _p(qkv.P), qkv.split, int(qkv.is_bf16)
     else:
-        src, P, split = _p(qkv), None, 1
-    check(lib.ka_paged_decode_rope(_p(out), src, P, split, _p(k_cache), _p(v_cache), _p(positions), _p(cos_sin),
+        src, P, split, pb = _p(qkv), None, 1, 0
+    check(lib.ka_paged_decode_rope(_p(out), src, P, split, pb, _p(k_cache), _p(v_cache), _p(positions), _p(cos_sin),
                                    _p(slot_mapping), _p(block_tables), block_tables.shape[1], _p(ctx_lens), B, hq,
                                    hkv, d, k_cache.shape[2], float(scale), _stream()), "paged_decode_rope")
     return out

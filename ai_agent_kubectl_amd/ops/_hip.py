@@ -37,7 +37,7 @@ _SIGS = {
     "ka_moe_topk": [P, P, P, I, I, I, P],
     "ka_paged_decode": [P, P, P, P, P, I, P, I, I, I, I, I, F, P],
     "ka_set_prefill_attn_chunk": [I],
-    "ka_paged_decode_rope": [P, P, P, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, P],
+    "ka_paged_decode_rope": [P, P, P, I, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, P],
     "ka_paged_prefill": [P, P, P, P, P, I, P, P, I, I, I, I, I, I, F, P],
     "ka_gemm_skinny": [P, P, P, P, I, I, I, I, P],
     "ka_gemv_swiglu": [P, P, P, P, I, I, I, I, P],

@@ -128,7 +128,7 @@ def test_paged_decode_padding_rows_zero():
 
 
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (4, 1)])
-@pytest.mark.parametrize("split", [0, 1, 4])
+@pytest.mark.parametrize("split", [0, 1, 4, -1, -4])
 def test_decode_attention_rope_fused(hq, hkv, split):
     """RoPE + KV append + paged decode in one kernel == rope_kv_write then attention_decode (fp32
     torch references), on bf16 qkv and on split-K partials; cache contents identical to the
@@ -144,12 +144,13 @@ def test_decode_attention_rope_fused(hq, hkv, split):
     pos = (ctx - 1).clamp(min=0)
     cs = ref.rope_cos_sin(4096, d, 5e5, device=DEV)
     width = (hq + 2 * hkv) * d
-    if split:
-        qkv = ops.SplitK(torch.randn(split, S, width, device=DEV), split)
-        qkv_bf = qkv.resolve()
-        P0 = qkv.P[0].clone()
-        for k in range(1, split):
-            P0 += qkv.P[k]
+    if split:   # split < 0: bf16 partials (gemm_tile p_bf16), summed in fp32 by the prologue
+        sp = abs(split)
+        P = torch.randn(sp, S, width, device=DEV)
+        qkv = ops.SplitK(P.to(BF) if split < 0 else P, sp)
+        P0 = qkv.P[0].float().clone()
+        for k in range(1, sp):
+            P0 += qkv.P[k].float()
         qkv_bf = P0.to(BF)                                   # the kernels' summation order
     else:
         qkv = qkv_bf = torch.randn(S, width, device=DEV, dtype=BF)
