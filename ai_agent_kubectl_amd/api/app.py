@@ -20,6 +20,7 @@ FastAPI's `JSONResponse` uses, skipping a redundant pydantic round trip per requ
 from __future__ import annotations
 
 import asyncio
+import os
 import contextlib
 import json
 import logging
@@ -30,6 +31,7 @@ from fastapi.responses import JSONResponse, Response
 
 from .. import safety
 from ..cache import TTLCache
+from ..shared_state import SharedFixedWindowLimiter, SharedTTLCache, open_from_settings
 from ..config import Settings
 from ..executor import execute_command_async, utcnow_iso
 from ..llm.base import LLMBackend, LLMUnavailableError, build_backend
@@ -86,10 +88,16 @@ def _generated_json(command: str, from_cache: bool, start: str, end: str) -> byt
 async def _lag_probe(metrics, period: float = 0.05) -> None:
     """Observe how late the event loop wakes a 50 ms sleeper (GIL / blocking-call diagnostics)."""
     loop = asyncio.get_running_loop()
+    # several API workers: /metrics is rendered by whichever worker gets the scrape, from every
+    # worker's shared samples, so each worker publishes its batched HTTP observations promptly
+    shared = bool(os.environ.get("PROMETHEUS_MULTIPROC_DIR"))
     while True:
         t0 = loop.time()
         await asyncio.sleep(period)
         metrics.loop_lag.observe(max(0.0, loop.time() - t0 - period))
+        if shared:
+            for flush in metrics.flush_hooks:
+                flush()
 
 
 class FastPathMiddleware:
@@ -181,9 +189,16 @@ class KubectlService:
         self.settings = settings
         self.backend = backend
         self.metrics = metrics
-        self.cache = TTLCache(maxsize=settings.CACHE_MAXSIZE, ttl=settings.CACHE_TTL)
         self.route_limits = parse_many(settings.RATE_LIMIT)
-        self.limiter = FixedWindowLimiter(default_limits=self.route_limits)
+        # several API workers (serve.py WORKERS > 1): one cache and one set of limit windows in
+        # shared memory, so from_cache and 429 are global as with the reference's single process
+        self.shared = open_from_settings(settings)
+        if self.shared is not None:
+            self.cache = SharedTTLCache(self.shared, maxsize=settings.CACHE_MAXSIZE, ttl=settings.CACHE_TTL)
+            self.limiter = SharedFixedWindowLimiter(self.shared, default_limits=self.route_limits)
+        else:
+            self.cache = TTLCache(maxsize=settings.CACHE_MAXSIZE, ttl=settings.CACHE_TTL)
+            self.limiter = FixedWindowLimiter(default_limits=self.route_limits)
 
     async def run_llm(self, query: str) -> str:
         """`run_llm_chain_async` (app.py:177-197): timeout + parser + HTTP error mapping."""

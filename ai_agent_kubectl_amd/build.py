@@ -40,6 +40,17 @@ def _run(cmd):
     return r.stdout
 
 
+def file_flags(src: str):
+    """Per-source hipcc flags from a `// KA_HIPCC_FLAGS: ...` line in the file's header comment."""
+    with open(src) as f:
+        for i, line in enumerate(f):
+            if line.startswith("// KA_HIPCC_FLAGS:"):
+                return line.split(":", 1)[1].split()
+            if i > 40:
+                break
+    return []
+
+
 def build_hip(force: bool = False, verbose: bool = False, extra_flags=()) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = glob.glob(os.path.join(CSRC, "*.h"))
@@ -54,7 +65,7 @@ def build_hip(force: bool = False, verbose: bool = False, extra_flags=()) -> str
     def compile_one(src):
         obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
         if force or _newer([src] + headers, obj):
-            _run([HIPCC, *flags, "-c", src, "-o", obj])
+            _run([HIPCC, *flags, *file_flags(src), "-c", src, "-o", obj])
         return obj
 
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))

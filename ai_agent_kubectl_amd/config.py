@@ -122,6 +122,10 @@ class Settings:
     MAX_NUM_BATCHED_TOKENS: int = 8192
     FAULT_LLM_DELAY_MS: int = 0
     FAULT_LLM_ERROR: str = ""
+    # --- multi-worker HTTP tier (serve.py) ---
+    WORKERS: int = 1                     # API worker processes sharing the port (SO_REUSEPORT)
+    SHARED_STATE: str = ""               # shared-memory segment name for the cache + limiter ("" = process-local)
+    ENGINE_DEVICES: str = ""             # DP replica devices, e.g. "cuda:0,cuda:1" or "cpu,cpu" ("" = cuda:0..DP-1)
 
     @property
     def log_level(self) -> str:

@@ -1,0 +1,895 @@
+// gemm_mfma: the engine's projection GEMM for every M >= 48 (decode batches, mixed steps and
+// prefill):  Y[M, N] = X[M, K] * W[N, K]^T, bf16 in, fp32 accumulate, fused epilogues.
+//
+// Design (cdna_hip_programming.md §5 "Canonical CDNA GEMM", T1, T2, "glds vs register staging"):
+//   * workgroup tile BN weight rows x BM activation rows, BK = 64; waves laid out WN x WM, each
+//     wave TN x TM MFMA 16x16x32 tiles.  W is the MFMA A operand and X the B operand, so a lane's
+//     four accumulator values are four consecutive output columns (8-B bf16 stores) and, for the
+//     interleaved gate_up weight, a lane holds gate and up of the same output element;
+//   * both operands are K-contiguous and staged HBM/L2 -> LDS by LDS-DMA (global_load_lds
+//     dwordx4): no VGPR round trip, one 16-B DMA per lane.  The LDS image is lane-linear per
+//     wave-instruction (8 rows x 128 B); the XOR swizzle (slot = chunk ^ ((row >> 1) & 7)) is
+//     applied to the per-lane GLOBAL source address and to the ds_read_b128 address (rule 21), and
+//     makes the 16 rows a ds_read_b128 lane group touches land on 16 distinct 16-B bank slots;
+//   * STAGES-deep LDS ring, one barrier per k-step: wait for the stage being computed with a
+//     counted vmcnt (STAGES - 2 stages stay in flight across the barrier), barrier (every wave's
+//     DMA of that stage has landed, every wave is done reading the slot about to be refilled),
+//     issue the DMA of stage t + STAGES - 1, then ds_read + MFMA on stage t;
+//   * XCD-aware tile order (T1): consecutive logical tiles share an XCD (bijective remap of the
+//     round-robin dispatch) and are grouped GM M-tiles x N so the W and X panels of the blocks
+//     running together on one XCD are L2 hits;
+//   * split-K over gridDim.z (fp32 or bf16 partial slabs for a fused consumer: RMSNorm, decode
+//     attention, SiLU) and epilogues: bf16 store, partial slab, SwiGLU (interleaved gate_up rows,
+//     silu(g) * u computed from the accumulators: the [M, 2I] gate_up output never exists).
+// KA_HIPCC_FLAGS: -mllvm -amdgpu-mfma-vgpr-form
+// (accumulators in VGPRs with in-place MFMAs: without it hipcc puts the one-wave-per-SIMD
+// kernels' accumulators in AGPRs with non-tied MFMAs and copies ~200 AGPRs per k-tile)
+#include "common.h"
+
+namespace gm {
+
+constexpr int BK = 64;
+
+enum Epi : int { EPI_BF16 = 0, EPI_P32 = 1, EPI_P16 = 2, EPI_SWIGLU = 3 };
+
+template <int BN_, int BM_, int WN_, int WM_, int STAGES_, int BK_ = 64>
+struct Cfg {
+  static constexpr int BN = BN_, BM = BM_, WN = WN_, WM = WM_, STAGES = STAGES_, KT = BK_;
+  static constexpr int NW = WN * WM, NT = 64 * NW;
+  static constexpr int TN = BN / WN / 16, TM = BM / WM / 16;
+  static constexpr int RB = KT * 2;                                  // bytes per staged row
+  static constexpr int A_BYTES = BN * RB, B_BYTES = BM * RB;         // one k-step of W / of X
+  static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  static constexpr int LDS = STAGES * STAGE_BYTES;
+  static constexpr int GA = A_BYTES / (NT * 16), GB = B_BYTES / (NT * 16);   // DMAs per thread per k-step
+  static_assert(KT == 64 || KT == 32, "k-step is 64 (128-B rows) or 32 (64-B rows)");
+  static_assert(TN * WN * 16 == BN && TM * WM * 16 == BM, "tile / wave layout mismatch");
+  static_assert(GA * NT * 16 == A_BYTES && GB * NT * 16 == B_BYTES, "tile rows must fill whole DMA waves");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+// 16-B slot of chunk `ch` of staged row `row` (bank-conflict-free ds_read_b128 fragment reads):
+// 128-B rows: ch ^ ((row >> 1) & 7); 64-B rows: ch ^ ((row >> 2) & 2)
+template <int KT>
+KA_DEV int swz(int row, int ch) {
+  if constexpr (KT == 64) return ch ^ ((row >> 1) & 7);
+  else return ch ^ ((row >> 2) & 2);
+}
+
+KA_DEV void glds16(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+template <int N>
+KA_DEV void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+KA_DEV void block_sync() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+struct Args {
+  const bf16_t* X;   // [M, ldx]
+  const bf16_t* W;   // [N, K]
+  void* Y;           // EPI_BF16: bf16 [M, ldy]; EPI_SWIGLU: bf16 [M, ldy] (= N / 2 columns)
+  void* P;           // EPI_P32 / EPI_P16: [split, M, N]
+  int M, N, K, ldx, ldy, kps, tiles_m, tiles_n, gm;
+};
+
+// logical tile -> (m tile, n tile): XCD-contiguous, then GM m-tiles x all n-tiles super-rows
+KA_DEV void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int per = gm * tiles_n;
+  const int g = L / per, first = g * gm;
+  const int rows = min(gm, tiles_m - first);
+  const int in = L - g * per;
+  tm = first + in % rows;
+  tn = in / rows;
+}
+
+template <class C, int EPI>
+__global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
+  char* const lds_c = reinterpret_cast<char*>(lds);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % C::WN, wm = wave / C::WN;
+  int tmi, tni;
+  tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tmi, tni);
+  const int n0 = tni * C::BN, m0 = tmi * C::BM;
+  const int kb = blockIdx.z * a.kps;
+  const int nk = min(a.kps, a.K - kb) / C::KT;
+
+  // per-lane DMA source offsets (bytes, 32-bit): wave-instruction j covers 1 KB = RPI staged rows
+  constexpr int CPR = C::RB / 16, RPI = 64 / CPR;   // 16-B chunks per row, rows per instruction
+  const int rl = lane / CPR, slot = lane % CPR;
+  uint32_t offA[C::GA], offB[C::GB];
+#pragma unroll
+  for (int j = 0; j < C::GA; ++j) {
+    const int row = (j * C::NW + wave) * RPI + rl;
+    const int ch = swz<C::KT>(row, slot);
+    offA[j] = (uint32_t)(min(n0 + row, a.N - 1) * (uint32_t)a.K + kb + ch * 8) * 2u;
+  }
+#pragma unroll
+  for (int j = 0; j < C::GB; ++j) {
+    const int row = (j * C::NW + wave) * RPI + rl;
+    const int ch = swz<C::KT>(row, slot);
+    offB[j] = (uint32_t)(min(m0 + row, a.M - 1) * (uint32_t)a.ldx + kb + ch * 8) * 2u;
+  }
+  const char* Wb = reinterpret_cast<const char*>(a.W);
+  const char* Xb = reinterpret_cast<const char*>(a.X);
+
+  auto issue = [&](int stage, int t) {
+    char* sa = lds_c + stage * C::STAGE_BYTES;
+    char* sb = sa + C::A_BYTES;
+    const uint32_t kofs = (uint32_t)t * C::RB;
+#pragma unroll
+    for (int j = 0; j < C::GA; ++j) glds16(Wb + offA[j] + kofs, sa + (j * C::NW + wave) * 1024);
+#pragma unroll
+    for (int j = 0; j < C::GB; ++j) glds16(Xb + offB[j] + kofs, sb + (j * C::NW + wave) * 1024);
+  };
+
+  f32x4 acc[C::TN][C::TM];
+#pragma unroll
+  for (int i = 0; i < C::TN; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read addresses: row (base + i*16 + r16), chunk swz(r16, kk*4 + grp) (the swizzle of
+  // a row depends only on row % 16)
+  const int r16 = lane & 15, grp = lane >> 4;
+  const int rdA = (wn * C::TN * 16 + r16) * C::RB, rdB = (wm * C::TM * 16 + r16) * C::RB;
+  const int ch0 = swz<C::KT>(r16, grp) * 16, ch1 = swz<C::KT>(r16, 4 + grp) * 16;
+
+  auto compute = [&](int stage) {
+    const char* sa = lds_c + stage * C::STAGE_BYTES;
+    const char* sb = sa + C::A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < C::KT / 32; ++kk) {
+      const int ch = kk ? ch1 : ch0;
+      bf16x8 fa[C::TN], fb[C::TM];
+#pragma unroll
+      for (int i = 0; i < C::TN; ++i)
+        fa[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(sa + rdA + i * 16 * C::RB + ch));
+#pragma unroll
+      for (int j = 0; j < C::TM; ++j)
+        fb[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(sb + rdB + j * 16 * C::RB + ch));
+#pragma unroll
+      for (int i = 0; i < C::TN; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // prologue: STAGES - 1 stages in flight
+#pragma unroll
+  for (int s = 0; s < C::STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+  constexpr int PER = C::GA + C::GB;
+  for (int t = 0; t < nk; ++t) {
+    // stage t landed (this wave's part): later stages may stay in flight
+    // outstanding after this point: stages t+1 .. min(nk-1, t+STAGES-2) of this wave
+    if constexpr (C::STAGES >= 3) {
+      const int ahead = min(nk - 1 - t, C::STAGES - 2);
+      if constexpr (C::STAGES >= 5) {
+        if (ahead >= 3) wait_vm<3 * PER>();
+        else if (ahead == 2) wait_vm<2 * PER>();
+        else if (ahead == 1) wait_vm<PER>();
+        else wait_vm<0>();
+      } else if constexpr (C::STAGES == 4) {
+        if (ahead >= 2) wait_vm<2 * PER>();
+        else if (ahead == 1) wait_vm<PER>();
+        else wait_vm<0>();
+      } else {
+        if (ahead >= 1) wait_vm<PER>(); else wait_vm<0>();
+      }
+    } else {
+      wait_vm<0>();
+    }
+    block_sync();
+    const int tn = t + C::STAGES - 1;
+    if (tn < nk) issue(tn % C::STAGES, tn);
+    compute(t % C::STAGES);
+  }
+
+  // epilogue: acc[i][j][r] = C[n = .. + i*16 + 4*grp + r][m = .. + j*16 + r16]
+  const int nb = n0 + wn * C::TN * 16 + 4 * grp;
+  const int mb = m0 + wm * C::TM * 16 + r16;
+  if constexpr (EPI == EPI_SWIGLU) {
+    // W rows interleaved in 16-row chunks (gate c, up c): tiles 2p / 2p+1 are the gate / up rows of
+    // output columns (n0 + wn*TN*16)/2 + 16p + 4*grp + r
+    static_assert(C::TN % 2 == 0, "SwiGLU epilogue needs gate/up tile pairs");
+    const int cb = (n0 + wn * C::TN * 16) / 2 + 4 * grp;
+#pragma unroll
+    for (int p = 0; p < C::TN / 2; ++p) {
+      const int c = cb + 16 * p;
+      if (2 * c >= a.N) continue;
+#pragma unroll
+      for (int j = 0; j < C::TM; ++j) {
+        const int m = mb + j * 16;
+        if (m >= a.M) continue;
+        const f32x4 g = acc[2 * p][j], u = acc[2 * p + 1][j];
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = g[r] / (1.f + __expf(-g[r])) * u[r];
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + c) =
+            make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < C::TN; ++i) {
+      const int n = nb + i * 16;
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int j = 0; j < C::TM; ++j) {
+        const int m = mb + j * 16;
+        if (m >= a.M) continue;
+        const f32x4 v = acc[i][j];
+        if constexpr (EPI == EPI_BF16) {
+          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        } else if constexpr (EPI == EPI_P16) {
+          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        } else {
+          *reinterpret_cast<f32x4*>(static_cast<float*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) = v;
+        }
+      }
+    }
+  }
+}
+
+// ---- 256 x 256 ping-pong kernel ----------------------------------------------------------------
+// Eight waves in two groups of four, one wave of each group per SIMD.  Group g computes W rows
+// [128g, 128g + 128) of the tile (its A half-tile is private to it) against X rows [64c, 64c + 64)
+// (c = wave & 3).  A k-tile is four phases; phase p = R_p (ds_read the fragments of quadrant p,
+// issue 2 LDS-DMAs of a future half-tile) | barrier | C_p (16 MFMAs of quadrant p) | barrier.
+// Group 1 runs one barrier behind group 0, so on every SIMD one wave issues MFMAs while its partner
+// reads LDS / issues DMAs (T3/T4 "8-phase" structure, counted vmcnt, raw s_barrier, setprio T5).
+//
+// LDS: 2 buffers x {A0, A1, B0, B1} half-tiles of 128 rows x 128 B (16 KB), XOR-swizzled.
+// Quadrant order (n-half, m-half) per tile: (0,0) (0,1) (1,1) (1,0); reads R_0: A-sub0 + B-sub0,
+// R_1: B-sub1, R_2: A-sub1, R_3: none (B-sub0 is kept in registers).
+// DMA schedule (half-tiles of tile t+1 into buffer (t+1)&1, of tile t+2 into buffer t&1):
+//   R_0: B1(t+1)   R_1: A0(t+1)   R_2: A1(t+1)   R_3: B0(t+2)
+// and the tile-t+1 wait `vmcnt(2)` (all but B0(t+2)) before the barrier that ends group 0's C_3
+// / group 1's R_3.  WAR: a half-tile is refilled only after the last reader group passed the
+// barrier following the C phase that consumed its reads (the analysis is in docs/ARCHITECTURE.md).
+struct PP {
+  static constexpr int BN = 256, BM = 256, NT = 512;
+  static constexpr int HALF = 16384, BUF = 4 * HALF, LDS = 2 * BUF;
+};
+
+#ifdef GM_STAMPS
+// diagnostic build only (tools/gemm_bench.hip -DGM_STAMPS): shader-clock stamps after every barrier
+// of block 0 for the first STAMP_TILES k-tiles, one row per wave (vector stores, all 64 lanes)
+__device__ unsigned long long* g_stamps;
+constexpr int STAMP_TILES = 16, STAMPS_PER_WAVE = 8 * STAMP_TILES + 4;
+#define STAMP(idx)                                                                                       \
+  do {                                                                                                   \
+    if (blockIdx.x == 0 && blockIdx.z == 0 && (idx) < STAMPS_PER_WAVE) {                                 \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                          \
+      g_stamps[((size_t)w * STAMPS_PER_WAVE + (idx)) * 64 + lane] = t_;                                    \
+    }                                                                                                    \
+  } while (0)
+#else
+#define STAMP(idx) do {} while (0)
+#endif
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_pp_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
+  char* const L = reinterpret_cast<char*>(lds);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = w >> 2, wc = w & 3;
+  int tmi, tni;
+  tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tmi, tni);
+  const int n0 = tni * PP::BN, m0 = tmi * PP::BM;
+  const int kb = blockIdx.z * a.kps;
+  const int nk = min(a.kps, a.K - kb) / BK;
+
+  // DMA sources: half-tile h (0: W rows 0-127, 1: W rows 128-255, 2: X rows 0-127, 3: X rows
+  // 128-255); this wave's instruction j covers half-tile rows (j*8 + w)*8 + lane/8
+  const int r8 = lane >> 3, slot = lane & 7;
+  uint32_t off[4][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (j * 8 + w) * 8 + r8;
+    const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
+    off[0][j] = ((uint32_t)min(n0 + row, a.N - 1) * (uint32_t)a.K + kb + ch) * 2u;
+    off[1][j] = ((uint32_t)min(n0 + 128 + row, a.N - 1) * (uint32_t)a.K + kb + ch) * 2u;
+    off[2][j] = ((uint32_t)min(m0 + row, a.M - 1) * (uint32_t)a.ldx + kb + ch) * 2u;
+    off[3][j] = ((uint32_t)min(m0 + 128 + row, a.M - 1) * (uint32_t)a.ldx + kb + ch) * 2u;
+  }
+  const char* Wb = reinterpret_cast<const char*>(a.W);
+  const char* Xb = reinterpret_cast<const char*>(a.X);
+  auto issue = [&](int h, int t) {   // half-tile h of k-tile t into buffer t & 1
+    if (t >= nk) return;
+    const char* src = h < 2 ? Wb : Xb;
+    char* dst = L + (t & 1) * PP::BUF + h * PP::HALF;
+    const uint32_t kofs = (uint32_t)t * (BK * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(src + off[h][j] + kofs, dst + (j * 8 + w) * 1024);
+  };
+
+  const int r16 = lane & 15, grp = lane >> 4, sw = (r16 >> 1) & 7;
+  const int ch0 = ((0 + grp) ^ sw) * 16, ch1 = ((4 + grp) ^ sw) * 16;
+  const int rdA = g * PP::HALF + r16 * 128;                                   // + i*2048 + ch
+  const int rdB = 2 * PP::HALF + (wc >> 1) * PP::HALF + (64 * (wc & 1) + r16) * 128;   // + j*2048 + ch
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+
+  auto rd = [&](const char* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); };
+  auto read_a = [&](const char* buf, int half) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[i][0] = rd(buf + rdA + (4 * half + i) * 2048 + ch0);
+      fa[i][1] = rd(buf + rdA + (4 * half + i) * 2048 + ch1);
+    }
+  };
+  auto read_b = [&](const char* buf, int half, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      fb[j][0] = rd(buf + rdB + (2 * half + j) * 2048 + ch0);
+      fb[j][1] = rd(buf + rdB + (2 * half + j) * 2048 + ch1);
+    }
+  };
+  auto mma = [&](int ah, int bh, const bf16x8 (&fb)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * ah + i][2 * bh + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb[j][kk], acc[4 * ah + i][2 * bh + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: tile 0 and B0 of tile 1; wait for tile 0; group 1 then falls one barrier behind
+  issue(0, 0); issue(1, 0); issue(2, 0); issue(3, 0); issue(2, 1);
+  if (nk > 1) wait_vm<2>(); else wait_vm<0>();
+  block_sync();
+  if (g == 1) block_sync();
+
+  STAMP(0);
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = L + (t & 1) * PP::BUF;
+    const bool more = t + 2 < nk;   // B0(t+2) issued this tile: tile t+1's wait leaves it in flight
+    // phase 0: quadrant (0, 0)
+    read_a(buf, 0); read_b(buf, 0, fb0); issue(3, t + 1);
+    block_sync();
+    STAMP(1 + 8 * t);
+    mma(0, 0, fb0);
+    block_sync();
+    STAMP(2 + 8 * t);
+    // phase 1: quadrant (0, 1)
+    read_b(buf, 1, fb1); issue(0, t + 1);
+    block_sync();
+    STAMP(3 + 8 * t);
+    mma(0, 1, fb1);
+    block_sync();
+    STAMP(4 + 8 * t);
+    // phase 2: quadrant (1, 1)
+    read_a(buf, 1); issue(1, t + 1);
+    block_sync();
+    STAMP(5 + 8 * t);
+    mma(1, 1, fb1);
+    block_sync();
+    STAMP(6 + 8 * t);
+    // phase 3: quadrant (1, 0)
+    issue(2, t + 2);
+    if (g == 1) { if (more) wait_vm<2>(); else wait_vm<0>(); }
+    block_sync();
+    STAMP(7 + 8 * t);
+    mma(1, 0, fb0);
+    if (g == 0) { if (more) wait_vm<2>(); else wait_vm<0>(); }
+    block_sync();
+    STAMP(8 + 8 * t);
+  }
+  if (g == 0) block_sync();
+
+  // epilogue (as gemm_kernel): acc[i][j][r] = C[n0 + 128g + 16i + 4grp + r][m0 + 64wc + 16j + r16]
+  const int nb = n0 + 128 * g + 4 * grp;
+  const int mb = m0 + 64 * wc + r16;
+  if constexpr (EPI == EPI_SWIGLU) {
+    const int cb = (n0 + 128 * g) / 2 + 4 * grp;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int c = cb + 16 * p;
+      if (2 * c >= a.N) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mb + j * 16;
+        if (m >= a.M) continue;
+        const f32x4 gv = acc[2 * p][j], u = acc[2 * p + 1][j];
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = gv[r] / (1.f + __expf(-gv[r])) * u[r];
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + c) =
+            make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int n = nb + i * 16;
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mb + j * 16;
+        if (m >= a.M) continue;
+        const f32x4 v = acc[i][j];
+        if constexpr (EPI == EPI_BF16) {
+          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        } else if constexpr (EPI == EPI_P16) {
+          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        } else {
+          *reinterpret_cast<f32x4*>(static_cast<float*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) = v;
+        }
+      }
+    }
+  }
+}
+
+// Two phases per k-tile (32 MFMAs per C phase: the barrier bubble measured by the s_memtime
+// stamps, ~120 cycles per barrier interval, is paid half as often).  Phase a: n-half 0 against
+// all of the wave's B columns (R_a: A-sub0 + B = 16 reads), phase b: n-half 1 (R_b: A-sub1).
+// DMA schedule (group 0 | group 1), tile t+2 into buffer t & 1:
+//   B0 B1 (t+2):  G0 in R_a(t+1) | G1 in R_b(t)       (B of tile t last read by G1's R_a(t))
+//   A0 A1 (t+2):  G0 in R_b(t+1) | G1 in R_a(t+1)     (A_g of tile t last read by group g's R_b(t))
+// Waits before the barrier that ends interval 4t+7: G0 (end of C_b(t+1)) vmcnt(0), G1 (end of its
+// R_b(t+1), which issued B(t+3)) vmcnt(4).
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
+  char* const L = reinterpret_cast<char*>(lds);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = w >> 2, wc = w & 3;
+  int tmi, tni;
+  tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tmi, tni);
+  const int n0 = tni * PP::BN, m0 = tmi * PP::BM;
+  const int kb = blockIdx.z * a.kps;
+  const int nk = min(a.kps, a.K - kb) / BK;
+
+  const int r8 = lane >> 3, slot = lane & 7;
+  uint32_t off[4][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (j * 8 + w) * 8 + r8;
+    const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
+    off[0][j] = ((uint32_t)min(n0 + row, a.N - 1) * (uint32_t)a.K + kb + ch) * 2u;
+    off[1][j] = ((uint32_t)min(n0 + 128 + row, a.N - 1) * (uint32_t)a.K + kb + ch) * 2u;
+    off[2][j] = ((uint32_t)min(m0 + row, a.M - 1) * (uint32_t)a.ldx + kb + ch) * 2u;
+    off[3][j] = ((uint32_t)min(m0 + 128 + row, a.M - 1) * (uint32_t)a.ldx + kb + ch) * 2u;
+  }
+  const char* Wb = reinterpret_cast<const char*>(a.W);
+  const char* Xb = reinterpret_cast<const char*>(a.X);
+  auto issue = [&](int h, int t) {
+    if (t >= nk) return;
+    const char* src = h < 2 ? Wb : Xb;
+    char* dst = L + (t & 1) * PP::BUF + h * PP::HALF;
+    const uint32_t kofs = (uint32_t)t * (BK * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(src + off[h][j] + kofs, dst + (j * 8 + w) * 1024);
+  };
+
+  const int r16 = lane & 15, grp = lane >> 4, sw = (r16 >> 1) & 7;
+  const int ch0 = ((0 + grp) ^ sw) * 16, ch1 = ((4 + grp) ^ sw) * 16;
+  const int rdA = g * PP::HALF + r16 * 128;
+  const int rdB = 2 * PP::HALF + (wc >> 1) * PP::HALF + (64 * (wc & 1) + r16) * 128;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[4][2], fb[4][2];
+
+  auto rd = [&](const char* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); };
+  auto read_a = [&](const char* buf, int half) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[i][0] = rd(buf + rdA + (4 * half + i) * 2048 + ch0);
+      fa[i][1] = rd(buf + rdA + (4 * half + i) * 2048 + ch1);
+    }
+  };
+  auto read_b = [&](const char* buf) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      fb[j][0] = rd(buf + rdB + j * 2048 + ch0);
+      fb[j][1] = rd(buf + rdB + j * 2048 + ch1);
+    }
+  };
+  auto mma = [&](int ah) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 * ah + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb[j][kk], acc[4 * ah + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: tiles 0 and 1 (all four half-tiles each); wait for tile 0; group 1 one barrier behind
+  for (int h = 0; h < 4; ++h) issue(h, 0);
+  for (int h = 0; h < 4; ++h) issue(h, 1);
+  if (nk > 1) wait_vm<8>(); else wait_vm<0>();
+  block_sync();
+  if (g == 1) block_sync();
+
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = L + (t & 1) * PP::BUF;
+    const int t1 = t == 0 ? nk : t + 1;   // tile 1 was issued whole by the prologue
+    // phase a
+    read_a(buf, 0); read_b(buf);
+    if (g == 0) { issue(2, t1); issue(3, t1); }   // B(t+1): G0 in R_a(t)
+    else { issue(0, t1); issue(1, t1); }          // A(t+1): G1 in R_a(t)
+    block_sync();
+    mma(0);
+    block_sync();
+    // phase b
+    read_a(buf, 1);
+    if (g == 0) { issue(0, t1); issue(1, t1); }   // A(t+1): G0 in R_b(t)
+    else { issue(2, t + 2); issue(3, t + 2); }    // B(t+2): G1 in R_b(t)
+    if (g == 1) { if (t + 2 < nk) wait_vm<4>(); else wait_vm<0>(); }
+    block_sync();
+    mma(1);
+    if (g == 0) wait_vm<0>();
+    block_sync();
+  }
+  if (g == 0) block_sync();
+
+  const int nb = n0 + 128 * g + 4 * grp;
+  const int mb = m0 + 64 * wc + r16;
+  if constexpr (EPI == EPI_SWIGLU) {
+    const int cb = (n0 + 128 * g) / 2 + 4 * grp;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int c = cb + 16 * p;
+      if (2 * c >= a.N) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mb + j * 16;
+        if (m >= a.M) continue;
+        const f32x4 gv = acc[2 * p][j], u = acc[2 * p + 1][j];
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = gv[r] / (1.f + __expf(-gv[r])) * u[r];
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + c) =
+            make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int n = nb + i * 16;
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mb + j * 16;
+        if (m >= a.M) continue;
+        const f32x4 v = acc[i][j];
+        if constexpr (EPI == EPI_BF16) {
+          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        } else if constexpr (EPI == EPI_P16) {
+          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        } else {
+          *reinterpret_cast<f32x4*>(static_cast<float*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) = v;
+        }
+      }
+    }
+  }
+}
+
+template <int EPI, bool TWO>
+static int launch_pp(const Args& a0, int split, hipStream_t st) {
+  static bool attr = false;
+  auto kern = TWO ? &gemm_pp2_kernel<EPI> : &gemm_pp_kernel<EPI>;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, PP::LDS);
+    attr = true;
+  }
+  Args a = a0;
+  a.tiles_m = (a.M + PP::BM - 1) / PP::BM;
+  a.tiles_n = (a.N + PP::BN - 1) / PP::BN;
+  hipLaunchKernelGGL(kern, dim3(a.tiles_m * a.tiles_n, 1, split), dim3(PP::NT), PP::LDS, st, a);
+  return (int)hipGetLastError();
+}
+
+// ---- one wave per SIMD: 4 waves, big per-wave tiles, software-pipelined fragment reads ---------
+// Measured on MI355X (profiles/pmc_gemm_r2.md): the LDS-staged kernels above keep two waves per
+// SIMD in lockstep behind a barrier per k-step (SQ_WAIT_ANY ~40 % of wave cycles, MFMA busy
+// 51-56 %); rocBLAS' MT256x256 Tensile kernel runs one wave per SIMD and reaches 85 % MFMA busy.
+// This kernel: 2 x 2 waves, each owning TN x TM 16x16 tiles (up to 128 x 128: 256 accumulator
+// registers, AGPRs), two LDS stages filled by LDS-DMA, and the two 32-deep halves (kk) of a k-tile
+// software-pipelined through two fragment register sets:
+//     [MFMA kk0(t) | ds_read kk1(t)]  lgkmcnt(0) vmcnt(0)  barrier  issue DMA(t+2)
+//     [MFMA kk1(t) | ds_read kk0(t+1)]
+// The barrier sits mid-tile, where tile t+1's DMA (issued a full k-tile earlier) has landed and
+// every wave has finished reading tile t, whose buffer the DMA of tile t+2 then refills.
+template <int TN_, int TM_>
+struct W4 {
+  static constexpr int TN = TN_, TM = TM_, BN = 2 * TN * 16, BM = 2 * TM * 16, NT = 256;
+  static constexpr int A_BYTES = BN * 128, B_BYTES = BM * 128, STAGE = A_BYTES + B_BYTES, LDS = 2 * STAGE;
+  static constexpr int GA = A_BYTES / (NT * 16), GB = B_BYTES / (NT * 16);
+  static_assert(GA * NT * 16 == A_BYTES && GB * NT * 16 == B_BYTES, "rows must fill whole DMA waves");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <class C, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
+  char* const L = reinterpret_cast<char*>(lds);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = w & 1, wm = w >> 1;
+  int tmi, tni;
+  tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tmi, tni);
+  const int n0 = tni * C::BN, m0 = tmi * C::BM;
+  const int kb = blockIdx.z * a.kps;
+  const int nk = min(a.kps, a.K - kb) / BK;
+
+  const int r8 = lane >> 3, slot = lane & 7;
+  uint32_t offA[C::GA], offB[C::GB];
+#pragma unroll
+  for (int j = 0; j < C::GA; ++j) {
+    const int row = (j * 4 + w) * 8 + r8;
+    offA[j] = ((uint32_t)min(n0 + row, a.N - 1) * (uint32_t)a.K + kb + (uint32_t)(slot ^ ((row >> 1) & 7)) * 8) * 2u;
+  }
+#pragma unroll
+  for (int j = 0; j < C::GB; ++j) {
+    const int row = (j * 4 + w) * 8 + r8;
+    offB[j] = ((uint32_t)min(m0 + row, a.M - 1) * (uint32_t)a.ldx + kb + (uint32_t)(slot ^ ((row >> 1) & 7)) * 8) * 2u;
+  }
+  const char* Wb = reinterpret_cast<const char*>(a.W);
+  const char* Xb = reinterpret_cast<const char*>(a.X);
+  auto issue = [&](int t) {
+    if (t >= nk) return;
+    char* sa = L + (t & 1) * C::STAGE;
+    char* sb = sa + C::A_BYTES;
+    const uint32_t kofs = (uint32_t)t * (BK * 2);
+#pragma unroll
+    for (int j = 0; j < C::GA; ++j) glds16(Wb + offA[j] + kofs, sa + (j * 4 + w) * 1024);
+#pragma unroll
+    for (int j = 0; j < C::GB; ++j) glds16(Xb + offB[j] + kofs, sb + (j * 4 + w) * 1024);
+  };
+
+  const int r16 = lane & 15, grp = lane >> 4, sw = (r16 >> 1) & 7;
+  const int ch0 = ((0 + grp) ^ sw) * 16, ch1 = ((4 + grp) ^ sw) * 16;
+  const int rdA = (wn * C::TN * 16 + r16) * 128, rdB = C::A_BYTES + (wm * C::TM * 16 + r16) * 128;
+
+  f32x4 acc[C::TN][C::TM];
+#pragma unroll
+  for (int i = 0; i < C::TN; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a0[C::TN], b0[C::TM], a1[C::TN], b1[C::TM];
+
+  auto rd = [&](const char* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); };
+  auto read_frags = [&](int t, int ch, bf16x8 (&fa)[C::TN], bf16x8 (&fb)[C::TM]) {
+    const char* s = L + (t & 1) * C::STAGE;
+#pragma unroll
+    for (int i = 0; i < C::TN; ++i) fa[i] = rd(s + rdA + i * 2048 + ch);
+#pragma unroll
+    for (int j = 0; j < C::TM; ++j) fb[j] = rd(s + rdB + j * 2048 + ch);
+  };
+  auto mma = [&](const bf16x8 (&fa)[C::TN], const bf16x8 (&fb)[C::TM]) {
+#pragma unroll
+    for (int i = 0; i < C::TN; ++i)
+#pragma unroll
+      for (int j = 0; j < C::TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  };
+
+  issue(0);
+  issue(1);
+  if (nk > 1) wait_vm<C::GA + C::GB>(); else wait_vm<0>();
+  block_sync();
+  read_frags(0, ch0, a0, b0);
+  for (int t = 0; t < nk; ++t) {
+    read_frags(t, ch1, a1, b1);
+    mma(a0, b0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    block_sync();
+    issue(t + 2);
+    if (t + 1 < nk) read_frags(t + 1, ch0, a0, b0);
+    mma(a1, b1);
+  }
+
+  const int nb = n0 + wn * C::TN * 16 + 4 * grp;
+  const int mb = m0 + wm * C::TM * 16 + r16;
+  if constexpr (EPI == EPI_SWIGLU) {
+    static_assert(C::TN % 2 == 0, "SwiGLU epilogue needs gate/up tile pairs");
+    const int cb = (n0 + wn * C::TN * 16) / 2 + 4 * grp;
+#pragma unroll
+    for (int p = 0; p < C::TN / 2; ++p) {
+      const int c = cb + 16 * p;
+      if (2 * c >= a.N) continue;
+#pragma unroll
+      for (int j = 0; j < C::TM; ++j) {
+        const int m = mb + j * 16;
+        if (m >= a.M) continue;
+        const f32x4 gv = acc[2 * p][j], u = acc[2 * p + 1][j];
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = gv[r] / (1.f + __expf(-gv[r])) * u[r];
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + c) =
+            make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < C::TN; ++i) {
+      const int n = nb + i * 16;
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int j = 0; j < C::TM; ++j) {
+        const int m = mb + j * 16;
+        if (m >= a.M) continue;
+        const f32x4 v = acc[i][j];
+        if constexpr (EPI == EPI_BF16) {
+          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        } else if constexpr (EPI == EPI_P16) {
+          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        } else {
+          *reinterpret_cast<f32x4*>(static_cast<float*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) = v;
+        }
+      }
+    }
+  }
+}
+
+template <class C, int EPI>
+static int launch_w4(const Args& a0, int split, hipStream_t st) {
+  if constexpr (EPI == EPI_SWIGLU && C::TN % 2 != 0) {
+    return (int)hipErrorInvalidValue;   // gate/up tile pairs need an even TN
+  } else {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_w4_kernel<C, EPI>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  Args a = a0;
+  a.tiles_m = (a.M + C::BM - 1) / C::BM;
+  a.tiles_n = (a.N + C::BN - 1) / C::BN;
+  hipLaunchKernelGGL((gemm_w4_kernel<C, EPI>), dim3(a.tiles_m * a.tiles_n, 1, split), dim3(C::NT), C::LDS, st, a);
+  return (int)hipGetLastError();
+  }
+}
+
+// ---- configurations ------------------------------------------------------------------------------
+// id: (BN x BM, waves WN x WM, stages)
+//   0: 256 x 256, 2 x 4 waves (128 x 64 per wave), 2 stages      (prefill, big M)
+//   1: 256 x 256, 4 x 2 waves ( 64 x 128 per wave), 2 stages
+//   2: 128 x 256, 2 x 4 waves ( 64 x 64 per wave), 3 stages       (decode M = 256, wide N)
+//   3: 256 x 128, 4 x 2 waves ( 64 x 64), 3 stages
+//   4: 128 x 128, 2 x 2 waves ( 64 x 64), 3 stages                (4 waves, 96 KB: 1 block/CU)
+//   5: 128 x  64, 2 x 1 waves ( 64 x 64), 3 stages                (decode M <= 64)
+//   6: 64 x 256, 1 x 4 waves ( 64 x 64), 3 stages
+//   7: 256 x 256 ping-pong (gemm_pp_kernel), 8 waves in two staggered groups
+//   8-11: 32-deep k-steps (64-B staged rows) in 4-6 stage rings: more bytes in flight per CU for
+//         the latency-bound decode shapes; 12: 128 x 128 with 4 stages of 64
+#define GM_CFGS(X)               \
+  X(0, 256, 256, 2, 4, 2, 64)    \
+  X(1, 256, 256, 4, 2, 2, 64)    \
+  X(2, 128, 256, 2, 4, 3, 64)    \
+  X(3, 256, 128, 4, 2, 3, 64)    \
+  X(4, 128, 128, 2, 2, 3, 64)    \
+  X(5, 128, 64, 2, 1, 3, 64)     \
+  X(6, 64, 256, 1, 4, 3, 64)     \
+  X(8, 256, 256, 2, 4, 5, 32)    \
+  X(9, 256, 256, 2, 4, 4, 32)    \
+  X(10, 128, 256, 2, 4, 6, 32)   \
+  X(11, 128, 128, 2, 2, 5, 32)   \
+  X(12, 128, 128, 2, 2, 4, 64)
+
+template <class C, int EPI>
+static int launch(const Args& a0, int split, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<C, EPI>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  Args a = a0;
+  a.tiles_m = (a.M + C::BM - 1) / C::BM;
+  a.tiles_n = (a.N + C::BN - 1) / C::BN;
+  hipLaunchKernelGGL((gemm_kernel<C, EPI>), dim3(a.tiles_m * a.tiles_n, 1, split), dim3(C::NT), C::LDS, st, a);
+  return (int)hipGetLastError();
+}
+
+// one wave per SIMD (gemm_w4_kernel): id, TN, TM -> tile (2*TN*16) x (2*TM*16)
+#define GM_W4_CFGS(X) X(13, 8, 8) X(14, 8, 4) X(15, 7, 4) X(16, 4, 8) X(17, 4, 4) X(18, 6, 8)
+
+template <int EPI>
+static int dispatch(int cfg, const Args& a, int split, hipStream_t st) {
+  if (cfg == 7) return launch_pp<EPI, false>(a, split, st);
+  if (cfg == 19) return launch_pp<EPI, true>(a, split, st);
+#define W_(id, tn, tm) \
+  if (cfg == id) return launch_w4<W4<tn, tm>, EPI>(a, split, st);
+  GM_W4_CFGS(W_)
+#undef W_
+#define X_(id, bn, bm, wn, wm, s, kt) \
+  if (cfg == id) return launch<Cfg<bn, bm, wn, wm, s, kt>, EPI>(a, split, st);
+  GM_CFGS(X_)
+#undef X_
+  return (int)hipErrorInvalidValue;
+}
+
+}  // namespace gm
+
+extern "C" int ka_gm_bn(int cfg) {
+  if (cfg == 7 || cfg == 19) return gm::PP::BN;
+#define W_(id, tn, tm) if (cfg == id) return gm::W4<tn, tm>::BN;
+  GM_W4_CFGS(W_)
+#undef W_
+#define X_(id, bn, bm, wn, wm, s, kt) if (cfg == id) return bn;
+  GM_CFGS(X_)
+#undef X_
+  return -1;
+}
+extern "C" int ka_gm_bm(int cfg) {
+  if (cfg == 7 || cfg == 19) return gm::PP::BM;
+#define W_(id, tn, tm) if (cfg == id) return gm::W4<tn, tm>::BM;
+  GM_W4_CFGS(W_)
+#undef W_
+#define X_(id, bn, bm, wn, wm, s, kt) if (cfg == id) return bm;
+  GM_CFGS(X_)
+#undef X_
+  return -1;
+}
+
+// Y = X W^T.  epi: 0 bf16 Y [M, ldy]; 1 / 2: fp32 / bf16 split-K slabs P [split, M, N] (Y unused);
+// 3: SwiGLU of interleaved gate/up rows -> Y [M, ldy] with N / 2 columns.
+// Requirements: K % (64 * split) == 0 (kps = K / split), N % 16 == 0, 16-B aligned rows
+// (ldx % 8 == 0); epi 3 needs N % 32 == 0 and split == 1.
+extern "C" void ka_splitk_reduce_launch(bf16_t* Y, const float* P, int split, long mn, hipStream_t stream);
+
+// epi 1 with Y != nullptr: the fp32 slabs are then reduced into Y [M, N] (ldy == N) by splitk_reduce.
+extern "C" int ka_gemm_mfma(void* Y, void* P, const void* X, const void* W, int M, int N, int K, int ldx, int ldy,
+                            int split, int cfg, int epi, int gm, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (split < 1 || K % (64 * split) != 0 || N % 16 != 0 || ldx % 8 != 0 || ka_gm_bn(cfg) < 0)
+    return (int)hipErrorInvalidValue;
+  if (epi == gm::EPI_SWIGLU && (split != 1 || N % 32 != 0)) return (int)hipErrorInvalidValue;
+  if ((epi == gm::EPI_BF16 || epi == gm::EPI_SWIGLU) && split != 1) return (int)hipErrorInvalidValue;
+  gm::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), Y, P, M, N, K, ldx, ldy, K / split,
+             0, 0, gm > 0 ? gm : 8};
+  switch (epi) {
+    case gm::EPI_BF16: return gm::dispatch<gm::EPI_BF16>(cfg, a, split, stream);
+    case gm::EPI_P32: {
+      const int rc = gm::dispatch<gm::EPI_P32>(cfg, a, split, stream);
+      if (rc || Y == nullptr) return rc;
+      if (ldy != N) return (int)hipErrorInvalidValue;
+      ka_splitk_reduce_launch(static_cast<bf16_t*>(Y), static_cast<const float*>(P), split, (long)M * N, stream);
+      return (int)hipGetLastError();
+    }
+    case gm::EPI_P16: return gm::dispatch<gm::EPI_P16>(cfg, a, split, stream);
+    case gm::EPI_SWIGLU: return gm::dispatch<gm::EPI_SWIGLU>(cfg, a, split, stream);
+  }
+  return (int)hipErrorInvalidValue;
+}

@@ -22,6 +22,7 @@ DP replicas) without duplicate-registration errors.
 from __future__ import annotations
 
 import bisect
+import os
 import time
 from typing import Callable, List, Optional
 
@@ -91,6 +92,12 @@ class ServiceMetrics:
     def render(self) -> bytes:
         for flush in self.flush_hooks:
             flush()
+        mdir = os.environ.get("PROMETHEUS_MULTIPROC_DIR")
+        if mdir:   # several API workers (parallel/workers.py): aggregate every worker's samples
+            from prometheus_client import multiprocess
+            reg = CollectorRegistry()
+            multiprocess.MultiProcessCollector(reg, path=mdir)
+            return generate_latest(reg)
         return generate_latest(self.registry)
 
 
@@ -137,6 +144,10 @@ class PrometheusMiddleware:
         self._children = {}
         self._pending: list = []
         metrics.flush_hooks.append(self.flush)
+        # KA_WORKER_HEADER=1 adds `x-ka-worker: <pid>` to every response (tests of the multi-worker
+        # tier); off by default so the wire format stays the reference's
+        self.worker_header = ((b"x-ka-worker", str(os.getpid()).encode())
+                              if os.environ.get("KA_WORKER_HEADER") == "1" else None)
 
     async def __call__(self, scope, receive, send):
         if scope["type"] != "http":
@@ -153,6 +164,8 @@ class PrometheusMiddleware:
                     if k == b"content-length":
                         resp_len[0] = int(v)
                         break
+                if self.worker_header is not None:   # opt-in diagnostics: which API worker answered
+                    message = dict(message, headers=list(message.get("headers", ())) + [self.worker_header])
             await send(message)
 
         try:

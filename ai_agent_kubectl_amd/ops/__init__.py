@@ -272,8 +272,8 @@ def skinny_split(M: int, N: int, K: int, target_wgs: int = 0) -> int:
     return split
 
 
-# (M, N, K) -> ("skinny", split) | ("tile", split, cfg) | ("blas", 0); filled by ops.autotune at
-# engine start for the decode batch buckets.
+# (M, N, K) -> ("skinny", split) | ("tile", split, cfg) | ("gm", split, cfg) | ("blas", 0); filled by
+# ops.autotune at engine start for the decode batch buckets.
 GEMM_PLAN: dict = {}
 TILE_MAX_M = 512
 
@@ -300,6 +300,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
             return torch.nn.functional.linear(x, w)
         elif plan[0] == "tile":
             return linear_tile(x, w, plan[2], plan[1], defer_reduce, bf16_partials)
+        elif plan[0] == "gm":
+            return linear_gm(x, w, plan[2], plan[1], defer_reduce, bf16_partials)
         else:
             split = plan[1]
     if M > SKINNY_MAX_M:
@@ -406,6 +408,47 @@ def linear_tile(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, defe
         return SplitK(ws, split)
     y = torch.empty((M, N), dtype=x.dtype, device=x.device)
     check(lib.ka_gemm_tile(_p(y), _p(x), _p(w), _p(ws), M, N, K, split, cfg, 0, _stream()), "gemm_tile")
+    return y
+
+
+# csrc/gemm_mfma.hip configurations (LDS-DMA staged MFMA GEMM family; ka_gm_bn / ka_gm_bm give the
+# tile): 0-6, 12 ring kernels, 7 / 19 the 256 x 256 ping-pong kernels, 8-11 32-deep rings,
+# 13-18 one wave per SIMD
+GM_CFGS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19)
+GM_EPI_BF16, GM_EPI_P32, GM_EPI_P16, GM_EPI_SWIGLU = 0, 1, 2, 3
+
+
+def gm_shape(cfg: int):
+    """(BN, BM) of a gemm_mfma configuration."""
+    lib = require()
+    return lib.ka_gm_bn(cfg), lib.ka_gm_bm(cfg)
+
+
+def linear_gm(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, defer_reduce: bool = False,
+              bf16_partials: bool = False):
+    """y = x @ w.T through csrc/gemm_mfma.hip (configuration `cfg`, split-K `split`; K must be a
+    multiple of 64 * split).  split > 1 with defer_reduce returns the fp32 (or bf16) partial slabs
+    as a `SplitK` for a fused consumer; without it the slabs are reduced by splitk_reduce."""
+    M, K = x.shape
+    N = w.shape[0]
+    if K % (64 * split) or N % 16 or x.stride(0) % 8:
+        raise ValueError(f"gemm_mfma needs K % (64*split) == 0, N % 16 == 0: N={N} K={K} split={split}")
+    lib = require()
+    st = _stream()
+    if split == 1:
+        y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+        check(lib.ka_gemm_mfma(_p(y), None, _p(x), _p(w), M, N, K, x.stride(0), N, 1, cfg, GM_EPI_BF16, 0, st),
+              "gemm_mfma")
+        return y
+    pb = defer_reduce and bf16_partials
+    ws = torch.empty((split, M, N), dtype=torch.bfloat16 if pb else torch.float32, device=x.device)
+    if defer_reduce:
+        check(lib.ka_gemm_mfma(None, _p(ws), _p(x), _p(w), M, N, K, x.stride(0), N, split, cfg,
+                               GM_EPI_P16 if pb else GM_EPI_P32, 0, st), "gemm_mfma")
+        return SplitK(ws, split)
+    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    check(lib.ka_gemm_mfma(_p(y), _p(ws), _p(x), _p(w), M, N, K, x.stride(0), N, split, cfg, GM_EPI_P32, 0, st),
+          "gemm_mfma")
     return y
 
 

@@ -13,8 +13,8 @@ from typing import Dict, List, Sequence, Tuple
 
 import torch
 
-from . import (GEMM_PLAN, SKINNY_MAX_M, TILE_CFGS, TILE_MAX_M, linear, linear_tile, rmsnorm, skinny_split,
-               tile_k_quantum, tile_shape)
+from . import (GEMM_PLAN, SKINNY_MAX_M, TILE_CFGS, TILE_MAX_M, gm_shape, linear, linear_gm, linear_tile, rmsnorm,
+               skinny_split, tile_k_quantum, tile_shape)
 
 logger = logging.getLogger("app.engine")
 
@@ -121,6 +121,34 @@ def tile_candidates(M: int, N: int, K: int, cfgs: Sequence[int] = ()):
     return out
 
 
+# csrc/gemm_mfma.hip configurations timed for decode M (profiles/gemm_mfma_r2.md: 128 x 128 and
+# 128 x 64 rings win O / down at M = 64-256; 128 x 256 / 256 x 128 rings and the 2-phase 256 x 256
+# ping-pong at wide N)
+GM_TUNE_CFGS = (2, 3, 4, 5, 12, 19)
+
+
+def gm_candidates(M: int, N: int, K: int, cfgs: Sequence[int] = ()):
+    """(cfg, split) pairs of csrc/gemm_mfma.hip worth timing: tiles no taller than twice M and a
+    grid of ~96-1024 workgroups on 256 CUs."""
+    out = []
+    if M < 32 or K % 64 or N % 16:
+        return out
+    for cfg in cfgs or GM_TUNE_CFGS:
+        bn, bm = gm_shape(cfg)
+        if bm > 2 * M and bm > 64:
+            continue
+        tiles = ((N + bn - 1) // bn) * ((M + bm - 1) // bm)
+        for split in (1, 2, 4, 8):
+            if K % (64 * split) or K // split < 256:
+                continue
+            if split > 1 and tiles * split > 1024:
+                continue
+            if tiles * split < 96 and split < 8:
+                continue
+            out.append((cfg, split))
+    return out
+
+
 def _tune(groups, Ms, norm_fed=frozenset(), bf16_partials: bool = True) -> Dict:
     report = {}
     for (N, K), ws in groups.items():
@@ -146,6 +174,10 @@ def _tune(groups, Ms, norm_fed=frozenset(), bf16_partials: bool = True) -> Dict:
                           ws)
                 if t < best[3]:
                     best = ("tile", sp, cfg, t)
+            for cfg, sp in gm_candidates(M, N, K):
+                t = _time(lambda w: norm(linear_gm(x, w, cfg, sp, defer_reduce=fed, bf16_partials=bf16_partials)), ws)
+                if t < best[3]:
+                    best = ("gm", sp, cfg, t)
             GEMM_PLAN[(M, N, K)] = (best[0], best[1], best[2])
             report[(M, N, K)] = {"choice": best[0], "split": best[1], "cfg": best[2], "us": round(best[3], 1),
                                  "blas_us": round(t_blas, 1), "with_norm": fed}

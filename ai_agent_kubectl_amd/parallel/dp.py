@@ -1,8 +1,10 @@
-"""Data parallelism for serving: N engine replicas (one process per GPU) behind one API process.
+"""Data parallelism for serving: N engine replicas (one process per GPU) behind the API process(es).
 
-SURVEY.md §2.5 DP row: the API process keeps the single TTL cache and rate limiter (so
-`from_cache` semantics match `/root/reference/app.py:312-322` exactly) and routes every cache miss to
-the replica with the fewest in-flight requests.  Replicas are spawned (multiprocessing "spawn")
+SURVEY.md §2.5 DP row: the API tier keeps the single TTL cache and rate limiter (so `from_cache`
+semantics match `/root/reference/app.py:312-322` exactly — process-local with one API worker,
+in shared memory with several: shared_state.py) and every API worker routes its cache misses to
+the replica with the fewest of its in-flight requests.  A replica serves several API workers:
+one request pipe per (replica, worker) and one reply queue per worker (`spawn_replicas`).  Replicas are spawned (multiprocessing "spawn")
 BEFORE the API process touches the GPU; each binds `cuda:i`, builds its engine (random-init or
 safetensors weights, hipGraph capture) and serves token-id requests from a queue.  Tokenisation
 and detokenisation stay in the API process; only int lists cross the process boundary.
@@ -17,6 +19,7 @@ import dataclasses
 import itertools
 import logging
 import multiprocessing as mp
+import os
 import sys
 import threading
 import time
@@ -87,8 +90,11 @@ class EngineMetricsProxy:
         return out
 
 
-def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> None:
-    """Entry point of one replica process."""
+def _replica_main(idx: int, device: str, settings_dict: dict, req_conns, resp_qs) -> None:
+    """Entry point of one replica process.  `req_conns[c]` / `resp_qs[c]` are the request pipe and
+    the reply queue of API client c (one per API worker process)."""
+    if not isinstance(req_conns, (list, tuple)):
+        req_conns, resp_qs = [req_conns], [resp_qs]
     import torch  # noqa: F401  (first CUDA use happens here, in the child)
 
     from ..config import Settings
@@ -113,20 +119,22 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> 
         eng.start()
         params = SamplingParams(max_new_tokens=s.MAX_NEW_TOKENS, ignore_eos=s.IGNORE_EOS, safe_decode=s.SAFE_DECODE)
         forced = forced_prefix(eng.tokenizer) if s.SAFE_DECODE else []
-        resp_q.put(("ready", idx, cpus))
+        for q in resp_qs:
+            q.put(("ready", idx, cpus))
     except Exception as e:  # pragma: no cover - reported to the router
-        resp_q.put(("dead", idx, repr(e)))
+        for q in resp_qs:
+            q.put(("dead", idx, repr(e)))
         return
 
-    # completions are batched: the engine thread appends, and one message per engine step carries
-    # all of them back (a wave of 256 finishing together = 1 pickle + 1 pipe write, not 256)
-    done_buf = []
+    # completions are batched: the engine thread appends, and one message per engine step and
+    # client carries all of them back (a wave of 256 finishing together = 1 pickle + 1 pipe write)
+    done_buf: Dict[int, list] = {}
     done_lock = threading.Lock()
 
-    def done(seq, rid):
+    def done(seq, key):
         err = repr(seq.error) if seq.error is not None else None
         with done_lock:
-            done_buf.append((rid, (seq.output_ids, err, seq.finish_reason)))
+            done_buf.setdefault(key[0], []).append((key[1], (seq.output_ids, err, seq.finish_reason)))
 
     last_obs = [0.0]
 
@@ -134,65 +142,125 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_q, resp_q) -> 
         nonlocal done_buf
         now = time.perf_counter()
         if done_buf or now - last_obs[0] > 0.05:
-            obs = eng.metrics.take()
+            obs = eng.metrics.take()   # engine-level observations go to client 0 only (counted once)
             if done_buf or obs is not None:
                 with done_lock:
-                    batch, done_buf = done_buf, []
+                    bufs, done_buf = done_buf, {}
                 last_obs[0] = now
-                resp_q.put(("done_batch", idx, (batch, obs)))
+                for c in range(len(resp_qs)):
+                    batch, o = bufs.get(c, []), (obs if c == 0 else None)
+                    if batch or o is not None:
+                        resp_qs[c].put(("done_batch", idx, (batch, o)))
 
     eng.step_end_hooks.append(flush)
 
-    recv = req_q.recv if hasattr(req_q, "recv") else req_q.get
+    from multiprocessing.connection import wait as _wait
 
     def requests():
-        while True:
-            try:
-                msg = recv()
-            except EOFError:   # the API process went away
-                msg = None
-            if msg is None:
-                yield None
-                return
-            if msg[0] == "batch":
-                yield from msg[2]
-            else:
-                yield msg
+        conns = list(req_conns)
+        client_of = {id(cn): c for c, cn in enumerate(req_conns)}
+        while conns:
+            for cn in _wait(conns):
+                try:
+                    msg = cn.recv()
+                except EOFError:   # that API process went away
+                    msg = None
+                if msg is None:
+                    conns.remove(cn)
+                    continue
+                c = client_of[id(cn)]
+                if msg[0] == "batch":
+                    for m in msg[2]:
+                        yield c, m
+                else:
+                    yield c, msg
 
     live = {}
-    for msg in requests():
-        if msg is None:
-            break
+    for client, msg in requests():
         op, rid, payload = msg
+        key = (client, rid)
         if op == "sync":           # barrier helper: all queued GPU work of this replica is done
             import torch as _t
             if device.startswith("cuda"):
                 _t.cuda.synchronize(device)
-            resp_q.put(("ctl", rid, dict(eng.runner.stats, prefix_hits=eng.bm.hits, prefix_queries=eng.bm.queries,
-                                         partial_tokens=getattr(eng.bm, "partial_tokens", 0),
-                                         chained_steps=eng.chained_steps, engine_idle_s=eng.idle_s,
-                                         build_s=getattr(eng, "build_seconds", 0.0))))
+            resp_qs[client].put(("ctl", rid, dict(eng.runner.stats, prefix_hits=eng.bm.hits,
+                                                  prefix_queries=eng.bm.queries,
+                                                  partial_tokens=getattr(eng.bm, "partial_tokens", 0),
+                                                  chained_steps=eng.chained_steps, engine_idle_s=eng.idle_s,
+                                                  build_s=getattr(eng, "build_seconds", 0.0))))
             continue
         if op == "gen":
-            seq = eng.submit(payload, params, lambda sq, rid=rid: done(sq, rid), forced_prefix=forced)
-            live[rid] = seq
-        elif op == "abort" and rid in live:
-            eng.abort(live.pop(rid))
+            seq = eng.submit(payload, params, lambda sq, key=key: done(sq, key), forced_prefix=forced)
+            live[key] = seq
+        elif op == "abort" and key in live:
+            eng.abort(live.pop(key))
         if len(live) > 4096:
             live = {k: v for k, v in live.items() if not v.finished}
     eng.shutdown()
 
 
 @dataclasses.dataclass
+class ReplicaEndpoints:
+    """What one API client (worker process) holds to talk to every replica."""
+    senders: list          # per replica: the write end of this client's request pipe
+    resp_q: object         # this client's reply queue (shared by all replicas)
+    pids: List[int]
+
+
+def engine_devices(settings, dp: int) -> List[str]:
+    devs = [d.strip() for d in (getattr(settings, "ENGINE_DEVICES", "") or "").split(",") if d.strip()]
+    return devs[:dp] if len(devs) >= dp else [f"cuda:{i}" for i in range(dp)]
+
+
+def spawn_replicas(settings, devices: List[str], n_clients: int):
+    """Start one engine replica process per device, each serving `n_clients` API clients.
+    Must run before the calling process touches the GPU (spawned children bind the devices)."""
+    ctx = mp.get_context("spawn")
+    resp_qs = [ctx.Queue() for _ in range(n_clients)]
+    sd = dataclasses.asdict(settings)
+    sd.update(TP=1, DP=1)
+    procs, senders = [], [[] for _ in range(n_clients)]
+    for i, dev in enumerate(devices):
+        r_ends = []
+        for c in range(n_clients):
+            r_end, w_end = ctx.Pipe(duplex=False)
+            r_ends.append(r_end)
+            senders[c].append(w_end)
+        p = ctx.Process(target=_replica_main, args=(i, dev, sd, r_ends, resp_qs), daemon=True)
+        p.start()
+        for r_end in r_ends:
+            r_end.close()
+        procs.append(p)
+    pids = [p.pid for p in procs]
+    return procs, [ReplicaEndpoints(senders[c], resp_qs[c], pids) for c in range(n_clients)]
+
+
+def _pid_alive(pid: Optional[int]) -> bool:
+    if not pid:
+        return False
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:  # pragma: no cover
+        return True
+    return True
+
+
+@dataclasses.dataclass
 class _Replica:
     idx: int
-    proc: mp.Process
+    proc: Optional[mp.Process]   # None when another process (serve.py's supervisor) owns it
     req_q: object
     inflight: int = 0
     up: bool = False
     outbox: list = dataclasses.field(default_factory=list)
     flush_scheduled: bool = False
     cpus: list = dataclasses.field(default_factory=list)   # NUMA-local CPUs the replica pinned to
+    pid: Optional[int] = None
+
+    def alive(self) -> bool:
+        return self.proc.is_alive() if self.proc is not None else _pid_alive(self.pid)
 
 
 class DPRouterLLM(LLMBackend):
@@ -200,7 +268,10 @@ class DPRouterLLM(LLMBackend):
 
     name = "engine-dp"
 
-    def __init__(self, settings, dp: int, devices: Optional[List[str]] = None, start_timeout: float = 900):
+    def __init__(self, settings, dp: int, devices: Optional[List[str]] = None, start_timeout: float = 900,
+                 endpoints: Optional[ReplicaEndpoints] = None):
+        """Spawns its own `dp` replicas, or (`endpoints`) attaches to replicas another process
+        spawned for several API workers (serve.py WORKERS > 1)."""
         from ..engine.tokenizer import get_tokenizer, tokenizer_path
         from ..models.config import get_config
         from ..prompt import PROMPT_PREFIX
@@ -211,18 +282,17 @@ class DPRouterLLM(LLMBackend):
         self._prefix = before + self.tok.encode(PROMPT_PREFIX)
         self._after = after
         self.settings = settings
-        self.devices = devices or [f"cuda:{i}" for i in range(dp)]
-        ctx = mp.get_context("spawn")
-        self.resp_q = ctx.Queue()
-        sd = dataclasses.asdict(settings)
-        sd.update(TP=1, DP=1)
-        self.replicas: List[_Replica] = []
-        for i, dev in enumerate(self.devices):
-            r_end, w_end = ctx.Pipe(duplex=False)
-            p = ctx.Process(target=_replica_main, args=(i, dev, sd, r_end, self.resp_q), daemon=True)
-            p.start()
-            r_end.close()
-            self.replicas.append(_Replica(i, p, _PipeSender(w_end)))
+        self.owner = endpoints is None
+        if endpoints is None:
+            self.devices = devices or engine_devices(settings, dp)
+            procs, eps = spawn_replicas(settings, self.devices, 1)
+            endpoints = eps[0]
+        else:
+            self.devices = [f"replica{i}" for i in range(len(endpoints.senders))]
+            procs = [None] * len(endpoints.senders)
+        self.resp_q = endpoints.resp_q
+        self.replicas: List[_Replica] = [_Replica(i, procs[i], _PipeSender(w), pid=endpoints.pids[i])
+                                         for i, w in enumerate(endpoints.senders)]
         # the reply-reader thread must get the GIL promptly while the event loop is busy
         sys.setswitchinterval(min(sys.getswitchinterval(), 0.001))
         self._pending: Dict[int, tuple] = {}
@@ -301,8 +371,8 @@ class DPRouterLLM(LLMBackend):
 
     def _check_alive(self) -> None:
         for r in self.replicas:
-            if r.up and not r.proc.is_alive():
-                logger.error("DP replica %d died (exit %s)", r.idx, r.proc.exitcode)
+            if r.up and not r.alive():
+                logger.error("DP replica %d died (exit %s)", r.idx, r.proc.exitcode if r.proc is not None else "?")
                 r.up = False
                 self._fail_replica(r)
 
@@ -322,12 +392,16 @@ class DPRouterLLM(LLMBackend):
         await loop.run_in_executor(None, self.wait_ready)
 
     async def close(self) -> None:
+        """Disconnect from every replica; an owning router also waits for its replicas to exit
+        (a replica serving several API workers exits when the last one disconnects)."""
         for r in self.replicas:
             try:
                 r.req_q.put(None)
             except Exception:
                 pass
         for r in self.replicas:
+            if r.proc is None:
+                continue
             r.proc.join(timeout=30)
             if r.proc.is_alive():
                 r.proc.terminate()

@@ -2,6 +2,8 @@
 
     python -m ai_agent_kubectl_amd.serve                       # stub or single-GPU engine
     LLM_BACKEND=engine DP=8 python -m ai_agent_kubectl_amd.serve          # 8 replicas, 1 API process
+    LLM_BACKEND=engine DP=8 WORKERS=8 python -m ai_agent_kubectl_amd.serve   # 8 replicas, 8 API workers
+                                                               # (shared cache + limiter, parallel/workers.py)
     LLM_BACKEND=engine TP=8 MODEL=llama3-70b torchrun --nproc-per-node 8 -m ai_agent_kubectl_amd.serve
 
 Settings come from the environment and `./.env` (same variables and defaults as the reference, plus
@@ -40,6 +42,10 @@ def main(argv=None) -> int:
             eng.runner.capture_graphs()
             eng.runner.worker_loop()
             return 0
+
+    if settings.WORKERS > 1:
+        from .parallel.workers import run_workers
+        return run_workers(settings, args.host, args.port)
 
     import uvicorn
 

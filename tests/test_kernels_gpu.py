@@ -500,3 +500,42 @@ def test_gemv_swiglu_fused_is_exact(M, N, I):
     g = gu.float()
     a = (torch.nn.functional.silu(g[:, :I]) * g[:, I:]).to(BF).float()
     close(got, a @ w.float().t(), atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [48, 200, 256, 777])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 1024), (1040, 512)])
+def test_gemm_mfma_all_configs(M, N, K):
+    """csrc/gemm_mfma.hip: every configuration (LDS-DMA rings, 32-deep rings, ping-pong, one wave
+    per SIMD), split-K 1/2/4 with fp32 partials reduced in-kernel and deferred fp32/bf16 slabs,
+    ragged M and N edges, against the fp32 reference."""
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(BF)
+    want = x.float() @ w.float().t()
+    for cfg in ops.GM_CFGS:
+        for split in (1, 2, 4):
+            if K % (64 * split):
+                continue
+            got = ops.linear_gm(x, w, cfg, split)
+            close(got, want, atol=3e-2, rtol=2e-2)
+        sk = ops.linear_gm(x, w, cfg, 2, defer_reduce=True, bf16_partials=True)
+        assert sk.is_bf16 and sk.split == 2
+        close(sk.P.float().sum(0), want, atol=4e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M", [64, 256, 1000])
+def test_gemm_mfma_swiglu_epilogue(M):
+    """SwiGLU epilogue: W13 rows interleaved in 16-row (gate, up) chunks -> silu(gate) * up computed
+    from the accumulators, equal to SiLU·mul of the fp32 reference product."""
+    I, K = 1024, 512
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    wg = (torch.randn(I, K, device=DEV) * 0.05).to(BF)
+    wu = (torch.randn(I, K, device=DEV) * 0.05).to(BF)
+    w13i = torch.stack([wg.view(I // 16, 16, K), wu.view(I // 16, 16, K)], 1).reshape(2 * I, K).contiguous()
+    g, u = x.float() @ wg.float().t(), x.float() @ wu.float().t()
+    want = torch.nn.functional.silu(g) * u
+    lib = _hip.require()
+    for cfg in (0, 2, 3, 4, 7, 13, 14, 19):
+        y = torch.empty(M, I, device=DEV, dtype=BF)
+        _hip.check(lib.ka_gemm_mfma(y.data_ptr(), None, x.data_ptr(), w13i.data_ptr(), M, 2 * I, K, K, I, 1, cfg,
+                                    ops.GM_EPI_SWIGLU, 0, ops._stream()), "gemm_mfma swiglu")
+        close(y, want, atol=3e-2, rtol=3e-2)

@@ -1,0 +1,214 @@
+// Standalone harness for csrc/gemm_mfma.hip: correctness against an fp32 reference kernel on
+// sampled rows, and timing against rocBLAS (bf16 in/out, fp32 compute, the TN layout torch's
+// F.linear uses) in the same process.  No torch: a fresh GPU box runs it in seconds.
+//
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form tools/gemm_bench.hip \
+//         -lrocblas -o tools/gemm_bench
+//   tools/gemm_bench [cases...]         case = M,N,K,cfg,split,epi[,gm]  (cfg -1 = rocBLAS)
+//
+// Weights rotate over enough copies to exceed the 256 MB Infinity Cache (every call streams W
+// from HBM, as in a decode step where each layer's weights are read once).
+#include "../ai_agent_kubectl_amd/csrc/gemm_mfma.hip"
+
+#include <rocblas/rocblas.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+__global__ void fill_kernel(bf16_t* p, size_t n, uint32_t seed, float scale) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+    p[i] = f2bf(((h & 0xffffff) / 8388608.f - 1.f) * scale);
+  }
+}
+
+// reference: out[s][n] = sum_k X[rows[s]][k] * W[n][k] in fp32 (interleaved gate/up -> SwiGLU)
+__global__ void ref_kernel(float* out, const bf16_t* X, const bf16_t* W, const int* rows, int S, int N, int K, int ldx) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
+  if (n >= N || s >= S) return;
+  const bf16_t* x = X + (size_t)rows[s] * ldx;
+  const bf16_t* w = W + (size_t)n * K;
+  float acc = 0.f;
+  for (int k = 0; k < K; ++k) acc += bf2f(x[k]) * bf2f(w[k]);
+  out[(size_t)s * N + n] = acc;
+}
+
+static double now_check(std::vector<float>& ref, std::vector<uint16_t>& got, int S, int N, int ld, bool swiglu,
+                        double* max_ref) {
+  double err = 0, mr = 0;
+  const int NO = swiglu ? N / 2 : N;
+  for (int s = 0; s < S; ++s)
+    for (int c = 0; c < NO; ++c) {
+      double r;
+      if (swiglu) {
+        const int chunk = c / 16, q = c % 16;
+        const double g = ref[(size_t)s * N + chunk * 32 + q], u = ref[(size_t)s * N + chunk * 32 + 16 + q];
+        r = g / (1.0 + std::exp(-g)) * u;
+      } else {
+        r = ref[(size_t)s * N + c];
+      }
+      const uint32_t b = (uint32_t)got[(size_t)s * ld + c] << 16;
+      float gv;
+      memcpy(&gv, &b, 4);
+      err = std::max(err, std::fabs(gv - r));
+      mr = std::max(mr, std::fabs(r));
+    }
+  *max_ref = mr;
+  return err;
+}
+
+int main(int argc, char** argv) {
+  std::vector<std::string> cases;
+  for (int i = 1; i < argc; ++i) cases.push_back(argv[i]);
+  rocblas_handle rb;
+  rocblas_create_handle(&rb);
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  rocblas_set_stream(rb, st);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int warm = getenv("GB_WARM") ? atoi(getenv("GB_WARM")) : 0;   // 1: no weight rotation
+#ifdef GM_STAMPS
+  unsigned long long* dst_;
+  const size_t nst = (size_t)8 * gm::STAMPS_PER_WAVE * 64;
+  CK(hipMalloc(&dst_, nst * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(gm::g_stamps), &dst_, sizeof(dst_)));
+#endif
+
+  for (auto& cs : cases) {
+    int M, N, K, cfg, split, epi, gm = 8;
+    if (sscanf(cs.c_str(), "%d,%d,%d,%d,%d,%d,%d", &M, &N, &K, &cfg, &split, &epi, &gm) < 6) {
+      fprintf(stderr, "bad case %s\n", cs.c_str());
+      return 2;
+    }
+    const size_t wbytes = (size_t)N * K * 2;
+    const int nrot = warm ? 1 : (int)std::max<size_t>(1, (size_t)(768ull << 20) / wbytes + 1);
+    bf16_t *X, *W, *Y;
+    void* P = nullptr;
+    CK(hipMalloc(&X, (size_t)M * K * 2));
+    CK(hipMalloc(&W, wbytes * nrot));
+    CK(hipMalloc(&Y, (size_t)M * N * 2));
+    if (epi == 1 || epi == 2) CK(hipMalloc(&P, (size_t)split * M * N * 4));
+    hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, st, X, (size_t)M * K, 1234u, 1.0f);
+    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, st, W, (size_t)N * K * nrot, 777u,
+                       1.0f / sqrtf((float)K));
+    CK(hipStreamSynchronize(st));
+
+    const bool sw = epi == 3;
+    const int ldy = sw ? N / 2 : N;
+    auto run = [&](int r) -> int {
+      const bf16_t* w = W + (size_t)(r % nrot) * N * K;
+      if (cfg < 0) {
+        const float alpha = 1.f, beta = 0.f;
+        return (int)rocblas_gemm_ex(rb, rocblas_operation_transpose, rocblas_operation_none, N, M, K, &alpha, w,
+                                    rocblas_datatype_bf16_r, K, X, rocblas_datatype_bf16_r, K, &beta, Y,
+                                    rocblas_datatype_bf16_r, N, Y, rocblas_datatype_bf16_r, N,
+                                    rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
+      }
+      return ka_gemm_mfma(Y, P, X, w, M, N, K, K, ldy, split, cfg, epi, gm, st);
+    };
+    int rc = run(0);
+    if (rc) {
+      printf("%s: launch error %d\n", cs.c_str(), rc);
+      continue;
+    }
+    CK(hipStreamSynchronize(st));
+    // correctness on sampled rows (the split-K slabs are summed on the host)
+    const int S = std::min(M, 24);
+    std::vector<int> rows(S);
+    for (int s = 0; s < S; ++s) rows[s] = (int)((long)s * (M - 1) / std::max(1, S - 1));
+    int* drows;
+    float* dref;
+    CK(hipMalloc(&drows, S * 4));
+    CK(hipMalloc(&dref, (size_t)S * N * 4));
+    CK(hipMemcpy(drows, rows.data(), S * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(ref_kernel, dim3((N + 255) / 256, S), dim3(256), 0, st, dref, X, W, drows, S, N, K, K);
+    CK(hipStreamSynchronize(st));
+    std::vector<float> ref((size_t)S * N);
+    CK(hipMemcpy(ref.data(), dref, ref.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<uint16_t> got((size_t)S * ldy);
+    if (epi == 1 || epi == 2) {
+      std::vector<float> full((size_t)S * N, 0.f);
+      for (int z = 0; z < split; ++z)
+        for (int s = 0; s < S; ++s) {
+          if (epi == 1) {
+            std::vector<float> row(N);
+            CK(hipMemcpy(row.data(), (float*)P + ((size_t)z * M + rows[s]) * N, N * 4, hipMemcpyDeviceToHost));
+            for (int n = 0; n < N; ++n) full[(size_t)s * N + n] += row[n];
+          } else {
+            std::vector<uint16_t> row(N);
+            CK(hipMemcpy(row.data(), (bf16_t*)P + ((size_t)z * M + rows[s]) * N, N * 2, hipMemcpyDeviceToHost));
+            for (int n = 0; n < N; ++n) { uint32_t u = (uint32_t)row[n] << 16; float f; memcpy(&f, &u, 4); full[(size_t)s * N + n] += f; }
+          }
+        }
+      for (size_t i = 0; i < full.size(); ++i) {
+        uint32_t u;
+        memcpy(&u, &full[i], 4);
+        got[i] = (uint16_t)((u + 0x7fff + ((u >> 16) & 1)) >> 16);
+      }
+    } else {
+      for (int s = 0; s < S; ++s)
+        CK(hipMemcpy(got.data() + (size_t)s * ldy, Y + (size_t)rows[s] * ldy, ldy * 2, hipMemcpyDeviceToHost));
+    }
+    double mr;
+    const double err = (cfg < 0 && sw) ? 0 : now_check(ref, got, S, N, ldy, sw && cfg >= 0, &mr);
+    CK(hipFree(drows));
+    CK(hipFree(dref));
+
+    for (int r = 0; r < 3; ++r) run(r + 1);
+    const int iters = 30;
+    CK(hipEventRecord(e0, st));
+    for (int r = 0; r < iters; ++r) run(r + 4);
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1e3 / iters;
+    const double tf = 2.0 * M * N * K / (us * 1e-6) / 1e12;
+    const double tb = (wbytes + (double)M * K * 2 + (double)M * N * 2) / (us * 1e-6) / 1e12;
+#ifdef GM_STAMPS
+    {
+      CK(hipMemset(dst_, 0, nst * 8));
+      run(0);
+      CK(hipStreamSynchronize(st));
+      std::vector<unsigned long long> h(nst);
+      CK(hipMemcpy(h.data(), dst_, nst * 8, hipMemcpyDeviceToHost));
+      for (int wv = 0; wv < 8; ++wv) {
+        printf("wave %d:", wv);
+        const unsigned long long t0 = h[((size_t)0 * gm::STAMPS_PER_WAVE + 0) * 64];
+        for (int i = 0; i < gm::STAMPS_PER_WAVE; ++i) {
+          const unsigned long long v = h[((size_t)wv * gm::STAMPS_PER_WAVE + i) * 64];
+          if (v) printf(" %lld", (long long)(v - t0));
+        }
+        printf("\n");
+      }
+    }
+#endif
+    printf("M=%5d N=%6d K=%5d cfg=%2d split=%2d epi=%d gm=%d : %8.2f us  %7.1f TF/s  %5.2f TB/s  maxerr %.3g (ref max %.3g)%s\n",
+           M, N, K, cfg, split, epi, gm, us, tf, tb, err, (cfg < 0 && sw) ? 0.0 : mr,
+           err > 0.02 * std::max(1.0, (cfg < 0 && sw) ? 1.0 : mr) ? "  <-- MISMATCH" : "");
+    fflush(stdout);
+    CK(hipFree(X));
+    CK(hipFree(W));
+    CK(hipFree(Y));
+    if (P) CK(hipFree(P));
+  }
+  rocblas_destroy_handle(rb);
+  return 0;
+}
