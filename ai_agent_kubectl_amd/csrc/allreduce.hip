@@ -85,6 +85,170 @@ __global__ __launch_bounds__(512) void allreduce_oneshot_kernel(ArArgs a, const 
   }
 }
 
+// One-shot all-gather on the same buffers, flags and epoch sequence (A3: the vocab-parallel
+// argmax winners; graph-capturable like the all-reduce, so a TP decode graph holds every
+// collective).  n16 = payload size in 16-bit units (multiple of 8); out receives world * n16
+// units in rank order.  Calls of both kernels share `ctr`: every rank issues the same sequence.
+__global__ __launch_bounds__(512) void allgather_oneshot_kernel(ArArgs a, const bf16_t* __restrict__ in,
+                                                                bf16_t* out, unsigned* ctr, unsigned* done,
+                                                                int* err, int rank, int world, int n, int cap) {
+  __shared__ unsigned s_epoch;
+  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+  const size_t half = (size_t)(epoch & 1u) * cap;
+  const int chunk = ((n + (int)gridDim.x - 1) / (int)gridDim.x + 7) / 8 * 8;
+  const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
+
+  bf16_t* mine = a.data[rank] + half;
+  for (int i = beg + threadIdx.x * 8; i < end; i += blockDim.x * 8)
+    *reinterpret_cast<u32x4*>(mine + i) = *reinterpret_cast<const u32x4*>(in + i);
+  __threadfence_system();
+  __syncthreads();
+  if ((int)threadIdx.x < world) {
+    const int p = threadIdx.x;
+    __hip_atomic_store(a.flags[p] + blockIdx.x * AR_MAX_RANKS + rank, epoch, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned* f = a.flags[rank] + blockIdx.x * AR_MAX_RANKS + p;
+    int spins = 0;
+    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      if (++spins > (1 << 22)) {
+        atomicExch(err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  for (int p = 0; p < world; ++p)
+    for (int i = beg + threadIdx.x * 8; i < end; i += blockDim.x * 8)
+      *reinterpret_cast<u32x4*>(out + (size_t)p * n + i) = *reinterpret_cast<const u32x4*>(a.data[p] + half + i);
+
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned prev = atomicAdd(done, 1u);
+    if (prev == gridDim.x - 1) {
+      *done = 0u;
+      __hip_atomic_store(ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// One-shot all-reduce fused with the residual add + RMSNorm that follows every row-parallel
+// projection (A1 after O-proj, A2 after down-proj): block b owns whole rows, so after the flag
+// handshake it sums its rows over the ranks, adds the residual (updated in place) and normalises —
+// the reduced activation never makes a round trip through memory and one launch replaces two.
+// Arithmetic is that of all-reduce -> rmsnorm_kernel (elementwise.hip) exactly: the rank sum is
+// rounded to bf16, the residual sum is rounded to bf16, fp32 sum of squares.  hidden <= 8192.
+__global__ __launch_bounds__(512) void allreduce_rmsnorm_kernel(ArArgs a, const bf16_t* __restrict__ in,
+                                                                bf16_t* __restrict__ out, bf16_t* residual,
+                                                                const bf16_t* __restrict__ w, float eps,
+                                                                unsigned* ctr, unsigned* done, int* err, int rank,
+                                                                int world, int rows, int hidden, int cap) {
+  __shared__ unsigned s_epoch;
+  __shared__ float red[8];
+  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+  const size_t half = (size_t)(epoch & 1u) * cap;
+  const int rpb = (rows + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  const int beg = r0 * hidden, end = r1 * hidden;
+
+  bf16_t* mine = a.data[rank] + half;
+  for (int i = beg + threadIdx.x * 8; i < end; i += blockDim.x * 8)
+    *reinterpret_cast<u32x4*>(mine + i) = *reinterpret_cast<const u32x4*>(in + i);
+  __threadfence_system();
+  __syncthreads();
+  if ((int)threadIdx.x < world) {
+    const int p = threadIdx.x;
+    __hip_atomic_store(a.flags[p] + blockIdx.x * AR_MAX_RANKS + rank, epoch, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned* f = a.flags[rank] + blockIdx.x * AR_MAX_RANKS + p;
+    int spins = 0;
+    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      if (++spins > (1 << 22)) {
+        atomicExch(err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+
+  const int nvec = hidden >> 3;
+  for (int row = r0; row < r1; ++row) {
+    float v[2][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = threadIdx.x + i * 512;
+      if (idx >= nvec) continue;
+      const size_t e = (size_t)row * hidden + idx * 8;
+      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int p = 0; p < world; ++p) {
+        const u32x4 pv = *reinterpret_cast<const u32x4*>(a.data[p] + half + e);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          s[2 * k] += lo_f(pv[k]);
+          s[2 * k + 1] += hi_f(pv[k]);
+        }
+      }
+      uint32_t o[4];
+      if (residual != nullptr) {
+        const u32x4 b = *reinterpret_cast<const u32x4*>(residual + e);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t aw = pack2(s[2 * k], s[2 * k + 1]);   // the all-reduce output, bf16
+          v[i][2 * k] = bf2f(f2bf(lo_f(aw) + lo_f(b[k])));
+          v[i][2 * k + 1] = bf2f(f2bf(hi_f(aw) + hi_f(b[k])));
+          o[k] = pack2(v[i][2 * k], v[i][2 * k + 1]);
+        }
+        *reinterpret_cast<u32x4*>(residual + e) = u32x4{o[0], o[1], o[2], o[3]};
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t aw = pack2(s[2 * k], s[2 * k + 1]);
+          v[i][2 * k] = lo_f(aw);
+          v[i][2 * k + 1] = hi_f(aw);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ss += v[i][k] * v[i][k];
+    }
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tot += red[i];
+    const float scale = rsqrtf(tot / (float)hidden + eps);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = threadIdx.x + i * 512;
+      if (idx >= nvec) continue;
+      const size_t e = (size_t)row * hidden + idx * 8;
+      const u32x4 g = *reinterpret_cast<const u32x4*>(w + idx * 8);
+      uint32_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        o[k] = pack2(v[i][2 * k] * scale * lo_f(g[k]), v[i][2 * k + 1] * scale * hi_f(g[k]));
+      *reinterpret_cast<u32x4*>(out + e) = u32x4{o[0], o[1], o[2], o[3]};
+    }
+    __syncthreads();   // red[] is rewritten by the next row
+  }
+
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned prev = atomicAdd(done, 1u);
+    if (prev == gridDim.x - 1) {
+      *done = 0u;
+      __hip_atomic_store(ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // ---- host helpers (ops/_hip.py ctypes; parallel/custom_allreduce.py) ----
 extern "C" int ka_ar_alloc(void** ptr, size_t bytes) {
   hipError_t e = hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached);
@@ -127,5 +291,46 @@ extern "C" int ka_allreduce_oneshot(void* out, const void* in, void* const* data
   hipLaunchKernelGGL(allreduce_oneshot_kernel, dim3(nblocks), dim3(512), 0, stream, a,
                      static_cast<const bf16_t*>(in), static_cast<bf16_t*>(out), static_cast<unsigned*>(ctr),
                      static_cast<unsigned*>(done), static_cast<int*>(err), rank, world, n, cap);
+  KA_CHECK_LAUNCH();
+}
+
+// out: world * n16 16-bit units; in: n16 units (n16 % 8 == 0, n16 <= cap)
+extern "C" int ka_allgather_oneshot(void* out, const void* in, void* const* data, void* const* flags, void* ctr,
+                                    void* done, void* err, int rank, int world, int n16, int cap, int nblocks,
+                                    hipStream_t stream) {
+  if (n16 <= 0) return 0;
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n16 % 8 || n16 > cap || nblocks < 1 ||
+      nblocks > AR_MAX_BLOCKS)
+    return (int)hipErrorInvalidValue;
+  ArArgs a;
+  for (int p = 0; p < AR_MAX_RANKS; ++p) {
+    a.data[p] = p < world ? static_cast<bf16_t*>(data[p]) : nullptr;
+    a.flags[p] = p < world ? static_cast<unsigned*>(flags[p]) : nullptr;
+  }
+  hipLaunchKernelGGL(allgather_oneshot_kernel, dim3(nblocks), dim3(512), 0, stream, a,
+                     static_cast<const bf16_t*>(in), static_cast<bf16_t*>(out), static_cast<unsigned*>(ctr),
+                     static_cast<unsigned*>(done), static_cast<int*>(err), rank, world, n16, cap);
+  KA_CHECK_LAUNCH();
+}
+
+// in: this rank's partial [rows, hidden] bf16; out: rmsnorm(sum + residual) * w; residual (may be
+// null) is updated in place to sum + residual.  rows * hidden <= cap, hidden % 8 == 0, <= 8192;
+// nblocks (identical on every rank) <= min(rows, AR_MAX_BLOCKS).
+extern "C" int ka_allreduce_rmsnorm(void* out, const void* in, void* residual, const void* w, float eps,
+                                    void* const* data, void* const* flags, void* ctr, void* done, void* err, int rank,
+                                    int world, int rows, int hidden, int cap, int nblocks, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || hidden % 8 || hidden > 8192 ||
+      (long)rows * hidden > cap || nblocks < 1 || nblocks > AR_MAX_BLOCKS || nblocks > rows)
+    return (int)hipErrorInvalidValue;
+  ArArgs a;
+  for (int p = 0; p < AR_MAX_RANKS; ++p) {
+    a.data[p] = p < world ? static_cast<bf16_t*>(data[p]) : nullptr;
+    a.flags[p] = p < world ? static_cast<unsigned*>(flags[p]) : nullptr;
+  }
+  hipLaunchKernelGGL(allreduce_rmsnorm_kernel, dim3(nblocks), dim3(512), 0, stream, a,
+                     static_cast<const bf16_t*>(in), static_cast<bf16_t*>(out), static_cast<bf16_t*>(residual),
+                     static_cast<const bf16_t*>(w), eps, static_cast<unsigned*>(ctr), static_cast<unsigned*>(done),
+                     static_cast<int*>(err), rank, world, rows, hidden, cap);
   KA_CHECK_LAUNCH();
 }

@@ -64,6 +64,9 @@ class LlamaModel:
         # split-K partials of the norm-feeding projections (o_proj, down) stored as bf16: half the
         # slab traffic; the fused reduce + RMSNorm still accumulates them in fp32
         self.bf16_partials = os.environ.get("KA_BF16_PARTIALS", "1") == "1"
+        # the QKV projection's split-K partials for the fused decode attention (its prologue sums
+        # them in fp32): a separate switch so the two can be A/B'd independently
+        self.bf16_qkv_partials = os.environ.get("KA_BF16_QKV_PARTIALS", "1") == "1"
         self.layers = [self._layer(i) for i in range(cfg.num_layers)]
 
     def _layer(self, i):
@@ -78,18 +81,20 @@ class LlamaModel:
         eps = cfg.norm_eps
         h = ops.embedding(input_ids, self.W["embed"])
         residual = None
+        pending = False   # h holds this rank's partial of a row-parallel output (TP all-reduce due)
         T = input_ids.shape[0]
         for li, L in enumerate(self.layers):
             if residual is None:
                 residual = h
                 x = ops.rmsnorm(h, L["ln1"], eps)
             else:
-                x = ops.rmsnorm(h, L["ln1"], eps, residual=residual)
+                x = self._reduce_norm(h, L["ln1"], eps, residual, pending)
             # column-parallel projections: no all-reduce before their consumer, so a split-K plan
-            # hands its fp32 partials to the RoPE / SiLU kernels, which reduce them on the fly
+            # hands its partials to the RoPE / attention / SiLU kernels, which reduce them on the fly
             fused = meta.is_decode and self.fuse_decode_rope
-            # the fused decode attention reduces bf16 partials too; rope_kv_write needs fp32 ones
-            qkv = ops.linear(x, L["wqkv"], defer_reduce=True, bf16_partials=fused and self.bf16_partials)
+            # the fused decode attention reduces bf16 QKV partials too (KA_BF16_QKV_PARTIALS);
+            # rope_kv_write needs fp32 ones
+            qkv = ops.linear(x, L["wqkv"], defer_reduce=True, bf16_partials=fused and self.bf16_qkv_partials)
             if fused:
                 # RoPE + KV append + attention in one kernel (the rotated q never goes to HBM)
                 a = ops.decode_attention_rope(qkv, meta.positions, self.cos_sin, meta.slot_mapping, k_cache[li],
@@ -102,11 +107,11 @@ class LlamaModel:
             if 0 < meta.num_tokens < T and not meta.is_decode:
                 a[meta.num_tokens:].zero_()   # padding rows: no sequence's attention writes them
             # TP = 1: the projections feeding a norm leave their split-K partials to the fused
-            # reduce + residual + RMSNorm kernel (ops.SplitK); with TP the all-reduce needs bf16
+            # reduce + residual + RMSNorm kernel (ops.SplitK); with TP the row-parallel output is
+            # bf16 and the all-reduce is fused with that norm (comm.all_reduce_rmsnorm, A1)
             fuse = self._local_comm
             h = ops.linear(a.view(T, self.hq * self.D), L["wo"], defer_reduce=fuse, bf16_partials=self.bf16_partials)
-            self.comm.all_reduce(h)
-            x = ops.rmsnorm(h, L["ln2"], eps, residual=residual)
+            x = self._reduce_norm(h, L["ln2"], eps, residual, True)
             combined = False
             if cfg.is_moe:
                 h, combined = moe_forward(x, L, cfg, self.ep_rank, self.ep_size, meta.is_decode, self.comm)
@@ -114,16 +119,25 @@ class LlamaModel:
                 # batch <= 4: SiLU·mul computed inside the down GEMV's X staging (ops.swiglu_linear)
                 h = ops.swiglu_linear(ops.linear(x, L["w13"], defer_reduce=True), L["w2"], defer_reduce=fuse,
                                       tile_fused=False, bf16_partials=self.bf16_partials)
-            if not combined:
-                self.comm.all_reduce(h)
+            pending = not combined   # A2: reduced together with the next norm
         if meta.is_decode:   # every row is its sequence's last token (logits_indices = arange)
-            return ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
+            return self._reduce_norm(h, self.W["norm"], eps, residual, pending)
+        if pending and not self._local_comm:
+            self.comm.all_reduce(h)
         if isinstance(h, ops.SplitK):
             x = ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
             return x.index_select(0, meta.logits_indices)
         # prefill: only the sequences' last rows are sampled, so only they are normed
         idx = meta.logits_indices
         return ops.rmsnorm(h.index_select(0, idx), self.W["norm"], eps, residual=residual.index_select(0, idx))
+
+    def _reduce_norm(self, h, w, eps, residual, pending: bool):
+        """residual += all_reduce(h) (when `pending`); return rmsnorm(residual) * w.  TP = 1: h may be
+        split-K partials (the reduction is fused into the norm kernel); TP > 1: the all-reduce is
+        fused with the norm for decode-size rows (one-shot kernel) or runs before it."""
+        if not pending or self._local_comm:
+            return ops.rmsnorm(h, w, eps, residual=residual)
+        return self.comm.all_reduce_rmsnorm(h, w, eps, residual)
 
     def _attention(self, q, meta: AttnMeta, kc: torch.Tensor, vc: torch.Tensor) -> torch.Tensor:
         if meta.is_decode:

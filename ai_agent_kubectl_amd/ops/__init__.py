@@ -53,9 +53,9 @@ def _stream() -> int:
 
 
 class SplitK(NamedTuple):
-    """Split-K partials of a projection whose reduction is deferred to the consumer (rmsnorm).
-    P is fp32, or bf16 when the producer was asked for `bf16_partials` (only rmsnorm and the fused
-    decode attention read those)."""
+    """Split-K partials of a projection whose reduction is deferred to the consumer (rmsnorm,
+    decode_attention_rope, rope_kv_write, silu_mul).  P is fp32, or bf16 when the producer was
+    asked for `bf16_partials` (only rmsnorm and the fused decode attention read those)."""
     P: torch.Tensor          # [split, M, N] fp32 | bf16
     split: int
 
@@ -283,10 +283,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
     """y = x @ w.T (w is [out, in]).  Decode-sized M goes to the hand-written weight-streaming
     kernel (M <= 256), the LDS-tiled MFMA kernel (M <= 512) or hipBLASLt, whichever the autotuned
     plan measured fastest for this (M, N, K); other shapes (prefill) go to hipBLASLt via F.linear.
-    defer_reduce: when the chosen kernel splits K, return its fp32 partials as a `SplitK` for a
-    consumer that fuses the reduction (rmsnorm) instead of running the reduce kernel.
-    bf16_partials: with defer_reduce, an LDS-tiled plan stores those partials as bf16 (half the
-    slab write + read; the rmsnorm consumer still sums them in fp32) — for rmsnorm consumers only."""
+    defer_reduce: when the chosen kernel splits K, return its partials as a `SplitK` for a consumer
+    that fuses the reduction instead of running the reduce kernel.
+    bf16_partials: with defer_reduce, an LDS-tiled / gemm_mfma plan stores those partials as bf16
+    (half the slab write + read).  Consumers that read bf16 partials (summing them in fp32):
+    rmsnorm (O-proj / down, `KA_BF16_PARTIALS`) and the fused decode attention
+    decode_attention_rope (QKV, `KA_BF16_QKV_PARTIALS`); RoPE / SiLU need fp32 partials."""
     M, K = x.shape
     N = w.shape[0]
     if _ref(x) or M > TILE_MAX_M or K % 64 != 0 or N % 4 != 0 or not x.is_contiguous():

@@ -56,6 +56,8 @@ _SIGS = {
     "ka_moe_gemm": [P, P, P, P, P, I, I, I, I, I, I, I, P, P],
     "ka_moe_combine": [P, P, P, I, P, P, I, I, I, I, I, P],
     "ka_allreduce_oneshot": [P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "ka_allgather_oneshot": [P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "ka_allreduce_rmsnorm": [P, P, P, P, F, P, P, P, P, P, I, I, I, I, I, I, P],
     "ka_ar_alloc": [P, ctypes.c_size_t],
     "ka_ar_free": [P],
     "ka_ar_get_handle": [P, P],

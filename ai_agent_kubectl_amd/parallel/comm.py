@@ -11,9 +11,10 @@ tests).  The model needs four collectives:
                       models/moe.py `moe_alltoall`, eager prefill).
 
 All are issued on the current stream so that they are captured inside decode hipGraphs.
-`LocalComm` is the TP=1 no-op.  `TorchComm` wraps a process group.  With KA_CUSTOM_AR=1 a
-hand-written one-shot all-reduce over IPC-mapped peer buffers (csrc/allreduce.hip,
-parallel/custom_allreduce.py) takes the small bf16 decode messages; RCCL keeps the rest.
+`LocalComm` is the TP=1 no-op.  `TorchComm` wraps a process group.  On GPU TP groups hand-written
+one-shot collectives over IPC-mapped peer buffers (csrc/allreduce.hip, parallel/custom_allreduce.py)
+take the small decode messages — the all-reduce fused with the RMSNorm that follows it
+(`all_reduce_rmsnorm`) and the argmax all-gather; RCCL keeps the large prefill messages.
 """
 from __future__ import annotations
 
@@ -77,6 +78,10 @@ class LocalComm:
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         return t.unsqueeze(0)
 
+    def all_reduce_rmsnorm(self, t, w, eps, residual=None):
+        from .. import ops
+        return ops.rmsnorm(t, w, eps, residual=residual)
+
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         return t
 
@@ -114,7 +119,20 @@ class TorchComm:
             self.timer.end(tok)
         return t
 
+    def all_reduce_rmsnorm(self, t: torch.Tensor, w: torch.Tensor, eps: float, residual=None) -> torch.Tensor:
+        """rmsnorm(all_reduce(t) (+ residual)) * w: one fused one-shot launch for decode-size bf16
+        rows (residual updated in place), else the all-reduce followed by the RMSNorm kernel."""
+        from .. import ops
+        if self.world_size > 1 and self.custom_ar is not None and self.custom_ar.can_fuse_norm(t):
+            self.allreduce_calls += 1
+            self.allreduce_bytes += t.numel() * t.element_size()
+            return self.custom_ar.all_reduce_rmsnorm(t, w, eps, residual)
+        self.all_reduce(t)
+        return ops.rmsnorm(t, w, eps, residual=residual)
+
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        if self.custom_ar is not None and self.custom_ar.should_gather(t):
+            return self.custom_ar.all_gather(t)
         flat = torch.empty(self.world_size * t.numel(), dtype=t.dtype, device=t.device)
         self.dist.all_gather_into_tensor(flat, t.contiguous().view(-1), group=self.group)
         return flat.view((self.world_size,) + tuple(t.shape))

@@ -11,8 +11,11 @@ on xGMI, a one-shot kernel reads every peer at once over its own link.  Setup (o
    epoch lives in device memory).
 
 `should_use` routes bf16 tensors up to `cap` elements here; larger (prefill) messages stay on RCCL.
-Enable with KA_CUSTOM_AR=1 (parallel/comm.py `TorchComm`); `err` is set by the kernel if a peer never
-arrived (bounded spin instead of a GPU hang) and is checked by `check()`.
+On by default for GPU TP groups (KA_CUSTOM_AR=0 disables it; parallel/comm.py `TorchComm`): the
+decode all-reduces run fused with the following residual add + RMSNorm (`all_reduce_rmsnorm`), the
+vocab-parallel argmax all-gather (`all_gather`) shares the buffers, so a TP decode hipGraph holds
+every collective.  `err` is set by a kernel if a peer never arrived (bounded spin instead of a GPU
+hang) and is checked by `check()`.
 """
 from __future__ import annotations
 
@@ -93,6 +96,45 @@ class OneShotAllReduce:
             self.rank, self.world, n, self.cap, self.blocks_for(n), ctypes.c_void_p(stream)), "allreduce_oneshot")
         return t
 
+    def can_fuse_norm(self, t: torch.Tensor) -> bool:
+        return self.should_use(t) and t.dim() == 2 and t.shape[1] % 8 == 0 and t.shape[1] <= 8192
+
+    def all_reduce_rmsnorm(self, t: torch.Tensor, w: torch.Tensor, eps: float, residual=None,
+                           out=None) -> torch.Tensor:
+        """rmsnorm(sum_ranks(t) (+ residual)) * w in one launch (residual updated in place)."""
+        rows, hidden = t.shape
+        out = torch.empty_like(t) if out is None else out
+        stream = torch.cuda.current_stream(t.device).cuda_stream
+        self.check_rc(self.lib.ka_allreduce_rmsnorm(
+            ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(t.data_ptr()),
+            ctypes.c_void_p(residual.data_ptr() if residual is not None else 0), ctypes.c_void_p(w.data_ptr()),
+            float(eps), self._data, self._flags, ctypes.c_void_p(self._ctr), ctypes.c_void_p(self._done),
+            ctypes.c_void_p(self._err), self.rank, self.world, rows, hidden, self.cap, min(rows, AR_MAX_BLOCKS),
+            ctypes.c_void_p(stream)), "allreduce_rmsnorm")
+        return out
+
+    def should_gather(self, t: torch.Tensor) -> bool:
+        nb = t.numel() * t.element_size()
+        return t.is_cuda and t.is_contiguous() and 0 < nb and (nb + 15) // 16 * 8 <= self.cap
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *t.shape] (A3: vocab-parallel argmax winners); same buffers / epoch as all_reduce,
+        graph-capturable.  Any dtype: moved as 16-byte units (padded)."""
+        nb = t.numel() * t.element_size()
+        n16 = (nb + 15) // 16 * 8
+        src = t.contiguous().view(torch.uint8)
+        if nb != n16 * 2:
+            padded = torch.zeros(n16 * 2, dtype=torch.uint8, device=t.device)
+            padded[:nb].copy_(src.view(-1))
+            src = padded
+        out = torch.empty((self.world, n16 * 2), dtype=torch.uint8, device=t.device)
+        stream = torch.cuda.current_stream(t.device).cuda_stream
+        self.check_rc(self.lib.ka_allgather_oneshot(
+            ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(src.data_ptr()), self._data, self._flags,
+            ctypes.c_void_p(self._ctr), ctypes.c_void_p(self._done), ctypes.c_void_p(self._err),
+            self.rank, self.world, n16, self.cap, self.blocks_for(n16), ctypes.c_void_p(stream)), "allgather_oneshot")
+        return out[:, :nb].contiguous().view(t.dtype).view((self.world,) + tuple(t.shape))
+
     def check(self) -> None:
         """Raise if any launch timed out waiting for a peer (the kernel's bounded spin)."""
         if int(self.state[2].item()):
@@ -109,8 +151,9 @@ class OneShotAllReduce:
 
 
 def maybe_enable(comm, device) -> None:
-    """Attach a one-shot all-reduce to a TorchComm when KA_CUSTOM_AR=1 and the ranks are on GPUs."""
-    if os.environ.get("KA_CUSTOM_AR", "0") != "1":
+    """Attach the one-shot collectives to a TorchComm whose ranks are on GPUs (default; KA_CUSTOM_AR=0
+    keeps every collective on RCCL)."""
+    if os.environ.get("KA_CUSTOM_AR", "1") != "1":
         return
     if getattr(comm, "world_size", 1) <= 1 or torch.device(device).type != "cuda":
         return

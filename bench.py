@@ -1,24 +1,42 @@
 """Headline benchmark: requests/sec + p50 end-to-end latency of POST /kubectl-command backed by
 Llama-3-8B (bf16, random-init weights, synthetic queries) on N MI355X GPUs (BASELINE.json metric).
 
-One process per GPU (torchrun); every rank is a data-parallel replica: this process runs the full
-ASGI app (auth, limiter, cache, Prometheus middleware, JSON) and the load generator, the engine runs
-in its own process on the rank's GPU (`--in-process` keeps it in this one).  Load is a closed loop
-of `--concurrency` clients per GPU, each sending its next distinct cache-miss query as soon as the
-previous reply arrives (BASELINE.md's concurrency-N method).  A "step" is C completed requests: W
-warm-up steps, then barrier + device sync, exactly K*C timed completions, sync + barrier; the job
-value is total timed requests / max-over-ranks elapsed (weak scaling: per-GPU work is fixed).
-`--waves` runs lock-step waves instead (C requests start together; the next wave after the last).
+One process per GPU (torchrun); every rank is a data-parallel replica with its own engine process
+on its GPU.  A "step" is C completed requests: W warm-up steps, then barrier + device sync,
+exactly K*C timed completions, sync + barrier; the job value is total timed requests / max-over-
+ranks elapsed (weak scaling: per-GPU work is fixed).
 
-  python bench.py                                   # 1 GPU, defaults
-  torchrun --nproc-per-node 8 bench.py --gpus 8     # driver form
+Transports (`--transport`):
+  asgi  (default) the full ASGI app (Prometheus + rate-limit middleware, routing, auth, validation,
+        cache, JSON) driven in-process by a minimal ASGI client — no sockets; the engine runs in
+        its own process on the rank's GPU.
+  tcp   the production server over real sockets: `python -m ai_agent_kubectl_amd.serve` with
+        `--api-workers` uvicorn workers on one port (SO_REUSEPORT, shared cache + limiter,
+        parallel/workers.py) in front of the engine replica, and `--client-procs` load-generator
+        processes speaking HTTP/1.1 keep-alive.  This is what the reference's 354 req/s plumbing
+        floor (uvicorn over TCP) measures.
+
+Load (`--load`): `closed` (default) C clients per GPU, each sending its next distinct cache-miss
+query as soon as the previous reply arrives (BASELINE.md's concurrency-N method); `open` Poisson
+arrivals at `--rate` req/s per GPU (latency under an arrival rate instead of a fixed population).
+`--mix` runs BASELINE config #5 instead of pure misses: cache hits, concurrent /execute calls
+(fake kubectl on PATH), and /metrics scrapes, with per-class counts and p50s in `detail`.
+
+  python bench.py                                   # 1 GPU, defaults (driver form)
+  python bench.py --gpus 8                          # spawns 8 ranks itself (torch.distributed.run)
+  torchrun --nproc-per-node 8 bench.py --gpus 8     # driver form for N > 1
+  python bench.py --transport tcp --api-workers 2   # over real sockets
 """
 import argparse
 import asyncio
 import json
 import os
+import random
+import socket
 import statistics
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -26,13 +44,14 @@ sys.path.insert(0, ROOT)
 
 METRIC = "requests/sec + p50 e2e latency, /kubectl-command Llama-3-8B 1/2/4/8 GPU"
 # reference app.py, cache-miss /kubectl-command at concurrency 32 = 354 req/s
-# (plumbing floor with an instant stub LLM; the reference publishes no OpenAI-backed number).
+# (plumbing floor with an instant stub LLM over TCP; the reference publishes no OpenAI-backed number).
 BASELINE_RPS = 354.0
 
 VERBS = ["list", "show", "get", "display", "find"]
 RES = ["pods", "services", "deployments", "nodes", "configmaps", "secrets", "jobs", "ingresses", "events",
        "statefulsets", "daemonsets", "replicasets", "namespaces", "cronjobs", "endpoints"]
 MODS = ["in namespace", "with label app", "sorted by age in", "that are failing in", "running in cluster"]
+FAKE_KUBECTL = "#!/bin/sh\nprintf 'NAME      READY   STATUS    RESTARTS   AGE\\nnginx-1   1/1     Running   0          5m\\n'\n"
 
 
 def make_query(rank, step, i):
@@ -45,7 +64,34 @@ def make_query(rank, step, i):
     return f"{i}.{step}.{rank} team: {v} all {r} {m} prod"
 
 
-def main():
+def hot_query(rank, j):
+    return f"hot {j}.{rank}: list all {RES[j % len(RES)]} in namespace prod"
+
+
+def cache_size(args):
+    """The reference default (100) for the miss-only headline; with --mix the cache holds the
+    working set (the hit class re-asks 32 hot queries while misses keep inserting)."""
+    return 50000 if args.mix else 100
+
+
+def prompt_len(model: str) -> int:
+    """Prompt tokens of a bench query (CPU only: tokenizer + chat template, as the engine sees it)."""
+    from ai_agent_kubectl_amd.engine.tokenizer import get_tokenizer
+    from ai_agent_kubectl_amd.models.config import get_config
+    from ai_agent_kubectl_amd.prompt import PROMPT_PREFIX, PROMPT_SUFFIX
+    cfg = get_config(model)
+    tok = get_tokenizer(cfg.vocab_size, cfg.tokenizer, None)
+    before, after = tok.chat_prefix_suffix()
+    return len(before + tok.encode(PROMPT_PREFIX) + tok.encode(make_query(0, 0, 0) + PROMPT_SUFFIX) + after)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -55,40 +101,301 @@ def main():
     ap.add_argument("--max-new-tokens", type=int, default=16)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--in-process", action="store_true",
-                    help="run the engine in this process (default: its own process on the same GPU)")
+                    help="asgi transport: run the engine in this process (default: its own process on the GPU)")
+    ap.add_argument("--transport", choices=["asgi", "tcp"], default=os.environ.get("BENCH_TRANSPORT", "asgi"))
+    ap.add_argument("--api-workers", type=int, default=int(os.environ.get("BENCH_API_WORKERS", 2)),
+                    help="tcp: uvicorn API worker processes sharing the port")
+    ap.add_argument("--client-procs", type=int, default=int(os.environ.get("BENCH_CLIENT_PROCS", 2)),
+                    help="tcp: load-generator processes")
+    ap.add_argument("--load", choices=["closed", "open"], default="closed")
+    ap.add_argument("--rate", type=float, default=0.0, help="open loop: arrivals per second per GPU")
+    ap.add_argument("--mix", action="store_true", help="BASELINE config #5: hits + misses + /execute + scrapes")
+    ap.add_argument("--hit-frac", type=float, default=0.5)
+    ap.add_argument("--exec-frac", type=float, default=0.1)
     ap.add_argument("--ramp-s", type=float, default=float(os.environ.get("BENCH_RAMP_S", 0.0)),
                     help="closed loop: client start times spread uniformly over this many seconds")
-    ap.add_argument("--waves", action="store_true",
-                    help="lock-step waves (all C requests start together, the next wave after the "
-                         "slowest) instead of the default closed loop of C clients")
-    ap.add_argument("--client", choices=["asgi", "httpx"], default="asgi",
-                    help="asgi: minimal in-process ASGI client (default); httpx: httpx.ASGITransport")
-    args = ap.parse_args()
+    ap.add_argument("--variable-len", action="store_true",
+                    help="EOS-terminated replies (IGNORE_EOS=0) instead of exactly --max-new-tokens")
+    return ap.parse_args(argv)
 
+
+# ---------------------------------------------------------------------------------------------
+# request classes for --mix (one draw per request)
+def pick_kind(rng, args):
+    if not args.mix:
+        return "miss"
+    x = rng.random()
+    if x < args.exec_frac:
+        return "exec"
+    if x < args.exec_frac + args.hit_frac:
+        return "hit"
+    return "miss"
+
+
+def body_for(kind, rank, n, i, rng):
+    if kind == "exec":
+        return "/execute", b'{"execute":"kubectl get pods -n prod"}'
+    q = hot_query(rank, rng.randrange(32)) if kind == "hit" else make_query(rank, n, i)
+    return "/kubectl-command", b'{"query":' + json.dumps(q).encode() + b"}"
+
+
+def reply_ok(kind, status, raw):
+    if kind == "exec":
+        return status == 200 and raw.startswith(b'{"kubectl_command":"kubectl get pods')
+    if status != 200 or not raw.startswith(b'{"kubectl_command":"kubectl '):
+        return False
+    return (b'"from_cache":true' in raw) if kind == "hit" else (b'"from_cache":false' in raw)
+
+
+# ---------------------------------------------------------------------------------------------
+# HTTP/1.1 keep-alive client (tcp transport)
+class HttpConn:
+    def __init__(self, host, port):
+        self.host, self.port = host, port
+        self.r = self.w = None
+
+    async def open(self):
+        self.r, self.w = await asyncio.open_connection(self.host, self.port)
+        sock = self.w.get_extra_info("socket")
+        if sock is not None:
+            sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+
+    async def request(self, method, path, body=b""):
+        if self.w is None:
+            await self.open()
+        head = b"%s %s HTTP/1.1\r\nhost: bench\r\ncontent-type: application/json\r\ncontent-length: %d\r\n\r\n" % (
+            method.encode(), path.encode(), len(body))
+        self.w.write(head + body)
+        hdr = await self.r.readuntil(b"\r\n\r\n")
+        status = int(hdr[9:12])
+        low = hdr.lower()
+        i = low.find(b"content-length:")
+        n = int(low[i + 15:low.index(b"\r\n", i)]) if i >= 0 else 0
+        return status, await self.r.readexactly(n)
+
+    def close(self):
+        if self.w is not None:
+            self.w.close()
+
+
+def _client_proc(cid, nproc, args, rank, port, C, shared, out_q):
+    """One load-generator process of the tcp transport: C/nproc closed-loop connections (or its
+    share of the open-loop arrival rate).  `shared`: phase (0 warm-up, 1 record, 2 stop) and a
+    completion counter the parent polls."""
+    phase, done = shared
+
+    async def run():
+        rng = random.Random(1000 * rank + cid)
+        lat = {"miss": [], "hit": [], "exec": []}
+        errors = []
+
+        async def one(conn, kind, path, body):
+            t0 = time.perf_counter()
+            status, raw = await conn.request("POST", path, body)
+            if not reply_ok(kind, status, raw):
+                errors.append(f"{kind} {status}: {raw[:200]!r}")
+                return
+            if phase.value == 1:
+                lat[kind].append(time.perf_counter() - t0)
+            with done.get_lock():
+                done.value += 1
+
+        if args.load == "closed":
+            conns = [i for i in range(C) if i % nproc == cid]
+
+            async def worker(i):
+                await asyncio.sleep(random.Random(i).uniform(0, args.ramp_s))
+                conn = HttpConn("127.0.0.1", port)
+                n = 0
+                while phase.value < 2 and not errors:
+                    kind = pick_kind(rng, args)
+                    path, body = body_for(kind, rank, n, i, rng)
+                    n += 1
+                    await one(conn, kind, path, body)
+                conn.close()
+
+            tasks = [asyncio.ensure_future(worker(i)) for i in conns]
+        else:
+            idle = []
+            rate = args.rate / nproc
+            tasks = []
+
+            async def arrival(n):
+                conn = idle.pop() if idle else HttpConn("127.0.0.1", port)
+                kind = pick_kind(rng, args)
+                path, body = body_for(kind, rank, n, cid, rng)
+                await one(conn, kind, path, body)
+                idle.append(conn)
+
+            async def arrivals():
+                n = 0
+                t_next = time.perf_counter()
+                while phase.value < 2 and not errors:
+                    t_next += rng.expovariate(rate)
+                    await asyncio.sleep(max(0.0, t_next - time.perf_counter()))
+                    tasks.append(asyncio.ensure_future(arrival(n)))
+                    n += 1
+
+            tasks.append(asyncio.ensure_future(arrivals()))
+        if args.mix and cid == 0:
+            async def scraper():
+                conn = HttpConn("127.0.0.1", port)
+                while phase.value < 2:
+                    t0 = time.perf_counter()
+                    await conn.request("GET", "/metrics")
+                    if phase.value == 1:
+                        lat.setdefault("scrape", []).append(time.perf_counter() - t0)
+                    await asyncio.sleep(1.0)
+                conn.close()
+            tasks.append(asyncio.ensure_future(scraper()))
+        while phase.value < 2 and not errors:
+            await asyncio.sleep(0.05)
+        await asyncio.sleep(0.2)
+        for t in tasks:
+            t.cancel()
+        out_q.put((cid, lat, errors[:5]))
+
+    asyncio.run(run())
+
+
+# ---------------------------------------------------------------------------------------------
+def service_env(args, C, buckets, local, port, kubectl_dir):
+    env = dict(os.environ, LLM_BACKEND="engine", MODEL=args.model, DP="1", ENGINE_DEVICES=os.environ.get(
+        "BENCH_DEVICE", f"cuda:{local}"), WORKERS=str(args.api_workers), HOST="127.0.0.1", PORT=str(port),
+        RATE_LIMIT="100000000/minute", CACHE_MAXSIZE=str(cache_size(args)), LLM_TIMEOUT="600", LOG_LEVEL="WARNING",
+        MAX_BATCH=str(max(C, 1)), MAX_NEW_TOKENS=str(args.max_new_tokens), IGNORE_EOS="0" if args.variable_len else "1",
+        MAX_NUM_BATCHED_TOKENS="16384", HIPGRAPH_BUCKETS=",".join(str(b) for b in buckets),
+        KV_CACHE_TOKENS=os.environ.get("KV_CACHE_TOKENS", str(max(65536, C * 256))),
+        MAX_MODEL_LEN=os.environ.get("MAX_MODEL_LEN", "512"), PYTHONPATH=ROOT,
+        PATH=kubectl_dir + os.pathsep + os.environ.get("PATH", ""))
+    env.pop("API_AUTH_KEY", None)
+    if args.no_graphs:
+        env["HIPGRAPH_BUCKETS"] = ""
+    return env
+
+
+def run_tcp(args, rank, local, world, C, buckets, dist):
+    """tcp transport: the production server as a child process + client processes."""
+    import multiprocessing as mp
+
+    kdir = tempfile.mkdtemp(prefix="ka_bench_bin_")
+    with open(os.path.join(kdir, "kubectl"), "w") as f:
+        f.write(FAKE_KUBECTL)
+    os.chmod(os.path.join(kdir, "kubectl"), 0o755)
+    port = _free_port()
+    t_build = time.perf_counter()
+    log_path = os.path.join(tempfile.gettempdir(), f"ka_bench_serve_{rank}_{os.getpid()}.log")
+    log = open(log_path, "w")
+    srv = subprocess.Popen([sys.executable, "-m", "ai_agent_kubectl_amd.serve"], env=service_env(
+        args, C, buckets, local, port, kdir), stdout=log, stderr=subprocess.STDOUT, start_new_session=True, cwd=kdir)
+
+    async def health():
+        conn = HttpConn("127.0.0.1", port)
+        try:
+            st, _ = await conn.request("GET", "/health")
+            return st == 200
+        finally:
+            conn.close()
+
+    try:
+        deadline = time.time() + 1500
+        while True:
+            if srv.poll() is not None:
+                raise RuntimeError("server exited: " + open(log_path).read()[-3000:])
+            try:
+                if asyncio.run(health()):
+                    break
+            except OSError:
+                pass
+            if time.time() > deadline:
+                raise RuntimeError("server did not come up")
+            time.sleep(1.0)
+        # the first request of each API worker waits for the engine replica (start + autotune +
+        # hipGraph capture): one request per worker before timing anything
+        async def prime():
+            conns = [HttpConn("127.0.0.1", port) for _ in range(4 * args.api_workers)]
+            rs = await asyncio.gather(*[c.request("POST", "/kubectl-command", b'{"query":"prime %d %d"}' % (rank, j))
+                                        for j, c in enumerate(conns)])
+            if args.mix:   # hot queries for the hit class
+                rs += [await conns[0].request("POST", "/kubectl-command", b'{"query":' + json.dumps(
+                    hot_query(rank, j)).encode() + b"}") for j in range(32)]
+            for c in conns:
+                c.close()
+            return rs
+        rs = asyncio.run(prime())
+        bad = [r for r in rs if r[0] != 200]
+        if bad:
+            raise RuntimeError(f"priming failed: {bad[:2]}")
+        t_build = time.perf_counter() - t_build
+
+        ctx = mp.get_context("spawn")
+        phase, done = ctx.Value("i", 0), ctx.Value("l", 0)
+        out_q = ctx.Queue()
+        P = max(1, min(args.client_procs, C if args.load == "closed" else 64))
+        procs = [ctx.Process(target=_client_proc, args=(c, P, args, rank, port, C, (phase, done), out_q))
+                 for c in range(P)]
+        for p in procs:
+            p.start()
+        warm_target = args.warmup * C
+        while done.value < warm_target:
+            time.sleep(0.005)
+        if world > 1:
+            dist.barrier()
+        with done.get_lock():
+            done.value = 0
+        phase.value = 1
+        t0 = time.perf_counter()
+        target = args.steps * C
+        while done.value < target:
+            time.sleep(0.001)
+        elapsed = time.perf_counter() - t0
+        phase.value = 2
+        if world > 1:
+            dist.barrier()
+        lat = {}
+        errors = []
+        for _ in procs:
+            _, l, e = out_q.get(timeout=120)
+            errors += e
+            for k, v in l.items():
+                lat.setdefault(k, []).extend(v)
+        for p in procs:
+            p.join(timeout=30)
+        if errors:
+            raise RuntimeError("bad replies: %s" % errors[:3])
+        return elapsed, lat, {}, t_build, None
+    finally:
+        if srv.poll() is None:
+            os.killpg(srv.pid, 15)
+            try:
+                srv.wait(60)
+            except subprocess.TimeoutExpired:
+                os.killpg(srv.pid, 9)
+        log.close()
+
+
+def run_asgi(args, rank, local, world, C, buckets, dist):
+    """asgi transport: the full app in this process, driven by a minimal in-process ASGI client."""
     import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    C = args.concurrency
-    buckets = tuple(b for b in (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512)
-                    if b <= max(C, 1))
-    if C not in buckets:
-        buckets = tuple(sorted(set(buckets) | {C}))
 
     from ai_agent_kubectl_amd.api import create_app
     from ai_agent_kubectl_amd.config import Settings
 
-    settings = Settings(RATE_LIMIT="100000000/minute", CACHE_MAXSIZE=100, LLM_TIMEOUT=600, LOG_LEVEL="WARNING",
+    kdir = tempfile.mkdtemp(prefix="ka_bench_bin_")
+    with open(os.path.join(kdir, "kubectl"), "w") as f:
+        f.write(FAKE_KUBECTL)
+    os.chmod(os.path.join(kdir, "kubectl"), 0o755)
+    os.environ["PATH"] = kdir + os.pathsep + os.environ.get("PATH", "")
+    settings = Settings(RATE_LIMIT="100000000/minute", CACHE_MAXSIZE=cache_size(args), LLM_TIMEOUT=600,
+                        LOG_LEVEL="WARNING",
                         LLM_BACKEND="engine", MODEL=args.model, MAX_BATCH=max(C, 1), MAX_NEW_TOKENS=args.max_new_tokens,
-                        IGNORE_EOS=True, MAX_NUM_BATCHED_TOKENS=16384,
+                        IGNORE_EOS=not args.variable_len, MAX_NUM_BATCHED_TOKENS=16384,
                         HIPGRAPH_BUCKETS=",".join(str(b) for b in buckets))
     os.environ.setdefault("KV_CACHE_TOKENS", str(max(65536, C * 256)))
     os.environ.setdefault("MAX_MODEL_LEN", "512")
     t_build = time.perf_counter()
     if not args.in_process:
-        # Engine in its own process on cuda:LOCAL_RANK (spawned before this process touches the
+        # engine in its own process on cuda:LOCAL_RANK (spawned before this process touches the
         # GPU); this process runs the ASGI app + load generator, so HTTP handling and the GPU loop
         # never share a GIL.  Barriers use gloo; the device sync runs inside the engine process.
         from ai_agent_kubectl_amd.parallel.dp import DPRouterLLM
@@ -99,7 +406,6 @@ def main():
         if not any(r.up for r in backend.replicas):
             raise RuntimeError("engine process failed to start")
         eng = None
-        cap_s = 0.0
     else:
         torch.cuda.set_device(local)
         dev = torch.device(f"cuda:{local}")
@@ -109,31 +415,29 @@ def main():
         from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM
         opts = EngineOptions(model=args.model, device=str(dev), max_batch=max(C, 1), graph_buckets=buckets,
                              kv_cache_tokens=max(65536, C * 256), max_model_len=512,
-                             use_graphs=not args.no_graphs, ignore_eos=True, max_batched_tokens=16384)
+                             use_graphs=not args.no_graphs, ignore_eos=not args.variable_len, max_batched_tokens=16384)
         eng = build_engine(opts)
-        cap_s = eng.runner.capture_graphs()
-        backend = EngineLLM(eng, max_new_tokens=args.max_new_tokens, ignore_eos=True)
+        eng.runner.capture_graphs()
+        backend = EngineLLM(eng, max_new_tokens=args.max_new_tokens, ignore_eos=not args.variable_len)
     t_build = time.perf_counter() - t_build
     import logging
     logging.getLogger("app").setLevel(logging.WARNING)
     app = create_app(settings, backend=backend)
-    import httpx
-
-    lat = []
+    lat = {"miss": [], "hit": [], "exec": []}
     headers = [(b"host", b"bench"), (b"content-type", b"application/json")]
 
-    async def asgi_post(path, body: bytes):
+    async def asgi_call(method, path, body: bytes):
         """Minimal in-process ASGI client: one HTTP/1.1 request through the full app stack
         (Prometheus + rate-limit middleware, routing, auth dep, validation, handler, JSON)."""
-        scope = {"type": "http", "asgi": {"version": "3.0"}, "http_version": "1.1", "method": "POST",
+        scope = {"type": "http", "asgi": {"version": "3.0"}, "http_version": "1.1", "method": method,
                  "scheme": "http", "path": path, "raw_path": path.encode(), "query_string": b"",
                  "root_path": "", "headers": headers + [(b"content-length", str(len(body)).encode())],
                  "client": ("127.0.0.1", 40000), "server": ("bench", 80)}
-        done = [False]
+        sent = [False]
 
         async def receive():
-            if not done[0]:
-                done[0] = True
+            if not sent[0]:
+                sent[0] = True
                 return {"type": "http.request", "body": body, "more_body": False}
             await asyncio.sleep(3600)
             return {"type": "http.disconnect"}
@@ -149,46 +453,6 @@ def main():
         await app(scope, receive, send)
         return out["status"], b"".join(out["body"])
 
-    async def one(client, q, record):
-        """One request; returns the reply (raw JSON bytes on the ASGI path, parsed on demand by
-        `command_of`).  The load generator shares this process's CPU with the service, so the
-        client side stays lean: the reply is checked on its bytes (200, a generated command,
-        from_cache false; the app emits compact JSON) instead of being parsed per request."""
-        t0 = time.perf_counter()
-        if client is None:
-            status, raw = await asgi_post("/kubectl-command", b'{"query":' + json.dumps(q).encode() + b"}")
-            ok = status == 200 and raw.startswith(b'{"kubectl_command":"kubectl ') and b'"from_cache":false' in raw
-            body = raw
-        else:
-            r = await client.post("/kubectl-command", json={"query": q})
-            status, body = r.status_code, r.json()
-            ok = status == 200 and body["from_cache"] is False
-        dt = time.perf_counter() - t0
-        if not ok:
-            raise RuntimeError(f"{status}: {body}")
-        if record:
-            lat.append(dt)
-        return body
-
-    def command_of(reply):
-        return json.loads(reply)["kubectl_command"] if isinstance(reply, bytes) else reply["kubectl_command"]
-
-    async def wave(client, step, record):
-        return await asyncio.gather(*[one(client, make_query(rank, step, i), record) for i in range(C)])
-
-    async def sync_all():
-        """barrier + device synchronize: every engine's queued GPU work is complete"""
-        if eng is None:
-            st = (await backend.control("sync"))[0]
-        else:
-            torch.cuda.synchronize()
-            st = dict(eng.runner.stats, prefix_hits=eng.bm.hits, prefix_queries=eng.bm.queries,
-                      partial_tokens=getattr(eng.bm, "partial_tokens", 0), chained_steps=eng.chained_steps,
-                      engine_idle_s=eng.idle_s)
-        if world > 1:
-            dist.barrier()
-        return st
-
     async def sync_barrier():
         """device sync + cross-rank barrier, run off the event loop so in-flight load keeps moving"""
         loop = asyncio.get_running_loop()
@@ -203,33 +467,66 @@ def main():
             await loop.run_in_executor(None, dist.barrier)
         return st
 
-    async def closed_loop(client):
-        """C concurrent clients, each sending its next request as soon as the previous reply
-        arrives (the closed-loop method BASELINE.md's concurrency-32 rows use).  W*C completions
-        warm up; then barrier + device sync, exactly K*C completions are timed, sync + barrier."""
-        import random
+    async def run():
+        await backend.start()
+        if args.mix:
+            for j in range(32):
+                st, raw = await asgi_call("POST", "/kubectl-command", b'{"query":' + json.dumps(
+                    hot_query(rank, j)).encode() + b"}")
+                assert st == 200, raw
         state = {"done": 0, "target": args.warmup * C, "record": False, "stop": False}
         reached = asyncio.Event()
         sample = []
+        errors = []
+        rng = random.Random(rank)
 
-        async def worker(i):
-            await asyncio.sleep(random.Random(i).uniform(0, args.ramp_s))   # de-phase the first arrivals
-            n = 0
-            while not state["stop"]:
-                t_start = time.perf_counter()
-                cmd = await one(client, make_query(rank, n, i), False)
-                n += 1
-                if state["stop"]:
-                    break
-                if not sample:
-                    sample.append(cmd)
-                state["done"] += 1
-                if state["record"]:
-                    lat.append(time.perf_counter() - t_start)
-                if state["done"] >= state["target"] and not reached.is_set():
-                    reached.set()
+        async def one(kind, path, body):
+            t_start = time.perf_counter()
+            status, raw = await asgi_call("POST", path, body)
+            if not reply_ok(kind, status, raw):
+                errors.append(f"{kind} {status}: {raw[:200]!r}")
+                reached.set()
+                return
+            if not sample and kind == "miss":
+                sample.append(raw)
+            state["done"] += 1
+            if state["record"]:
+                lat[kind].append(time.perf_counter() - t_start)
+            if state["done"] >= state["target"] and not reached.is_set():
+                reached.set()
 
-        tasks = [asyncio.ensure_future(worker(i)) for i in range(C)]
+        tasks = []
+        if args.load == "closed":
+            async def worker(i):
+                await asyncio.sleep(random.Random(i).uniform(0, args.ramp_s))   # de-phase the first arrivals
+                n = 0
+                while not state["stop"] and not errors:
+                    kind = pick_kind(rng, args)
+                    path, body = body_for(kind, rank, n, i, rng)
+                    n += 1
+                    await one(kind, path, body)
+            tasks = [asyncio.ensure_future(worker(i)) for i in range(C)]
+        else:
+            async def arrivals():
+                n = 0
+                t_next = time.perf_counter()
+                while not state["stop"] and not errors:
+                    t_next += rng.expovariate(args.rate)
+                    await asyncio.sleep(max(0.0, t_next - time.perf_counter()))
+                    kind = pick_kind(rng, args)
+                    path, body = body_for(kind, rank, n, n % 997, rng)
+                    n += 1
+                    tasks.append(asyncio.ensure_future(one(kind, path, body)))
+            tasks.append(asyncio.ensure_future(arrivals()))
+        if args.mix:
+            async def scraper():
+                while not state["stop"]:
+                    t0 = time.perf_counter()
+                    await asgi_call("GET", "/metrics", b"")
+                    if state["record"]:
+                        lat.setdefault("scrape", []).append(time.perf_counter() - t0)
+                    await asyncio.sleep(1.0)
+            tasks.append(asyncio.ensure_future(scraper()))
         if state["target"] > 0:
             await reached.wait()
         st0 = await sync_barrier()
@@ -241,29 +538,14 @@ def main():
         st1 = await sync_barrier()
         el = time.perf_counter() - t0
         state["stop"] = True
-        await asyncio.gather(*tasks)
-        return el, sample, st0, st1
-
-    async def waves(client):
-        sample = None
-        for s in range(args.warmup):
-            sample = await wave(client, s, False)
-        st0 = await sync_all()
-        t0 = time.perf_counter()
-        for s in range(args.steps):
-            await wave(client, args.warmup + s, True)
-        st1 = await sync_all()
-        return time.perf_counter() - t0, sample, st0, st1
-
-    async def run():
-        await backend.start()
-        limits = httpx.Limits(max_connections=None, max_keepalive_connections=None)
-        async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://bench",
-                                     limits=limits, timeout=600) as hc:
-            client = hc if args.client == "httpx" else None
-            el, sample, st0, st1 = await (waves(client) if args.waves else closed_loop(client))
+        for t in tasks:
+            t.cancel()
+        await asyncio.gather(*tasks, return_exceptions=True)
         await backend.close()
-        return el, sample, {k: st1[k] - st0[k] for k in st1 if isinstance(st1[k], (int, float))}
+        if errors:
+            raise RuntimeError("bad replies: %s" % errors[:3])
+        stats = {k: st1[k] - st0[k] for k in st1 if isinstance(st1[k], (int, float))}
+        return el, sample, stats
 
     if os.environ.get("KA_PROFILE_API"):
         import cProfile
@@ -276,41 +558,89 @@ def main():
             pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(50)
     else:
         elapsed, sample, st = asyncio.run(run())
+    reply = json.loads(sample[0])["kubectl_command"] if sample else None
+    return elapsed, lat, st, t_build, (reply, backend.prompt_ids(make_query(0, 0, 0)))
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N`: spawn the N ranks ourselves, before anything touches a GPU,
+        # as a child torch.distributed.run job (one process per GPU), and exit with its status
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} does not match WORLD_SIZE={world}")
+    if args.load == "open" and args.rate <= 0:
+        sys.exit("bench.py: --load open needs --rate")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    C = args.concurrency
+    buckets = tuple(b for b in (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512)
+                    if b <= max(C, 1))
+    if C not in buckets:
+        buckets = tuple(sorted(set(buckets) | {C}))
+
+    import torch.distributed as dist
+
+    if args.transport == "tcp":
+        if world > 1:
+            dist.init_process_group("gloo")
+        elapsed, lat, st, t_build, extra = run_tcp(args, rank, local, world, C, buckets, dist)
+        reply, seq_len = None, prompt_len(args.model) + args.max_new_tokens
+    else:
+        elapsed, lat, st, t_build, extra = run_asgi(args, rank, local, world, C, buckets, dist)
+        reply, prompt = extra
+        seq_len = len(prompt) + args.max_new_tokens
+
     n_req = C * args.steps
-    p50 = statistics.median(lat) * 1e3
+    allv = [v for k in ("miss", "hit", "exec") for v in lat.get(k, [])]
+    p50 = statistics.median(allv) * 1e3 if allv else float("nan")
     if world > 1:
-        t = torch.tensor([elapsed, p50], dtype=torch.float64,
-                         device="cpu" if eng is None else torch.device(f"cuda:{local}"))
+        import torch
+        t = torch.tensor([elapsed, p50], dtype=torch.float64)
         gathered = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(gathered, t)
         elapsed = max(g[0].item() for g in gathered)
         p50 = statistics.median([g[1].item() for g in gathered])
     value = n_req * world / elapsed
+
+    def pct(v, q):
+        return round(sorted(v)[int(q * (len(v) - 1))] * 1e3, 2) if v else None
+
     if rank == 0:
+        detail = {"concurrency_per_gpu": C, "new_tokens": args.max_new_tokens, "transport": args.transport,
+                  "load": args.load + (f"@{args.rate}/s" if args.load == "open" else ""),
+                  "p99_ms": pct(allv, 0.99), "build_s": round(t_build, 1), "sample_reply": reply,
+                  "baseline": "BASELINE.md reference plumbing floor, cache-miss conc 32 = 354 req/s (uvicorn, TCP)"}
+        if args.transport == "tcp":
+            detail.update(api_workers=args.api_workers, client_procs=args.client_procs)
+        if args.mix:
+            detail["mix"] = {k: {"n": len(v), "p50_ms": pct(v, 0.5), "p99_ms": pct(v, 0.99)} for k, v in lat.items()}
+        if st:
+            detail.update({
+                "decode_steps": st.get("decode_steps"), "prefill_steps": st.get("prefill_steps"),
+                "decode_ms_per_step": round(st["decode_ms"] / max(1, st["decode_steps"]), 3),
+                "prefill_ms_per_step": round(st["prefill_ms"] / max(1, st["prefill_steps"]), 3),
+                "prefill_tokens": st.get("prefill_tokens"), "graph_replays": st.get("graph_replays"),
+                "prefix_cache_hit_rate": round(st.get("prefix_hits", 0) / max(1, st.get("prefix_queries", 0)), 3),
+                "sub_block_reused_tokens": st.get("partial_tokens", 0),
+                "overlapped_decode_steps": st.get("chained_steps", 0),
+                "engine_idle_ms_per_step": round(st.get("engine_idle_s", 0.0) * 1e3 / args.steps, 2),
+                "engine_process": not args.in_process})
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "req/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": round(value / BASELINE_RPS, 3),
             "dtype": "bf16", "data": "synthetic queries, random-init weights",
             "config": {"model": "Llama-3-8B-Instruct" if args.model == "llama3-8b" else args.model,
-                       "global_batch": C * world, "seq_len": len(backend.prompt_ids(make_query(0, 0, 0))) +
-                       args.max_new_tokens, "parallelism": f"dp{world}"},
-            "p50_ms": round(p50, 2),
-            "detail": {"concurrency_per_gpu": C, "new_tokens": args.max_new_tokens,
-                       "load": "waves" if args.waves else "closed-loop",
-                       "p99_ms": round(sorted(lat)[int(0.99 * (len(lat) - 1))] * 1e3, 2) if lat else None,
-                       "decode_steps": st.get("decode_steps"), "prefill_steps": st.get("prefill_steps"),
-                       "decode_ms_per_step": round(st["decode_ms"] / max(1, st["decode_steps"]), 3),
-                       "prefill_ms_per_step": round(st["prefill_ms"] / max(1, st["prefill_steps"]), 3),
-                       "prefill_tokens": st.get("prefill_tokens"), "graph_replays": st.get("graph_replays"),
-                       "prefix_cache_hit_rate": round(st.get("prefix_hits", 0) / max(1, st.get("prefix_queries", 0)), 3),
-                       "sub_block_reused_tokens": st.get("partial_tokens", 0),
-                       "overlapped_decode_steps": st.get("chained_steps", 0),
-                       "engine_idle_ms_per_step": round(st.get("engine_idle_s", 0.0) * 1e3 / args.steps, 2),
-                       "build_s": round(t_build, 1), "engine_process": eng is None,
-                       "sample_reply": command_of(sample[0]) if sample else None,
-                       "baseline": "BASELINE.md reference plumbing floor, cache-miss conc 32 = 354 req/s"},
+                       "global_batch": C * world, "seq_len": seq_len, "parallelism": f"dp{world}"},
+            "p50_ms": round(p50, 2), "detail": detail,
         }
+        if args.mix:
+            out["config"]["mix"] = f"hit {args.hit_frac} exec {args.exec_frac} miss {1 - args.hit_frac - args.exec_frac}"
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -21,12 +21,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(args, world):
+def _run(args, world, launcher="torchrun"):
     env = dict(os.environ, BENCH_DEVICE="cpu", PYTHONUNBUFFERED="1")
     bench = [os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "1", "--warmup", "1",
-             "--concurrency", "4", "--model", "tiny-llama"]
-    if world == 1:
-        cmd = [sys.executable] + bench
+             "--concurrency", "4", "--model", "tiny-llama"] + list(args)
+    if world == 1 or launcher == "self":
+        cmd = [sys.executable] + bench     # --gpus N > 1: bench.py spawns its N ranks itself
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr", "127.0.0.1", f"--master-port={_free_port()}"] + bench
@@ -37,9 +37,9 @@ def _run(args, world):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("world", [1, 2])
-def test_bench_prints_one_json_line(world):
-    out = _run([], world)
+@pytest.mark.parametrize("world,launcher", [(1, "self"), (2, "torchrun"), (2, "self")])
+def test_bench_prints_one_json_line(world, launcher):
+    out = _run([], world, launcher)
     assert KEYS <= set(out)
     assert out["n_gpus"] == world and out["steps"] == 1 and out["warmup"] == 1
     assert out["higher_is_better"] is True and out["scaling"] == "weak" and out["unit"] == "req/s"
@@ -47,3 +47,30 @@ def test_bench_prints_one_json_line(world):
     assert out["config"]["parallelism"] == f"dp{world}" and out["config"]["global_batch"] == 4 * world
     # value = total timed requests over the slowest rank's elapsed time
     assert out["value"] == pytest.approx(4 * world / (out["ms_per_step"] / 1e3), rel=0.02)
+
+
+def test_bench_gpus_must_match_world_size():
+    """Under torchrun, --gpus N with a different WORLD_SIZE is refused (never silently measures
+    fewer GPUs)."""
+    env = dict(os.environ, BENCH_DEVICE="cpu", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=120, env=env, cwd="/tmp")
+    assert r.returncode != 0 and "does not match WORLD_SIZE" in r.stderr
+
+
+def test_bench_tcp_transport():
+    """--transport tcp: the production server (2 API workers on one port, shared cache/limiter) over
+    real sockets, 2 client processes."""
+    out = _run(["--transport", "tcp", "--api-workers", "2", "--client-procs", "2"], 1)
+    assert out["detail"]["transport"] == "tcp" and out["detail"]["api_workers"] == 2
+    assert out["value"] == pytest.approx(4 / (out["ms_per_step"] / 1e3), rel=0.02)
+    assert out["config"]["seq_len"] > 16
+
+
+def test_bench_open_loop_mixed_stream():
+    """--load open --mix: Poisson arrivals of hits, misses and /execute calls plus /metrics scrapes
+    (BASELINE config #5); per-class latencies are reported."""
+    out = _run(["--load", "open", "--rate", "40", "--mix"], 1)
+    mix = out["detail"]["mix"]
+    assert out["detail"]["load"].startswith("open")
+    assert sum(v["n"] for k, v in mix.items() if k != "scrape") >= 4

@@ -33,6 +33,23 @@ def _worker(rank, world, port, q):
             ar.all_reduce(t)
             torch.cuda.synchronize()
             errs.append((t.float().cpu() - want).abs().max().item())
+        # fused all-reduce + residual add + RMSNorm == all-reduce then the RMSNorm kernel, bit for bit
+        from ai_agent_kubectl_amd import ops
+        for rows, hidden in ((1, 4096), (3, 8192), (70, 4096)):
+            g = torch.Generator().manual_seed(77 + rows)
+            parts = [torch.randn(rows, hidden, generator=g).to(torch.bfloat16) for _ in range(world)]
+            res0 = torch.randn(rows, hidden, generator=g).to(torch.bfloat16).cuda()
+            wgt = (torch.rand(hidden, generator=g) + 0.5).to(torch.bfloat16).cuda()
+            t1, r1 = parts[rank].cuda(), res0.clone()
+            ar.all_reduce(t1)
+            want_out = ops.rmsnorm(t1, wgt, 1e-5, residual=r1)
+            t2, r2 = parts[rank].cuda(), res0.clone()
+            got_out = ar.all_reduce_rmsnorm(t2, wgt, 1e-5, r2)
+            torch.cuda.synchronize()
+            errs.append(0.0 if torch.equal(got_out, want_out) and torch.equal(r2, r1) else 1.0)
+            t3 = torch.arange(rows * 4, dtype=torch.int32, device="cuda").view(rows, 4) + 1000 * rank
+            gath = ar.all_gather(t3)
+            errs.append(0.0 if all(torch.equal(gath[p], t3 - 1000 * rank + 1000 * p) for p in range(world)) else 1.0)
         # hipGraph capture + replay (epoch read from device memory each replay)
         x = torch.zeros(4096, dtype=torch.bfloat16, device="cuda")
         s = torch.cuda.Stream()

@@ -322,6 +322,16 @@ def test_virtual_tp2_matches_tp1_cpu(model):
     assert torch.equal(a.argmax(-1), b.argmax(-1))
 
 
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-mixtral"])
+def test_virtual_tp2_generate_matches_tp1_cpu(model):
+    """Driver / worker TP protocol (header + metadata broadcasts, worker_loop, vocab-parallel
+    argmax, EP all-to-all prefill for Mixtral) with one rank per thread: same greedy tokens."""
+    sys.path.insert(0, ROOT)
+    from tests.virtual_tp import virtual_tp_generate
+    qs = ["list all pods", "show services in prod", "scale web to 3"]
+    assert virtual_tp_generate(model, 2, qs, device="cpu") == virtual_tp_generate(model, 1, qs, device="cpu")
+
+
 def test_openai_compatible_chat(tiny_engine):
     from fastapi.testclient import TestClient
     from ai_agent_kubectl_amd.api import create_app

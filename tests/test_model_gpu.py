@@ -163,6 +163,23 @@ def test_virtual_tp_matches_tp1():
     assert cos.min().item() > 0.999
 
 
+@pytest.mark.parametrize("model,tp", [("llama3-70b-2l", 4), ("llama3-70b-2l", 8), ("mixtral-2l", 8)])
+def test_virtual_tp_spec_geometry_tokens_match_tp1(model, tp):
+    """TP = 4 / 8 at Llama-3-70B geometry (64 q / 8 kv heads: 1 KV head and 8 q heads per rank at
+    TP = 8, GQA group 8 in the HIP attention kernels) and EP = 8 for Mixtral (one expert per rank,
+    all-to-all prefill dispatch): the real driver / worker TP engine code, one rank per thread on
+    this GPU, generates the same greedy tokens as TP = 1 (SURVEY.md §4.3 'TP numerics (1 GPU)')."""
+    from tests.virtual_tp import assert_same_or_near_tie, virtual_tp_generate
+    qs = QUERIES[:3]
+    ref = virtual_tp_generate(model, 1, qs)
+    got = virtual_tp_generate(model, tp, qs)
+    torch.cuda.empty_cache()
+    if got != ref:   # bf16 partial sums: only a near-tie of the TP = 1 logits may flip a token
+        eng = _engine(model, graphs=False)
+        be = EngineLLM(eng, max_new_tokens=6, ignore_eos=True)
+        assert_same_or_near_tie(eng, [be.prompt_ids(q) for q in qs], ref, got)
+
+
 def test_mixtral_forward_hip_vs_reference():
     eng = _engine("mixtral-2l", graphs=False)
     be = EngineLLM(eng, max_new_tokens=8)

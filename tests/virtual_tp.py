@@ -9,6 +9,7 @@ the TP=1 weights that Megatron sharding assigns it.
 from __future__ import annotations
 
 import threading
+import traceback
 
 import torch
 
@@ -22,9 +23,9 @@ from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM
 
 
 class VirtualComm:
-    def __init__(self, world: int):
+    def __init__(self, world: int, timeout: float = 300.0):
         self.world_size = world
-        self._bar = threading.Barrier(world)
+        self._bar = threading.Barrier(world, timeout=timeout)   # a failing rank breaks it: no hang
         self._slots = [None] * world
         self._out = None
 
@@ -68,7 +69,21 @@ class VirtualComm:
                 return torch.cat(pieces)
 
             def broadcast(self, t, src=0):
+                if rank == src:
+                    parent._slots[src] = t
+                parent._bar.wait()
+                if rank != src:
+                    t.copy_(parent._slots[src])
+                parent._bar.wait()
                 return t
+
+            def barrier(self):
+                parent._bar.wait()
+
+            def all_reduce_rmsnorm(self, t, w, eps, residual=None):
+                from ai_agent_kubectl_amd import ops
+                self.all_reduce(t)
+                return ops.rmsnorm(t, w, eps, residual=residual)
 
         return _R()
 
@@ -125,3 +140,77 @@ def virtual_tp_logits(cfg, tp: int, device="cuda", queries=("list all pods", "ge
     for t in threads:
         t.join()
     return torch.cat(results, dim=-1)
+
+
+def virtual_tp_generate(model: str, tp: int, queries, max_new_tokens: int = 6, device: str = "cuda"):
+    """Greedy generation through the real TP engine code on ONE device: `tp` threads, each a full
+    TP rank (build_engine with tp_rank / tp_size: sharded weights, KV heads and vocab), rank 0 the
+    driver (scheduler + metadata broadcast, LLMEngine.generate_blocking) and the others in
+    `ModelRunner.worker_loop()` — the multi-process protocol with VirtualComm as the transport.
+    Eager steps (the host-side VirtualComm cannot be captured).  Returns rank 0's output ids."""
+    from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine
+    from ai_agent_kubectl_amd.engine.sequence import SamplingParams
+    vc = VirtualComm(tp)
+    out, errs = {}, []
+
+    def run(r):
+        try:
+            eng = build_engine(EngineOptions(model=model, device=device, tp_rank=r, tp_size=tp, ep_size=tp,
+                                             max_batch=4, graph_buckets=(1, 2, 4), kv_cache_tokens=4096,
+                                             max_model_len=256, use_graphs=False), comm=vc.view(r))
+            if r != 0:
+                eng.runner.worker_loop()
+                return
+            be = EngineLLM(eng, max_new_tokens=max_new_tokens, ignore_eos=True)
+            params = SamplingParams(max_new_tokens=max_new_tokens, ignore_eos=True)
+            seqs = eng.generate_blocking([be.prompt_ids(q) for q in queries], params, forced_prefix=be._forced)
+            eng.runner.stop_workers()
+            out["ids"] = [s.output_ids for s in seqs]
+        except Exception:
+            errs.append(traceback.format_exc())
+            vc._bar.abort()
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(tp)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errs:
+        raise RuntimeError(errs[0])
+    return out["ids"]
+
+
+@torch.inference_mode()
+def next_token_logits(eng, ids):
+    """Logits of the token after `ids` from `eng`'s model (one prefill of the whole sequence)."""
+    from ai_agent_kubectl_amd.engine.sequence import Sequence
+    r = eng.runner
+    seq = Sequence(prompt_ids=list(ids), params=SamplingParams())
+    seq.block_table, _, seq.block_hashes = eng.bm.allocate_prompt(seq.all_ids)
+    try:
+        batch = Batch([seq], [seq.total_len], is_decode=False, prefill_seqs=[seq])
+        host = torch.from_numpy(r._pack_prefill(batch)).to(r.device)
+        T, S, mb = batch.num_tokens, 1, r.max_blocks
+        o = 3 * T
+        meta = AttnMeta(positions=host[T:2 * T], slot_mapping=host[2 * T:3 * T],
+                        block_tables=host[o + 4 * S + 1:o + 4 * S + 1 + S * mb].view(S, mb),
+                        ctx_lens=host[o + S + 1:o + 2 * S + 1], logits_indices=host[o + 3 * S + 1:o + 4 * S + 1].long(),
+                        is_decode=False, q_starts=host[o:o + S + 1], max_q_len=T)
+        h = r.model.forward(host[:T], meta, r.k_cache, r.v_cache)
+        return r.model.logits(h)[0].float()
+    finally:
+        eng.bm.free_table(seq.block_table)
+
+
+def assert_same_or_near_tie(eng_ref, prompts, want, got, rel=0.01, abs_tol=0.05):
+    """Greedy outputs of two numerically different but equivalent runs (TP = 1 vs TP = t in bf16):
+    identical, or the first token where they part is a near-tie of the reference model — its
+    logits for the two candidates (teacher-forced on the shared prefix) differ by less than
+    rel * |logit| + abs_tol.  Anything else is a real divergence."""
+    for p, w, g in zip(prompts, want, got):
+        if w == g:
+            continue
+        k = next(i for i in range(min(len(w), len(g))) if w[i] != g[i])
+        lg = next_token_logits(eng_ref, list(p) + list(w[:k]))
+        lw, lgot = lg[w[k]].item(), lg[g[k]].item()
+        assert lw - lgot <= rel * abs(lw) + abs_tol, (k, w[k], g[k], lw, lgot)
