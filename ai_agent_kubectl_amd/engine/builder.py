@@ -35,7 +35,7 @@ class EngineOptions:
     ep_size: int = 1
     max_batch: int = 256
     max_batched_tokens: int = 8192
-    max_model_len: int = 2048
+    max_model_len: int = 8192      # Llama-3's context; long prompts prefill in chunks
     block_size: int = 16
     kv_cache_tokens: int = 1 << 18
     gpu_mem_fraction: float = 0.90
@@ -53,7 +53,7 @@ class EngineOptions:
                    graph_buckets=tuple(b for b in s.graph_buckets() if b <= s.MAX_BATCH) or (1,),
                    safe_decode=s.SAFE_DECODE, ignore_eos=s.IGNORE_EOS, prefix_caching=s.PREFIX_CACHING,
                    kv_cache_tokens=int(os.environ.get("KV_CACHE_TOKENS", 1 << 18)),
-                   max_model_len=int(os.environ.get("MAX_MODEL_LEN", 2048)),
+                   max_model_len=int(os.environ.get("MAX_MODEL_LEN", 8192)),
                    device="cuda" if torch.cuda.is_available() else "cpu")
 
 
@@ -77,7 +77,9 @@ def build_engine(opts: EngineOptions, comm=None, metrics=None) -> LLMEngine:
     weights = build_weights(opts.weights, cfg, par, device=dev, dtype=dtype)
     # ---- KV pool size ----
     per_block = cfg.num_layers * 2 * (cfg.num_kv_heads // opts.tp_size) * cfg.head_dim * opts.block_size * 2
-    want_blocks = max(opts.kv_cache_tokens // opts.block_size, opts.max_batch * (opts.max_model_len // opts.block_size + 1))
+    # KV_CACHE_TOKENS of pooled KV (not max_batch x max_model_len: with an 8192-token context that
+    # would be 2M tokens); at least one full-length sequence fits, the rest is preemption's job
+    want_blocks = max(opts.kv_cache_tokens // opts.block_size, opts.max_model_len // opts.block_size + 1)
     if dev.type == "cuda":
         free, _total = torch.cuda.mem_get_info(dev)
         budget = int(free * opts.gpu_mem_fraction) - (2 << 30)   # headroom for activations / graphs

@@ -56,6 +56,7 @@ class LLMEngine:
         self.step_t0: Optional[float] = None   # perf_counter at the start of the running step
         self.watchdog = None       # parallel/watchdog.py (TP/EP > 1, rank 0)
         self._ar_bytes_seen = 0
+        self._t_done = 0.0         # perf_counter of the last step readback (step-time metric)
 
     def mark_unhealthy(self, reason: str) -> None:
         """Watchdog verdict (worker heartbeat lost / step stalled): new requests get 503."""
@@ -136,11 +137,15 @@ class LLMEngine:
         now = time.perf_counter()
         m = self.metrics
         prefill = {id(s) for s in batch.prefill_seqs}
+        partial = batch.partial
         for s, nq, tok in zip(batch.seqs, batch.num_query, tokens):
             if s.finished:
                 continue
             was_prefill = id(s) in prefill
             s.num_computed += nq
+            if id(s) in partial:   # a chunk of a long prompt: its KV is cached, nothing is sampled
+                self.bm.register_computed(s.block_table, s.all_ids[:s.num_computed], s.block_hashes)
+                continue
             s.output_ids.append(int(tok))
             if was_prefill:
                 self.bm.register_computed(s.block_table, s.all_ids[:s.num_computed], s.block_hashes)
@@ -148,6 +153,7 @@ class LLMEngine:
                     s.t_first_token = now
                     if m is not None:
                         m.llm_ttft.observe(now - s.t_arrival)
+                        m.llm_queue_wait.observe((s.t_scheduled or now) - s.t_arrival)
             eos = (not s.params.ignore_eos) and self.tokenizer.is_eos(int(tok))
             if eos or s.num_generated >= s.params.max_new_tokens:
                 if m is not None and s.t_first_token is not None and s.num_generated > 1:
@@ -160,7 +166,7 @@ class LLMEngine:
         `prev`, a sequence finished / was aborted, or KV capacity for one more token is missing.
         (An EOS sampled by `prev` is only seen at collect: that row's next token is discarded.)"""
         sch = self.scheduler
-        if sch.waiting and sch._should_prefill():
+        if prev.partial or (sch.waiting and sch._should_prefill()):
             return None
         for s in prev.seqs:
             if s.finished or s.num_generated + 1 >= s.params.max_new_tokens:
@@ -173,21 +179,27 @@ class LLMEngine:
         from .scheduler import Batch
         return Batch(list(prev.seqs), [1] * len(prev.seqs), is_decode=True)
 
-    def _finish_step(self, batch, tokens) -> None:
+    def _finish_step(self, batch, tokens, t_launch: float) -> None:
         self._apply(batch, tokens)
         self.scheduler.on_step_done(batch)
         self.steps += 1
+        m = self.metrics
+        if m is not None:   # a step's share of the pipeline: from its launch (or the previous
+            now = time.perf_counter()   # step's completion, when it was queued behind it) to its readback
+            m.llm_step.labels("decode" if batch.is_decode else "prefill").observe(now - max(t_launch, self._t_done))
+            self._t_done = now
 
     def step(self) -> int:
         """Run one scheduler step; returns the number of sequences processed."""
         self._drain_inbox()
         if self._inflight is not None:
-            prev, handle = self._inflight
+            prev, handle, t_prev = self._inflight
             nxt = self._chain(prev)
+            t_nxt = time.perf_counter()
             nh = self.runner.launch_decode_async(nxt, chained=True) if nxt is not None else None
             self.chained_steps += nxt is not None
-            self._finish_step(prev, self.runner.collect(handle))
-            self._inflight = (nxt, nh) if nxt is not None else None
+            self._finish_step(prev, self.runner.collect(handle), t_prev)
+            self._inflight = (nxt, nh, t_nxt) if nxt is not None else None
             batch = prev
         else:
             if not self.scheduler.has_work():
@@ -195,8 +207,9 @@ class LLMEngine:
             batch = self.scheduler.schedule()
             if not batch.seqs:
                 return 0
+            t0 = time.perf_counter()
             if self.overlap and batch.is_decode and self.runner.can_overlap(len(batch.seqs)):
-                self._inflight = (batch, self.runner.launch_decode_async(batch))
+                self._inflight = (batch, self.runner.launch_decode_async(batch), t0)
                 return len(batch.seqs)
             if (self.overlap and not batch.is_decode and len(batch.prefill_seqs) == len(batch.seqs)
                     and self.runner.can_overlap(len(batch.seqs))):
@@ -205,13 +218,14 @@ class LLMEngine:
                 # prefill back, so the GPU does not idle while the host applies ~256 prompts
                 ph = self.runner.launch_prefill_async(batch)
                 nxt = self._chain(batch)
+                t_nxt = time.perf_counter()
                 nh = self.runner.launch_decode_async(nxt, chained=True) if nxt is not None else None
                 self.chained_steps += nxt is not None
                 self.prefill_chains += nxt is not None
-                self._finish_step(batch, self.runner.collect(ph))
-                self._inflight = (nxt, nh) if nxt is not None else None
+                self._finish_step(batch, self.runner.collect(ph), t0)
+                self._inflight = (nxt, nh, t_nxt) if nxt is not None else None
                 return len(batch.seqs)
-            self._finish_step(batch, self.runner.execute(batch))
+            self._finish_step(batch, self.runner.execute(batch), t0)
         m = self.metrics
         if m is not None:
             m.llm_batch_size.set(len(batch.seqs))
@@ -229,9 +243,11 @@ class LLMEngine:
 
     def _fail_all(self, err: BaseException) -> None:
         self._inflight = None
-        seqs = list(self.scheduler.running) + list(self.scheduler.waiting)
-        self.scheduler.running.clear()
-        self.scheduler.waiting.clear()
+        sch = self.scheduler
+        seqs = list(sch.running) + list(sch.prefilling) + list(sch.waiting)
+        sch.running.clear()
+        sch.prefilling.clear()
+        sch.waiting.clear()
         for s in seqs:
             if not s.finished:
                 self._finish(s, SeqStatus.ABORTED, "error", error=err)
@@ -306,10 +322,10 @@ class LLMEngine:
                 self._wake.clear()
                 self.idle_s += time.perf_counter() - t_idle
         if self._inflight is not None:   # stopping with a step in flight: finish it cleanly
-            prev, handle = self._inflight
+            prev, handle, t_prev = self._inflight
             self._inflight = None
             try:
-                self._finish_step(prev, self.runner.collect(handle))
+                self._finish_step(prev, self.runner.collect(handle), t_prev)
             except Exception:  # pragma: no cover
                 logger.exception("in-flight step failed at shutdown")
 

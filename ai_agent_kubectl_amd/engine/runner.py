@@ -122,12 +122,35 @@ class ModelRunner:
                     groups.setdefault(tuple(w.shape), []).append(w)
                     if local and k in ("wo", "w2"):   # llama.py defers their split-K reduce into the norm
                         norm_fed.add(tuple(w.shape))
-                    # not QKV: timed with a norm standing in for the fused decode attention, its
-                    # split-K plan won (25.8 vs 26.9 us at M = 256) but the attention prologue that
-                    # reduces the partials grew 24.1 -> 29.7 us (profiles/phase_profile_c256_qkv_proxy_negative.txt)
         lm = self.model.W["lm_head"]
         groups.setdefault(tuple(lm.shape), []).append(lm)
-        return tune_linear(groups, self.buckets, norm_fed, getattr(self.model, "bf16_partials", False))
+        consumers = {}
+        m = self.model
+        if m.fuse_decode_rope and m.D == 128 and self.block_size == 16 and "wqkv" in m.layers[0]:
+            # QKV is timed with its real consumer, the fused RoPE + KV append + decode attention
+            # on a synthetic 128-token context (a norm stand-in picked a split plan whose partials
+            # then slowed the attention prologue: profiles/phase_profile_c256_qkv_proxy_negative.txt)
+            consumers[tuple(m.layers[0]["wqkv"].shape)] = (self._attention_consumer(), m.bf16_qkv_partials)
+        return tune_linear(groups, self.buckets, norm_fed, getattr(self.model, "bf16_partials", False), consumers)
+
+    def _attention_consumer(self, ctx: int = 128):
+        """fn(qkv, M): decode_attention_rope over M synthetic sequences of `ctx` cached tokens in
+        layer 0's cache (autotune runs before serving: the KV written here is never read)."""
+        m, bs = self.model, self.block_size
+        nb = (ctx + bs - 1) // bs
+        memo = {}
+
+        def consume(qkv, M):
+            if M not in memo:
+                bt = (torch.arange(M * nb, dtype=torch.int32, device=self.device) % self.num_blocks).view(M, nb)
+                pos = torch.full((M,), ctx - 1, dtype=torch.int32, device=self.device)
+                slots = (bt[:, -1] * bs + (ctx - 1) % bs).to(torch.int32)
+                lens = torch.full((M,), ctx, dtype=torch.int32, device=self.device)
+                memo[M] = (pos, slots, bt.contiguous(), lens)
+            pos, slots, bt, lens = memo[M]
+            return ops.decode_attention_rope(qkv, pos, m.cos_sin, slots, self.k_cache[0], self.v_cache[0], bt, lens,
+                                             m.hq, m.hkv, m.D, m.scale)
+        return consume
 
     @torch.inference_mode()
     def capture_graphs(self, autotune: bool = True) -> float:
@@ -296,17 +319,17 @@ class ModelRunner:
         tot = np.empty(S, dtype=np.int64)
         toks: list = []
         for i, (s, nq) in enumerate(zip(batch.seqs, batch.num_query)):
-            n = s.total_len
+            start = s.num_computed               # query = all_ids[start:n] (a chunk may end early)
+            n = start + nq
             tot[i] = n
             ng = len(s.output_ids) - s.n_forced
             lp = len(s.prompt_ids)
-            start = n - nq
             if start >= lp:                      # decode row (mixed step): generated tokens only
                 toks.extend(s.output_ids[s.n_forced + start - lp:s.n_forced + n - lp])
             else:
-                toks.extend(s.prompt_ids[start:])
-                if ng:
-                    toks.extend(s.output_ids[s.n_forced:])
+                toks.extend(s.prompt_ids[start:min(n, lp)])
+                if n > lp:
+                    toks.extend(s.output_ids[s.n_forced:s.n_forced + n - lp])
             tbl = s.block_table
             bt[i, :len(tbl)] = tbl
             mask[i] = mask_index_for(ng, s.params.safe_decode)

@@ -10,6 +10,12 @@ Each engine step runs ONE forward over a batch:
 
 New sequences join the running set the step after their prefill; finished sequences leave
 immediately and free their blocks, so the batch composition changes every step.
+
+Chunked prefill: a prompt whose uncached tail exceeds the step's token budget is
+prefilled in budget-sized chunks over consecutive mixed steps (`prefilling`), so a long context
+(up to MAX_MODEL_LEN = 8192) neither blows the step's activation size nor stalls the running
+decodes for a whole 8k-token forward.  A chunk row samples nothing; the row that computes the last
+prompt token samples the first output token as usual.
 """
 from __future__ import annotations
 
@@ -30,6 +36,7 @@ class Batch:
     is_decode: bool
     prefill_seqs: List[Sequence] = field(default_factory=list)
     copies: List[tuple] = field(default_factory=list)     # (src, dst) KV block copies before the step
+    partial: frozenset = frozenset()     # id() of chunk rows: prompt not finished, nothing sampled
 
     @property
     def num_tokens(self) -> int:
@@ -41,7 +48,8 @@ class Scheduler:
                  max_model_len: int = 4096, mix_decode_into_prefill: bool = True,
                  prefill_max_wait_s: Optional[float] = None, prefill_min_frac: Optional[float] = None,
                  partial_block_reuse: bool = True, gather_max_s: float = 0.0, gather_quiet_s: float = 0.0015,
-                 hold_steps: Optional[int] = None, hold_max_s: Optional[float] = None):
+                 hold_steps: Optional[int] = None, hold_max_s: Optional[float] = None,
+                 chunked_prefill: Optional[bool] = None, min_chunk: int = 256):
         # Prefill batching under continuous arrivals: a prefill step is an eager (non-graph) step,
         # so while sequences are decoding, new arrivals are admitted together — when at least
         # max(4, prefill_min_frac * running) are waiting or the oldest has waited
@@ -85,6 +93,11 @@ class Scheduler:
         self.partial_reuse = partial_block_reuse and hasattr(block_manager, "reuse_partial")
         self.waiting: Deque[Sequence] = collections.deque()
         self.running: List[Sequence] = []
+        if chunked_prefill is None:
+            chunked_prefill = os.environ.get("KA_CHUNKED_PREFILL", "1") == "1"
+        self.chunked = chunked_prefill
+        self.min_chunk = min_chunk          # a later row is chunked only if this much budget is left
+        self.prefilling: List[Sequence] = []   # admitted, prompt partially computed (chunked)
 
     def add(self, seq: Sequence) -> None:
         if seq.total_len + seq.params.max_new_tokens > self.max_model_len:
@@ -93,21 +106,38 @@ class Scheduler:
         self.waiting.append(seq)
 
     def has_work(self) -> bool:
-        return bool(self.waiting or self.running)
+        return bool(self.waiting or self.running or self.prefilling)
 
     def abort(self, seq: Sequence) -> None:
         if seq in self.waiting:
             self.waiting.remove(seq)
         if seq in self.running:
             self.running.remove(seq)
+        if seq in self.prefilling:
+            self.prefilling.remove(seq)
         self.bm.free_table(seq.block_table)
         seq.status = SeqStatus.ABORTED
 
     # ------------------------------------------------------------------------------------------
-    def _admit(self, copies: List[tuple]) -> List[Sequence]:
+    def _admit(self, copies: List[tuple]):
+        """-> (rows, query lengths, partial ids): the chunked prompts first, then new arrivals."""
         admitted: List[Sequence] = []
+        nqs: List[int] = []
+        partial = set()
         budget = self.max_batched_tokens - (len(self.running) if self.mix else 0)
-        while self.waiting and len(self.running) + len(admitted) < self.max_batch:
+        for seq in self.prefilling:   # continue the chunked prompts (oldest first)
+            rem = seq.total_len - seq.num_computed
+            c = min(rem, budget)
+            if c <= 0:
+                break
+            admitted.append(seq)
+            nqs.append(c)
+            if c < rem:
+                partial.add(id(seq))
+            budget -= c
+        n_busy = len(self.running) + len(self.prefilling)
+        n_cont = len(admitted)     # continued chunk rows are already counted in n_busy
+        while self.waiting and budget > 0 and n_busy + len(admitted) - n_cont < self.max_batch:
             seq = self.waiting[0]
             try:
                 table, cached, hashes = self.bm.allocate_prompt(seq.all_ids)
@@ -115,11 +145,15 @@ class Scheduler:
                 break
             part = self.bm.reuse_partial(table, seq.all_ids, cached, hashes) if self.partial_reuse else None
             q = seq.total_len - cached - (part[1] if part else 0)
-            if q > budget and admitted:
-                if part:
-                    self.bm.unpin(part[0])
-                self.bm.free_table(table)
-                break
+            c = q
+            if q > budget:
+                if admitted and not (self.chunked and budget >= self.min_chunk):
+                    if part:
+                        self.bm.unpin(part[0])
+                    self.bm.free_table(table)
+                    break
+                if self.chunked:
+                    c = budget
             if part:   # sub-block reuse: copy the sibling's KV rows, skip its first r tokens
                 copies.append((part[0], table[cached // self.bm.block_size]))
                 cached += part[1]
@@ -128,9 +162,14 @@ class Scheduler:
             seq.num_computed = cached
             seq.num_cached_prompt = cached
             seq.status = SeqStatus.RUNNING
+            if seq.t_scheduled is None:
+                seq.t_scheduled = time.perf_counter()
             admitted.append(seq)
-            budget -= q
-        return admitted
+            nqs.append(c)
+            if c < q:
+                partial.add(id(seq))
+            budget -= c
+        return admitted, nqs, partial
 
     def gathering(self) -> bool:
         """Idle engine, requests still streaming in: hold the admission for a moment.  The window
@@ -159,6 +198,8 @@ class Scheduler:
         return left <= self.hold_steps
 
     def _should_prefill(self) -> bool:
+        if self.prefilling:   # a chunked prompt continues every step
+            return True
         if not self.waiting:
             return False
         if not self.running:
@@ -173,7 +214,7 @@ class Scheduler:
 
     def schedule(self) -> Batch:
         copies: List[tuple] = []
-        admitted = self._admit(copies) if self._should_prefill() else []
+        admitted, nqs, partial = self._admit(copies) if self._should_prefill() else ([], [], set())
         # decode rows need a slot for their next token
         decodes: List[Sequence] = []
         if not admitted or self.mix:
@@ -196,8 +237,9 @@ class Scheduler:
                     decodes.append(seq)
         if admitted:
             seqs = decodes + admitted
-            nq = [1] * len(decodes) + [s.total_len - s.num_computed for s in admitted]
-            return Batch(seqs, nq, is_decode=False, prefill_seqs=admitted, copies=copies)
+            nq = [1] * len(decodes) + nqs
+            return Batch(seqs, nq, is_decode=False, prefill_seqs=admitted, copies=copies,
+                         partial=frozenset(partial))
         return Batch(decodes, [1] * len(decodes), is_decode=True)
 
     def _preempt(self, seq: Sequence) -> None:
@@ -213,8 +255,14 @@ class Scheduler:
         for src, _ in batch.copies:   # the copy is enqueued before the step's kernels: release the pin
             self.bm.unpin(src)
         for s in batch.prefill_seqs:
-            if not s.finished:
-                self.running.append(s)
+            chunk = id(s) in batch.partial
+            if s.finished or not chunk:
+                if s in self.prefilling:
+                    self.prefilling.remove(s)
+                if not s.finished:
+                    self.running.append(s)
+            elif s not in self.prefilling:
+                self.prefilling.append(s)
         before = len(self.running)
         self.running = [s for s in self.running if not s.finished]
         if not self.running and before:

@@ -41,6 +41,7 @@ class Sequence:
     finish_reason: Optional[str] = None
     error: Optional[BaseException] = None
     t_arrival: float = field(default_factory=time.perf_counter)
+    t_scheduled: Optional[float] = None     # first admission into a prefill step (queue wait ends)
     t_first_token: Optional[float] = None
     t_finish: Optional[float] = None
 

@@ -70,8 +70,13 @@ class ServiceMetrics:
         self.llm_tpot = Histogram("llm_tpot_seconds", "Time per output token after the first.",
                                   buckets=(0.001, 0.002, 0.003, 0.005, 0.0075, 0.01, 0.02, 0.05, 0.1, 0.25),
                                   registry=r)
-        self.llm_queue_wait = Histogram("llm_queue_wait_seconds", "Scheduler queue wait.",
+        self.llm_queue_wait = Histogram("llm_queue_wait_seconds",
+                                        "Arrival to first admission into a prefill step.",
                                         buckets=HIGHR_BUCKETS, registry=r)
+        self.llm_step = Histogram("llm_step_seconds", "Engine step time (launch or previous readback to "
+                                  "readback) by phase.", ("phase",),
+                                  buckets=(0.001, 0.002, 0.004, 0.006, 0.008, 0.01, 0.015, 0.02, 0.03, 0.05, 0.1,
+                                           0.2, 0.5, 1.0), registry=r)
         self.llm_batch_size = Gauge("llm_batch_size", "Sequences in the last engine step.", registry=r)
         self.llm_queue_depth = Gauge("llm_queue_depth", "Requests waiting for the engine.", registry=r)
         self.llm_kv_blocks_used = Gauge("llm_kv_blocks_used", "Paged-KV blocks in use.", registry=r)

@@ -291,7 +291,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
     decode_attention_rope (QKV, `KA_BF16_QKV_PARTIALS`); RoPE / SiLU need fp32 partials."""
     M, K = x.shape
     N = w.shape[0]
-    if _ref(x) or M > TILE_MAX_M or K % 64 != 0 or N % 4 != 0 or not x.is_contiguous():
+    if _ref(x):
+        return ref.linear(x, w)
+    if M > TILE_MAX_M or K % 64 != 0 or N % 4 != 0 or not x.is_contiguous():
         return torch.nn.functional.linear(x, w)
     if not split:
         plan = GEMM_PLAN.get((M, N, K))

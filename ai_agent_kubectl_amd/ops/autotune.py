@@ -9,7 +9,7 @@ captured graphs contain the fastest kernel per shape.
 from __future__ import annotations
 
 import logging
-from typing import Dict, List, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -78,15 +78,19 @@ def _tunableop_end() -> None:
 
 @torch.inference_mode()
 def tune_linear(groups: Dict[Tuple[int, int], List[torch.Tensor]], Ms: Sequence[int],
-                norm_fed: Sequence[Tuple[int, int]] = (), bf16_partials: bool = True) -> Dict:
+                norm_fed: Sequence[Tuple[int, int]] = (), bf16_partials: bool = True,
+                consumers: Optional[Dict[Tuple[int, int], Tuple[Callable, bool]]] = None) -> Dict:
     """groups: (N, K) -> list of weight tensors of that shape (one per layer).
     norm_fed: shapes whose output goes straight into the fused residual + RMSNorm (o_proj and down
     at TP = 1).  Their candidates are timed together with that norm, split-K ones with the
     reduction deferred into it (as the model runs them), so a split plan is not charged for a
-    reduce kernel the model never launches."""
+    reduce kernel the model never launches.
+    consumers: (N, K) -> (fn(out, M), bf16) for other fused consumers — QKV -> the fused RoPE +
+    KV-append + decode attention, which reduces split-K partials (bf16 ones when `bf16`) in its
+    prologue: candidates are timed with that kernel, in the form the model runs them."""
     tunable = _tunableop_begin()
     try:
-        return _tune(groups, Ms, set(norm_fed), bf16_partials)
+        return _tune(groups, Ms, set(norm_fed), bf16_partials, consumers or {})
     finally:
         if tunable:
             _tunableop_end()
@@ -149,17 +153,25 @@ def gm_candidates(M: int, N: int, K: int, cfgs: Sequence[int] = ()):
     return out
 
 
-def _tune(groups, Ms, norm_fed=frozenset(), bf16_partials: bool = True) -> Dict:
+def _tune(groups, Ms, norm_fed=frozenset(), bf16_partials: bool = True, consumers=None) -> Dict:
     report = {}
+    consumers = consumers or {}
     for (N, K), ws in groups.items():
         ws = ws[: max(2, min(len(ws), 16))]
-        fed = (N, K) in norm_fed
+        cons = consumers.get((N, K))
+        fed = (N, K) in norm_fed or cons is not None    # partials handed to a fused consumer
+        bf16 = cons[1] if cons is not None else bf16_partials
         dev, dt = ws[0].device, ws[0].dtype
         g = torch.ones(N, device=dev, dtype=dt)
         for M in sorted(set(int(m) for m in Ms if m <= TILE_MAX_M)):
             x = torch.randn(M, K, device=dev, dtype=dt)
             res = torch.zeros(M, N, device=dev, dtype=dt)
-            norm = (lambda h: rmsnorm(h, g, 1e-5, residual=res)) if fed else (lambda h: h)
+            if cons is not None:
+                norm = (lambda h, M=M, fn=cons[0]: fn(h, M))
+            elif fed:
+                norm = (lambda h: rmsnorm(h, g, 1e-5, residual=res))
+            else:
+                norm = (lambda h: h)
             GEMM_PLAN.pop((M, N, K), None)
             t_blas = _time(lambda w: norm(torch.nn.functional.linear(x, w)), ws)
             best = ("blas", 0, 0, t_blas)
@@ -170,16 +182,16 @@ def _tune(groups, Ms, norm_fed=frozenset(), bf16_partials: bool = True) -> Dict:
                     if t < best[3]:
                         best = ("skinny", sp, 0, t)
             for cfg, sp in tile_candidates(M, N, K):
-                t = _time(lambda w: norm(linear_tile(x, w, cfg, sp, defer_reduce=fed, bf16_partials=bf16_partials)),
-                          ws)
+                t = _time(lambda w: norm(linear_tile(x, w, cfg, sp, defer_reduce=fed, bf16_partials=bf16)), ws)
                 if t < best[3]:
                     best = ("tile", sp, cfg, t)
             for cfg, sp in gm_candidates(M, N, K):
-                t = _time(lambda w: norm(linear_gm(x, w, cfg, sp, defer_reduce=fed, bf16_partials=bf16_partials)), ws)
+                t = _time(lambda w: norm(linear_gm(x, w, cfg, sp, defer_reduce=fed, bf16_partials=bf16)), ws)
                 if t < best[3]:
                     best = ("gm", sp, cfg, t)
             GEMM_PLAN[(M, N, K)] = (best[0], best[1], best[2])
             report[(M, N, K)] = {"choice": best[0], "split": best[1], "cfg": best[2], "us": round(best[3], 1),
-                                 "blas_us": round(t_blas, 1), "with_norm": fed}
+                                 "blas_us": round(t_blas, 1),
+                                 "with": "attention" if cons is not None else "norm" if fed else None}
     logger.info("gemm plan: %s", report)
     return report

@@ -12,6 +12,11 @@ import torch
 import torch.nn.functional as F
 
 
+def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """y = x @ w.T computed in fp32 (the reference for every projection), returned in x's dtype."""
+    return torch.nn.functional.linear(x.float(), w.float()).to(x.dtype)
+
+
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     if residual is not None:
         r = (x.float() + residual.float()).to(x.dtype)

@@ -157,4 +157,6 @@ def maybe_enable(comm, device) -> None:
         return
     if getattr(comm, "world_size", 1) <= 1 or torch.device(device).type != "cuda":
         return
+    if not hasattr(comm, "group"):   # not a torch.distributed comm (e.g. the virtual-TP test comm)
+        return
     comm.custom_ar = OneShotAllReduce(comm.group, device, int(os.environ.get("KA_CUSTOM_AR_ELEMS", 4 << 20)))

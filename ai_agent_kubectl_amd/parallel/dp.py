@@ -56,6 +56,22 @@ class _Obs:
         self.sink.append(v)
 
 
+class _Labelled:
+    """`metric.labels(phase).observe(v)` recorded as (phase, v)."""
+
+    def __init__(self, sink: list):
+        self.sink = sink
+
+    def labels(self, phase):
+        sink = self.sink
+
+        class _O:
+            @staticmethod
+            def observe(v):
+                sink.append((phase, v))
+        return _O
+
+
 class _Gauge:
     def __init__(self, store: dict, name: str):
         self.store, self.name = store, name
@@ -73,19 +89,24 @@ class EngineMetricsProxy:
     def __init__(self):
         self.ttft: list = []
         self.tpot: list = []
+        self.qwait: list = []
+        self.steps: list = []      # (phase, seconds)
         self.gauges: dict = {}
         self.llm_ttft = _Obs(self.ttft)
         self.llm_tpot = _Obs(self.tpot)
+        self.llm_queue_wait = _Obs(self.qwait)
+        self.llm_step = _Labelled(self.steps)
         self.llm_batch_size = _Gauge(self.gauges, "llm_batch_size")
         self.llm_queue_depth = _Gauge(self.gauges, "llm_queue_depth")
         self.llm_kv_blocks_used = _Gauge(self.gauges, "llm_kv_blocks_used")
 
     def take(self):
-        if not (self.ttft or self.tpot or self.gauges):
+        if not (self.ttft or self.tpot or self.qwait or self.steps or self.gauges):
             return None
-        out = {"ttft": self.ttft[:], "tpot": self.tpot[:], "gauges": dict(self.gauges)}
-        self.ttft.clear()
-        self.tpot.clear()
+        out = {"ttft": self.ttft[:], "tpot": self.tpot[:], "qwait": self.qwait[:], "steps": self.steps[:],
+               "gauges": dict(self.gauges)}
+        for lst in (self.ttft, self.tpot, self.qwait, self.steps):
+            lst.clear()
         self.gauges.clear()
         return out
 
@@ -364,6 +385,10 @@ class DPRouterLLM(LLMBackend):
             m.llm_ttft.observe(v)
         for v in obs["tpot"]:
             m.llm_tpot.observe(v)
+        for v in obs.get("qwait", ()):
+            m.llm_queue_wait.observe(v)
+        for phase, v in obs.get("steps", ()):
+            m.llm_step.labels(phase).observe(v)
         if obs["gauges"]:
             self._gauges[idx] = {**self._gauges.get(idx, {}), **obs["gauges"]}
             for name in ("llm_batch_size", "llm_queue_depth", "llm_kv_blocks_used"):

@@ -265,7 +265,7 @@ def service_env(args, C, buckets, local, port, kubectl_dir):
         RATE_LIMIT="100000000/minute", CACHE_MAXSIZE=str(cache_size(args)), LLM_TIMEOUT="600", LOG_LEVEL="WARNING",
         MAX_BATCH=str(max(C, 1)), MAX_NEW_TOKENS=str(args.max_new_tokens), IGNORE_EOS="0" if args.variable_len else "1",
         MAX_NUM_BATCHED_TOKENS="16384", HIPGRAPH_BUCKETS=",".join(str(b) for b in buckets),
-        KV_CACHE_TOKENS=os.environ.get("KV_CACHE_TOKENS", str(max(65536, C * 256))),
+        KV_CACHE_TOKENS=os.environ.get("KV_CACHE_TOKENS", str(max(65536, C * 528))),
         MAX_MODEL_LEN=os.environ.get("MAX_MODEL_LEN", "512"), PYTHONPATH=ROOT,
         PATH=kubectl_dir + os.pathsep + os.environ.get("PATH", ""))
     env.pop("API_AUTH_KEY", None)
@@ -391,7 +391,7 @@ def run_asgi(args, rank, local, world, C, buckets, dist):
                         LLM_BACKEND="engine", MODEL=args.model, MAX_BATCH=max(C, 1), MAX_NEW_TOKENS=args.max_new_tokens,
                         IGNORE_EOS=not args.variable_len, MAX_NUM_BATCHED_TOKENS=16384,
                         HIPGRAPH_BUCKETS=",".join(str(b) for b in buckets))
-    os.environ.setdefault("KV_CACHE_TOKENS", str(max(65536, C * 256)))
+    os.environ.setdefault("KV_CACHE_TOKENS", str(max(65536, C * 528)))
     os.environ.setdefault("MAX_MODEL_LEN", "512")
     t_build = time.perf_counter()
     if not args.in_process:
@@ -414,7 +414,7 @@ def run_asgi(args, rank, local, world, C, buckets, dist):
         from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine
         from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM
         opts = EngineOptions(model=args.model, device=str(dev), max_batch=max(C, 1), graph_buckets=buckets,
-                             kv_cache_tokens=max(65536, C * 256), max_model_len=512,
+                             kv_cache_tokens=max(65536, C * 528), max_model_len=512,
                              use_graphs=not args.no_graphs, ignore_eos=not args.variable_len, max_batched_tokens=16384)
         eng = build_engine(opts)
         eng.runner.capture_graphs()

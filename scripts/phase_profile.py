@@ -44,7 +44,7 @@ def main():
     C = a.concurrency
     buckets = tuple(b for b in (1, 8, 16, 32, 64, 128, 192, 256, 384, 512) if b <= C) + ((C,) if C not in (1, 8, 16, 32, 64, 128, 192, 256, 384, 512) else ())
     eng = build_engine(EngineOptions(model=a.model, device="cuda:0", max_batch=C, graph_buckets=buckets,
-                                     kv_cache_tokens=max(65536, C * 256), max_model_len=512, ignore_eos=True,
+                                     kv_cache_tokens=max(65536, C * 528), max_model_len=512, ignore_eos=True,
                                      max_batched_tokens=16384))
     eng.runner.capture_graphs()
     be = EngineLLM(eng, max_new_tokens=16, ignore_eos=True)

@@ -159,6 +159,53 @@ def test_scheduler_preempts_when_out_of_blocks():
     assert len(sch.waiting) == 1 and sch.waiting[0].status is SeqStatus.WAITING
 
 
+def _step(sch, b, tok=1):
+    """Apply a scheduled batch the way LLMEngine._apply does (chunk rows sample nothing)."""
+    for s, n in zip(b.seqs, b.num_query):
+        s.num_computed += n
+        if id(s) not in b.partial:
+            s.output_ids.append(tok)
+    sch.on_step_done(b)
+
+
+def test_scheduler_chunks_long_prompt():
+    """A prompt over the step budget is prefilled in budget-sized chunks; the
+    running decodes keep their row in every chunk step; an arrival waits for budget."""
+    bm = BlockManager(64, 4, enable_prefix_caching=False)
+    sch = Scheduler(bm, max_batch=4, max_batched_tokens=20, prefill_max_wait_s=0.0, chunked_prefill=True,
+                    min_chunk=8, hold_steps=0)
+    short = _seq(6, new=8)
+    sch.add(short)
+    b = sch.schedule()
+    assert b.num_query == [6] and not b.partial
+    _step(sch, b)
+    long_ = _seq(50)
+    sch.add(long_)
+    b = sch.schedule()     # 1 decode row + 19-token chunk
+    assert b.seqs == [short, long_] and b.num_query == [1, 19] and b.partial == {id(long_)}
+    _step(sch, b)
+    assert sch.prefilling == [long_] and long_.output_ids == [] and long_.num_computed == 19
+    late = _seq(5)
+    sch.add(late)
+    b = sch.schedule()     # the chunked prompt continues first; the late arrival does not fit
+    assert b.seqs == [short, long_] and b.num_query == [1, 19]
+    _step(sch, b)
+    b = sch.schedule()     # last 12 prompt tokens sample the first token; 7 left for the arrival
+    assert b.seqs == [short, long_, late] and b.num_query == [1, 12, 5] and not b.partial
+    _step(sch, b)
+    assert sch.prefilling == [] and long_.num_computed == 50 and long_.output_ids == [1]
+    assert sch.running == [short, long_, late]
+    assert sch.schedule().is_decode
+
+
+def test_scheduler_unchunked_admits_over_budget_prompt_whole():
+    bm = BlockManager(64, 4, enable_prefix_caching=False)
+    sch = Scheduler(bm, max_batch=4, max_batched_tokens=20, prefill_max_wait_s=0.0, chunked_prefill=False)
+    sch.add(_seq(50))
+    b = sch.schedule()
+    assert b.num_query == [50] and not b.partial
+
+
 # ---------------- engine end to end (CPU) ----------------
 @pytest.fixture(scope="module")
 def tiny_engine():
@@ -294,6 +341,30 @@ def test_overlapped_decode_matches_sync(tiny_engine):
     assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
 
 
+def test_chunked_prefill_matches_whole_prefill(tiny_engine):
+    """Prompts prefilled in 24-token chunks (through the threaded engine: mixed chunk + decode
+    steps, overlapped decode) sample the same tokens as one whole-prompt prefill."""
+    eng, be = tiny_engine
+    params = SamplingParams(max_new_tokens=6, ignore_eos=True)
+    prompts = [be.prompt_ids(q) for q in ("list pods", "get services in namespace kube-system -o wide",
+                                          "describe deployment api-gateway")]
+    eng.bm.reset_prefix_cache()
+    whole = [s.output_ids for s in eng.generate_blocking(prompts, params, forced_prefix=be._forced)]
+    sch = eng.scheduler
+    saved = sch.max_batched_tokens, sch.min_chunk
+    sch.max_batched_tokens, sch.min_chunk = 24, 4
+    try:
+        eng.bm.reset_prefix_cache()
+        chunked = [s.output_ids for s in eng.generate_blocking(prompts, params, forced_prefix=be._forced)]
+        eng.bm.reset_prefix_cache()
+        threaded = [s.output_ids for s in _run_thread(eng, prompts, params, be._forced)]
+    finally:
+        sch.max_batched_tokens, sch.min_chunk = saved
+    assert min(len(p) for p in prompts) + len(be._forced) > 24   # every prompt really was chunked
+    assert chunked == whole and threaded == whole
+    assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
+
+
 def test_api_with_engine_backend(tiny_engine):
     from fastapi.testclient import TestClient
     from ai_agent_kubectl_amd.api import create_app
@@ -307,6 +378,8 @@ def test_api_with_engine_backend(tiny_engine):
         assert c.post("/kubectl-command", json={"query": "list all pods"}).json()["from_cache"] is True
         m = c.get("/metrics").text
         assert "llm_ttft_seconds_count 1.0" in m
+        assert "llm_queue_wait_seconds_count 1.0" in m
+        assert 'llm_step_seconds_count{phase="prefill"}' in m and 'llm_step_seconds_count{phase="decode"}' in m
 
 
 # ---------------- tensor parallel numerics ----------------
@@ -524,7 +597,9 @@ def test_pack_prefill_matches_per_sequence_reference():
     eng.generate_blocking([prompts[0]], params, forced_prefix=forced)     # warm the prefix cache
     for s in seqs[:2]:                                                   # two sequences already decoding
         eng.scheduler.add(s)
+    eng.scheduler.gather_max_s = 0.0    # admit now (no burst gathering)
     b0 = eng.scheduler.schedule()
+    assert len(b0.prefill_seqs) == 2
     eng._apply(b0, eng.runner.execute(b0))
     eng.scheduler.on_step_done(b0)
     for s in seqs[:2]:

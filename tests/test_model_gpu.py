@@ -24,9 +24,9 @@ QUERIES = ["list all pods", "show services in namespace prod", "scale web to 3 r
            "get nodes with labels", "describe deployment api", "logs of pod api-1"]
 
 
-def _engine(model, graphs, buckets=(1, 2, 4, 8), **kw):
-    opts = EngineOptions(model=model, device="cuda", max_batch=8, graph_buckets=buckets, kv_cache_tokens=16384,
-                         max_model_len=512, use_graphs=graphs, **kw)
+def _engine(model, graphs, buckets=(1, 2, 4, 8), max_batch=8, kv_cache_tokens=16384, **kw):
+    opts = EngineOptions(model=model, device="cuda", max_batch=max_batch, graph_buckets=buckets,
+                         kv_cache_tokens=kv_cache_tokens, max_model_len=512, use_graphs=graphs, **kw)
     eng = build_engine(opts)
     if graphs:
         eng.runner.capture_graphs()
@@ -69,6 +69,65 @@ def test_llama_forward_hip_vs_reference():
     cos = torch.nn.functional.cosine_similarity(lg_hip, lg_ref, dim=-1)
     assert cos.min().item() > 0.995, cos
     torch.testing.assert_close(h_hip.float(), h_ref.float(), atol=0.1, rtol=0.05)
+
+
+@pytest.mark.parametrize("B", [1, 4, 256])
+def test_decode_chain_vs_fp32_reference(B):
+    """The real decode chain — autotuned GEMM plan (tile / gemm_mfma kernels at M = 256 with bf16
+    split-K partials reduced inside the fused RoPE + KV-append + attention kernel and inside the
+    fused residual + RMSNorm, GEMV / skinny kernels at M = 1 / 4), the fused decode attention, the
+    LM head — over 8 decode steps, each step against the same forward through the fp32 torch
+    references (`ops.force_reference`: fp32 GEMMs, reference attention / RoPE / norms) on a copy
+    of the same KV cache.  Hidden states and logits to bf16 tolerance (bf16 partials)."""
+    from ai_agent_kubectl_amd.engine.sequence import Sequence
+    from ai_agent_kubectl_amd.models.llama import AttnMeta
+    eng = _engine("llama3-8b-2l", graphs=True, buckets=(1, 4, 256), max_batch=256, kv_cache_tokens=65536)
+    be = EngineLLM(eng, max_new_tokens=40, ignore_eos=True)
+    params = SamplingParams(max_new_tokens=40, ignore_eos=True)
+    sch, r = eng.scheduler, eng.runner
+    sch.prefill_max_wait_s = 0.0
+    sch.gather_max_s = 0.0
+    sch.hold_steps = 0
+    if B >= 48:   # the tile / gemm_mfma plans (and their bf16 partials) are what runs at this size
+        assert any(v[0] in ("tile", "gm") for (m, _, _), v in ops.GEMM_PLAN.items() if m == B), ops.GEMM_PLAN
+    with torch.inference_mode():
+        for i in range(B):
+            sch.add(Sequence(prompt_ids=be.prompt_ids(QUERIES[i % len(QUERIES)] + f" #{i}"), params=params,
+                             forced_prefix=list(be._forced)))
+        while sch.waiting:
+            b = sch.schedule()
+            eng._apply(b, r.execute(b))
+            sch.on_step_done(b)
+        assert len(sch.running) == B
+        worst = 1.0
+        for step in range(8):
+            batch = sch.schedule()
+            assert batch.is_decode and len(batch.seqs) == B
+            Bp = r.buckets[r.buckets.index(B)]
+            r._pack_decode(batch, Bp)
+            n = r._off["bt"] + Bp * r.max_blocks
+            r.d_stage[:n].copy_(r.h_stage[:n])
+            meta = AttnMeta(positions=r._view("pos", Bp), slot_mapping=r._view("slots", Bp),
+                            block_tables=r._view("bt", Bp), ctx_lens=r._view("ctx", Bp),
+                            logits_indices=r.d_logits_idx[:Bp], is_decode=True)
+            ids = r._view("ids", Bp)
+            kc, vc = r.k_cache.clone(), r.v_cache.clone()
+            h = r.model.forward(ids, meta, r.k_cache, r.v_cache)
+            lg = r.model.logits(h).float()
+            with ops.force_reference():
+                h_ref = r.model.forward(ids, meta, kc, vc)
+                lg_ref = r.model.logits(h_ref).float()
+            cos = torch.nn.functional.cosine_similarity(lg[:B], lg_ref[:B], dim=-1)
+            worst = min(worst, cos.min().item())
+            assert cos.min().item() > 0.995, (step, cos.min().item())
+            torch.testing.assert_close(h[:B].float(), h_ref[:B].float(), atol=0.1, rtol=0.05)
+            torch.testing.assert_close(lg[:B], lg_ref[:B], atol=0.15, rtol=0.05)
+            del kc, vc
+            mask = r._view("mask", Bp) if r.mask_bits is not None else None
+            tok = r.model.sample(h, r.mask_bits, mask)[:B].tolist()
+            eng._apply(batch, tok)
+            sch.on_step_done(batch)
+    print(f"B={B}: worst logits cosine over 8 steps {worst:.5f}")
 
 
 def test_graph_decode_equals_eager():

@@ -42,8 +42,9 @@ def _post(port, path, body, timeout=120):
         c.close()
 
 
-def _get(port, path, timeout=30):
-    c = http.client.HTTPConnection("127.0.0.1", port, timeout=timeout)
+def _get(port, path, timeout=30, source=None):
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=timeout,
+                                   source_address=(source, 0) if source else None)
     try:
         c.request("GET", path)
         r = c.getresponse()
@@ -75,6 +76,18 @@ def service(tmp_path):
                 time.sleep(0.5)
         else:
             raise AssertionError("service did not come up:\n" + (tmp_path / "serve.log").read_text())
+        # the first /health answer only proves ONE worker is listening: probe from other loopback
+        # source addresses (each its own rate-limit key, and a different SO_REUSEPORT hash) until
+        # every worker has answered
+        seen, i = set(), 10
+        while len(seen) < 3 and time.time() < deadline + 60:
+            try:
+                st, w, _ = _get(port, "/health", timeout=5, source="127.0.0.%d" % i)
+                if st == 200:
+                    seen.add(w)
+            except OSError:
+                time.sleep(0.2)
+            i = 10 + (i - 9) % 200
         yield port, p, tmp_path
     finally:
         if p.poll() is None:
