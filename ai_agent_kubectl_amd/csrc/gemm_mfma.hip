@@ -92,11 +92,28 @@ KA_DEV void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int gm, int& tm,
   tn = in / rows;
 }
 
+#ifdef GM_BSTAMPS
+// diagnostic build only (tools/gemm_bench.hip -DGM_BSTAMPS): per-block wall-clock stamps
+// (s_memrealtime, 100 MHz) of wave 0 — 0 start, 1 first stage landed, 2 k-loop done, 3 epilogue
+// issued — stored by all 64 lanes (vector stores) to [block][stamp][lane]
+__device__ unsigned long long* g_bstamps;
+#define BSTAMP(i)                                                                                        \
+  do {                                                                                                   \
+    if (tid < 64) {                                                                                      \
+      const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                    \
+      g_bstamps[(((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4 + (i)) * 64 + tid] = t_;              \
+    }                                                                                                    \
+  } while (0)
+#else
+#define BSTAMP(i) do {} while (0)
+#endif
+
 template <class C, int EPI>
 __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
   char* const lds_c = reinterpret_cast<char*>(lds);
   const int tid = threadIdx.x, lane = tid & 63;
+  BSTAMP(0);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave % C::WN, wm = wave / C::WN;
   int tmi, tni;
@@ -193,10 +210,12 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
       wait_vm<0>();
     }
     block_sync();
+    if (t == 0) BSTAMP(1);
     const int tn = t + C::STAGES - 1;
     if (tn < nk) issue(tn % C::STAGES, tn);
     compute(t % C::STAGES);
   }
+  BSTAMP(2);
 
   // epilogue: acc[i][j][r] = C[n = .. + i*16 + 4*grp + r][m = .. + j*16 + r16]
   const int nb = n0 + wn * C::TN * 16 + 4 * grp;
@@ -244,6 +263,7 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
       }
     }
   }
+  BSTAMP(3);
 }
 
 // ---- 256 x 256 ping-pong kernel ----------------------------------------------------------------
@@ -793,6 +813,8 @@ static int launch_w4(const Args& a0, int split, hipStream_t st) {
 //   7: 256 x 256 ping-pong (gemm_pp_kernel), 8 waves in two staggered groups
 //   8-11: 32-deep k-steps (64-B staged rows) in 4-6 stage rings: more bytes in flight per CU for
 //         the latency-bound decode shapes; 12: 128 x 128 with 4 stages of 64
+//   20-25: 64-row weight tiles against the whole decode batch (M <= 256 in one or two tiles):
+//         many small blocks, two per CU where the ring fits 80 KB (20, 22, 24, 25)
 #define GM_CFGS(X)               \
   X(0, 256, 256, 2, 4, 2, 64)    \
   X(1, 256, 256, 4, 2, 2, 64)    \
@@ -805,7 +827,13 @@ static int launch_w4(const Args& a0, int split, hipStream_t st) {
   X(9, 256, 256, 2, 4, 4, 32)    \
   X(10, 128, 256, 2, 4, 6, 32)   \
   X(11, 128, 128, 2, 2, 5, 32)   \
-  X(12, 128, 128, 2, 2, 4, 64)
+  X(12, 128, 128, 2, 2, 4, 64)   \
+  X(20, 64, 256, 1, 4, 2, 64)    \
+  X(21, 64, 256, 1, 8, 3, 64)    \
+  X(22, 64, 256, 1, 4, 4, 32)    \
+  X(23, 64, 256, 1, 4, 6, 32)    \
+  X(24, 64, 128, 1, 2, 3, 64)    \
+  X(25, 64, 128, 1, 2, 4, 64)
 
 template <class C, int EPI>
 static int launch(const Args& a0, int split, hipStream_t st) {

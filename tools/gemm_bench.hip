@@ -3,6 +3,7 @@
 // F.linear uses) in the same process.  No torch: a fresh GPU box runs it in seconds.
 //
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form tools/gemm_bench.hip \
+//         ai_agent_kubectl_amd/csrc/gemm_skinny.hip \
 //         -lrocblas -o tools/gemm_bench
 //   tools/gemm_bench [cases...]         case = M,N,K,cfg,split,epi[,gm]  (cfg -1 = rocBLAS)
 //
@@ -89,6 +90,12 @@ int main(int argc, char** argv) {
   const size_t nst = (size_t)8 * gm::STAMPS_PER_WAVE * 64;
   CK(hipMalloc(&dst_, nst * 8));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(gm::g_stamps), &dst_, sizeof(dst_)));
+#endif
+#ifdef GM_BSTAMPS
+  unsigned long long* bst_;
+  const size_t nbst = (size_t)65536 * 4 * 64;   // up to 65536 blocks
+  CK(hipMalloc(&bst_, nbst * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(gm::g_bstamps), &bst_, sizeof(bst_)));
 #endif
 
   for (auto& cs : cases) {
@@ -198,6 +205,36 @@ int main(int argc, char** argv) {
         }
         printf("\n");
       }
+    }
+#endif
+#ifdef GM_BSTAMPS
+    if (cfg >= 0) {   // per-block timeline of one more launch (ring kernels only record stamps)
+      CK(hipMemset(bst_, 0, nbst * 8));
+      run(1);
+      CK(hipStreamSynchronize(st));
+      std::vector<unsigned long long> h(nbst);
+      CK(hipMemcpy(h.data(), bst_, nbst * 8, hipMemcpyDeviceToHost));
+      std::vector<double> st0, lat, loop, epi_t, end;
+      unsigned long long tmin = ~0ull;
+      for (size_t b = 0; b < 65536; ++b) {
+        const unsigned long long s0 = h[(b * 4 + 0) * 64];
+        if (!s0) continue;
+        tmin = std::min(tmin, s0);
+      }
+      for (size_t b = 0; b < 65536; ++b) {
+        const unsigned long long* v = &h[b * 4 * 64];
+        const unsigned long long s0 = v[0], s1 = v[64], s2 = v[128], s3 = v[192];
+        if (!s0 || !s3) continue;
+        st0.push_back((s0 - tmin) * 0.01);   // us (100 MHz)
+        lat.push_back((s1 - s0) * 0.01);
+        loop.push_back((s2 - s1) * 0.01);
+        epi_t.push_back((s3 - s2) * 0.01);
+        end.push_back((s3 - tmin) * 0.01);
+      }
+      auto q = [](std::vector<double> v, double p) { std::sort(v.begin(), v.end()); return v.empty() ? 0.0 : v[(size_t)(p * (v.size() - 1))]; };
+      printf("  blocks %zu | start p50 %.2f max %.2f | first-stage p50 %.2f p90 %.2f | k-loop p50 %.2f p90 %.2f | "
+             "epilogue p50 %.2f | end p50 %.2f max %.2f (us)\n", st0.size(), q(st0, .5), q(st0, 1), q(lat, .5), q(lat, .9),
+             q(loop, .5), q(loop, .9), q(epi_t, .5), q(end, .5), q(end, 1));
     }
 #endif
     printf("M=%5d N=%6d K=%5d cfg=%2d split=%2d epi=%d gm=%d : %8.2f us  %7.1f TF/s  %5.2f TB/s  maxerr %.3g (ref max %.3g)%s\n",
