@@ -49,7 +49,7 @@ struct DecodeFuse {
 
 __device__ __forceinline__ uint2 dq_ld4(const DecodeFuse& f, size_t off) {
   if (f.P == nullptr) return *reinterpret_cast<const uint2*>(f.qkv + off);
-  if (f.pbf16) {   // bf16 slices (gemm_tile p_bf16): summed in fp32
+  if (f.pbf16) {   // bf16 slices (gemm_mfma EPI_P16): summed in fp32
     const bf16_t* pb = reinterpret_cast<const bf16_t*>(f.P);
     uint2 q = *reinterpret_cast<const uint2*>(pb + off);
     f32x4 s = f32x4{lo_f(q.x), hi_f(q.x), lo_f(q.y), hi_f(q.y)};
@@ -312,146 +312,12 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
 }
 
 
-// Decode variant: one WAVE per (sequence, kv head), 4 independent pairs per workgroup.  The wave
-// walks all of its context's 32-token chunks (next chunk's K/V prefetched into registers) with the
-// same online softmax: no cross-wave merge, no workgroup barrier.  Measured slightly slower than
-// the split kernel at B = 256, ctx 120-1024 (26.0 vs 23.1 us at ctx 120), so it is opt-in
-// (KA_DECODE_WAVE_MIN = minimum B * Hkv).
-__global__ __launch_bounds__(256) void paged_decode_wave_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
-                                                                const bf16_t* __restrict__ k_cache,
-                                                                const bf16_t* __restrict__ v_cache,
-                                                                const int* __restrict__ block_tables, int max_blocks,
-                                                                const int* __restrict__ ctx_lens, int batch, int hq,
-                                                                int hkv, float scale_log2) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int pair = blockIdx.x * 4 + wave;
-  if (pair >= batch * hkv) return;            // whole wave exits; no block-level sync below
-  const int b = pair / hkv, h = pair % hkv;
-  const int G = hq / hkv;
-  const int col = lane & 15, grp = lane >> 4;
-  const int ctx = ctx_lens[b];
-  __shared__ __attribute__((aligned(16))) bf16_t p_lds[4][16 * 32];
-  bf16_t* pw = p_lds[wave];
-
-  bf16x8 qf[4];
-  if (col < G) {
-    const bf16_t* qp = q + ((size_t)b * hq + h * G + col) * HD + 8 * grp;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(*reinterpret_cast<const uint4*>(qp + 32 * ks));
-  } else {
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(make_uint4(0, 0, 0, 0));
-  }
-  float m[4], l[4];
-  f32x4 o[8];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    m[r] = -INFINITY;
-    l[r] = 0.f;
-  }
-#pragma unroll
-  for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int* bt = block_tables + (size_t)b * max_blocks;
-  const int nchunks = (ctx + 31) >> 5;
-  const size_t head_stride = (size_t)KBS * HD;
-  // register double buffer: chunk c+1's K and V fragments are loaded before chunk c is computed
-  uint4 kr[2][4], vr[8];
-  auto load_k = [&](int c, uint4 (&kk)[2][4]) {
-    const int t0 = c * 32;
-    const int blk0 = bt[2 * c];
-    const int blk1 = (t0 + 16 < ctx) ? bt[2 * c + 1] : blk0;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const bf16_t* kp = k_cache + ((size_t)(j ? blk1 : blk0) * hkv + h) * head_stride + col * HD + 8 * grp;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) kk[j][ks] = *reinterpret_cast<const uint4*>(kp + 32 * ks);
-    }
-  };
-  auto load_v = [&](int c, uint4 (&vv)[8]) {
-    const int t0 = c * 32;
-    const int blk = (grp >> 1) ? ((t0 + 16 < ctx) ? bt[2 * c + 1] : bt[2 * c]) : bt[2 * c];
-    const bf16_t* vp = v_cache + ((size_t)blk * hkv + h) * head_stride + col * KBS + 8 * (grp & 1);
-#pragma unroll
-    for (int n = 0; n < 8; ++n) vv[n] = *reinterpret_cast<const uint4*>(vp + (size_t)n * 16 * KBS);
-  };
-  if (nchunks > 0) {
-    load_k(0, kr);
-    load_v(0, vr);
-  }
-  for (int c = 0; c < nchunks; ++c) {
-    const int t0 = c * 32;
-    f32x4 s[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) acc = mfma16x16x32(qf[ks], as_bf16x8(kr[j][ks]), acc);
-      s[j] = acc;
-    }
-    uint4 vc[8];
-#pragma unroll
-    for (int n = 0; n < 8; ++n) vc[n] = vr[n];
-    if (c + 1 < nchunks) {   // wave-uniform: issue the next chunk's loads under this chunk's math
-      load_k(c + 1, kr);
-      load_v(c + 1, vr);
-    }
-    float alpha[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float x0 = (t0 + col < ctx) ? s[0][r] * scale_log2 : -INFINITY;
-      float x1 = (t0 + 16 + col < ctx) ? s[1][r] * scale_log2 : -INFINITY;
-      const float mx = row16_max(fmaxf(x0, x1));
-      const float mn = fmaxf(m[r], mx);
-      alpha[r] = exp2f(m[r] - mn);
-      const float p0 = exp2f(x0 - mn), p1 = exp2f(x1 - mn);
-      l[r] = l[r] * alpha[r] + row16_sum(p0 + p1);
-      m[r] = mn;
-      const int prow = 4 * grp + r;
-      const int sw = (prow >> 2) & 3;
-      pw[prow * 32 + ((((col >> 3)) ^ sw) << 3) + (col & 7)] = f2bf(p0);
-      pw[prow * 32 + ((((16 + col) >> 3) ^ sw) << 3) + (col & 7)] = f2bf(p1);
-    }
-#pragma unroll
-    for (int n = 0; n < 8; ++n) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[n][r] *= alpha[r];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const bf16x8 pf = as_bf16x8(*reinterpret_cast<const uint4*>(pw + col * 32 + ((grp ^ ((col >> 2) & 3)) << 3)));
-#pragma unroll
-    for (int n = 0; n < 8; ++n) o[n] = mfma16x16x32(pf, as_bf16x8(vc[n]), o[n]);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-  // o[n][r] = row 4*grp + r, dim n*16 + col; rows >= G are padding
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = 4 * grp + r;
-    if (row < G) {
-      const float inv = l[r] > 0.f ? 1.f / l[r] : 0.f;
-      bf16_t* op = out + ((size_t)b * hq + h * G + row) * HD + col;
-#pragma unroll
-      for (int n = 0; n < 8; ++n) op[n * 16] = f2bf(o[n][r] * inv);
-    }
-  }
-}
-
 extern "C" int ka_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache,
                                const int* block_tables, int max_blocks, const int* ctx_lens, int batch, int hq,
                                int hkv, int head_dim, int block_size, float scale, hipStream_t stream) {
   if (batch <= 0) return 0;
   if (head_dim != HD || block_size != KBS || hq % hkv != 0 || hq / hkv > 16) return (int)hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
-  // the wave kernel measured slower than the split kernel at serving context lengths
-  // (scripts/bench_decode_attn.py): opt-in only
-  static const int wave_min = getenv("KA_DECODE_WAVE_MIN") ? atoi(getenv("KA_DECODE_WAVE_MIN")) : (1 << 30);
-  if (batch * hkv >= wave_min) {
-    hipLaunchKernelGGL(paged_decode_wave_kernel, dim3((batch * hkv + 3) / 4), dim3(256), 0, stream,
-                       static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
-                       static_cast<const bf16_t*>(v_cache), block_tables, max_blocks, ctx_lens, batch, hq, hkv,
-                       scale_log2);
-    KA_CHECK_LAUNCH();
-  }
   hipLaunchKernelGGL(paged_decode_kernel<false>, dim3(hkv, batch), dim3(256), 0, stream, static_cast<bf16_t*>(out),
                      static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
                      static_cast<const bf16_t*>(v_cache), block_tables, max_blocks, ctx_lens, hq, hkv, scale_log2,
@@ -653,165 +519,6 @@ __global__ __launch_bounds__(256, 3) void paged_prefill_kernel(bf16_t* __restric
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Varlen paged prefill, chunk-resident version.  The serving shape is short: ~30 new tokens per
-// sequence over a ~120-token context, so the tile-by-tile register pipeline above pays one loaded
-// latency per 32-token tile and re-stages K/V for every 64-row query tile.  Here a workgroup of NW
-// waves owns NW x 16 query rows (up to 128 = 32 tokens x G=4 heads: one workgroup per (sequence,
-// kv head) at the serving shape) and brings a whole 128-token chunk of K and V^T into LDS in one go
-// by LDS-DMA (`global_load_lds_dwordx4`: 64 x 1 KB wave-instructions, all in flight together,
-// lane-linear images XOR-swizzled on the SOURCE address), one vmcnt(0) + barrier per chunk, then
-// runs the four 32-token tiles of the chunk from LDS with the same MFMA / online-softmax body.
-//   K image:   kc[tok 0..127][16 x 16-B chunks], chunk c of token t at slot c ^ (t & 15);
-//   V^T image: vc[dim 0..127][16 x 16-B chunks of 8 tokens], chunk c of dim r at slot c ^ (r & 15).
-template <int NW>
-__global__ __launch_bounds__(64 * NW, 2) void paged_prefill_chunk_kernel(
-    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_cache,
-    const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int max_blocks,
-    const int* __restrict__ q_starts, const int* __restrict__ ctx_lens, int hq, int hkv, float scale_log2) {
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  constexpr int ROWS = NW * 16;
-  extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
-  uint4* kimg = lds_dyn;                                  // [128][16]  32 KiB
-  uint4* vimg = lds_dyn + 128 * 16;                       // [128][16]  32 KiB
-  bf16_t* pscr = reinterpret_cast<bf16_t*>(lds_dyn + 2 * 128 * 16);   // [NW][16 * 32]
-
-  const int qt = blockIdx.x, h = blockIdx.y, sq = blockIdx.z;
-  const int G = hq / hkv;
-  const int tpt = ROWS / G;  // tokens per tile
-  const int q0 = q_starts[sq];
-  const int qlen = q_starts[sq + 1] - q0;
-  const int tile_tok0 = qt * tpt;
-  if (tile_tok0 >= qlen) return;
-  const int ctx = ctx_lens[sq];
-  const int base_pos = ctx - qlen;
-  const int last_tok = min(tile_tok0 + tpt, qlen) - 1;
-  const int kv_end = base_pos + last_tok + 1;
-  const int nblocks = (ctx + KBS - 1) / KBS;
-  const int* bt = block_tables + (size_t)sq * max_blocks;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int col = lane & 15, grp = lane >> 4;
-  const size_t head_stride = (size_t)KBS * HD;
-
-  bf16x8 qf[4];
-  {
-    const int row = wave * 16 + col;
-    const int tok = tile_tok0 + row / G;
-    const int g = row % G;
-    if (tok < qlen) {
-      const bf16_t* qp = q + ((size_t)(q0 + tok) * hq + h * G + g) * HD + 8 * grp;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(*reinterpret_cast<const uint4*>(qp + 32 * ks));
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(make_uint4(0, 0, 0, 0));
-    }
-  }
-  int qpos[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = wave * 16 + 4 * grp + r;
-    const int tok = tile_tok0 + row / G;
-    qpos[r] = tok < qlen ? base_pos + tok : kv_end - 1;
-  }
-  float m[4], l[4];
-  f32x4 o[8];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    m[r] = -INFINITY;
-    l[r] = 0.f;
-  }
-#pragma unroll
-  for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16_t* pw = pscr + wave * (16 * 32);
-
-  for (int c0 = 0; c0 < kv_end; c0 += 128) {
-    // ---- stage K and V^T of tokens c0 .. c0+127 (64 DMA wave-instructions of 1 KB) ----
-    for (int i = wave; i < 64; i += NW) {
-      if (i < 32) {   // K: 4 tokens x 16 chunks per instruction
-        const int tok = i * 4 + (lane >> 4), slot = lane & 15;
-        const int ch = slot ^ (tok & 15);
-        const int bi = (c0 + tok) >> 4;
-        const int blk = bi < nblocks ? bt[bi] : bt[0];
-        const bf16_t* src = k_cache + ((size_t)blk * hkv + h) * head_stride + ((c0 + tok) & 15) * HD + ch * 8;
-        __builtin_amdgcn_global_load_lds((void*)src, (lds_ptr_t)(kimg + i * 64), 16, 0, 0);
-      } else {        // V^T: 4 dims x 16 chunks (of 8 tokens) per instruction
-        const int dim = (i - 32) * 4 + (lane >> 4), slot = lane & 15;
-        const int ch = slot ^ (dim & 15);
-        const int bi = (c0 + ch * 8) >> 4;
-        const int blk = bi < nblocks ? bt[bi] : bt[0];
-        const bf16_t* src = v_cache + ((size_t)blk * hkv + h) * head_stride + dim * KBS + (ch & 1) * 8;
-        __builtin_amdgcn_global_load_lds((void*)src, (lds_ptr_t)(vimg + (i - 32) * 64), 16, 0, 0);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    const int ntiles = min(4, (kv_end - c0 + 31) >> 5);
-    for (int t = 0; t < ntiles; ++t) {
-      const int t0 = c0 + t * 32;
-      f32x4 sc[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int tok = t * 32 + 16 * j + col;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const uint4 kf = kimg[tok * 16 + ((4 * ks + grp) ^ (tok & 15))];
-          acc = mfma16x16x32(qf[ks], as_bf16x8(kf), acc);
-        }
-        sc[j] = acc;
-      }
-      float alpha[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float x0 = (t0 + col <= qpos[r]) ? sc[0][r] * scale_log2 : -INFINITY;
-        const float x1 = (t0 + 16 + col <= qpos[r]) ? sc[1][r] * scale_log2 : -INFINITY;
-        const float mx = row16_max(fmaxf(x0, x1));
-        const float mn = fmaxf(m[r], mx);
-        alpha[r] = (mn == -INFINITY) ? 1.f : exp2f(m[r] - mn);
-        const float p0 = (mn == -INFINITY) ? 0.f : exp2f(x0 - mn);
-        const float p1 = (mn == -INFINITY) ? 0.f : exp2f(x1 - mn);
-        l[r] = l[r] * alpha[r] + row16_sum(p0 + p1);
-        m[r] = mn;
-        const int prow = 4 * grp + r;
-        const int sw = (prow >> 2) & 3;
-        pw[prow * 32 + (((col >> 3) ^ sw) << 3) + (col & 7)] = f2bf(p0);
-        pw[prow * 32 + ((((16 + col) >> 3) ^ sw) << 3) + (col & 7)] = f2bf(p1);
-      }
-#pragma unroll
-      for (int n = 0; n < 8; ++n) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[n][r] *= alpha[r];
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const bf16x8 pf = as_bf16x8(*reinterpret_cast<const uint4*>(pw + col * 32 + ((grp ^ ((col >> 2) & 3)) << 3)));
-#pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        const int dim = n * 16 + col;
-        const uint4 vf = vimg[dim * 16 + ((t * 4 + grp) ^ (dim & 15))];
-        o[n] = mfma16x16x32(pf, as_bf16x8(vf), o[n]);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // P scratch reads done before the next tile's writes
-    }
-    asm volatile("s_barrier" ::: "memory");   // every wave is done with this chunk's images
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = wave * 16 + 4 * grp + r;
-    const int tok = tile_tok0 + row / G;
-    const int g = row % G;
-    if (tok >= qlen) continue;
-    const float inv = l[r] > 0.f ? 1.f / l[r] : 0.f;
-    bf16_t* op = out + ((size_t)(q0 + tok) * hq + h * G + g) * HD + col;
-#pragma unroll
-    for (int n = 0; n < 8; ++n) op[n * 16] = f2bf(o[n][r] * inv);
-  }
-}
-
-static int g_prefill_chunk = -1;   // -1: from KA_PREFILL_ATTN_CHUNK at first use
-extern "C" void ka_set_prefill_attn_chunk(int on) { g_prefill_chunk = on ? 1 : 0; }
-
 extern "C" int ka_paged_prefill(void* out, const void* q, const void* k_cache, const void* v_cache,
                                 const int* block_tables, int max_blocks, const int* q_starts, const int* ctx_lens,
                                 int num_seqs, int max_q_len, int hq, int hkv, int head_dim, int block_size,
@@ -820,36 +527,6 @@ extern "C" int ka_paged_prefill(void* out, const void* q, const void* k_cache, c
   const int G = hkv > 0 ? hq / hkv : 0;
   if (head_dim != HD || block_size != KBS || hq % hkv != 0 || G > 64 || 64 % G != 0) return (int)hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
-  // chunk-resident kernel: opt-in (KA_PREFILL_ATTN_CHUNK=1).  It wins the isolated microbenchmark
-  // (81 vs 96 us/layer, scripts/bench_prefill_attn.py) but loses inside the real 8k-token prefill
-  // step (137 vs 106 us/layer, scripts/phase_profile.py), where the tile kernel's load/compute
-  // overlap across 32-token tiles matters more than one DMA burst per chunk.
-  if (g_prefill_chunk < 0) g_prefill_chunk = getenv("KA_PREFILL_ATTN_CHUNK") && atoi(getenv("KA_PREFILL_ATTN_CHUNK")) == 1;
-  if (g_prefill_chunk == 1 && G <= 16) {
-    const int nw = max_q_len * G > 64 ? 8 : 4;
-    const int tpt = nw * 16 / G;
-    const int qtiles = (max_q_len + tpt - 1) / tpt;
-    const int lds = 2 * 128 * 16 * 16 + nw * 16 * 32 * 2;
-    static bool attr = false;
-    if (!attr) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&paged_prefill_chunk_kernel<4>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 128 * 16 * 16 + 4 * 16 * 32 * 2);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&paged_prefill_chunk_kernel<8>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 128 * 16 * 16 + 8 * 16 * 32 * 2);
-      attr = true;
-    }
-    if (nw == 8)
-      hipLaunchKernelGGL(paged_prefill_chunk_kernel<8>, dim3(qtiles, hkv, num_seqs), dim3(512), lds, stream,
-                         static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q),
-                         static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), block_tables,
-                         max_blocks, q_starts, ctx_lens, hq, hkv, scale_log2);
-    else
-      hipLaunchKernelGGL(paged_prefill_chunk_kernel<4>, dim3(qtiles, hkv, num_seqs), dim3(256), lds, stream,
-                         static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q),
-                         static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), block_tables,
-                         max_blocks, q_starts, ctx_lens, hq, hkv, scale_log2);
-    KA_CHECK_LAUNCH();
-  }
   const int tpt = 64 / G;
   const int qtiles = (max_q_len + tpt - 1) / tpt;
   hipLaunchKernelGGL(paged_prefill_kernel, dim3(qtiles, hkv, num_seqs), dim3(256), 0, stream,

@@ -73,8 +73,8 @@ KA_DEV bf16x8 as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); 
 #define KA_CHECK_LAUNCH() return (int)hipGetLastError()
 
 // X[m][k] = bf16(silu(GU[m][k]) * GU[m][K + k]) for 8 bf16 lanes — bit-identical to silu_mul_kernel
-// (elementwise.hip), so GEMMs that compute the activation while staging their X operand (gemm_tile
-// SWIGLU, gemv_ring SWIGLU) match the unfused SiLU kernel + GEMM exactly.
+// (elementwise.hip), so GEMMs that compute the activation while staging their X operand (gemv_ring
+// SWIGLU) match the unfused SiLU kernel + GEMM exactly.
 KA_DEV u32x4 swiglu8(u32x4 g, u32x4 u) {
   u32x4 o;
 #pragma unroll

@@ -14,9 +14,9 @@
 // RMSNorm, optionally fused with the residual add:   r = x (+ residual);  residual = r;
 //                                                  out = r * rsqrt(mean(r^2) + eps) * w
 // and optionally with the split-K reduction of the GEMM that produced x: x = bf16(sum_k P[k]) where P
-// holds `split` fp32 partial slabs of [rows, hidden] (gemm_skinny / gemm_tile with no output), so
+// holds `split` fp32 partial slabs of [rows, hidden] (gemm_skinny / gemm_mfma with no output), so
 // the projection's reduce kernel and its bf16 round trip through HBM disappear.
-// PT: element type of the split-K slices P (float, or bf16_t from gemm_tile's p_bf16 mode).
+// PT: element type of the split-K slices P (float, or bf16_t from gemm_mfma EPI_P16).
 template <typename PT>
 KA_DEV void ld_part8(const PT* p, f32x4& s0, f32x4& s1) {
   if constexpr (sizeof(PT) == 4) {

@@ -22,8 +22,7 @@
 //     attention, SiLU) and epilogues: bf16 store, partial slab, SwiGLU (interleaved gate_up rows,
 //     silu(g) * u computed from the accumulators: the [M, 2I] gate_up output never exists).
 // KA_HIPCC_FLAGS: -mllvm -amdgpu-mfma-vgpr-form
-// (accumulators in VGPRs with in-place MFMAs: without it hipcc puts the one-wave-per-SIMD
-// kernels' accumulators in AGPRs with non-tied MFMAs and copies ~200 AGPRs per k-tile)
+// (accumulators in VGPRs with in-place MFMAs; the tables in profiles/r2/ were measured with it)
 #include "common.h"
 
 namespace gm {
@@ -269,204 +268,17 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
 // ---- 256 x 256 ping-pong kernel ----------------------------------------------------------------
 // Eight waves in two groups of four, one wave of each group per SIMD.  Group g computes W rows
 // [128g, 128g + 128) of the tile (its A half-tile is private to it) against X rows [64c, 64c + 64)
-// (c = wave & 3).  A k-tile is four phases; phase p = R_p (ds_read the fragments of quadrant p,
-// issue 2 LDS-DMAs of a future half-tile) | barrier | C_p (16 MFMAs of quadrant p) | barrier.
-// Group 1 runs one barrier behind group 0, so on every SIMD one wave issues MFMAs while its partner
-// reads LDS / issues DMAs (T3/T4 "8-phase" structure, counted vmcnt, raw s_barrier, setprio T5).
-//
-// LDS: 2 buffers x {A0, A1, B0, B1} half-tiles of 128 rows x 128 B (16 KB), XOR-swizzled.
-// Quadrant order (n-half, m-half) per tile: (0,0) (0,1) (1,1) (1,0); reads R_0: A-sub0 + B-sub0,
-// R_1: B-sub1, R_2: A-sub1, R_3: none (B-sub0 is kept in registers).
-// DMA schedule (half-tiles of tile t+1 into buffer (t+1)&1, of tile t+2 into buffer t&1):
-//   R_0: B1(t+1)   R_1: A0(t+1)   R_2: A1(t+1)   R_3: B0(t+2)
-// and the tile-t+1 wait `vmcnt(2)` (all but B0(t+2)) before the barrier that ends group 0's C_3
-// / group 1's R_3.  WAR: a half-tile is refilled only after the last reader group passed the
-// barrier following the C phase that consumed its reads (the analysis is in docs/ARCHITECTURE.md).
+// (c = wave & 3).  Group 1 runs one barrier behind group 0, so on every SIMD one wave issues MFMAs
+// while its partner reads LDS / issues DMAs (T3/T4 structure, counted vmcnt, raw s_barrier, setprio
+// T5).  LDS: 2 buffers x {A0, A1, B0, B1} half-tiles of 128 rows x 128 B (16 KB), XOR-swizzled.
+// WAR: a half-tile is refilled only after the last reader group passed the barrier following the
+// C phase that consumed its reads (the analysis is in docs/ARCHITECTURE.md).  A 4-phase variant
+// (16 MFMAs per phase) measured slower than this 2-phase one (profiles/r2/gemm_pp_phase_stamps.txt:
+// ~120 cycles of barrier bubble per interval) and was removed.
 struct PP {
   static constexpr int BN = 256, BM = 256, NT = 512;
   static constexpr int HALF = 16384, BUF = 4 * HALF, LDS = 2 * BUF;
 };
-
-#ifdef GM_STAMPS
-// diagnostic build only (tools/gemm_bench.hip -DGM_STAMPS): shader-clock stamps after every barrier
-// of block 0 for the first STAMP_TILES k-tiles, one row per wave (vector stores, all 64 lanes)
-__device__ unsigned long long* g_stamps;
-constexpr int STAMP_TILES = 16, STAMPS_PER_WAVE = 8 * STAMP_TILES + 4;
-#define STAMP(idx)                                                                                       \
-  do {                                                                                                   \
-    if (blockIdx.x == 0 && blockIdx.z == 0 && (idx) < STAMPS_PER_WAVE) {                                 \
-      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                          \
-      g_stamps[((size_t)w * STAMPS_PER_WAVE + (idx)) * 64 + lane] = t_;                                    \
-    }                                                                                                    \
-  } while (0)
-#else
-#define STAMP(idx) do {} while (0)
-#endif
-
-template <int EPI>
-__global__ __launch_bounds__(512) void gemm_pp_kernel(Args a) {
-  extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
-  char* const L = reinterpret_cast<char*>(lds);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = w >> 2, wc = w & 3;
-  int tmi, tni;
-  tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tmi, tni);
-  const int n0 = tni * PP::BN, m0 = tmi * PP::BM;
-  const int kb = blockIdx.z * a.kps;
-  const int nk = min(a.kps, a.K - kb) / BK;
-
-  // DMA sources: half-tile h (0: W rows 0-127, 1: W rows 128-255, 2: X rows 0-127, 3: X rows
-  // 128-255); this wave's instruction j covers half-tile rows (j*8 + w)*8 + lane/8
-  const int r8 = lane >> 3, slot = lane & 7;
-  uint32_t off[4][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = (j * 8 + w) * 8 + r8;
-    const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
-    off[0][j] = ((uint32_t)min(n0 + row, a.N - 1) * (uint32_t)a.K + kb + ch) * 2u;
-    off[1][j] = ((uint32_t)min(n0 + 128 + row, a.N - 1) * (uint32_t)a.K + kb + ch) * 2u;
-    off[2][j] = ((uint32_t)min(m0 + row, a.M - 1) * (uint32_t)a.ldx + kb + ch) * 2u;
-    off[3][j] = ((uint32_t)min(m0 + 128 + row, a.M - 1) * (uint32_t)a.ldx + kb + ch) * 2u;
-  }
-  const char* Wb = reinterpret_cast<const char*>(a.W);
-  const char* Xb = reinterpret_cast<const char*>(a.X);
-  auto issue = [&](int h, int t) {   // half-tile h of k-tile t into buffer t & 1
-    if (t >= nk) return;
-    const char* src = h < 2 ? Wb : Xb;
-    char* dst = L + (t & 1) * PP::BUF + h * PP::HALF;
-    const uint32_t kofs = (uint32_t)t * (BK * 2);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(src + off[h][j] + kofs, dst + (j * 8 + w) * 1024);
-  };
-
-  const int r16 = lane & 15, grp = lane >> 4, sw = (r16 >> 1) & 7;
-  const int ch0 = ((0 + grp) ^ sw) * 16, ch1 = ((4 + grp) ^ sw) * 16;
-  const int rdA = g * PP::HALF + r16 * 128;                                   // + i*2048 + ch
-  const int rdB = 2 * PP::HALF + (wc >> 1) * PP::HALF + (64 * (wc & 1) + r16) * 128;   // + j*2048 + ch
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
-
-  auto rd = [&](const char* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); };
-  auto read_a = [&](const char* buf, int half) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      fa[i][0] = rd(buf + rdA + (4 * half + i) * 2048 + ch0);
-      fa[i][1] = rd(buf + rdA + (4 * half + i) * 2048 + ch1);
-    }
-  };
-  auto read_b = [&](const char* buf, int half, bf16x8 (&fb)[2][2]) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      fb[j][0] = rd(buf + rdB + (2 * half + j) * 2048 + ch0);
-      fb[j][1] = rd(buf + rdB + (2 * half + j) * 2048 + ch1);
-    }
-  };
-  auto mma = [&](int ah, int bh, const bf16x8 (&fb)[2][2]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 * ah + i][2 * bh + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb[j][kk], acc[4 * ah + i][2 * bh + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  // prologue: tile 0 and B0 of tile 1; wait for tile 0; group 1 then falls one barrier behind
-  issue(0, 0); issue(1, 0); issue(2, 0); issue(3, 0); issue(2, 1);
-  if (nk > 1) wait_vm<2>(); else wait_vm<0>();
-  block_sync();
-  if (g == 1) block_sync();
-
-  STAMP(0);
-  for (int t = 0; t < nk; ++t) {
-    const char* buf = L + (t & 1) * PP::BUF;
-    const bool more = t + 2 < nk;   // B0(t+2) issued this tile: tile t+1's wait leaves it in flight
-    // phase 0: quadrant (0, 0)
-    read_a(buf, 0); read_b(buf, 0, fb0); issue(3, t + 1);
-    block_sync();
-    STAMP(1 + 8 * t);
-    mma(0, 0, fb0);
-    block_sync();
-    STAMP(2 + 8 * t);
-    // phase 1: quadrant (0, 1)
-    read_b(buf, 1, fb1); issue(0, t + 1);
-    block_sync();
-    STAMP(3 + 8 * t);
-    mma(0, 1, fb1);
-    block_sync();
-    STAMP(4 + 8 * t);
-    // phase 2: quadrant (1, 1)
-    read_a(buf, 1); issue(1, t + 1);
-    block_sync();
-    STAMP(5 + 8 * t);
-    mma(1, 1, fb1);
-    block_sync();
-    STAMP(6 + 8 * t);
-    // phase 3: quadrant (1, 0)
-    issue(2, t + 2);
-    if (g == 1) { if (more) wait_vm<2>(); else wait_vm<0>(); }
-    block_sync();
-    STAMP(7 + 8 * t);
-    mma(1, 0, fb0);
-    if (g == 0) { if (more) wait_vm<2>(); else wait_vm<0>(); }
-    block_sync();
-    STAMP(8 + 8 * t);
-  }
-  if (g == 0) block_sync();
-
-  // epilogue (as gemm_kernel): acc[i][j][r] = C[n0 + 128g + 16i + 4grp + r][m0 + 64wc + 16j + r16]
-  const int nb = n0 + 128 * g + 4 * grp;
-  const int mb = m0 + 64 * wc + r16;
-  if constexpr (EPI == EPI_SWIGLU) {
-    const int cb = (n0 + 128 * g) / 2 + 4 * grp;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int c = cb + 16 * p;
-      if (2 * c >= a.N) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = mb + j * 16;
-        if (m >= a.M) continue;
-        const f32x4 gv = acc[2 * p][j], u = acc[2 * p + 1][j];
-        float o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = gv[r] / (1.f + __expf(-gv[r])) * u[r];
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + c) =
-            make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-      }
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int n = nb + i * 16;
-      if (n >= a.N) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = mb + j * 16;
-        if (m >= a.M) continue;
-        const f32x4 v = acc[i][j];
-        if constexpr (EPI == EPI_BF16) {
-          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + n) =
-              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        } else if constexpr (EPI == EPI_P16) {
-          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) =
-              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        } else {
-          *reinterpret_cast<f32x4*>(static_cast<float*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) = v;
-        }
-      }
-    }
-  }
-}
 
 // Two phases per k-tile (32 MFMAs per C phase: the barrier bubble measured by the s_memtime
 // stamps, ~120 cycles per barrier interval, is paid half as often).  Phase a: n-half 0 against
@@ -623,10 +435,10 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
   }
 }
 
-template <int EPI, bool TWO>
+template <int EPI>
 static int launch_pp(const Args& a0, int split, hipStream_t st) {
   static bool attr = false;
-  auto kern = TWO ? &gemm_pp2_kernel<EPI> : &gemm_pp_kernel<EPI>;
+  auto kern = &gemm_pp2_kernel<EPI>;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, PP::LDS);
     attr = true;
@@ -638,202 +450,21 @@ static int launch_pp(const Args& a0, int split, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// ---- one wave per SIMD: 4 waves, big per-wave tiles, software-pipelined fragment reads ---------
-// Measured on MI355X (profiles/pmc_gemm_r2.md): the LDS-staged kernels above keep two waves per
-// SIMD in lockstep behind a barrier per k-step (SQ_WAIT_ANY ~40 % of wave cycles, MFMA busy
-// 51-56 %); rocBLAS' MT256x256 Tensile kernel runs one wave per SIMD and reaches 85 % MFMA busy.
-// This kernel: 2 x 2 waves, each owning TN x TM 16x16 tiles (up to 128 x 128: 256 accumulator
-// registers, AGPRs), two LDS stages filled by LDS-DMA, and the two 32-deep halves (kk) of a k-tile
-// software-pipelined through two fragment register sets:
-//     [MFMA kk0(t) | ds_read kk1(t)]  lgkmcnt(0) vmcnt(0)  barrier  issue DMA(t+2)
-//     [MFMA kk1(t) | ds_read kk0(t+1)]
-// The barrier sits mid-tile, where tile t+1's DMA (issued a full k-tile earlier) has landed and
-// every wave has finished reading tile t, whose buffer the DMA of tile t+2 then refills.
-template <int TN_, int TM_>
-struct W4 {
-  static constexpr int TN = TN_, TM = TM_, BN = 2 * TN * 16, BM = 2 * TM * 16, NT = 256;
-  static constexpr int A_BYTES = BN * 128, B_BYTES = BM * 128, STAGE = A_BYTES + B_BYTES, LDS = 2 * STAGE;
-  static constexpr int GA = A_BYTES / (NT * 16), GB = B_BYTES / (NT * 16);
-  static_assert(GA * NT * 16 == A_BYTES && GB * NT * 16 == B_BYTES, "rows must fill whole DMA waves");
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-};
-
-template <class C, int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(Args a) {
-  extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
-  char* const L = reinterpret_cast<char*>(lds);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = w & 1, wm = w >> 1;
-  int tmi, tni;
-  tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tmi, tni);
-  const int n0 = tni * C::BN, m0 = tmi * C::BM;
-  const int kb = blockIdx.z * a.kps;
-  const int nk = min(a.kps, a.K - kb) / BK;
-
-  const int r8 = lane >> 3, slot = lane & 7;
-  uint32_t offA[C::GA], offB[C::GB];
-#pragma unroll
-  for (int j = 0; j < C::GA; ++j) {
-    const int row = (j * 4 + w) * 8 + r8;
-    offA[j] = ((uint32_t)min(n0 + row, a.N - 1) * (uint32_t)a.K + kb + (uint32_t)(slot ^ ((row >> 1) & 7)) * 8) * 2u;
-  }
-#pragma unroll
-  for (int j = 0; j < C::GB; ++j) {
-    const int row = (j * 4 + w) * 8 + r8;
-    offB[j] = ((uint32_t)min(m0 + row, a.M - 1) * (uint32_t)a.ldx + kb + (uint32_t)(slot ^ ((row >> 1) & 7)) * 8) * 2u;
-  }
-  const char* Wb = reinterpret_cast<const char*>(a.W);
-  const char* Xb = reinterpret_cast<const char*>(a.X);
-  auto issue = [&](int t) {
-    if (t >= nk) return;
-    char* sa = L + (t & 1) * C::STAGE;
-    char* sb = sa + C::A_BYTES;
-    const uint32_t kofs = (uint32_t)t * (BK * 2);
-#pragma unroll
-    for (int j = 0; j < C::GA; ++j) glds16(Wb + offA[j] + kofs, sa + (j * 4 + w) * 1024);
-#pragma unroll
-    for (int j = 0; j < C::GB; ++j) glds16(Xb + offB[j] + kofs, sb + (j * 4 + w) * 1024);
-  };
-
-  const int r16 = lane & 15, grp = lane >> 4, sw = (r16 >> 1) & 7;
-  const int ch0 = ((0 + grp) ^ sw) * 16, ch1 = ((4 + grp) ^ sw) * 16;
-  const int rdA = (wn * C::TN * 16 + r16) * 128, rdB = C::A_BYTES + (wm * C::TM * 16 + r16) * 128;
-
-  f32x4 acc[C::TN][C::TM];
-#pragma unroll
-  for (int i = 0; i < C::TN; ++i)
-#pragma unroll
-    for (int j = 0; j < C::TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 a0[C::TN], b0[C::TM], a1[C::TN], b1[C::TM];
-
-  auto rd = [&](const char* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); };
-  auto read_frags = [&](int t, int ch, bf16x8 (&fa)[C::TN], bf16x8 (&fb)[C::TM]) {
-    const char* s = L + (t & 1) * C::STAGE;
-#pragma unroll
-    for (int i = 0; i < C::TN; ++i) fa[i] = rd(s + rdA + i * 2048 + ch);
-#pragma unroll
-    for (int j = 0; j < C::TM; ++j) fb[j] = rd(s + rdB + j * 2048 + ch);
-  };
-  auto mma = [&](const bf16x8 (&fa)[C::TN], const bf16x8 (&fb)[C::TM]) {
-#pragma unroll
-    for (int i = 0; i < C::TN; ++i)
-#pragma unroll
-      for (int j = 0; j < C::TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-  };
-
-  issue(0);
-  issue(1);
-  if (nk > 1) wait_vm<C::GA + C::GB>(); else wait_vm<0>();
-  block_sync();
-  read_frags(0, ch0, a0, b0);
-  for (int t = 0; t < nk; ++t) {
-    read_frags(t, ch1, a1, b1);
-    mma(a0, b0);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    block_sync();
-    issue(t + 2);
-    if (t + 1 < nk) read_frags(t + 1, ch0, a0, b0);
-    mma(a1, b1);
-  }
-
-  const int nb = n0 + wn * C::TN * 16 + 4 * grp;
-  const int mb = m0 + wm * C::TM * 16 + r16;
-  if constexpr (EPI == EPI_SWIGLU) {
-    static_assert(C::TN % 2 == 0, "SwiGLU epilogue needs gate/up tile pairs");
-    const int cb = (n0 + wn * C::TN * 16) / 2 + 4 * grp;
-#pragma unroll
-    for (int p = 0; p < C::TN / 2; ++p) {
-      const int c = cb + 16 * p;
-      if (2 * c >= a.N) continue;
-#pragma unroll
-      for (int j = 0; j < C::TM; ++j) {
-        const int m = mb + j * 16;
-        if (m >= a.M) continue;
-        const f32x4 gv = acc[2 * p][j], u = acc[2 * p + 1][j];
-        float o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = gv[r] / (1.f + __expf(-gv[r])) * u[r];
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + c) =
-            make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-      }
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < C::TN; ++i) {
-      const int n = nb + i * 16;
-      if (n >= a.N) continue;
-#pragma unroll
-      for (int j = 0; j < C::TM; ++j) {
-        const int m = mb + j * 16;
-        if (m >= a.M) continue;
-        const f32x4 v = acc[i][j];
-        if constexpr (EPI == EPI_BF16) {
-          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + n) =
-              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        } else if constexpr (EPI == EPI_P16) {
-          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) =
-              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        } else {
-          *reinterpret_cast<f32x4*>(static_cast<float*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) = v;
-        }
-      }
-    }
-  }
-}
-
-template <class C, int EPI>
-static int launch_w4(const Args& a0, int split, hipStream_t st) {
-  if constexpr (EPI == EPI_SWIGLU && C::TN % 2 != 0) {
-    return (int)hipErrorInvalidValue;   // gate/up tile pairs need an even TN
-  } else {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_w4_kernel<C, EPI>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    attr = true;
-  }
-  Args a = a0;
-  a.tiles_m = (a.M + C::BM - 1) / C::BM;
-  a.tiles_n = (a.N + C::BN - 1) / C::BN;
-  hipLaunchKernelGGL((gemm_w4_kernel<C, EPI>), dim3(a.tiles_m * a.tiles_n, 1, split), dim3(C::NT), C::LDS, st, a);
-  return (int)hipGetLastError();
-  }
-}
-
 // ---- configurations ------------------------------------------------------------------------------
-// id: (BN x BM, waves WN x WM, stages)
-//   0: 256 x 256, 2 x 4 waves (128 x 64 per wave), 2 stages      (prefill, big M)
-//   1: 256 x 256, 4 x 2 waves ( 64 x 128 per wave), 2 stages
-//   2: 128 x 256, 2 x 4 waves ( 64 x 64 per wave), 3 stages       (decode M = 256, wide N)
+// id: BN x BM tile, WN x WM waves (per-wave tile), ring stages of BK = 64:
+//   2: 128 x 256, 2 x 4 waves (64 x 64), 3 stages                (8 waves, 144 KB: 1 block/CU)
 //   3: 256 x 128, 4 x 2 waves ( 64 x 64), 3 stages
 //   4: 128 x 128, 2 x 2 waves ( 64 x 64), 3 stages                (4 waves, 96 KB: 1 block/CU)
 //   5: 128 x  64, 2 x 1 waves ( 64 x 64), 3 stages                (decode M <= 64)
-//   6: 64 x 256, 1 x 4 waves ( 64 x 64), 3 stages
-//   7: 256 x 256 ping-pong (gemm_pp_kernel), 8 waves in two staggered groups
-//   8-11: 32-deep k-steps (64-B staged rows) in 4-6 stage rings: more bytes in flight per CU for
-//         the latency-bound decode shapes; 12: 128 x 128 with 4 stages of 64
-//   20-25: 64-row weight tiles against the whole decode batch (M <= 256 in one or two tiles):
-//         many small blocks, two per CU where the ring fits 80 KB (20, 22, 24, 25)
+//  12: 128 x 128 with 4 stages
+//  19: 256 x 256 2-phase ping-pong (gemm_pp2_kernel), 8 waves in two staggered groups
+// (ids are stable across rounds: the removed configurations' numbers are not reused)
 #define GM_CFGS(X)               \
-  X(0, 256, 256, 2, 4, 2, 64)    \
-  X(1, 256, 256, 4, 2, 2, 64)    \
   X(2, 128, 256, 2, 4, 3, 64)    \
   X(3, 256, 128, 4, 2, 3, 64)    \
   X(4, 128, 128, 2, 2, 3, 64)    \
   X(5, 128, 64, 2, 1, 3, 64)     \
-  X(6, 64, 256, 1, 4, 3, 64)     \
-  X(8, 256, 256, 2, 4, 5, 32)    \
-  X(9, 256, 256, 2, 4, 4, 32)    \
-  X(10, 128, 256, 2, 4, 6, 32)   \
-  X(11, 128, 128, 2, 2, 5, 32)   \
-  X(12, 128, 128, 2, 2, 4, 64)   \
-  X(20, 64, 256, 1, 4, 2, 64)    \
-  X(21, 64, 256, 1, 8, 3, 64)    \
-  X(22, 64, 256, 1, 4, 4, 32)    \
-  X(23, 64, 256, 1, 4, 6, 32)    \
-  X(24, 64, 128, 1, 2, 3, 64)    \
-  X(25, 64, 128, 1, 2, 4, 64)
+  X(12, 128, 128, 2, 2, 4, 64)
 
 template <class C, int EPI>
 static int launch(const Args& a0, int split, hipStream_t st) {
@@ -850,17 +481,9 @@ static int launch(const Args& a0, int split, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// one wave per SIMD (gemm_w4_kernel): id, TN, TM -> tile (2*TN*16) x (2*TM*16)
-#define GM_W4_CFGS(X) X(13, 8, 8) X(14, 8, 4) X(15, 7, 4) X(16, 4, 8) X(17, 4, 4) X(18, 6, 8)
-
 template <int EPI>
 static int dispatch(int cfg, const Args& a, int split, hipStream_t st) {
-  if (cfg == 7) return launch_pp<EPI, false>(a, split, st);
-  if (cfg == 19) return launch_pp<EPI, true>(a, split, st);
-#define W_(id, tn, tm) \
-  if (cfg == id) return launch_w4<W4<tn, tm>, EPI>(a, split, st);
-  GM_W4_CFGS(W_)
-#undef W_
+  if (cfg == 19) return launch_pp<EPI>(a, split, st);
 #define X_(id, bn, bm, wn, wm, s, kt) \
   if (cfg == id) return launch<Cfg<bn, bm, wn, wm, s, kt>, EPI>(a, split, st);
   GM_CFGS(X_)
@@ -871,20 +494,14 @@ static int dispatch(int cfg, const Args& a, int split, hipStream_t st) {
 }  // namespace gm
 
 extern "C" int ka_gm_bn(int cfg) {
-  if (cfg == 7 || cfg == 19) return gm::PP::BN;
-#define W_(id, tn, tm) if (cfg == id) return gm::W4<tn, tm>::BN;
-  GM_W4_CFGS(W_)
-#undef W_
+  if (cfg == 19) return gm::PP::BN;
 #define X_(id, bn, bm, wn, wm, s, kt) if (cfg == id) return bn;
   GM_CFGS(X_)
 #undef X_
   return -1;
 }
 extern "C" int ka_gm_bm(int cfg) {
-  if (cfg == 7 || cfg == 19) return gm::PP::BM;
-#define W_(id, tn, tm) if (cfg == id) return gm::W4<tn, tm>::BM;
-  GM_W4_CFGS(W_)
-#undef W_
+  if (cfg == 19) return gm::PP::BM;
 #define X_(id, bn, bm, wn, wm, s, kt) if (cfg == id) return bm;
   GM_CFGS(X_)
 #undef X_

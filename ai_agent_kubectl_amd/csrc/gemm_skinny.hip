@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(bf16_t* __restrict__
   }
 }
 
-// Y[mn] = sum_k P[k][mn] in bf16 (also used by gemm_tile.hip's split-K path)
+// Y[mn] = sum_k P[k][mn] in bf16 (also gemm_mfma.hip's EPI_P32 path with an output)
 extern "C" void ka_splitk_reduce_launch(bf16_t* Y, const float* P, int split, long mn, hipStream_t stream) {
   long blocks = (mn / 4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;

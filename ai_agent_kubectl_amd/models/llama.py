@@ -118,7 +118,7 @@ class LlamaModel:
             else:
                 # batch <= 4: SiLU·mul computed inside the down GEMV's X staging (ops.swiglu_linear)
                 h = ops.swiglu_linear(ops.linear(x, L["w13"], defer_reduce=True), L["w2"], defer_reduce=fuse,
-                                      tile_fused=False, bf16_partials=self.bf16_partials)
+                                      bf16_partials=self.bf16_partials)
             pending = not combined   # A2: reduced together with the next norm
         if meta.is_decode:   # every row is its sequence's last token (logits_indices = arange)
             return self._reduce_norm(h, self.W["norm"], eps, residual, pending)

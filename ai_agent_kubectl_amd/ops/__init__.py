@@ -154,11 +154,6 @@ def attention_prefill(q, k_cache, v_cache, block_tables, q_starts, ctx_lens, max
     return out
 
 
-def set_prefill_attention_chunk(on: bool) -> None:
-    """Select the chunk-resident prefill attention kernel (opt-in; default: the tile pipeline)."""
-    require().ka_set_prefill_attn_chunk(1 if on else 0)
-
-
 def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float,
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if _ref(q):
@@ -272,20 +267,21 @@ def skinny_split(M: int, N: int, K: int, target_wgs: int = 0) -> int:
     return split
 
 
-# (M, N, K) -> ("skinny", split) | ("tile", split, cfg) | ("gm", split, cfg) | ("blas", 0); filled by
-# ops.autotune at engine start for the decode batch buckets.
+# (M, N, K) -> ("skinny", split) | ("gm", split, cfg) | ("blas", 0); filled by ops.autotune at
+# engine start for the decode batch buckets.
 GEMM_PLAN: dict = {}
-TILE_MAX_M = 512
+TILE_MAX_M = 512      # largest M the autotuner plans for (decode buckets and small mixed steps)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool = False,
            bf16_partials: bool = False):
     """y = x @ w.T (w is [out, in]).  Decode-sized M goes to the hand-written weight-streaming
-    kernel (M <= 256), the LDS-tiled MFMA kernel (M <= 512) or hipBLASLt, whichever the autotuned
-    plan measured fastest for this (M, N, K); other shapes (prefill) go to hipBLASLt via F.linear.
+    kernel (M <= 256, csrc/gemm_skinny.hip), the LDS-DMA MFMA kernel (M <= 512, csrc/gemm_mfma.hip)
+    or hipBLASLt, whichever the autotuned plan measured fastest for this (M, N, K); other shapes
+    (prefill) go to hipBLASLt via F.linear.
     defer_reduce: when the chosen kernel splits K, return its partials as a `SplitK` for a consumer
     that fuses the reduction instead of running the reduce kernel.
-    bf16_partials: with defer_reduce, an LDS-tiled / gemm_mfma plan stores those partials as bf16
+    bf16_partials: with defer_reduce, a gemm_mfma plan stores those partials as bf16
     (half the slab write + read).  Consumers that read bf16 partials (summing them in fp32):
     rmsnorm (O-proj / down, `KA_BF16_PARTIALS`) and the fused decode attention
     decode_attention_rope (QKV, `KA_BF16_QKV_PARTIALS`); RoPE / SiLU need fp32 partials."""
@@ -302,8 +298,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
                 return torch.nn.functional.linear(x, w)
         elif plan[0] == "blas":
             return torch.nn.functional.linear(x, w)
-        elif plan[0] == "tile":
-            return linear_tile(x, w, plan[2], plan[1], defer_reduce, bf16_partials)
         elif plan[0] == "gm":
             return linear_gm(x, w, plan[2], plan[1], defer_reduce, bf16_partials)
         else:
@@ -323,32 +317,16 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
     return y
 
 
-# csrc/gemm_tile.hip configurations (BN x BM tiles; 5-9: W in VGPRs; 10-14: csrc/gemm_stream.hip,
-# deep-prefetch LDS-DMA stages; 15-16: 256 x 256 register-staged tiles; 17-20: two register stages
-# in flight)
-TILE_CFGS = tuple(range(21))
-
-
-def tile_k_quantum(cfg: int) -> int:
-    return 128 if cfg >= 17 else 64 if cfg >= 15 else 32 if cfg >= 10 else 128 if cfg >= 5 else 64
-
-
-GEMV_SWIGLU_MAX_M = 4   # csrc/gemm_skinny.hip GEMV_MAX_M
-
-
-def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, tile_fused: bool = True,
-                  bf16_partials: bool = False):
+def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, bf16_partials: bool = False):
     """y = (silu(gu[:, :I]) * gu[:, I:]) @ w.T — the MLP down projection fed directly by the fused
     gate_up output (a bf16 tensor; a `SplitK` goes through silu_mul's fused reduce).
 
     * M <= 4 (batch-1..4 decode, the model's path): the GEMV computes the activation while staging
       its X slice once per workgroup (ka_gemv_swiglu, bit-identical to SiLU·mul + GEMV): one kernel
       and one launch boundary less per layer;
-    * tile_fused and the autotuned plan for (M, N, I) is an LDS-tiled kernel: the activation is
-      computed inside its X staging (ka_gemm_tile_swiglu).  The model passes tile_fused=False:
-      measured 138 us vs 47 + 6 us unfused at M=256 (Llama-3-8B down), because every one of the
-      N/BN column tiles re-stages X and so recomputes the activation;
-    * otherwise SiLU·mul then `linear`."""
+    * otherwise SiLU·mul then `linear` (an activation computed inside a tiled GEMM's X staging
+      measured 138 us vs 47 + 6 us unfused at M=256, Llama-3-8B down: every one of the N/BN
+      column tiles re-stages X and so recomputes it)."""
     if isinstance(gu, SplitK) or _ref(gu) or not gu.is_contiguous():
         return linear(silu_mul(gu), w, defer_reduce=defer_reduce, bf16_partials=bf16_partials)
     M, I2 = gu.shape
@@ -367,58 +345,12 @@ def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, tile_fused: b
             y = torch.empty((M, N), dtype=gu.dtype, device=gu.device)
             check(lib.ka_gemv_swiglu(_p(y), _p(gu), _p(w), _p(ws), M, N, I, split, _stream()), "gemv_swiglu")
             return y
-    if tile_fused:
-        plan = GEMM_PLAN.get((M, N, I))
-        if plan is not None and plan[0] == "tile" and plan[2] <= 4 and I % 64 == 0 and N % 16 == 0:
-            cfg, split = plan[2], plan[1]
-            lib = require()
-            kps = ((I // split + 63) // 64) * 64
-            split = (I + kps - 1) // kps
-            ws = torch.empty((split, M, N), dtype=torch.float32, device=gu.device) if split > 1 else None
-            if defer_reduce and split > 1:
-                check(lib.ka_gemm_tile_swiglu(None, _p(gu), _p(w), _p(ws), M, N, I, split, cfg, _stream()),
-                      "gemm_tile_swiglu")
-                return SplitK(ws, split)
-            y = torch.empty((M, N), dtype=gu.dtype, device=gu.device)
-            check(lib.ka_gemm_tile_swiglu(_p(y), _p(gu), _p(w), _p(ws), M, N, I, split, cfg, _stream()),
-                  "gemm_tile_swiglu")
-            return y
     return linear(silu_mul(gu), w, defer_reduce=defer_reduce, bf16_partials=bf16_partials)
 
 
-def tile_shape(cfg: int):
-    """(BN, BM) of a gemm_tile configuration."""
-    lib = require()
-    return lib.ka_gemm_tile_bn(cfg), lib.ka_gemm_tile_bm(cfg)
-
-
-def linear_tile(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, defer_reduce: bool = False,
-                bf16_partials: bool = False):
-    """y = x @ w.T through the LDS-tiled MFMA kernel (csrc/gemm_tile.hip), split-K `split`.
-    bf16_partials (with defer_reduce; configurations 0-4 and 15-20): bf16 split-K slices."""
-    M, K = x.shape
-    N = w.shape[0]
-    kq = tile_k_quantum(cfg)
-    if K % kq or N % 16:
-        raise ValueError(f"gemm_tile cfg {cfg} needs K % {kq} == 0 and N % 16 == 0, got N={N} K={K}")
-    lib = require()
-    kps = ((K // split + kq - 1) // kq) * kq
-    split = (K + kps - 1) // kps
-    pb = int(defer_reduce and split > 1 and bf16_partials and not 5 <= cfg < 15)
-    ws = (torch.empty((split, M, N), dtype=torch.bfloat16 if pb else torch.float32, device=x.device)
-          if split > 1 else None)
-    if defer_reduce and split > 1:
-        check(lib.ka_gemm_tile(None, _p(x), _p(w), _p(ws), M, N, K, split, cfg, pb, _stream()), "gemm_tile")
-        return SplitK(ws, split)
-    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
-    check(lib.ka_gemm_tile(_p(y), _p(x), _p(w), _p(ws), M, N, K, split, cfg, 0, _stream()), "gemm_tile")
-    return y
-
-
 # csrc/gemm_mfma.hip configurations (LDS-DMA staged MFMA GEMM family; ka_gm_bn / ka_gm_bm give the
-# tile): 0-6, 12 ring kernels, 7 / 19 the 256 x 256 ping-pong kernels, 8-11 32-deep rings,
-# 13-18 one wave per SIMD
-GM_CFGS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19)
+# tile): 2-5, 12 ring kernels, 19 the 2-phase 256 x 256 ping-pong kernel
+GM_CFGS = (2, 3, 4, 5, 12, 19)
 GM_EPI_BF16, GM_EPI_P32, GM_EPI_P16, GM_EPI_SWIGLU = 0, 1, 2, 3
 
 

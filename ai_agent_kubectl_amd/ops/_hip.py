@@ -36,7 +36,6 @@ _SIGS = {
     "ka_argmax_slices": [I, I],
     "ka_moe_topk": [P, P, P, I, I, I, P],
     "ka_paged_decode": [P, P, P, P, P, I, P, I, I, I, I, I, F, P],
-    "ka_set_prefill_attn_chunk": [I],
     "ka_paged_decode_rope": [P, P, P, I, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, P],
     "ka_paged_prefill": [P, P, P, P, P, I, P, P, I, I, I, I, I, I, F, P],
     "ka_gemm_skinny": [P, P, P, P, I, I, I, I, P],
@@ -45,10 +44,6 @@ _SIGS = {
     "ka_rope_kv_splitk": [P, P, P, P, I, P, P, P, I, I, I, I, I, P],
     "ka_silu_mul_splitk": [P, P, I, I, I, P],
     "ka_kv_block_copy": [P, P, P, P, I, I, ctypes.c_long, ctypes.c_long, P],
-    "ka_gemm_tile": [P, P, P, P, I, I, I, I, I, I, P],
-    "ka_gemm_tile_swiglu": [P, P, P, P, I, I, I, I, I, P],
-    "ka_gemm_tile_bm": [I],
-    "ka_gemm_tile_bn": [I],
     "ka_gemm_mfma": [P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "ka_gm_bn": [I],
     "ka_gm_bm": [I],

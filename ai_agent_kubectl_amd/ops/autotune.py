@@ -13,8 +13,7 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from . import (GEMM_PLAN, SKINNY_MAX_M, TILE_CFGS, TILE_MAX_M, gm_shape, linear, linear_gm, linear_tile, rmsnorm,
-               skinny_split, tile_k_quantum, tile_shape)
+from . import GEMM_PLAN, SKINNY_MAX_M, TILE_MAX_M, gm_shape, linear, linear_gm, rmsnorm, skinny_split
 
 logger = logging.getLogger("app.engine")
 
@@ -96,38 +95,10 @@ def tune_linear(groups: Dict[Tuple[int, int], List[torch.Tensor]], Ms: Sequence[
             _tunableop_end()
 
 
-# configurations worth timing on MI355X (bench_gemm_tile.py: the W-in-VGPR variants 5-8 and the
-# 64x128-per-wave cfg 3 never made the top three for the Llama/Mixtral projection shapes; the
-# LDS-DMA stream kernels 10-14 and 256x256 tiles 15-16 never beat the best of these, while the
-# two-stage-prefetch tiles 17/19/20 win QKV / O / down by 3-7 % — profiles/gemm_stream_vs_tile_*.txt)
-TUNE_CFGS = (0, 1, 2, 4, 9, 17, 19, 20)
-
-
-def tile_candidates(M: int, N: int, K: int, cfgs: Sequence[int] = ()):
-    """(cfg, split) pairs of the LDS-tiled kernel worth timing for this shape: tiles no taller than
-    twice M, split-K so that the grid lands between ~1/2 and ~4 waves of workgroups on 256 CUs."""
-    out = []
-    if M < 48 or K % 32 or N % 16:
-        return out
-    for cfg in cfgs or TUNE_CFGS:
-        bn, bm = tile_shape(cfg)
-        if bm > 2 * M and bm > 128:
-            continue
-        tiles = ((N + bn - 1) // bn) * ((M + bm - 1) // bm)
-        for split in (1, 2, 3, 4, 6, 8, 16):
-            if K % (tile_k_quantum(cfg) * split) or K // split < 256:
-                continue
-            if split > 1 and tiles * split > 1024:
-                continue
-            if tiles * split < 96 and split < 8:
-                continue
-            out.append((cfg, split))
-    return out
-
-
-# csrc/gemm_mfma.hip configurations timed for decode M (profiles/gemm_mfma_r2.md: 128 x 128 and
-# 128 x 64 rings win O / down at M = 64-256; 128 x 256 / 256 x 128 rings and the 2-phase 256 x 256
-# ping-pong at wide N)
+# csrc/gemm_mfma.hip configurations timed for decode M (profiles/r2/autotune_*.txt: 128 x 64 rings
+# win at M = 32-64, 128 x 128 at 96-256, 128 x 256 / 256 x 128 / 4-stage 128 x 128 at 192-256; the
+# configurations that never won — one wave per SIMD, 32-deep rings, 64-row weight tiles, the 4-phase
+# ping-pong — were removed: profiles/r2/gemm_sweep_v*.txt)
 GM_TUNE_CFGS = (2, 3, 4, 5, 12, 19)
 
 
@@ -181,10 +152,6 @@ def _tune(groups, Ms, norm_fed=frozenset(), bf16_partials: bool = True, consumer
                     t = _time(lambda w: norm(linear(x, w, split=sp, defer_reduce=fed)), ws)
                     if t < best[3]:
                         best = ("skinny", sp, 0, t)
-            for cfg, sp in tile_candidates(M, N, K):
-                t = _time(lambda w: norm(linear_tile(x, w, cfg, sp, defer_reduce=fed, bf16_partials=bf16)), ws)
-                if t < best[3]:
-                    best = ("tile", sp, cfg, t)
             for cfg, sp in gm_candidates(M, N, K):
                 t = _time(lambda w: norm(linear_gm(x, w, cfg, sp, defer_reduce=fed, bf16_partials=bf16)), ws)
                 if t < best[3]:

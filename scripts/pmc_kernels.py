@@ -48,6 +48,6 @@ for i in range(8):
 wd = [(torch.randn(4096, 14336, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(3)]
 x256 = torch.randn(256, 14336, device="cuda", dtype=torch.bfloat16)
 for i in range(8):
-    ops.linear_tile(x256, wd[i % 3], 19, 8)
+    ops.linear_gm(x256, wd[i % 3], 4, 8, defer_reduce=True)
 torch.cuda.synchronize()
 print("done", flush=True)

@@ -97,9 +97,9 @@ def test_paged_decode(hq, hkv, ctx_lens):
     close(ops.attention_decode(q, kc, vc, bt, ctx, scale), ref.attention_decode(q, kc, vc, bt, ctx, scale), atol=2e-2)
 
 
-def test_paged_decode_wave_kernel_large_batch():
-    """B * Hkv >= 512 selects the wave-per-(sequence, kv head) kernel: mixed lengths, padding rows
-    (ctx 0 -> zeros) and a long context walked by a single wave."""
+def test_paged_decode_large_batch_mixed_lengths():
+    """80 sequences of mixed lengths, a padding row (ctx 0 -> zeros) and a 1000-token context whose
+    chunks each wave walks in several passes."""
     import random
     rng = random.Random(0)
     S, hq, hkv = 80, 32, 8
@@ -144,7 +144,7 @@ def test_decode_attention_rope_fused(hq, hkv, split):
     pos = (ctx - 1).clamp(min=0)
     cs = ref.rope_cos_sin(4096, d, 5e5, device=DEV)
     width = (hq + 2 * hkv) * d
-    if split:   # split < 0: bf16 partials (gemm_tile p_bf16), summed in fp32 by the prologue
+    if split:   # split < 0: bf16 partials (gemm_mfma EPI_P16), summed in fp32 by the prologue
         sp = abs(split)
         P = torch.randn(sp, S, width, device=DEV)
         qkv = ops.SplitK(P.to(BF) if split < 0 else P, sp)
@@ -167,10 +167,8 @@ def test_decode_attention_rope_fused(hq, hkv, split):
 
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 8)])
 @pytest.mark.parametrize("qlens,ctxs", [([90], [90]), ([7, 1, 33, 20], [71, 130, 33, 84]), ([130, 1], [130, 5])])
-@pytest.mark.parametrize("chunk", [False, True])
-def test_paged_prefill(hq, hkv, qlens, ctxs, chunk):
-    """Both prefill attention kernels: the tile pipeline (default) and the chunk-resident one."""
-    ops.set_prefill_attention_chunk(chunk)
+def test_paged_prefill(hq, hkv, qlens, ctxs):
+    """Varlen paged prefill attention with cached context (prefix hits / chunked prefill)."""
     S = len(qlens)
     kc, vc = _cache(200, hkv)
     bt = _tables(S, ctxs, 200, 16)
@@ -179,10 +177,7 @@ def test_paged_prefill(hq, hkv, qlens, ctxs, chunk):
     starts = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
     ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
     scale = 128 ** -0.5
-    try:
-        got = ops.attention_prefill(q, kc, vc, bt, starts, ctx, max(qlens), scale)
-    finally:
-        ops.set_prefill_attention_chunk(False)
+    got = ops.attention_prefill(q, kc, vc, bt, starts, ctx, max(qlens), scale)
     want = ref.attention_prefill(q, kc, vc, bt, starts, ctx, scale)
     close(got, want, atol=2e-2)
 
@@ -334,7 +329,7 @@ def test_kv_block_copy():
 def test_linear_defer_reduce_roundtrip():
     x = torch.randn(64, 4096, device=DEV, dtype=BF)
     w = (torch.randn(4096, 4096, device=DEV) * 0.02).to(BF)
-    sk = ops.linear_tile(x, w, 2, 4, defer_reduce=True)
+    sk = ops.linear_gm(x, w, 4, 4, defer_reduce=True)
     assert isinstance(sk, ops.SplitK) and sk.split == 4
     close(sk.resolve(), x.float() @ w.float().t(), atol=3e-2, rtol=2e-2)
     sk2 = ops.linear(x, w, split=4, defer_reduce=True)
@@ -342,15 +337,15 @@ def test_linear_defer_reduce_roundtrip():
     close(sk2.resolve(), x.float() @ w.float().t(), atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("cfg", [0, 2, 4, 15, 17])
-def test_gemm_tile_bf16_partials_into_rmsnorm(cfg):
+@pytest.mark.parametrize("cfg", [2, 4, 5, 12, 19])
+def test_gemm_mfma_bf16_partials_into_rmsnorm(cfg):
     """bf16 split-K slices (o_proj / down at decode) -> fused reduce + residual + RMSNorm matches the
     fp32 reference of the whole chain, and the slices themselves are bf16(fp32 slices)."""
     M, N, K = 256, 4096, 4096
     x = torch.randn(M, K, device=DEV, dtype=BF)
     w = (torch.randn(N, K, device=DEV) * 0.02).to(BF)
-    sk32 = ops.linear_tile(x, w, cfg, 4, defer_reduce=True)
-    sk16 = ops.linear_tile(x, w, cfg, 4, defer_reduce=True, bf16_partials=True)
+    sk32 = ops.linear_gm(x, w, cfg, 4, defer_reduce=True)
+    sk16 = ops.linear_gm(x, w, cfg, 4, defer_reduce=True, bf16_partials=True)
     assert sk16.is_bf16 and not sk32.is_bf16 and sk16.split == sk32.split
     assert torch.equal(sk16.P, sk32.P.to(BF))
     with pytest.raises(TypeError):
@@ -364,50 +359,16 @@ def test_gemm_tile_bf16_partials_into_rmsnorm(cfg):
     close(r1, r2, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M", [48, 128, 200, 256, 384, 512])
-@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1040, 512)])
-def test_gemm_tile(M, N, K):
-    """LDS-tiled MFMA GEMM, every configuration, with and without split-K, ragged M and N tiles."""
-    x = torch.randn(M, K, device=DEV, dtype=BF)
-    w = (torch.randn(N, K, device=DEV) * 0.02).to(BF)
-    want = x.float() @ w.float().t()
-    for cfg in ops.TILE_CFGS:
-        for split in (1, 2, 4):
-            got = ops.linear_tile(x, w, cfg, split)
-            close(got, want, atol=3e-2, rtol=2e-2)
-
-
-@pytest.mark.parametrize("M", [48, 256, 300])
-def test_gemm_tile_swiglu_fused_is_exact(M):
-    """down(silu(gate) * up) with the activation computed in the GEMM's X staging is bit-identical to
-    SiLU·mul followed by the same tiled GEMM (same cfg / split-K)."""
-    I, N = 1024, 4096
-    gu = torch.randn(M, 2 * I, device=DEV, dtype=BF)
-    w = (torch.randn(N, I, device=DEV) * 0.02).to(BF)
-    h = ops.silu_mul(gu)
-    for cfg in range(5):
-        for split in (1, 4):
-            want = ops.linear_tile(h, w, cfg, split)
-            ops.GEMM_PLAN[(M, N, I)] = ("tile", split, cfg)
-            try:
-                got = ops.swiglu_linear(gu, w)
-                sk = ops.swiglu_linear(gu, w, defer_reduce=True)
-            finally:
-                ops.GEMM_PLAN.pop((M, N, I))
-            assert torch.equal(got, want), (cfg, split)
-            if split > 1:
-                assert isinstance(sk, ops.SplitK)
-                close(sk.resolve(), want, atol=2e-2)
-    close(want, ref.silu_mul(gu).float() @ w.float().t(), atol=3e-2, rtol=2e-2)
-
-
-def test_gemm_tile_autotune_plan_dispatch():
+def test_gemm_autotune_plan_dispatch():
+    """tune_linear fills GEMM_PLAN for every bucket (skinny / gm / blas) and ops.linear follows it."""
     from ai_agent_kubectl_amd.ops.autotune import tune_linear
     ws = [(torch.randn(6144, 4096, device=DEV) * 0.02).to(BF) for _ in range(3)]
     rep = tune_linear({(6144, 4096): ws}, [1, 64, 256, 320])
     assert set(k[0] for k in rep) == {1, 64, 256, 320}
-    x = torch.randn(320, 4096, device=DEV, dtype=BF)
-    close(ops.linear(x, ws[0]), x.float() @ ws[0].float().t(), atol=3e-2, rtol=2e-2)
+    assert all(v["choice"] in ("skinny", "gm", "blas") for v in rep.values())
+    for M in (1, 64, 256, 320):
+        x = torch.randn(M, 4096, device=DEV, dtype=BF)
+        close(ops.linear(x, ws[0]), x.float() @ ws[0].float().t(), atol=3e-2, rtol=2e-2)
     for key in list(ops.GEMM_PLAN):
         if key[1:] == (6144, 4096):
             ops.GEMM_PLAN.pop(key)
@@ -534,7 +495,7 @@ def test_gemm_mfma_swiglu_epilogue(M):
     g, u = x.float() @ wg.float().t(), x.float() @ wu.float().t()
     want = torch.nn.functional.silu(g) * u
     lib = _hip.require()
-    for cfg in (0, 2, 3, 4, 7, 13, 14, 19):
+    for cfg in ops.GM_CFGS:
         y = torch.empty(M, I, device=DEV, dtype=BF)
         _hip.check(lib.ka_gemm_mfma(y.data_ptr(), None, x.data_ptr(), w13i.data_ptr(), M, 2 * I, K, K, I, 1, cfg,
                                     ops.GM_EPI_SWIGLU, 0, ops._stream()), "gemm_mfma swiglu")

@@ -85,12 +85,6 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int warm = getenv("GB_WARM") ? atoi(getenv("GB_WARM")) : 0;   // 1: no weight rotation
-#ifdef GM_STAMPS
-  unsigned long long* dst_;
-  const size_t nst = (size_t)8 * gm::STAMPS_PER_WAVE * 64;
-  CK(hipMalloc(&dst_, nst * 8));
-  CK(hipMemcpyToSymbol(HIP_SYMBOL(gm::g_stamps), &dst_, sizeof(dst_)));
-#endif
 #ifdef GM_BSTAMPS
   unsigned long long* bst_;
   const size_t nbst = (size_t)65536 * 4 * 64;   // up to 65536 blocks
@@ -189,24 +183,6 @@ int main(int argc, char** argv) {
     const double us = ms * 1e3 / iters;
     const double tf = 2.0 * M * N * K / (us * 1e-6) / 1e12;
     const double tb = (wbytes + (double)M * K * 2 + (double)M * N * 2) / (us * 1e-6) / 1e12;
-#ifdef GM_STAMPS
-    {
-      CK(hipMemset(dst_, 0, nst * 8));
-      run(0);
-      CK(hipStreamSynchronize(st));
-      std::vector<unsigned long long> h(nst);
-      CK(hipMemcpy(h.data(), dst_, nst * 8, hipMemcpyDeviceToHost));
-      for (int wv = 0; wv < 8; ++wv) {
-        printf("wave %d:", wv);
-        const unsigned long long t0 = h[((size_t)0 * gm::STAMPS_PER_WAVE + 0) * 64];
-        for (int i = 0; i < gm::STAMPS_PER_WAVE; ++i) {
-          const unsigned long long v = h[((size_t)wv * gm::STAMPS_PER_WAVE + i) * 64];
-          if (v) printf(" %lld", (long long)(v - t0));
-        }
-        printf("\n");
-      }
-    }
-#endif
 #ifdef GM_BSTAMPS
     if (cfg >= 0) {   // per-block timeline of one more launch (ring kernels only record stamps)
       CK(hipMemset(bst_, 0, nbst * 8));
