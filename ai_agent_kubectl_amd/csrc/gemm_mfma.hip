@@ -77,6 +77,11 @@ struct Args {
   void* Y;           // EPI_BF16: bf16 [M, ldy]; EPI_SWIGLU: bf16 [M, ldy] (= N / 2 columns)
   void* P;           // EPI_P32 / EPI_P16: [split, M, N]
   int M, N, K, ldx, ldy, kps, tiles_m, tiles_n, gm;
+  // grouped (MoE expert) GEMMs: W is [groups, N, K]; group e owns the output rows
+  // lists[e * lstride + i], i < counts[e], whose X row is lists[..] / src_div
+  const int* counts;
+  const int* lists;
+  int lstride, src_div, groups;
 };
 
 // logical tile -> (m tile, n tile): XCD-contiguous, then GM m-tiles x all n-tiles super-rows
@@ -107,7 +112,11 @@ __device__ unsigned long long* g_bstamps;
 #define BSTAMP(i) do {} while (0)
 #endif
 
-template <class C, int EPI>
+// GROUPED: blockIdx.x = n tile, blockIdx.y = chunk of BM rows over all groups in order (the grid
+// holds ceil(R / BM) + groups chunks, an upper bound computed on the host without reading counts;
+// chunks past the last group's rows exit at once).  X rows are gathered through the row lists by
+// the LDS-DMA source addresses, output rows scattered through them in the epilogue.
+template <class C, int EPI, bool GROUPED = false>
 __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
   char* const lds_c = reinterpret_cast<char*>(lds);
@@ -116,7 +125,25 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave % C::WN, wm = wave / C::WN;
   int tmi, tni;
-  tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tmi, tni);
+  const bf16_t* Wg = a.W;
+  const int* rows_of = nullptr;   // GROUPED: this chunk's output rows
+  int nrows = 0;                  // GROUPED: valid rows in this chunk (may exceed BM: clamped on use)
+  if constexpr (GROUPED) {
+    tni = blockIdx.x;
+    int g = blockIdx.y, e = 0;
+    for (; e < a.groups; ++e) {
+      const int c = (a.counts[e] + C::BM - 1) / C::BM;
+      if (g < c) break;
+      g -= c;
+    }
+    if (e == a.groups) return;    // uniform: the whole block leaves before any LDS / barrier use
+    tmi = g;
+    nrows = a.counts[e] - g * C::BM;
+    rows_of = a.lists + (size_t)e * a.lstride + g * C::BM;
+    Wg = a.W + (size_t)e * a.N * a.K;
+  } else {
+    tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tmi, tni);
+  }
   const int n0 = tni * C::BN, m0 = tmi * C::BM;
   const int kb = blockIdx.z * a.kps;
   const int nk = min(a.kps, a.K - kb) / C::KT;
@@ -135,9 +162,12 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   for (int j = 0; j < C::GB; ++j) {
     const int row = (j * C::NW + wave) * RPI + rl;
     const int ch = swz<C::KT>(row, slot);
-    offB[j] = (uint32_t)(min(m0 + row, a.M - 1) * (uint32_t)a.ldx + kb + ch * 8) * 2u;
+    int src;
+    if constexpr (GROUPED) src = rows_of[min(row, nrows - 1)] / a.src_div;   // padding rows: re-read a real row
+    else src = min(m0 + row, a.M - 1);
+    offB[j] = (uint32_t)(src * (uint32_t)a.ldx + kb + ch * 8) * 2u;
   }
-  const char* Wb = reinterpret_cast<const char*>(a.W);
+  const char* Wb = reinterpret_cast<const char*>(Wg);
   const char* Xb = reinterpret_cast<const char*>(a.X);
 
   auto issue = [&](int stage, int t) {
@@ -223,6 +253,7 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
     // W rows interleaved in 16-row chunks (gate c, up c): tiles 2p / 2p+1 are the gate / up rows of
     // output columns (n0 + wn*TN*16)/2 + 16p + 4*grp + r
     static_assert(C::TN % 2 == 0, "SwiGLU epilogue needs gate/up tile pairs");
+    static_assert(!GROUPED, "grouped GEMMs store bf16 rows or partial slabs");
     const int cb = (n0 + wn * C::TN * 16) / 2 + 4 * grp;
 #pragma unroll
     for (int p = 0; p < C::TN / 2; ++p) {
@@ -241,14 +272,24 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
       }
     }
   } else {
+    int mrow[C::TM];   // output row of accumulator column j (-1: none)
+#pragma unroll
+    for (int j = 0; j < C::TM; ++j) {
+      if constexpr (GROUPED) {
+        const int lr = mb - m0 + j * 16;
+        mrow[j] = lr < nrows && lr < C::BM ? rows_of[lr] : -1;
+      } else {
+        mrow[j] = mb + j * 16 < a.M ? mb + j * 16 : -1;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < C::TN; ++i) {
       const int n = nb + i * 16;
       if (n >= a.N) continue;
 #pragma unroll
       for (int j = 0; j < C::TM; ++j) {
-        const int m = mb + j * 16;
-        if (m >= a.M) continue;
+        const int m = mrow[j];
+        if (m < 0) continue;
         const f32x4 v = acc[i][j];
         if constexpr (EPI == EPI_BF16) {
           *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + n) =
@@ -450,6 +491,21 @@ static int launch_pp(const Args& a0, int split, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+template <class C, int EPI>
+static int launch_grouped(const Args& a0, int split, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<C, EPI, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  Args a = a0;
+  a.tiles_n = (a.N + C::BN - 1) / C::BN;
+  const int chunks = (a.M + C::BM - 1) / C::BM + a.groups;
+  hipLaunchKernelGGL((gemm_kernel<C, EPI, true>), dim3(a.tiles_n, chunks, split), dim3(C::NT), C::LDS, st, a);
+  return (int)hipGetLastError();
+}
+
 // ---- configurations ------------------------------------------------------------------------------
 // id: BN x BM tile, WN x WM waves (per-wave tile), ring stages of BK = 64:
 //   2: 128 x 256, 2 x 4 waves (64 x 64), 3 stages                (8 waves, 144 KB: 1 block/CU)
@@ -489,6 +545,15 @@ static int dispatch(int cfg, const Args& a, int split, hipStream_t st) {
   GM_CFGS(X_)
 #undef X_
   return (int)hipErrorInvalidValue;
+}
+
+template <int EPI>
+static int dispatch_grouped(int cfg, const Args& a, int split, hipStream_t st) {
+#define X_(id, bn, bm, wn, wm, s, kt) \
+  if (cfg == id) return launch_grouped<Cfg<bn, bm, wn, wm, s, kt>, EPI>(a, split, st);
+  GM_CFGS(X_)
+#undef X_
+  return (int)hipErrorInvalidValue;   // the ping-pong kernel has no grouped form
 }
 
 }  // namespace gm
@@ -535,6 +600,28 @@ extern "C" int ka_gemm_mfma(void* Y, void* P, const void* X, const void* W, int 
     }
     case gm::EPI_P16: return gm::dispatch<gm::EPI_P16>(cfg, a, split, stream);
     case gm::EPI_SWIGLU: return gm::dispatch<gm::EPI_SWIGLU>(cfg, a, split, stream);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+// Grouped (MoE expert) GEMM with device-side routing, no host read of the counts:
+//   for e < groups, i < counts[e]: r = lists[e * lstride + i];
+//     Y[r, :] = X[r / src_div, :] @ W[e]^T          (epi 0: bf16 Y [R, ldy])
+//     P[z, r, :] = split-K slice z of it            (epi 1 / 2: fp32 / bf16 slabs [split, R, N])
+// R bounds the row indices (and sizes the launch: ceil(R / BM) + groups row chunks per n tile).
+extern "C" int ka_gemm_mfma_grouped(void* Y, void* P, const void* X, const void* W, const int* counts, const int* lists,
+                                    int lstride, int src_div, int groups, int R, int N, int K, int ldx, int ldy,
+                                    int split, int cfg, int epi, hipStream_t stream) {
+  if (R <= 0 || N <= 0 || groups <= 0) return 0;
+  if (split < 1 || K % (64 * split) != 0 || N % 16 != 0 || ldx % 8 != 0 || src_div < 1 || ka_gm_bn(cfg) < 0)
+    return (int)hipErrorInvalidValue;
+  if (epi == gm::EPI_SWIGLU || (epi == gm::EPI_BF16 && split != 1)) return (int)hipErrorInvalidValue;
+  gm::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), Y, P, R, N, K, ldx, ldy, K / split,
+             0, 0, 8, counts, lists, lstride, src_div, groups};
+  switch (epi) {
+    case gm::EPI_BF16: return gm::dispatch_grouped<gm::EPI_BF16>(cfg, a, split, stream);
+    case gm::EPI_P32: return gm::dispatch_grouped<gm::EPI_P32>(cfg, a, split, stream);
+    case gm::EPI_P16: return gm::dispatch_grouped<gm::EPI_P16>(cfg, a, split, stream);
   }
   return (int)hipErrorInvalidValue;
 }

@@ -20,8 +20,11 @@ Execution shapes:
 * `moe_hip` (decode, T*k <= 512): device-side routing lists, grouped weight-streaming MFMA GEMMs
   over only the routed rows and a weighted combine (csrc/moe.hip) — shape-static, captured in
   the decode hipGraphs, every local expert's weights streamed once per step;
-* `moe_sorted` (prefill / CPU): rows sorted by expert on the device, one host read of the counts
-  per layer, hipBLASLt GEMMs per contiguous expert segment (ragged, eager);
+* `moe_hip_grouped` (prefill on the GPU): the same device-side routing lists feeding the grouped
+  LDS-DMA MFMA GEMM (csrc/gemm_mfma.hip, gathered X rows, scattered output rows) — no host sync,
+  one launch per projection for all local experts;
+* `moe_sorted` (CPU): rows sorted by expert, one host read of the counts per layer, one GEMM per
+  contiguous expert segment;
 * `moe_grouped`: per-expert nonzero() bucketing (one host sync per expert), kept as a reference;
 * `moe_batched`: dense all-experts formulation, kept as a second reference.
 """
@@ -113,6 +116,14 @@ def moe_hip(x, L, cfg, ep_rank, ep_size):
     return ops.moe_experts(x, L["w13"], L["w2"], w, ids, ep_rank * el)
 
 
+def moe_hip_grouped(x, L, cfg, ep_rank, ep_size):
+    """Prefill-sized MoE block on the GPU without host syncs (ops.moe_experts_grouped)."""
+    logits = ops.linear(x, L["router"])
+    w, ids = ops.moe_topk(logits, cfg.top_k)
+    el = cfg.num_experts // ep_size
+    return ops.moe_experts_grouped(x, L["w13"], L["w2"], w, ids, ep_rank * el)
+
+
 def _local_experts(xr, er, L, e0):
     """FFN_{er[r]}(xr[r]) for received rows whose expert id er[r] (global) is one of this rank's;
     unweighted (the source applies the router weight).  [R, H] in xr's dtype."""
@@ -120,9 +131,10 @@ def _local_experts(xr, er, L, e0):
     if R == 0:
         return xr.new_zeros((0, xr.shape[1]))
     w13, w2 = L["w13"], L["w2"]
-    if xr.is_cuda and not ops._FORCE_REF and R <= MOE_HIP_MAX_ROWS:
+    if xr.is_cuda and not ops._FORCE_REF:
         ones = torch.ones((R, 1), dtype=torch.float32, device=xr.device)
-        return ops.moe_experts(xr, w13, w2, ones, er.view(R, 1).to(torch.int32), e0)
+        fn = ops.moe_experts if R <= MOE_HIP_MAX_ROWS else ops.moe_experts_grouped
+        return fn(xr, w13, w2, ones, er.view(R, 1).to(torch.int32), e0)
     out = torch.empty_like(xr)
     el = er.long() - e0
     order = torch.argsort(el, stable=True)
@@ -183,6 +195,8 @@ def moe_forward(x, L, cfg, ep_rank, ep_size, is_decode: bool, comm=None):
     if (comm is not None and ep_size > 1 and not is_decode and moe_dispatch_mode() == "a2a"
             and not (x.is_cuda and torch.cuda.is_current_stream_capturing())):
         return moe_alltoall(x, L, cfg, comm), True
-    if x.is_cuda and not ops._FORCE_REF and x.shape[0] * cfg.top_k <= MOE_HIP_MAX_ROWS:
-        return moe_hip(x, L, cfg, ep_rank, ep_size), False
+    if x.is_cuda and not ops._FORCE_REF:
+        if x.shape[0] * cfg.top_k <= MOE_HIP_MAX_ROWS:
+            return moe_hip(x, L, cfg, ep_rank, ep_size), False
+        return moe_hip_grouped(x, L, cfg, ep_rank, ep_size), False
     return moe_sorted(x, L, cfg, ep_rank, ep_size), False

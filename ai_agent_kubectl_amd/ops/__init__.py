@@ -317,6 +317,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
     return y
 
 
+GEMV_SWIGLU_MAX_M = 4   # csrc/gemm_skinny.hip GEMV_MAX_M
+
+
 def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, bf16_partials: bool = False):
     """y = (silu(gu[:, :I]) * gu[:, I:]) @ w.T — the MLP down projection fed directly by the fused
     gate_up output (a bf16 tensor; a `SplitK` goes through silu_mul's fused reduce).
@@ -352,6 +355,8 @@ def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, bf16_partials
 # tile): 2-5, 12 ring kernels, 19 the 2-phase 256 x 256 ping-pong kernel
 GM_CFGS = (2, 3, 4, 5, 12, 19)
 GM_EPI_BF16, GM_EPI_P32, GM_EPI_P16, GM_EPI_SWIGLU = 0, 1, 2, 3
+# grouped (MoE prefill) configuration: 256 weight rows x 128 gathered rows, 3-stage ring
+MOE_GROUPED_CFG = int(os.environ.get("KA_MOE_GROUPED_CFG", "3"))
 
 
 def gm_shape(cfg: int):
@@ -386,6 +391,22 @@ def linear_gm(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, defer_
     check(lib.ka_gemm_mfma(_p(y), _p(ws), _p(x), _p(w), M, N, K, x.stride(0), N, split, cfg, GM_EPI_P32, 0, st),
           "gemm_mfma")
     return y
+
+
+def linear_grouped(x: torch.Tensor, w: torch.Tensor, counts: torch.Tensor, lists: torch.Tensor, rows: int,
+                   src_div: int = 1, cfg: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Y[r] = x[r // src_div] @ w[e].T for every row r listed for group e (lists [G, stride], counts
+    [G], device-side: no host read) through csrc/gemm_mfma.hip's grouped ring kernel.  Y is
+    [rows, N]; rows listed for no group are left unwritten."""
+    G, N, K = w.shape
+    cfg = MOE_GROUPED_CFG if cfg is None else cfg
+    if K % 64 or N % 16 or x.stride(0) % 8:
+        raise ValueError(f"grouped gemm_mfma needs K % 64 == 0 and N % 16 == 0: N={N} K={K}")
+    out = torch.empty((rows, N), dtype=x.dtype, device=x.device) if out is None else out
+    lib = require()
+    check(lib.ka_gemm_mfma_grouped(_p(out), None, _p(x), _p(w), _p(counts), _p(lists), lists.shape[1], src_div, G,
+                                   rows, N, K, x.stride(0), N, 1, cfg, GM_EPI_BF16, _stream()), "gemm_mfma_grouped")
+    return out
 
 
 # ---- Mixtral MoE (K12): device-side routing lists + grouped weight-streaming GEMM + combine ----
@@ -444,6 +465,28 @@ def moe_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: to
               "moe_gemm2")
         check(lib.ka_moe_combine(_p(out), _p(y2), None, 1, _p(topk_w), _p(topk_ids), T, k, H, e0, El, st),
               "moe_combine")
+    return out
+
+
+def moe_experts_grouped(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
+                        topk_ids: torch.Tensor, e0: int) -> torch.Tensor:
+    """Prefill-sized MoE block, device-resident end to end (no host sync): routing lists
+    (moe_align) -> grouped MFMA gate_up GEMM over the gathered token rows -> SiLU·mul -> grouped
+    down GEMM -> weighted combine.  Same contract as `moe_experts`."""
+    lib = require()
+    T, H = x.shape
+    k = topk_ids.shape[1]
+    El, two_i, _ = w13.shape
+    R = T * k
+    st = _stream()
+    counts = torch.empty(El, dtype=torch.int32, device=x.device)
+    lists = torch.empty((El, R), dtype=torch.int32, device=x.device)
+    check(lib.ka_moe_align(_p(counts), _p(lists), _p(topk_ids), R, e0, El, st), "moe_align")
+    y1 = linear_grouped(x, w13, counts, lists, R, src_div=k)          # slot rows of local experts
+    y2 = linear_grouped(silu_mul(y1), w2, counts, lists, R)          # other rows: never read
+    out = torch.empty((T, H), dtype=x.dtype, device=x.device)
+    check(lib.ka_moe_combine(_p(out), _p(y2), None, 1, _p(topk_w), _p(topk_ids), T, k, H, e0, El, st),
+          "moe_combine")
     return out
 
 

@@ -395,7 +395,66 @@ def test_moe_experts_vs_reference(T, e0, el):
     close(got, want, atol=5e-2, rtol=5e-2)
 
 
-@pytest.mark.parametrize("R", [1, 29, 200])
+def _moe_dense_ref(x, w13, w2, tw, tid, e0):
+    """fp32 reference of the local experts' weighted FFN (activation rounded to bf16 like the kernels)."""
+    T, H = x.shape
+    el, two_i, _ = w13.shape
+    I = two_i // 2
+    out = torch.zeros(T, H, device=x.device)
+    for e in range(el):
+        sel = (tid.long() == e0 + e)                      # [T, k]
+        wt = (tw * sel).sum(1)                            # router weight of expert e per token
+        rows = torch.nonzero(sel.any(1)).squeeze(1)
+        if rows.numel() == 0:
+            continue
+        g = x[rows].float() @ w13[e].float().t()
+        a = (torch.nn.functional.silu(g[:, :I]) * g[:, I:]).to(BF).float()
+        out[rows] += wt[rows].unsqueeze(1) * (a @ w2[e].float().t())
+    return out
+
+
+@pytest.mark.parametrize("src_div", [1, 2])
+def test_gemm_mfma_grouped_gather_scatter(src_div):
+    """Grouped ring GEMM: rows gathered through device lists (empty groups, groups larger than a
+    tile, ragged tails), output rows scattered; rows listed for no group stay untouched."""
+    G, N, K, R = 5, 400, 512, 900
+    counts_h = [0, 1, 300, 17, 260]
+    perm = torch.randperm(R)
+    lists = torch.zeros(G, R, dtype=torch.int32)
+    o = 0
+    for e, c in enumerate(counts_h):
+        lists[e, :c] = perm[o:o + c]
+        o += c
+    lists, counts = lists.to(DEV), torch.tensor(counts_h, dtype=torch.int32, device=DEV)
+    x = torch.randn(R // src_div + 1, K, device=DEV, dtype=BF)
+    w = (torch.randn(G, N, K, device=DEV) * 0.05).to(BF)
+    for cfg in [c for c in ops.GM_CFGS if c != 19]:
+        out = torch.full((R, N), 7.0, device=DEV, dtype=BF)
+        ops.linear_grouped(x, w, counts, lists, R, src_div=src_div, cfg=cfg, out=out)
+        for e, c in enumerate(counts_h):
+            r = lists[e, :c].long()
+            if c:
+                close(out[r], x[r // src_div].float() @ w[e].float().t(), atol=3e-2, rtol=2e-2)
+        untouched = perm[o:].to(DEV).long()
+        assert torch.all(out[untouched] == 7.0), cfg
+
+
+@pytest.mark.parametrize("T", [300, 1100])
+@pytest.mark.parametrize("e0,el", [(0, 8), (4, 4)])
+def test_moe_experts_grouped_prefill(T, e0, el):
+    """Prefill-sized MoE block (T * k > MOE_HIP_MAX_ROWS): device routing + grouped MFMA GEMMs ==
+    fp32 reference, and == the decode-path kernels on the same rows."""
+    E, H, I, k = 8, 512, 384, 2
+    x = torch.randn(T, H, device=DEV, dtype=BF)
+    w13 = (torch.randn(el, 2 * I, H, device=DEV) * 0.05).to(BF)
+    w2 = (torch.randn(el, H, I, device=DEV) * 0.05).to(BF)
+    tw, tid = ops.moe_topk(torch.randn(T, E, device=DEV, dtype=BF), k)
+    got = ops.moe_experts_grouped(x, w13, w2, tw, tid, e0)
+    close(got, _moe_dense_ref(x, w13, w2, tw, tid, e0), atol=5e-2, rtol=5e-2)
+    close(got, ops.moe_experts(x, w13, w2, tw, tid, e0), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("R", [1, 29, 200, 700])
 def test_moe_local_experts_received_rows(R):
     """Receive side of the A5 all-to-all (models/moe.py `_local_experts`): rows tagged with a global
     expert id, unweighted FFN of this rank's experts through the HIP grouped GEMMs."""
@@ -452,10 +511,10 @@ def test_gemv_swiglu_fused_is_exact(M, N, I):
     gu = torch.randn(M, 2 * I, device=DEV, dtype=BF)
     w = (torch.randn(N, I, device=DEV) * 0.02).to(BF)
     split = ops.skinny_split(M, N, I, 256)
-    got = ops.swiglu_linear(gu, w, tile_fused=False)
+    got = ops.swiglu_linear(gu, w)
     want = ops.linear(ops.silu_mul(gu), w, split=split)
     assert torch.equal(got, want)
-    parts = ops.swiglu_linear(gu, w, defer_reduce=True, tile_fused=False)
+    parts = ops.swiglu_linear(gu, w, defer_reduce=True)
     if isinstance(parts, ops.SplitK):
         close(parts.resolve(), want, atol=1e-2, rtol=1e-2)
     g = gu.float()
