@@ -96,6 +96,24 @@ KA_DEV void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int gm, int& tm,
   tn = in / rows;
 }
 
+// grouped GEMMs: global row chunk `c` (of BM rows, over all groups in order) -> its group's weights,
+// output-row list and row count; false past the last group's rows
+template <int BM>
+KA_DEV bool group_chunk(const Args& a, int c, const bf16_t*& Wg, const int*& rows_of, int& nrows, int& chunk) {
+  int e = 0;
+  for (; e < a.groups; ++e) {
+    const int n = (a.counts[e] + BM - 1) / BM;
+    if (c < n) break;
+    c -= n;
+  }
+  if (e == a.groups) return false;
+  chunk = c;
+  nrows = a.counts[e] - c * BM;
+  rows_of = a.lists + (size_t)e * a.lstride + c * BM;
+  Wg = a.W + (size_t)e * a.N * a.K;
+  return true;
+}
+
 #ifdef GM_BSTAMPS
 // diagnostic build only (tools/gemm_bench.hip -DGM_BSTAMPS): per-block wall-clock stamps
 // (s_memrealtime, 100 MHz) of wave 0 — 0 start, 1 first stage landed, 2 k-loop done, 3 epilogue
@@ -130,17 +148,8 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   int nrows = 0;                  // GROUPED: valid rows in this chunk (may exceed BM: clamped on use)
   if constexpr (GROUPED) {
     tni = blockIdx.x;
-    int g = blockIdx.y, e = 0;
-    for (; e < a.groups; ++e) {
-      const int c = (a.counts[e] + C::BM - 1) / C::BM;
-      if (g < c) break;
-      g -= c;
-    }
-    if (e == a.groups) return;    // uniform: the whole block leaves before any LDS / barrier use
-    tmi = g;
-    nrows = a.counts[e] - g * C::BM;
-    rows_of = a.lists + (size_t)e * a.lstride + g * C::BM;
-    Wg = a.W + (size_t)e * a.N * a.K;
+    // uniform: a block past the last group's rows leaves before any LDS / barrier use
+    if (!group_chunk<C::BM>(a, blockIdx.y, Wg, rows_of, nrows, tmi)) return;
   } else {
     tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tmi, tni);
   }
@@ -329,7 +338,7 @@ struct PP {
 //   A0 A1 (t+2):  G0 in R_b(t+1) | G1 in R_a(t+1)     (A_g of tile t last read by group g's R_b(t))
 // Waits before the barrier that ends interval 4t+7: G0 (end of C_b(t+1)) vmcnt(0), G1 (end of its
 // R_b(t+1), which issued B(t+3)) vmcnt(4).
-template <int EPI>
+template <int EPI, bool GROUPED = false>
 __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
   char* const L = reinterpret_cast<char*>(lds);
@@ -337,7 +346,15 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = w >> 2, wc = w & 3;
   int tmi, tni;
-  tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tmi, tni);
+  const bf16_t* Wg = a.W;
+  const int* rows_of = nullptr;
+  int nrows = 0;
+  if constexpr (GROUPED) {   // as gemm_kernel's grouped mode
+    tni = blockIdx.x;
+    if (!group_chunk<PP::BM>(a, blockIdx.y, Wg, rows_of, nrows, tmi)) return;
+  } else {
+    tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tmi, tni);
+  }
   const int n0 = tni * PP::BN, m0 = tmi * PP::BM;
   const int kb = blockIdx.z * a.kps;
   const int nk = min(a.kps, a.K - kb) / BK;
@@ -350,10 +367,18 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
     const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
     off[0][j] = ((uint32_t)min(n0 + row, a.N - 1) * (uint32_t)a.K + kb + ch) * 2u;
     off[1][j] = ((uint32_t)min(n0 + 128 + row, a.N - 1) * (uint32_t)a.K + kb + ch) * 2u;
-    off[2][j] = ((uint32_t)min(m0 + row, a.M - 1) * (uint32_t)a.ldx + kb + ch) * 2u;
-    off[3][j] = ((uint32_t)min(m0 + 128 + row, a.M - 1) * (uint32_t)a.ldx + kb + ch) * 2u;
+    uint32_t x0, x1;
+    if constexpr (GROUPED) {
+      x0 = rows_of[min(row, nrows - 1)] / a.src_div;
+      x1 = rows_of[min(128 + row, nrows - 1)] / a.src_div;
+    } else {
+      x0 = min(m0 + row, a.M - 1);
+      x1 = min(m0 + 128 + row, a.M - 1);
+    }
+    off[2][j] = (x0 * (uint32_t)a.ldx + kb + ch) * 2u;
+    off[3][j] = (x1 * (uint32_t)a.ldx + kb + ch) * 2u;
   }
-  const char* Wb = reinterpret_cast<const char*>(a.W);
+  const char* Wb = reinterpret_cast<const char*>(Wg);
   const char* Xb = reinterpret_cast<const char*>(a.X);
   auto issue = [&](int h, int t) {
     if (t >= nk) return;
@@ -435,6 +460,7 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
   const int nb = n0 + 128 * g + 4 * grp;
   const int mb = m0 + 64 * wc + r16;
   if constexpr (EPI == EPI_SWIGLU) {
+    static_assert(!GROUPED, "grouped GEMMs store bf16 rows or partial slabs");
     const int cb = (n0 + 128 * g) / 2 + 4 * grp;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -453,14 +479,24 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
       }
     }
   } else {
+    int mrow[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (GROUPED) {
+        const int lr = mb - m0 + j * 16;
+        mrow[j] = lr < nrows ? rows_of[lr] : -1;
+      } else {
+        mrow[j] = mb + j * 16 < a.M ? mb + j * 16 : -1;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int n = nb + i * 16;
       if (n >= a.N) continue;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int m = mb + j * 16;
-        if (m >= a.M) continue;
+        const int m = mrow[j];
+        if (m < 0) continue;
         const f32x4 v = acc[i][j];
         if constexpr (EPI == EPI_BF16) {
           *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + n) =
@@ -474,6 +510,21 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
       }
     }
   }
+}
+
+template <int EPI>
+static int launch_pp_grouped(const Args& a0, int split, hipStream_t st) {
+  static bool attr = false;
+  auto kern = &gemm_pp2_kernel<EPI, true>;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, PP::LDS);
+    attr = true;
+  }
+  Args a = a0;
+  a.tiles_n = (a.N + PP::BN - 1) / PP::BN;
+  const int chunks = (a.M + PP::BM - 1) / PP::BM + a.groups;
+  hipLaunchKernelGGL(kern, dim3(a.tiles_n, chunks, split), dim3(PP::NT), PP::LDS, st, a);
+  return (int)hipGetLastError();
 }
 
 template <int EPI>
@@ -549,11 +600,12 @@ static int dispatch(int cfg, const Args& a, int split, hipStream_t st) {
 
 template <int EPI>
 static int dispatch_grouped(int cfg, const Args& a, int split, hipStream_t st) {
+  if (cfg == 19) return launch_pp_grouped<EPI>(a, split, st);
 #define X_(id, bn, bm, wn, wm, s, kt) \
   if (cfg == id) return launch_grouped<Cfg<bn, bm, wn, wm, s, kt>, EPI>(a, split, st);
   GM_CFGS(X_)
 #undef X_
-  return (int)hipErrorInvalidValue;   // the ping-pong kernel has no grouped form
+  return (int)hipErrorInvalidValue;
 }
 
 }  // namespace gm

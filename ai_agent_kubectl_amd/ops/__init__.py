@@ -355,8 +355,8 @@ def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, bf16_partials
 # tile): 2-5, 12 ring kernels, 19 the 2-phase 256 x 256 ping-pong kernel
 GM_CFGS = (2, 3, 4, 5, 12, 19)
 GM_EPI_BF16, GM_EPI_P32, GM_EPI_P16, GM_EPI_SWIGLU = 0, 1, 2, 3
-# grouped (MoE prefill) configuration: 256 weight rows x 128 gathered rows, 3-stage ring
-MOE_GROUPED_CFG = int(os.environ.get("KA_MOE_GROUPED_CFG", "3"))
+# grouped (MoE prefill) configuration: the 256 x 256 ping-pong kernel (profiles/r2/bench_moe_prefill.txt)
+MOE_GROUPED_CFG = int(os.environ.get("KA_MOE_GROUPED_CFG", "19"))
 
 
 def gm_shape(cfg: int):
