@@ -514,6 +514,30 @@ def test_scheduler_gathers_a_streaming_burst_when_idle():
     assert not sch2.gathering() and len(sch2.schedule().prefill_seqs) >= 2
 
 
+def test_scheduler_gather_is_short_for_steady_arrivals():
+    """Without a drained burst (open-loop arrivals into an idle engine) the gather window closes
+    after two quiet gaps even while requests keep arriving; after a large batch drains it may run
+    to gather_max_s."""
+    import time
+    sch = Scheduler(BlockManager(256, 16), max_batch=64, max_batched_tokens=4096, gather_max_s=0.1,
+                    gather_quiet_s=0.005)
+    sch.add(_seq(10))
+    t0 = time.perf_counter()
+    while sch.gathering() and time.perf_counter() - t0 < 0.2:
+        sch.add(_seq(10))              # an arrival every ~2 ms keeps the quiet gap from closing
+        time.sleep(0.002)
+    assert time.perf_counter() - t0 < 0.05
+    sch2 = Scheduler(BlockManager(256, 16), max_batch=64, max_batched_tokens=4096, gather_max_s=0.1,
+                     gather_quiet_s=0.005)
+    sch2._idle_since, sch2._drained = time.perf_counter(), 64     # a 64-request wave just drained
+    sch2.add(_seq(10))
+    t0 = time.perf_counter()
+    while sch2.gathering() and time.perf_counter() - t0 < 0.2:
+        sch2.add(_seq(10))
+        time.sleep(0.002)
+    assert time.perf_counter() - t0 > 0.03
+
+
 def test_scheduler_batches_prefills_while_decoding():
     bm = BlockManager(64, 4, enable_prefix_caching=False)
     sch = Scheduler(bm, max_batch=16, max_batched_tokens=1000, prefill_max_wait_s=10.0, hold_steps=0)

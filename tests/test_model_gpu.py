@@ -73,12 +73,14 @@ def test_llama_forward_hip_vs_reference():
 
 @pytest.mark.parametrize("B", [1, 4, 256])
 def test_decode_chain_vs_fp32_reference(B):
-    """The real decode chain — autotuned GEMM plan (tile / gemm_mfma kernels at M = 256 with bf16
-    split-K partials reduced inside the fused RoPE + KV-append + attention kernel and inside the
-    fused residual + RMSNorm, GEMV / skinny kernels at M = 1 / 4), the fused decode attention, the
-    LM head — over 8 decode steps, each step against the same forward through the fp32 torch
+    """The real decode chain — autotuned GEMM plan (gemm_mfma kernels at M = 256 with bf16 split-K
+    partials reduced inside the fused RoPE + KV-append + attention kernel and inside the fused
+    residual + RMSNorm, GEMV / skinny kernels at M = 1 / 4), the fused decode attention, the LM
+    head — over 8 decode steps, each step against the same forward through the fp32 torch
     references (`ops.force_reference`: fp32 GEMMs, reference attention / RoPE / norms) on a copy
-    of the same KV cache.  Hidden states and logits to bf16 tolerance (bf16 partials)."""
+    of the same KV cache.  Hidden states and logits to bf16 tolerance; the same step with fp32
+    split-K partials (KA_BF16_PARTIALS=0, KA_BF16_QKV_PARTIALS=0) gives the error the bf16
+    partials are compared against."""
     from ai_agent_kubectl_amd.engine.sequence import Sequence
     from ai_agent_kubectl_amd.models.llama import AttnMeta
     eng = _engine("llama3-8b-2l", graphs=True, buckets=(1, 4, 256), max_batch=256, kv_cache_tokens=65536)
@@ -88,8 +90,8 @@ def test_decode_chain_vs_fp32_reference(B):
     sch.prefill_max_wait_s = 0.0
     sch.gather_max_s = 0.0
     sch.hold_steps = 0
-    if B >= 48:   # the tile / gemm_mfma plans (and their bf16 partials) are what runs at this size
-        assert any(v[0] in ("tile", "gm") for (m, _, _), v in ops.GEMM_PLAN.items() if m == B), ops.GEMM_PLAN
+    if B >= 48:   # the gemm_mfma plans (and their bf16 partials) are what runs at this size
+        assert any(v[0] == "gm" for (m, _, _), v in ops.GEMM_PLAN.items() if m == B), ops.GEMM_PLAN
     with torch.inference_mode():
         for i in range(B):
             sch.add(Sequence(prompt_ids=be.prompt_ids(QUERIES[i % len(QUERIES)] + f" #{i}"), params=params,
@@ -100,6 +102,9 @@ def test_decode_chain_vs_fp32_reference(B):
             sch.on_step_done(b)
         assert len(sch.running) == B
         worst = 1.0
+        errs = {True: 0.0, False: 0.0}
+        m = r.model
+        flags = (m.bf16_partials, m.bf16_qkv_partials)
         for step in range(8):
             batch = sch.schedule()
             assert batch.is_decode and len(batch.seqs) == B
@@ -112,11 +117,20 @@ def test_decode_chain_vs_fp32_reference(B):
                             logits_indices=r.d_logits_idx[:Bp], is_decode=True)
             ids = r._view("ids", Bp)
             kc, vc = r.k_cache.clone(), r.v_cache.clone()
+            k32, v32 = r.k_cache.clone(), r.v_cache.clone()
             h = r.model.forward(ids, meta, r.k_cache, r.v_cache)
             lg = r.model.logits(h).float()
             with ops.force_reference():
                 h_ref = r.model.forward(ids, meta, kc, vc)
                 lg_ref = r.model.logits(h_ref).float()
+            m.bf16_partials = m.bf16_qkv_partials = False
+            try:
+                lg32 = m.logits(m.forward(ids, meta, k32, v32)).float()
+            finally:
+                m.bf16_partials, m.bf16_qkv_partials = flags
+            errs[True] = max(errs[True], (lg[:B] - lg_ref[:B]).abs().max().item())
+            errs[False] = max(errs[False], (lg32[:B] - lg_ref[:B]).abs().max().item())
+            del k32, v32
             cos = torch.nn.functional.cosine_similarity(lg[:B], lg_ref[:B], dim=-1)
             worst = min(worst, cos.min().item())
             assert cos.min().item() > 0.995, (step, cos.min().item())
@@ -127,7 +141,9 @@ def test_decode_chain_vs_fp32_reference(B):
             tok = r.model.sample(h, r.mask_bits, mask)[:B].tolist()
             eng._apply(batch, tok)
             sch.on_step_done(batch)
-    print(f"B={B}: worst logits cosine over 8 steps {worst:.5f}")
+    print(f"B={B}: worst logits cosine over 8 steps {worst:.5f}; max |logit - fp32 ref|: bf16 partials "
+          f"{errs[True]:.4f}, fp32 partials {errs[False]:.4f}")
+    assert errs[True] <= 2 * errs[False] + 0.05, errs
 
 
 def test_graph_decode_equals_eager():
