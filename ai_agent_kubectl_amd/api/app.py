@@ -253,7 +253,7 @@ class KubectlService:
         except ValueError as ve:
             self.metrics.llm_errors.labels("unsafe").inc()
             logger.error(f"LLM generated unsafe command: {ve}")
-            raise HTTPException(status_code=status.HTTP_422_UNPROCESSABLE_ENTITY,
+            raise HTTPException(status_code=422,
                                 detail=f"LLM generated unsafe command: {ve}")
         except Exception as e:
             self.metrics.llm_errors.labels("error").inc()

@@ -26,6 +26,28 @@
 #define HD 128
 #define KBS 16
 
+// P re-layout scratch (per wave): the softmax probabilities leave the MFMA C layout (lane (col, grp)
+// holds rows 4 grp + r, keys col and 16 + col) and are re-read in the A layout (lane holds row col,
+// keys 8 grp .. 8 grp + 7).  16 rows x PSTR = 40 bf16 (64 B of P + 16 B of padding); 16-B chunk c of
+// row x sits at slot c ^ p_slot_xor(x >> 2).  Neighbouring lanes swap one probability so that every
+// lane stores one dword (even lanes keys col, col + 1; odd lanes keys 15 + col, 16 + col).  With the
+// 80-B stride and this XOR both the stores (2 x 32 lanes on 32 banks) and the ds_read_b128 reads
+// (4 x 16 lanes on 64 banks, MI355X_MICROARCH.md §LDS) are conflict-free — found by exhaustive search
+// over strides and XOR maps; the previous 64-B rows cost 15-20 % extra LDS cycles.
+constexpr int PSTR = 40;
+KA_DEV int p_slot_xor(int q) { return (q ^ (q >> 1)) & 1; }
+KA_DEV void p_store(bf16_t* pw, int prow, int col, float p0, float p1) {
+  const float q0 = dpp_f<0xB1>(p0), q1 = dpp_f<0xB1>(p1);   // lane ^ 1
+  const bool even = (col & 1) == 0;
+  const int key = even ? col : 15 + col;
+  const uint32_t v = even ? pack2(p0, q0) : pack2(q1, p1);
+  const int slot = (key >> 3) ^ p_slot_xor(prow >> 2);
+  *reinterpret_cast<uint32_t*>(pw + prow * PSTR + (slot << 3) + (key & 7)) = v;
+}
+KA_DEV bf16x8 p_load(const bf16_t* pw, int col, int grp) {
+  return as_bf16x8(*reinterpret_cast<const uint4*>(pw + col * PSTR + ((grp ^ p_slot_xor((col >> 2) & 3)) << 3)));
+}
+
 // ------------------------------------------------------------------------------------------------
 // Fused decode step (FUSED = true): the workgroup of (kv head h, sequence b) first does what
 // rope_kv_kernel would do for its slice of the QKV projection (reducing the split-K partials on the
@@ -79,7 +101,7 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
   const int ctx = ctx_lens[b] - (FUSED ? 1 : 0);
 
   __shared__ __attribute__((aligned(16))) float smem[4 * 16 * 2 + 4 * 16 * (HD + 4)];
-  __shared__ __attribute__((aligned(16))) bf16_t p_lds[4][16 * 32];
+  __shared__ __attribute__((aligned(16))) bf16_t p_lds[4][16 * PSTR];
   // fused: new token's value and per-row score (the rotated q rows and k are staged in p_lds)
   __shared__ __attribute__((aligned(16))) float new_lds[FUSED ? HD / 2 + 16 : 4];
   float* sm = smem;                 // [4][16]
@@ -239,10 +261,7 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
       const float p0 = exp2f(x0 - mn), p1 = exp2f(x1 - mn);
       l[r] = l[r] * alpha[r] + row16_sum(p0 + p1);
       m[r] = mn;
-      const int prow = 4 * grp + r;
-      const int sw = (prow >> 2) & 3;
-      pw[prow * 32 + ((((col >> 3)) ^ sw) << 3) + (col & 7)] = f2bf(p0);
-      pw[prow * 32 + ((((16 + col) >> 3) ^ sw) << 3) + (col & 7)] = f2bf(p1);
+      p_store(pw, 4 * grp + r, col, p0, p1);
     }
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
@@ -250,7 +269,7 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
       for (int r = 0; r < 4; ++r) o[n][r] *= alpha[r];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const bf16x8 pf = as_bf16x8(*reinterpret_cast<const uint4*>(pw + col * 32 + ((grp ^ ((col >> 2) & 3)) << 3)));
+    const bf16x8 pf = p_load(pw, col, grp);
 #pragma unroll
     for (int n = 0; n < 8; ++n) o[n] = mfma16x16x32(pf, as_bf16x8(vr[n]), o[n]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // P scratch reads done before next chunk's writes
@@ -352,8 +371,8 @@ extern "C" int ka_paged_decode_rope(void* out, const void* qkv, const float* P, 
 // already in the cache: shared prefix blocks or previous chunks).  Causal within the context.
 struct PrefillSmem {
   uint4 k[32][16];        // [token][16-B chunk ^ (token & 15)]            8 KiB
-  uint4 v[HD][4];         // [dim][16-B chunk ^ ((dim >> 2) & 3)] tokens    8 KiB
-  bf16_t p[4][16 * 32];   // per-wave P scratch                             4 KiB
+  uint4 v[HD][4];         // [dim][16-B chunk ^ (((dim >> 2) & 1) << 1)] tokens 8 KiB
+  bf16_t p[4][16 * PSTR]; // per-wave P scratch (p_store / p_load)         5 KiB
 };
 
 __device__ __forceinline__ void prefill_load_tile(u32x4 (&kreg)[2], u32x4 (&vreg)[2], const bf16_t* __restrict__ k_cache,
@@ -389,7 +408,7 @@ __device__ __forceinline__ void prefill_store_tile(PrefillSmem& s, const u32x4 (
     const int tok = p >> 4, ch = p & 15;
     reinterpret_cast<u32x4*>(s.k[tok])[ch ^ (tok & 15)] = kreg[i];
     const int dim = p >> 2, vc = p & 3;
-    reinterpret_cast<u32x4*>(s.v[dim])[vc ^ ((dim >> 2) & 3)] = vreg[i];
+    reinterpret_cast<u32x4*>(s.v[dim])[vc ^ (((dim >> 2) & 1) << 1)] = vreg[i];
   }
 }
 
@@ -486,10 +505,7 @@ __global__ __launch_bounds__(256, 3) void paged_prefill_kernel(bf16_t* __restric
       const float p1 = (mn == -INFINITY) ? 0.f : exp2f(x1 - mn);
       l[r] = l[r] * alpha[r] + row16_sum(p0 + p1);
       m[r] = mn;
-      const int prow = 4 * grp + r;
-      const int sw = (prow >> 2) & 3;
-      pw[prow * 32 + (((col >> 3) ^ sw) << 3) + (col & 7)] = f2bf(p0);
-      pw[prow * 32 + ((((16 + col) >> 3) ^ sw) << 3) + (col & 7)] = f2bf(p1);
+      p_store(pw, 4 * grp + r, col, p0, p1);
     }
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
@@ -497,11 +513,11 @@ __global__ __launch_bounds__(256, 3) void paged_prefill_kernel(bf16_t* __restric
       for (int r = 0; r < 4; ++r) o[n][r] *= alpha[r];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const bf16x8 pf = as_bf16x8(*reinterpret_cast<const uint4*>(pw + col * 32 + ((grp ^ ((col >> 2) & 3)) << 3)));
+    const bf16x8 pf = p_load(pw, col, grp);
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
       const int dim = n * 16 + col;
-      const uint4 vf = s.v[dim][grp ^ ((dim >> 2) & 3)];
+      const uint4 vf = s.v[dim][grp ^ (((dim >> 2) & 1) << 1)];   // 64-B rows: conflict-free ds_read_b128
       o[n] = mfma16x16x32(pf, as_bf16x8(vf), o[n]);
     }
   }

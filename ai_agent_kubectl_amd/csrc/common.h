@@ -34,33 +34,43 @@ KA_DEV uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
 }
 
-template <typename T>
-KA_DEV T wave_sum(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Cross-lane exchange within a row of 16 lanes by DPP (a VALU operand modifier: no LDS traffic, unlike
+// __shfl_xor, which compiles to ds_bpermute_b32).  Controls (gfx9 DPP): quad_perm [1,0,3,2] = 0xB1,
+// quad_perm [2,3,0,1] = 0x4E, row_half_mirror = 0x141, row_mirror = 0x140.
+template <int CTRL>
+KA_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
 
-template <typename T>
-KA_DEV T wave_max(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
-// reduce over the 16 lanes that share (lane >> 4): the column index of an MFMA 16x16 C tile.
+// reduce over the 16 lanes that share (lane >> 4): the column index of an MFMA 16x16 C tile.  Each
+// step pairs lanes whose partial results are equal sets of the row, so all 16 lanes end with the
+// same (bitwise) value: neighbours, quads, half-rows (mirror within 8), rows (mirror within 16).
 KA_DEV float row16_max(float v) {
-  v = fmaxf(v, __shfl_xor(v, 1, 64));
-  v = fmaxf(v, __shfl_xor(v, 2, 64));
-  v = fmaxf(v, __shfl_xor(v, 4, 64));
-  v = fmaxf(v, __shfl_xor(v, 8, 64));
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
   return v;
 }
 KA_DEV float row16_sum(float v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  return v;
+}
+
+// whole-wave reductions: the 16-lane row by DPP, then the four rows by two lane swaps
+KA_DEV float wave_sum(float v) {
+  v = row16_sum(v);
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+KA_DEV float wave_max(float v) {
+  v = row16_max(v);
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  v = fmaxf(v, __shfl_xor(v, 32, 64));
   return v;
 }
 

@@ -21,7 +21,9 @@ from __future__ import annotations
 import asyncio
 import datetime
 import logging
+import os
 import shlex
+import signal
 import sys
 import time
 from typing import Any, Dict, List
@@ -71,6 +73,14 @@ def _error_result(kind: str, message: str, start_iso: str, start_ts: float, stri
     }
 
 
+def _signal_group(process, sig) -> None:
+    """Signal the child's process group (it was started in its own session)."""
+    try:
+        os.killpg(process.pid, sig)
+    except ProcessLookupError:
+        pass
+
+
 async def execute_command_async(command: str, timeout: float, kubectl_bin: str = "kubectl",
                                 strict_compat: bool = False) -> Dict[str, Any]:
     start_time = utcnow_iso()
@@ -83,8 +93,10 @@ async def execute_command_async(command: str, timeout: float, kubectl_bin: str =
             raise ValueError("invalid_command", "Command does not start with kubectl")
         if kubectl_bin != "kubectl":
             args[0] = kubectl_bin
+        # own process group: a timeout stops kubectl's children too (exec credential plugins),
+        # which would otherwise keep the pipes open after kubectl itself is gone
         process = await asyncio.create_subprocess_exec(
-            *args, stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.PIPE)
+            *args, stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.PIPE, start_new_session=True)
         stdout, stderr = await asyncio.wait_for(process.communicate(), timeout=timeout)
         end_ts = time.time()
         metadata = {
@@ -107,13 +119,16 @@ async def execute_command_async(command: str, timeout: float, kubectl_bin: str =
         return result
     except asyncio.TimeoutError:
         logger.error(f"Command execution timed out after {timeout}s: {command}")
+        # drain the pipes as well as reaping the child (communicate, not wait): the subprocess
+        # transport closes only once both pipes hit EOF, else it outlives the request
         try:
-            process.terminate()
-            await asyncio.wait_for(process.wait(), timeout=2)
+            _signal_group(process, signal.SIGTERM)
+            await asyncio.wait_for(process.communicate(), timeout=2)
         except Exception as kill_err:
-            logger.error(f"Error terminating timed-out process: {kill_err}")
+            logger.error(f"Error terminating timed-out process: {kill_err!r}")
             try:
-                process.kill()
+                _signal_group(process, signal.SIGKILL)
+                await asyncio.wait_for(process.communicate(), timeout=2)
             except Exception:
                 pass
         t = int(timeout) if float(timeout).is_integer() else timeout
