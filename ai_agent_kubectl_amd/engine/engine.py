@@ -212,7 +212,7 @@ class LLMEngine:
                 self._inflight = (batch, self.runner.launch_decode_async(batch), t0)
                 return len(batch.seqs)
             if (self.overlap and not batch.is_decode and len(batch.prefill_seqs) == len(batch.seqs)
-                    and self.runner.can_overlap(len(batch.seqs))):
+                    and self.runner.can_overlap_prefill(len(batch.seqs))):
                 # a pure prefill step: queue the first decode step of the same rows behind it
                 # (input ids copied on the device from the prefill's samples) before reading the
                 # prefill back, so the GPU does not idle while the host applies ~256 prompts

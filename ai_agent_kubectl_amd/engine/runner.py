@@ -86,6 +86,12 @@ class ModelRunner:
         self.d_out = torch.zeros(B, dtype=torch.int32, device=self.device)
         self.h_out = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
         self.d_hdr = torch.zeros(HDR, dtype=torch.int32, device=self.device)
+        self._h_hdrs = [torch.zeros(HDR, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        # TP decode overlap: rank 0 queues step t+1 (header + staging broadcast + graph) before
+        # reading step t back.  Needs collectives that are stream-ordered on the device (RCCL):
+        # with a host-synchronous transport (gloo) the step still works, it just does not overlap.
+        ov = os.environ.get("KA_TP_OVERLAP", "1")
+        self.tp_overlap = tp_size > 1 and (ov == "force" or (ov == "1" and getattr(self.comm, "device_ordered", False)))
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
         self.stats = {"decode_steps": 0, "prefill_steps": 0, "graph_replays": 0, "decode_ms": 0.0,
@@ -209,14 +215,19 @@ class ModelRunner:
                 h[o[name] + B:o[name] + Bp] = val
 
     def can_overlap(self, B: int) -> bool:
-        # (on CPU the "async" launch simply runs synchronously: same code path, testable)
+        """A decode step of B rows can be queued before the previous one is read back.
+        (on CPU the "async" launch simply runs synchronously: same code path, testable)"""
+        return (self.tp_size == 1 or self.tp_overlap) and B <= self.bmax
+
+    def can_overlap_prefill(self, B: int) -> bool:
         return self.tp_size == 1 and B <= self.bmax
 
     @torch.inference_mode()
     def launch_decode_async(self, batch: Batch, chained: bool = False):
-        """Queue one decode step without waiting for it (TP = 1).  chained: `batch` is the step after
-        the one in flight (same sequences, same row order): its input ids are copied on the device
-        from the previous step's sampled tokens.  Returns a handle for `collect`."""
+        """Queue one decode step without waiting for it.  chained: `batch` is the step after the one
+        in flight (same sequences, same row order): its input ids are copied on the device from the
+        previous step's sampled tokens (with TP, on rank 0 before the staging broadcast, so the other
+        ranks receive them; every rank samples the same token).  Returns a handle for `collect`."""
         B = len(batch.seqs)
         i = bisect.bisect_left(self.buckets, B)
         Bp = self.buckets[i] if i < len(self.buckets) else B
@@ -226,6 +237,11 @@ class ModelRunner:
         hs, ho = self._h_stages[k], self._h_outs[k]
         self._pack_decode(batch, Bp, hs.numpy(), ahead=1 if chained else 0)
         n_copy = self._off["bt"] + Bp * self.max_blocks
+        if self.tp_size > 1:   # header from pinned memory: the copy stays asynchronous
+            hh = self._h_hdrs[k]
+            hh.numpy()[:3] = (KIND_DECODE, Bp, n_copy)
+            self.d_hdr.copy_(hh, non_blocking=True)
+            self.comm.broadcast(self.d_hdr, src=0)
         self.d_stage[:n_copy].copy_(hs[:n_copy], non_blocking=True)
         if chained:
             o = self._off["ids"]

@@ -100,6 +100,8 @@ class TorchComm:
         self.group = group
         self.world_size = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        # RCCL collectives are ordered on the device stream (the host does not wait for them)
+        self.device_ordered = dist.get_backend(group) == "nccl"
         self.custom_ar = None  # optional one-shot all-reduce (parallel/custom_allreduce.py)
         self.allreduce_calls = 0
         self.allreduce_bytes = 0

@@ -163,6 +163,30 @@ def test_graph_decode_equals_eager():
     assert outs[0] == outs[1]
 
 
+def test_long_context_chunked_prefill_matches_whole():
+    """A ~5k-token prompt (MAX_MODEL_LEN 8192) prefilled in 1024-token chunks over several mixed
+    steps — each chunk's attention reads the previous chunks from the paged cache — against the
+    whole prompt in one step: last-position logits to bf16 tolerance, greedy tokens identical or
+    parting only at a near-tie (the two runs sum attention over different query tilings)."""
+    from tests.virtual_tp import assert_same_or_near_tie
+    eng = build_engine(EngineOptions(model="llama3-8b-2l", device="cuda", max_batch=4, graph_buckets=(1, 2),
+                                     kv_cache_tokens=32768, max_model_len=8192, max_batched_tokens=8192))
+    be = EngineLLM(eng, max_new_tokens=6, ignore_eos=True)
+    params = SamplingParams(max_new_tokens=6, ignore_eos=True)
+    long_q = " ".join(f"pod-{i} in namespace team-{i % 17} restarted" for i in range(320))
+    prompt = be.prompt_ids(long_q)
+    assert 4000 < len(prompt) < 8000, len(prompt)
+    outs = {}
+    for budget in (8192, 1024):
+        eng.scheduler.max_batched_tokens = budget
+        eng.bm.reset_prefix_cache()
+        steps0 = eng.runner.stats["prefill_steps"]
+        outs[budget] = eng.generate_blocking([prompt], params, forced_prefix=be._forced)[0].output_ids
+        n_prefill = eng.runner.stats["prefill_steps"] - steps0
+        assert n_prefill == -(-(len(prompt) + len(be._forced)) // budget), n_prefill
+    assert_same_or_near_tie(eng, [prompt], [outs[8192]], [outs[1024]])
+
+
 def test_prefix_cache_hit_matches_cold():
     params = SamplingParams(max_new_tokens=8, ignore_eos=True)
     eng = _engine("llama3-8b-2l", graphs=True)

@@ -28,11 +28,11 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, model, q):
+def _rank(rank, world, port, model, q, overlap=False):
     try:
         sys.path.insert(0, ROOT)
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                          MASTER_PORT=str(port), KA_CUSTOM_AR="1")
+                          MASTER_PORT=str(port), KA_CUSTOM_AR="1", KA_TP_OVERLAP="force" if overlap else "0")
         import torch.distributed as dist
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -53,9 +53,25 @@ def _rank(rank, world, port, model, q):
             return
         be = EngineLLM(eng, max_new_tokens=6, ignore_eos=True)
         params = SamplingParams(max_new_tokens=6, ignore_eos=True)
-        seqs = eng.generate_blocking([be.prompt_ids(x) for x in QUERIES], params, forced_prefix=be._forced)
-        replays = eng.runner.stats["graph_replays"]
-        eng.runner.stop_workers()
+        if overlap:   # the threaded engine loop: decode step t+1 queued before step t is read back
+            import threading
+            done = threading.Event()
+            seqs, left = [], [len(QUERIES)]
+
+            def cb(_s):
+                left[0] -= 1
+                if left[0] == 0:
+                    done.set()
+            eng.start()
+            seqs = [eng.submit(be.prompt_ids(x), params, cb, forced_prefix=be._forced) for x in QUERIES]
+            assert done.wait(300)
+            assert eng.chained_steps > 0
+            replays = eng.runner.stats["graph_replays"]
+            eng.shutdown()   # also stops the workers
+        else:
+            seqs = eng.generate_blocking([be.prompt_ids(x) for x in QUERIES], params, forced_prefix=be._forced)
+            replays = eng.runner.stats["graph_replays"]
+            eng.runner.stop_workers()
         comm.custom_ar.check()
         q.put((0, ([s.output_ids for s in seqs], replays), None))
     except Exception:
@@ -63,12 +79,12 @@ def _rank(rank, world, port, model, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-def _run(model, world):
+def _run(model, world, overlap=False):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, model, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, model, q, overlap)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -109,6 +125,20 @@ def test_tp_processes_one_gpu_graphs_oneshot_collectives(world):
     assert replays > 0           # decode ran through the captured graphs (collectives inside)
     # bf16 partial sums over t ranks vs one GEMM: identical tokens, or a divergence only at a
     # near-tie of the TP = 1 model's own logits
+    assert_same_or_near_tie(eng1, prompts, want, got)
+    del eng1
+    torch.cuda.empty_cache()
+
+
+def test_tp_overlapped_decode_matches_tp1():
+    """TP = 4 through the threaded engine with overlapped (chained) decode steps: rank 0 queues the
+    header + staging broadcast + graph of step t+1 before reading step t back, the chained input ids
+    copied on rank 0's device before the broadcast (KA_TP_OVERLAP=force: gloo stands in for RCCL)."""
+    from tests.virtual_tp import assert_same_or_near_tie
+    model = "llama3-70b-2l"
+    eng1, prompts, want = _tp1(model)
+    got, replays = _run(model, 4, overlap=True)
+    assert replays > 0
     assert_same_or_near_tie(eng1, prompts, want, got)
     del eng1
     torch.cuda.empty_cache()
