@@ -186,6 +186,8 @@ class Scheduler:
         # gather_max_s; otherwise (steady arrivals into an idle engine) only for two quiet gaps, so an
         # open-loop stream is not held back (profiles/r2/sched: p50 +10 ms at 900 req/s otherwise)
         burst = self._drained >= self.burst_min and newest - self._idle_since < self.gather_max_s
+        if burst and len(self.waiting) >= self._drained:
+            return False      # as many requests are back as just finished: the whole wave is here
         cap = self.gather_max_s if burst else min(self.gather_max_s, 2 * self.gather_quiet_s)
         if now - max(self.waiting[0].t_arrival, self._idle_since) >= cap:
             return False

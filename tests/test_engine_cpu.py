@@ -536,6 +536,15 @@ def test_scheduler_gather_is_short_for_steady_arrivals():
         sch2.add(_seq(10))
         time.sleep(0.002)
     assert time.perf_counter() - t0 > 0.03
+    # ... but it closes as soon as as many requests are back as just finished
+    sch3 = Scheduler(BlockManager(256, 16), max_batch=64, max_batched_tokens=4096, gather_max_s=10.0,
+                     gather_quiet_s=5.0)
+    sch3._idle_since, sch3._drained = time.perf_counter(), 40
+    for _ in range(39):
+        sch3.add(_seq(10))
+    assert sch3.gathering()
+    sch3.add(_seq(10))
+    assert not sch3.gathering()
 
 
 def test_scheduler_batches_prefills_while_decoding():
