@@ -274,6 +274,29 @@ def service_env(args, C, buckets, local, port, kubectl_dir):
     return env
 
 
+async def scrape_engine_metrics(port):
+    """Engine step / queue-wait histogram sums and counts from the server's /metrics (aggregated
+    over the API workers): the TCP transport's view of the engine (llm_step_seconds{phase},
+    llm_queue_wait_seconds)."""
+    conn = HttpConn("127.0.0.1", port)
+    try:
+        st, body = await conn.request("GET", "/metrics")
+    finally:
+        conn.close()
+    out = {}
+    if st != 200:
+        return out
+    for line in body.decode().splitlines():
+        for name, key in (('llm_step_seconds_sum{phase="decode"}', "decode_sum"),
+                          ('llm_step_seconds_count{phase="decode"}', "decode_count"),
+                          ('llm_step_seconds_sum{phase="prefill"}', "prefill_sum"),
+                          ('llm_step_seconds_count{phase="prefill"}', "prefill_count"),
+                          ("llm_queue_wait_seconds_sum", "qwait_sum"), ("llm_queue_wait_seconds_count", "qwait_count")):
+            if line.startswith(name + " "):
+                out[key] = out.get(key, 0.0) + float(line.rsplit(" ", 1)[1])
+    return out
+
+
 def run_tcp(args, rank, local, world, C, buckets, dist):
     """tcp transport: the production server as a child process + client processes."""
     import multiprocessing as mp
@@ -341,6 +364,7 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
             time.sleep(0.005)
         if world > 1:
             dist.barrier()
+        m0 = asyncio.run(scrape_engine_metrics(port))
         with done.get_lock():
             done.value = 0
         phase.value = 1
@@ -350,6 +374,7 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
             time.sleep(0.001)
         elapsed = time.perf_counter() - t0
         phase.value = 2
+        m1 = asyncio.run(scrape_engine_metrics(port))
         if world > 1:
             dist.barrier()
         lat = {}
@@ -363,7 +388,11 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
             p.join(timeout=30)
         if errors:
             raise RuntimeError("bad replies: %s" % errors[:3])
-        return elapsed, lat, {}, t_build, None
+        d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1}
+        st = {"decode_steps": int(d.get("decode_count", 0)), "decode_ms": d.get("decode_sum", 0.0) * 1e3,
+              "prefill_steps": int(d.get("prefill_count", 0)), "prefill_ms": d.get("prefill_sum", 0.0) * 1e3,
+              "queue_wait_ms_mean": round(d.get("qwait_sum", 0.0) * 1e3 / max(1.0, d.get("qwait_count", 0.0)), 2)}
+        return elapsed, lat, st, t_build, None
     finally:
         if srv.poll() is None:
             os.killpg(srv.pid, 15)
@@ -619,7 +648,13 @@ def main():
             detail.update(api_workers=args.api_workers, client_procs=args.client_procs)
         if args.mix:
             detail["mix"] = {k: {"n": len(v), "p50_ms": pct(v, 0.5), "p99_ms": pct(v, 0.99)} for k, v in lat.items()}
-        if st:
+        if st and args.transport == "tcp":   # from the server's Prometheus histograms
+            detail.update({
+                "decode_steps": st["decode_steps"], "prefill_steps": st["prefill_steps"],
+                "decode_ms_per_step": round(st["decode_ms"] / max(1, st["decode_steps"]), 3),
+                "prefill_ms_per_step": round(st["prefill_ms"] / max(1, st["prefill_steps"]), 3),
+                "queue_wait_ms_mean": st["queue_wait_ms_mean"], "engine_stats_from": "/metrics"})
+        elif st:
             detail.update({
                 "decode_steps": st.get("decode_steps"), "prefill_steps": st.get("prefill_steps"),
                 "decode_ms_per_step": round(st["decode_ms"] / max(1, st["decode_steps"]), 3),

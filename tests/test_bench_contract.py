@@ -65,6 +65,10 @@ def test_bench_tcp_transport():
     assert out["detail"]["transport"] == "tcp" and out["detail"]["api_workers"] == 2
     assert out["value"] == pytest.approx(4 / (out["ms_per_step"] / 1e3), rel=0.02)
     assert out["config"]["seq_len"] > 16
+    # engine view through the server's Prometheus histograms (llm_step_seconds, llm_queue_wait_seconds)
+    d = out["detail"]
+    assert d["engine_stats_from"] == "/metrics" and d["decode_steps"] > 0 and d["prefill_steps"] > 0
+    assert d["decode_ms_per_step"] > 0 and d["queue_wait_ms_mean"] >= 0
 
 
 def test_bench_open_loop_mixed_stream():
