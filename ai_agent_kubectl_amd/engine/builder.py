@@ -85,7 +85,7 @@ def build_engine(opts: EngineOptions, comm=None, metrics=None) -> LLMEngine:
     if dev.type == "cuda":
         free, _total = torch.cuda.mem_get_info(dev)
         budget = int(free * opts.gpu_mem_fraction) - (4 << 30)   # headroom for activations / graphs
-        fit = budget // per_block
+        fit = min(budget // per_block, 1 << 20)   # (16M tokens: more than any batch here can hold)
         want_blocks = max(opts.kv_cache_tokens // opts.block_size, min_blocks) if opts.kv_cache_tokens > 0 else fit
         num_blocks = max(64, min(want_blocks, fit))
     else:

@@ -137,7 +137,25 @@ class ModelRunner:
             # on a synthetic 128-token context (a norm stand-in picked a split plan whose partials
             # then slowed the attention prologue: profiles/phase_profile_c256_qkv_proxy_negative.txt)
             consumers[tuple(m.layers[0]["wqkv"].shape)] = (self._attention_consumer(), m.bf16_qkv_partials)
-        return tune_linear(groups, self.buckets, norm_fed, getattr(self.model, "bf16_partials", False), consumers)
+        bf16 = getattr(self.model, "bf16_partials", False)
+        ctx_of = {nk: ("attn" + ("-bf16" if consumers[nk][1] else "")) if nk in consumers else
+                  ("norm" + ("-bf16" if bf16 else "")) if nk in norm_fed else "plain" for nk in groups}
+        from ..ops import TILE_MAX_M
+        from ..ops.autotune import DEFAULT_PLAN_FILE, load_plan, save_plan
+        wanted = {(M, N, K): ctx_of[(N, K)] for (N, K) in groups for M in set(self.buckets) if M <= TILE_MAX_M}
+        mode = os.environ.get("KA_GEMM_PLAN", "file")
+        path = os.environ.get("KA_GEMM_PLAN_FILE", DEFAULT_PLAN_FILE)
+        Ms = self.buckets
+        if mode == "file":
+            missing = load_plan(path, wanted)
+            if not missing:
+                return {"from": path}
+            Ms = sorted({M for (M, _, _) in missing})
+            groups = {nk: ws for nk, ws in groups.items() if any((M,) + nk in missing for M in Ms)}
+        report = tune_linear(groups, Ms, norm_fed, bf16, consumers)
+        if mode == "write":
+            save_plan(path, report, ctx_of)
+        return report
 
     def _attention_consumer(self, ctx: int = 128):
         """fn(qkv, M): decode_attention_rope over M synthetic sequences of `ctx` cached tokens in

@@ -1,0 +1,27 @@
+"""Tune the decode GEMM plan of a model on this GPU for every batch bucket up to 512 and merge it into
+ai_agent_kubectl_amd/ops/tuned/gemm_plan_mi355x.json (KA_GEMM_PLAN=write), which engines then load at
+start instead of re-timing candidates (ops/autotune.py: persisted plans).
+
+    python scripts/write_gemm_plan.py [model ...]        (default llama3-8b)
+"""
+import os
+import sys
+
+os.environ["KA_GEMM_PLAN"] = "write"
+os.environ.setdefault("KA_AUTOTUNE_ROUNDS", "5")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine  # noqa: E402
+
+BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512)
+for model in sys.argv[1:] or ["llama3-8b"]:
+    eng = build_engine(EngineOptions(model=model, device="cuda", max_batch=512, graph_buckets=BUCKETS,
+                                     kv_cache_tokens=65536, max_model_len=512))
+    rep = eng.runner.autotune()
+    print(model, len(rep), "plan entries", flush=True)
+    for k in sorted(rep):
+        print(" ", k, rep[k], flush=True)
+    del eng
+    torch.cuda.empty_cache()

@@ -689,3 +689,31 @@ def test_moe_sorted_matches_grouped_and_batched():
         c = moe_batched(x, L, cfg, ep_rank, ep_size)
         torch.testing.assert_close(a, b, atol=1e-4, rtol=1e-4)
         torch.testing.assert_close(a, c, atol=1e-4, rtol=1e-4)
+
+
+def test_gemm_plan_file_roundtrip(tmp_path):
+    """Persisted decode GEMM plans (ops/autotune.py): save merges entries keyed by M,N,K,consumer;
+    load fills GEMM_PLAN for what it holds and reports what is missing; the committed MI355X file
+    covers every Llama-3-8B decode bucket up to 512."""
+    from ai_agent_kubectl_amd import ops
+    from ai_agent_kubectl_amd.ops.autotune import DEFAULT_PLAN_FILE, load_plan, save_plan
+    path = str(tmp_path / "plan.json")
+    rep = {(64, 4096, 4096): {"choice": "gm", "split": 8, "cfg": 5, "us": 13.0, "blas_us": 20.0},
+           (256, 28672, 4096): {"choice": "blas", "split": 0, "cfg": 0, "us": 66.0, "blas_us": 66.0}}
+    save_plan(path, rep, {(4096, 4096): "norm-bf16", (28672, 4096): "plain"})
+    saved = dict(ops.GEMM_PLAN)
+    try:
+        missing = load_plan(path, {(64, 4096, 4096): "norm-bf16", (256, 28672, 4096): "plain",
+                                   (128, 28672, 4096): "plain", (64, 4096, 4096 * 2): "plain"})
+        assert missing == {(128, 28672, 4096), (64, 4096, 8192)}
+        assert ops.GEMM_PLAN[(64, 4096, 4096)] == ("gm", 8, 5) and ops.GEMM_PLAN[(256, 28672, 4096)] == ("blas", 0, 0)
+        # a different consumer context is a different entry
+        assert load_plan(path, {(64, 4096, 4096): "plain"}) == {(64, 4096, 4096)}
+        ctx = {(6144, 4096): "attn-bf16", (4096, 4096): "norm-bf16", (28672, 4096): "plain",
+               (4096, 14336): "norm-bf16", (128256, 4096): "plain"}
+        wanted = {(M, N, K): c for (N, K), c in ctx.items()
+                  for M in (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512)}
+        assert load_plan(DEFAULT_PLAN_FILE, wanted) == set()
+    finally:
+        ops.GEMM_PLAN.clear()
+        ops.GEMM_PLAN.update(saved)
