@@ -11,9 +11,25 @@ os.environ["KA_GEMM_PLAN"] = "write"
 os.environ.setdefault("KA_AUTOTUNE_ROUNDS", "5")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+import shutil  # noqa: E402
+import threading  # noqa: E402
+import time  # noqa: E402
+
 import torch  # noqa: E402
 
 from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine  # noqa: E402
+from ai_agent_kubectl_amd.ops.autotune import DEFAULT_PLAN_FILE  # noqa: E402
+
+
+def _heartbeat():   # big models build and tune silently for minutes
+    t0 = time.time()
+    while True:
+        time.sleep(30)
+        print(f"... {time.time() - t0:.0f} s", flush=True)
+
+
+threading.Thread(target=_heartbeat, daemon=True).start()
+COPY_TO = os.environ.get("PLAN_COPY_TO")   # e.g. gpurun_out/tuned: a copy after every model
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512)
 for model in sys.argv[1:] or ["llama3-8b"]:
@@ -21,6 +37,9 @@ for model in sys.argv[1:] or ["llama3-8b"]:
                                      kv_cache_tokens=65536, max_model_len=512))
     rep = eng.runner.autotune()
     print(model, len(rep), "plan entries", flush=True)
+    if COPY_TO:
+        os.makedirs(COPY_TO, exist_ok=True)
+        shutil.copy(DEFAULT_PLAN_FILE, COPY_TO)
     for k in sorted(rep):
         print(" ", k, rep[k], flush=True)
     del eng
