@@ -34,7 +34,7 @@ class EngineOptions:
     tp_size: int = 1
     ep_size: int = 1
     max_batch: int = 256
-    max_batched_tokens: int = 8192
+    max_batched_tokens: int = 4096
     max_model_len: int = 8192      # Llama-3's context; long prompts prefill in chunks
     block_size: int = 16
     kv_cache_tokens: int = 1 << 18  # <= 0: every byte of the GPU_MEM_FRACTION budget

@@ -99,6 +99,9 @@ def parse_args(argv=None):
     ap.add_argument("--concurrency", type=int, default=int(os.environ.get("BENCH_CONCURRENCY", 256)))
     ap.add_argument("--model", default=os.environ.get("BENCH_MODEL", "llama3-8b"))
     ap.add_argument("--max-new-tokens", type=int, default=16)
+    ap.add_argument("--max-batched-tokens", type=int,
+                    default=int(os.environ.get("BENCH_MAX_BATCHED_TOKENS", 4096)),
+                    help="engine token budget per step (prefill chunks + decode rows)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--in-process", action="store_true",
                     help="asgi transport: run the engine in this process (default: its own process on the GPU)")
@@ -264,7 +267,7 @@ def service_env(args, C, buckets, local, port, kubectl_dir):
         "BENCH_DEVICE", f"cuda:{local}"), WORKERS=str(args.api_workers), HOST="127.0.0.1", PORT=str(port),
         RATE_LIMIT="100000000/minute", CACHE_MAXSIZE=str(cache_size(args)), LLM_TIMEOUT="600", LOG_LEVEL="WARNING",
         MAX_BATCH=str(max(C, 1)), MAX_NEW_TOKENS=str(args.max_new_tokens), IGNORE_EOS="0" if args.variable_len else "1",
-        MAX_NUM_BATCHED_TOKENS="16384", HIPGRAPH_BUCKETS=",".join(str(b) for b in buckets),
+        MAX_NUM_BATCHED_TOKENS=str(args.max_batched_tokens), HIPGRAPH_BUCKETS=",".join(str(b) for b in buckets),
         KV_CACHE_TOKENS=os.environ.get("KV_CACHE_TOKENS", str(max(65536, C * 528))),
         MAX_MODEL_LEN=os.environ.get("MAX_MODEL_LEN", "512"), PYTHONPATH=ROOT,
         PATH=kubectl_dir + os.pathsep + os.environ.get("PATH", ""))
@@ -418,7 +421,7 @@ def run_asgi(args, rank, local, world, C, buckets, dist):
     settings = Settings(RATE_LIMIT="100000000/minute", CACHE_MAXSIZE=cache_size(args), LLM_TIMEOUT=600,
                         LOG_LEVEL="WARNING",
                         LLM_BACKEND="engine", MODEL=args.model, MAX_BATCH=max(C, 1), MAX_NEW_TOKENS=args.max_new_tokens,
-                        IGNORE_EOS=not args.variable_len, MAX_NUM_BATCHED_TOKENS=16384,
+                        IGNORE_EOS=not args.variable_len, MAX_NUM_BATCHED_TOKENS=args.max_batched_tokens,
                         HIPGRAPH_BUCKETS=",".join(str(b) for b in buckets))
     os.environ.setdefault("KV_CACHE_TOKENS", str(max(65536, C * 528)))
     os.environ.setdefault("MAX_MODEL_LEN", "512")
@@ -444,7 +447,7 @@ def run_asgi(args, rank, local, world, C, buckets, dist):
         from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM
         opts = EngineOptions(model=args.model, device=str(dev), max_batch=max(C, 1), graph_buckets=buckets,
                              kv_cache_tokens=max(65536, C * 528), max_model_len=512,
-                             use_graphs=not args.no_graphs, ignore_eos=not args.variable_len, max_batched_tokens=16384)
+                             use_graphs=not args.no_graphs, ignore_eos=not args.variable_len, max_batched_tokens=args.max_batched_tokens)
         eng = build_engine(opts)
         eng.runner.capture_graphs()
         backend = EngineLLM(eng, max_new_tokens=args.max_new_tokens, ignore_eos=not args.variable_len)
