@@ -25,8 +25,6 @@
 // (accumulators in VGPRs with in-place MFMAs; the tables in profiles/r2/ were measured with it)
 #include "common.h"
 
-#include <type_traits>
-
 namespace gm {
 
 constexpr int BK = 64;
@@ -559,248 +557,6 @@ static int launch_grouped(const Args& a0, int split, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// ---- direct-weight decode kernel (M <= 256) ----------------------------------------------------
-// Decode GEMMs at M = 128-256 move 2-3x more activation bytes than weight bytes through every CU
-// (each BN-column tile re-reads the whole X panel), and the LDS-DMA ring kernels above are bound by
-// what a CU can keep in flight through LDS (profiles/r2/gemm_decode_analysis.md: 37-55 GB/s per
-// CU, flat in ring depth).  Here only X goes through LDS (one LDS-DMA ring shared by every wave);
-// each wave owns TN 16-row weight tiles and loads its W fragments straight from global memory
-// into VGPRs in the MFMA A-operand layout (lane = row r16, 16-B k-chunk grp: 16 rows x 64 B per
-// wave-instruction, the two k-halves of a 64-deep step complete each 128-B line), PW k-steps
-// ahead in a register ring — the register file, not LDS, holds the weight stream's bytes in
-// flight.  Every k-step issues the same loads (tail steps re-read the last step's addresses into
-// slots no live step uses), so one counted vmcnt covers "X of step t landed" in every iteration:
-// per iteration the wave issues X(t + PX) then W(t + PW), and the ops after X(t) are W(t - PX + PW)
-// plus PX - 1 whole iterations (PW == PX: W(t) is the younger, only the PX - 1 iterations).
-template <int BM_, int NW_, int TN_, int PX_, int PW_>
-struct DW {
-  static constexpr int BM = BM_, NW = NW_, TN = TN_, PX = PX_, PW = PW_;
-  static constexpr int NT = 64 * NW, BN = NW * TN * 16, TM = BM / 16;
-  static constexpr int SX = PX + 1, RW = PW + 1;      // X LDS stages, W register slots
-  static constexpr int XB = BM * 128;                 // one 64-deep k-step of X
-  static constexpr int LDS = SX * XB;
-  static constexpr int GX = XB / (NT * 16), GW = 2 * TN;
-  static constexpr int PER = GX + GW;
-  // ops younger than the later-issued of {X(t), W(t)}: X(t) when PW > PX, W(t) when PW == PX
-  static constexpr int WAIT = (PW > PX ? GW : 0) + (PX - 1) * PER;
-  static_assert(PW >= PX && PX >= 1, "weights run at least as far ahead as X");
-  static_assert(GX * NT * 16 == XB, "X stage must fill whole DMA waves");
-  static_assert(PW * PER <= 63, "vmcnt range: every op in flight stays countable");
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-};
-
-// 16-B global load the compiler does not track: its waits come from the kernel's own counted
-// vmcnt (a compiler-tracked register ring is copied between slots at the loop back edge, and each
-// copy of a pending load drains vmcnt)
-KA_DEV void gload16_untracked(u32x4& d, const void* p) {
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
-}
-
-// f(std::integral_constant<int, 0>) ... f(std::integral_constant<int, N - 1>)
-template <int N, int I = 0, class F>
-KA_DEV void unroll_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    unroll_for<N, I + 1>(f);
-  }
-}
-
-template <class C, int EPI>
-__global__ __launch_bounds__(C::NT) void gemm_dw_kernel(Args a) {
-  extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
-  char* const L = reinterpret_cast<char*>(lds);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int tmi, tni;
-  tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tmi, tni);
-  const int n0 = tni * C::BN, m0 = tmi * C::BM;
-  const int kb = blockIdx.z * a.kps;
-  const int nk = min(a.kps, a.K - kb) / BK;
-  const int r16 = lane & 15, grp = lane >> 4;
-
-  // X: LDS-DMA, lane-linear 8 rows x 128 B per wave-instruction, XOR-swizzled (as gemm_kernel)
-  const int rl = lane >> 3, slot = lane & 7;
-  uint32_t offX[C::GX];
-#pragma unroll
-  for (int j = 0; j < C::GX; ++j) {
-    const int row = (j * C::NW + wave) * 8 + rl;
-    offX[j] = ((uint32_t)min(m0 + row, a.M - 1) * (uint32_t)a.ldx + kb + swz<64>(row, slot) * 8) * 2u;
-  }
-  const char* Xb = reinterpret_cast<const char*>(a.X);
-  // W: tile i of this wave, k-half kk: row n0 + (wave*TN + i)*16 + r16, chunk kk*4 + grp
-  const char* Wrow[C::TN];
-#pragma unroll
-  for (int i = 0; i < C::TN; ++i)
-    Wrow[i] = reinterpret_cast<const char*>(a.W) +
-              ((size_t)min(n0 + (wave * C::TN + i) * 16 + r16, a.N - 1) * a.K + kb + grp * 8) * 2;
-
-  u32x4 wf[C::RW][C::TN][2];
-  auto issue_x = [&](int t) {
-    const int s = min(t, nk - 1);
-    char* dst = L + (t % C::SX) * C::XB;
-    const uint32_t kofs = (uint32_t)s * 128u;
-#pragma unroll
-    for (int j = 0; j < C::GX; ++j) glds16(Xb + offX[j] + kofs, dst + (j * C::NW + wave) * 1024);
-  };
-  auto issue_w = [&](int t, u32x4 (&dst)[C::TN][2]) {
-    const size_t kofs = (size_t)min(t, nk - 1) * 128;
-#pragma unroll
-    for (int i = 0; i < C::TN; ++i) {
-      gload16_untracked(dst[i][0], Wrow[i] + kofs);
-      gload16_untracked(dst[i][1], Wrow[i] + kofs + 64);
-    }
-  };
-
-  f32x4 acc[C::TN][C::TM];
-#pragma unroll
-  for (int i = 0; i < C::TN; ++i)
-#pragma unroll
-    for (int j = 0; j < C::TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int rdB = r16 * 128;
-  const int ch0 = swz<64>(r16, grp) * 16, ch1 = swz<64>(r16, 4 + grp) * 16;
-
-  // prologue: W(0 .. PW-PX-1), then PX iterations' worth of {X(s), W(s + PW - PX)}
-#pragma unroll
-  for (int s = 0; s < C::PW - C::PX; ++s) issue_w(s, wf[s]);
-#pragma unroll
-  for (int s = 0; s < C::PX; ++s) {
-    issue_x(s);
-    issue_w(s + C::PW - C::PX, wf[s + C::PW - C::PX]);
-  }
-
-  // one k-step; `u` = t % RW is a compile-time register slot after unrolling
-  auto step = [&](int t, auto uc) {
-    constexpr int u = decltype(uc)::value;
-    wait_vm<C::WAIT>();
-    block_sync();
-    issue_x(t + C::PX);
-    issue_w(t + C::PW, wf[(u + C::PW) % C::RW]);
-    const char* sb = L + (t % C::SX) * C::XB + rdB;
-    // all of this step's X fragments are read up front (k-half 1's reads are issued before
-    // k-half 0's MFMAs): one wave per SIMD cannot hide a ds_read latency per MFMA pair
-    if constexpr (C::NW >= 8) {   // two waves per SIMD: the partner hides the read latency
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 fb[C::TM];
-#pragma unroll
-        for (int j = 0; j < C::TM; ++j)
-          fb[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(sb + j * 2048 + (kk ? ch1 : ch0)));
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < C::TM; ++j)
-#pragma unroll
-          for (int i = 0; i < C::TN; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[u][i][kk]), fb[j],
-                                                                acc[i][j], 0, 0, 0);
-      }
-    } else {
-      bf16x8 fb[2][C::TM];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int j = 0; j < C::TM; ++j)
-          fb[kk][j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(sb + j * 2048 + (kk ? ch1 : ch0)));
-      __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs (the scheduler pairs them)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int j = 0; j < C::TM; ++j)
-#pragma unroll
-          for (int i = 0; i < C::TN; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[u][i][kk]), fb[kk][j],
-                                                                acc[i][j], 0, 0, 0);
-    }
-  };
-  // whole groups of RW steps, no guard inside: the host requires nk % RW == 0 (a guarded body would
-  // merge register-slot values over several paths, and the compiler would copy slots while their
-  // loads are in flight)
-  for (int t0 = 0; t0 < nk; t0 += C::RW)
-    unroll_for<C::RW>([&](auto uc) { step(t0 + decltype(uc)::value, uc); });
-  wait_vm<0>();   // the tail's redundant loads land before the wave's registers / LDS are released
-  // ... and their (never read) destination registers stay allocated until then: the compiler does
-  // not know the asm loads are in flight and would hand a dead slot to another value
-#pragma unroll
-  for (int s = 0; s < C::RW; ++s)
-#pragma unroll
-    for (int i = 0; i < C::TN; ++i) asm volatile("" ::"v"(wf[s][i][0]), "v"(wf[s][i][1]));
-
-  // epilogue: acc[i][j][r] = C[n = nb + i*16 + r][m = mb + j*16]
-  const int nb = n0 + wave * C::TN * 16 + 4 * grp;
-  const int mb = m0 + r16;
-  if constexpr (EPI == EPI_SWIGLU) {
-    static_assert(C::TN % 2 == 0, "SwiGLU epilogue needs gate/up tile pairs");
-    const int cb = (n0 + wave * C::TN * 16) / 2 + 4 * grp;
-#pragma unroll
-    for (int p = 0; p < C::TN / 2; ++p) {
-      const int c = cb + 16 * p;
-      if (2 * c >= a.N) continue;
-#pragma unroll
-      for (int j = 0; j < C::TM; ++j) {
-        const int m = mb + j * 16;
-        if (m >= a.M) continue;
-        const f32x4 g = acc[2 * p][j], u = acc[2 * p + 1][j];
-        float o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = g[r] / (1.f + __expf(-g[r])) * u[r];
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + c) =
-            make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-      }
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < C::TN; ++i) {
-      const int n = nb + i * 16;
-      if (n >= a.N) continue;
-#pragma unroll
-      for (int j = 0; j < C::TM; ++j) {
-        const int m = mb + j * 16;
-        if (m >= a.M) continue;
-        const f32x4 v = acc[i][j];
-        if constexpr (EPI == EPI_BF16) {
-          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.Y) + (size_t)m * a.ldy + n) =
-              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        } else if constexpr (EPI == EPI_P16) {
-          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) =
-              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        } else {
-          *reinterpret_cast<f32x4*>(static_cast<float*>(a.P) + ((size_t)blockIdx.z * a.M + m) * a.N + n) = v;
-        }
-      }
-    }
-  }
-}
-
-template <class C, int EPI>
-static int launch_dw(const Args& a0, int split, hipStream_t st) {
-  if constexpr (EPI == EPI_SWIGLU && C::TN % 2 != 0) {
-    return (int)hipErrorInvalidValue;   // gate/up tile pairs live in one wave
-  } else {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_dw_kernel<C, EPI>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    attr = true;
-  }
-  Args a = a0;
-  if ((a.kps / BK) % C::RW != 0 || a.K % a.kps != 0) return (int)hipErrorInvalidValue;
-  a.tiles_m = (a.M + C::BM - 1) / C::BM;
-  a.tiles_n = (a.N + C::BN - 1) / C::BN;
-  hipLaunchKernelGGL((gemm_dw_kernel<C, EPI>), dim3(a.tiles_m * a.tiles_n, 1, split), dim3(C::NT), C::LDS, st, a);
-  return (int)hipGetLastError();
-  }
-}
-
-// direct-weight configurations: id: BM X rows, NW waves x TN weight tiles (BN = NW*TN*16),
-// PX / PW k-steps of X / W in flight (RW = PW + 1 must divide the k-steps per split)
-#define GM_DW_CFGS(X)      \
-  X(30, 256, 4, 2, 2, 3)   \
-  X(31, 256, 8, 1, 4, 7)   \
-  X(32, 128, 4, 2, 3, 3)   \
-  X(33, 128, 8, 1, 3, 7)   \
-  X(34, 256, 4, 2, 3, 3)   \
-  X(35, 256, 8, 1, 3, 7)
-
 // ---- configurations ------------------------------------------------------------------------------
 // id: BN x BM tile, WN x WM waves (per-wave tile), ring stages of BK = 64:
 //   2: 128 x 256, 2 x 4 waves (64 x 64), 3 stages                (8 waves, 144 KB: 1 block/CU)
@@ -835,10 +591,6 @@ static int launch(const Args& a0, int split, hipStream_t st) {
 template <int EPI>
 static int dispatch(int cfg, const Args& a, int split, hipStream_t st) {
   if (cfg == 19) return launch_pp<EPI>(a, split, st);
-#define XD_(id, bm, nw, tn, px, pw) \
-  if (cfg == id) return launch_dw<DW<bm, nw, tn, px, pw>, EPI>(a, split, st);
-  GM_DW_CFGS(XD_)
-#undef XD_
 #define X_(id, bn, bm, wn, wm, s, kt) \
   if (cfg == id) return launch<Cfg<bn, bm, wn, wm, s, kt>, EPI>(a, split, st);
   GM_CFGS(X_)
@@ -849,7 +601,6 @@ static int dispatch(int cfg, const Args& a, int split, hipStream_t st) {
 template <int EPI>
 static int dispatch_grouped(int cfg, const Args& a, int split, hipStream_t st) {
   if (cfg == 19) return launch_pp_grouped<EPI>(a, split, st);
-  if (cfg >= 30) return (int)hipErrorInvalidValue;   // direct-weight kernels: dense GEMMs only
 #define X_(id, bn, bm, wn, wm, s, kt) \
   if (cfg == id) return launch_grouped<Cfg<bn, bm, wn, wm, s, kt>, EPI>(a, split, st);
   GM_CFGS(X_)
@@ -861,26 +612,13 @@ static int dispatch_grouped(int cfg, const Args& a, int split, hipStream_t st) {
 
 extern "C" int ka_gm_bn(int cfg) {
   if (cfg == 19) return gm::PP::BN;
-#define XD_(id, bm, nw, tn, px, pw) if (cfg == id) return nw * tn * 16;
-  GM_DW_CFGS(XD_)
-#undef XD_
 #define X_(id, bn, bm, wn, wm, s, kt) if (cfg == id) return bn;
   GM_CFGS(X_)
 #undef X_
   return -1;
 }
-// k-steps (of 64) per split must be a multiple of this (direct-weight kernels: the register ring)
-extern "C" int ka_gm_kmult(int cfg) {
-#define XD_(id, bm, nw, tn, px, pw) if (cfg == id) return pw + 1;
-  GM_DW_CFGS(XD_)
-#undef XD_
-  return ka_gm_bn(cfg) > 0 ? 1 : -1;
-}
 extern "C" int ka_gm_bm(int cfg) {
   if (cfg == 19) return gm::PP::BM;
-#define XD_(id, bm, nw, tn, px, pw) if (cfg == id) return bm;
-  GM_DW_CFGS(XD_)
-#undef XD_
 #define X_(id, bn, bm, wn, wm, s, kt) if (cfg == id) return bm;
   GM_CFGS(X_)
 #undef X_

@@ -351,11 +351,9 @@ def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, bf16_partials
     return linear(silu_mul(gu), w, defer_reduce=defer_reduce, bf16_partials=bf16_partials)
 
 
-# csrc/gemm_mfma.hip configurations (MFMA GEMM family; ka_gm_bn / ka_gm_bm give the tile): 2-5, 12
-# LDS-DMA ring kernels, 19 the 2-phase 256 x 256 ping-pong kernel, 30-34 the direct-weight decode
-# kernels (weights streamed global -> VGPR, X through an LDS ring; K / split / 64 must be a
-# multiple of ka_gm_kmult)
-GM_CFGS = (2, 3, 4, 5, 12, 19, 30, 31, 32, 33, 34)
+# csrc/gemm_mfma.hip configurations (LDS-DMA staged MFMA GEMM family; ka_gm_bn / ka_gm_bm give the
+# tile): 2-5, 12 ring kernels, 19 the 2-phase 256 x 256 ping-pong kernel
+GM_CFGS = (2, 3, 4, 5, 12, 19)
 GM_EPI_BF16, GM_EPI_P32, GM_EPI_P16, GM_EPI_SWIGLU = 0, 1, 2, 3
 # grouped (MoE prefill) configuration: the 256 x 256 ping-pong kernel (profiles/r2/bench_moe_prefill.txt)
 MOE_GROUPED_CFG = int(os.environ.get("KA_MOE_GROUPED_CFG", "19"))
@@ -365,11 +363,6 @@ def gm_shape(cfg: int):
     """(BN, BM) of a gemm_mfma configuration."""
     lib = require()
     return lib.ka_gm_bn(cfg), lib.ka_gm_bm(cfg)
-
-
-def gm_kmult(cfg: int) -> int:
-    """The 64-deep k-steps per split of configuration `cfg` must be a multiple of this."""
-    return require().ka_gm_kmult(cfg)
 
 
 def linear_gm(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, defer_reduce: bool = False,

@@ -48,7 +48,6 @@ _SIGS = {
     "ka_gemm_mfma_grouped": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
     "ka_gm_bn": [I],
     "ka_gm_bm": [I],
-    "ka_gm_kmult": [I],
     "ka_moe_align": [P, P, P, I, I, I, P],
     "ka_moe_gemm": [P, P, P, P, P, I, I, I, I, I, I, I, P, P],
     "ka_moe_combine": [P, P, P, I, P, P, I, I, I, I, I, P],

@@ -13,7 +13,7 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from . import GEMM_PLAN, SKINNY_MAX_M, TILE_MAX_M, gm_kmult, gm_shape, linear, linear_gm, rmsnorm, skinny_split
+from . import GEMM_PLAN, SKINNY_MAX_M, TILE_MAX_M, gm_shape, linear, linear_gm, rmsnorm, skinny_split
 
 logger = logging.getLogger("app.engine")
 
@@ -156,7 +156,7 @@ def tune_linear(groups: Dict[Tuple[int, int], List[torch.Tensor]], Ms: Sequence[
 # win at M = 32-64, 128 x 128 at 96-256, 128 x 256 / 256 x 128 / 4-stage 128 x 128 at 192-256; the
 # configurations that never won — one wave per SIMD, 32-deep rings, 64-row weight tiles, the 4-phase
 # ping-pong — were removed: profiles/r2/gemm_sweep_v*.txt)
-GM_TUNE_CFGS = (2, 3, 4, 5, 12, 19, 30, 31, 32, 33, 34)
+GM_TUNE_CFGS = (2, 3, 4, 5, 12, 19)
 
 
 def gm_candidates(M: int, N: int, K: int, cfgs: Sequence[int] = ()):
@@ -169,10 +169,9 @@ def gm_candidates(M: int, N: int, K: int, cfgs: Sequence[int] = ()):
         bn, bm = gm_shape(cfg)
         if bm > 2 * M and bm > 64:
             continue
-        kmult = gm_kmult(cfg)
         tiles = ((N + bn - 1) // bn) * ((M + bm - 1) // bm)
-        for split in (1, 2, 4, 7, 8):
-            if K % (64 * split) or K // split < 256 or (K // split // 64) % kmult:
+        for split in (1, 2, 4, 8):
+            if K % (64 * split) or K // split < 256:
                 continue
             if split > 1 and tiles * split > 1024:
                 continue
