@@ -55,9 +55,10 @@ KA_DEV int swz(int row, int ch) {
   else return ch ^ ((row >> 2) & 2);
 }
 
+template <int AUX = 0>
 KA_DEV void glds16(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, AUX);
 }
 
 template <int N>
@@ -82,6 +83,7 @@ struct Args {
   const int* counts;
   const int* lists;
   int lstride, src_div, groups;
+  int wnt;   // 1: weight DMAs non-temporal (aux = 2) so the streamed weights do not evict X from L2
 };
 
 // logical tile -> (m tile, n tile): XCD-contiguous, then GM m-tiles x all n-tiles super-rows
@@ -183,8 +185,13 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
     char* sa = lds_c + stage * C::STAGE_BYTES;
     char* sb = sa + C::A_BYTES;
     const uint32_t kofs = (uint32_t)t * C::RB;
+    if (a.wnt) {
 #pragma unroll
-    for (int j = 0; j < C::GA; ++j) glds16(Wb + offA[j] + kofs, sa + (j * C::NW + wave) * 1024);
+      for (int j = 0; j < C::GA; ++j) glds16<2>(Wb + offA[j] + kofs, sa + (j * C::NW + wave) * 1024);
+    } else {
+#pragma unroll
+      for (int j = 0; j < C::GA; ++j) glds16(Wb + offA[j] + kofs, sa + (j * C::NW + wave) * 1024);
+    }
 #pragma unroll
     for (int j = 0; j < C::GB; ++j) glds16(Xb + offB[j] + kofs, sb + (j * C::NW + wave) * 1024);
   };
@@ -385,8 +392,13 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
     const char* src = h < 2 ? Wb : Xb;
     char* dst = L + (t & 1) * PP::BUF + h * PP::HALF;
     const uint32_t kofs = (uint32_t)t * (BK * 2);
+    if (h < 2 && a.wnt) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(src + off[h][j] + kofs, dst + (j * 8 + w) * 1024);
+      for (int j = 0; j < 2; ++j) glds16<2>(src + off[h][j] + kofs, dst + (j * 8 + w) * 1024);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) glds16(src + off[h][j] + kofs, dst + (j * 8 + w) * 1024);
+    }
   };
 
   const int r16 = lane & 15, grp = lane >> 4, sw = (r16 >> 1) & 7;
@@ -641,6 +653,8 @@ extern "C" int ka_gemm_mfma(void* Y, void* P, const void* X, const void* W, int 
   if ((epi == gm::EPI_BF16 || epi == gm::EPI_SWIGLU) && split != 1) return (int)hipErrorInvalidValue;
   gm::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), Y, P, M, N, K, ldx, ldy, K / split,
              0, 0, gm > 0 ? gm : 8};
+  a.wnt = M <= 512;   // decode-sized: each weight byte is read once per step (2-4 % faster with nt,
+                      // prefill re-reads weight panels from L2 and loses 1-2 %: profiles/r2/gemm_wnt_ab.txt)
   switch (epi) {
     case gm::EPI_BF16: return gm::dispatch<gm::EPI_BF16>(cfg, a, split, stream);
     case gm::EPI_P32: {
@@ -670,6 +684,7 @@ extern "C" int ka_gemm_mfma_grouped(void* Y, void* P, const void* X, const void*
   if (epi == gm::EPI_SWIGLU || (epi == gm::EPI_BF16 && split != 1)) return (int)hipErrorInvalidValue;
   gm::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), Y, P, R, N, K, ldx, ldy, K / split,
              0, 0, 8, counts, lists, lstride, src_div, groups};
+  a.wnt = 0;          // grouped expert GEMMs re-read each expert's weights for every row chunk
   switch (epi) {
     case gm::EPI_BF16: return gm::dispatch_grouped<gm::EPI_BF16>(cfg, a, split, stream);
     case gm::EPI_P32: return gm::dispatch_grouped<gm::EPI_P32>(cfg, a, split, stream);
