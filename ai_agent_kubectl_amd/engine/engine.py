@@ -23,7 +23,7 @@ from typing import Callable, List, Optional
 from .block_manager import make_block_manager
 from .runner import ModelRunner
 from .scheduler import Scheduler
-from .sequence import SamplingParams, Sequence, SeqStatus
+from .sequence import PLACEHOLDER, SamplingParams, Sequence, SeqStatus
 
 logger = logging.getLogger("app.engine")
 
@@ -52,6 +52,10 @@ class LLMEngine:
         self._inflight = None
         self.chained_steps = 0
         self.prefill_chains = 0    # decode steps queued behind a prefill before its readback
+        # steps whose batch composition changes (admissions, finished rows, chunk continuations) are
+        # scheduled from a provisional advance of the in-flight step and queued before its readback
+        self.lookahead = os.environ.get("KA_LOOKAHEAD", "1") == "1"
+        self.lookahead_steps = 0
         self.idle_s = 0.0          # time the loop slept with no work (waiting for requests)
         self.step_t0: Optional[float] = None   # perf_counter at the start of the running step
         self.watchdog = None       # parallel/watchdog.py (TP/EP > 1, rank 0)
@@ -195,9 +199,14 @@ class LLMEngine:
         if self._inflight is not None:
             prev, handle, t_prev = self._inflight
             nxt = self._chain(prev)
+            if nxt is None and self.lookahead and self.runner.can_lookahead():
+                n = self._lookahead_step(prev, handle, t_prev)
+                self._step_metrics(prev)
+                return n
             t_nxt = time.perf_counter()
             nh = self.runner.launch_decode_async(nxt, chained=True) if nxt is not None else None
             self.chained_steps += nxt is not None
+            self.prefill_chains += nxt is not None and not prev.is_decode
             self._finish_step(prev, self.runner.collect(handle), t_prev)
             self._inflight = (nxt, nh, t_nxt) if nxt is not None else None
             batch = prev
@@ -211,21 +220,17 @@ class LLMEngine:
             if self.overlap and batch.is_decode and self.runner.can_overlap(len(batch.seqs)):
                 self._inflight = (batch, self.runner.launch_decode_async(batch), t0)
                 return len(batch.seqs)
-            if (self.overlap and not batch.is_decode and len(batch.prefill_seqs) == len(batch.seqs)
-                    and self.runner.can_overlap_prefill(len(batch.seqs))):
-                # a pure prefill step: queue the first decode step of the same rows behind it
-                # (input ids copied on the device from the prefill's samples) before reading the
-                # prefill back, so the GPU does not idle while the host applies ~256 prompts
-                ph = self.runner.launch_prefill_async(batch)
-                nxt = self._chain(batch)
-                t_nxt = time.perf_counter()
-                nh = self.runner.launch_decode_async(nxt, chained=True) if nxt is not None else None
-                self.chained_steps += nxt is not None
-                self.prefill_chains += nxt is not None
-                self._finish_step(batch, self.runner.collect(ph), t0)
-                self._inflight = (nxt, nh, t_nxt) if nxt is not None else None
+            if (self.overlap and not batch.is_decode and self.runner.can_overlap_prefill(len(batch.seqs))
+                    and (self.lookahead or len(batch.prefill_seqs) == len(batch.seqs))):
+                # a prefill / mixed step is queued and left in flight: the next call queues the step
+                # after it (a decode chain of the same rows, or a lookahead step) before reading it back
+                self._inflight = (batch, self.runner.launch_prefill_async(batch), t0)
                 return len(batch.seqs)
             self._finish_step(batch, self.runner.execute(batch), t0)
+        self._step_metrics(batch)
+        return len(batch.seqs)
+
+    def _step_metrics(self, batch) -> None:
         m = self.metrics
         if m is not None:
             m.llm_batch_size.set(len(batch.seqs))
@@ -239,7 +244,88 @@ class LLMEngine:
                 if nbytes > self._ar_bytes_seen:
                     m.rccl_allreduce_bytes.inc(nbytes - self._ar_bytes_seen)
                     self._ar_bytes_seen = nbytes
-        return len(batch.seqs)
+
+    # ---- lookahead: the next step scheduled and queued before the in-flight one is read back ----
+    def _provisional(self, batch) -> None:
+        """Advance the sequences of the in-flight `batch` as if it had been read back: KV counts move
+        on and every sampling row gets a PLACEHOLDER token (its value is still on the device; the next
+        step's inputs take it from there)."""
+        partial = batch.partial
+        for row, (s, nq) in enumerate(zip(batch.seqs, batch.num_query)):
+            if s.finished:
+                continue
+            s.num_computed += nq
+            if id(s) in partial:
+                continue
+            s.output_ids.append(PLACEHOLDER)
+            s.ph_row = row
+        self.scheduler.on_step_done(batch)
+
+    def _finalize(self, batch, tokens, t_launch: float) -> None:
+        """`_apply` for a batch `_provisional` advanced: placeholders get their sampled tokens, prefix
+        blocks are published, EOS / max_new_tokens finish sequences (a row the step queued ahead
+        computed for a sequence finished here is discarded at its own readback)."""
+        now = time.perf_counter()
+        m = self.metrics
+        prefill = {id(s) for s in batch.prefill_seqs}
+        for s, tok in zip(batch.seqs, tokens):
+            if s.finished:
+                continue
+            if id(s) in batch.partial:
+                self.bm.register_computed(s.block_table, s.all_ids[:s.num_computed], s.block_hashes)
+                continue
+            if s.ph_row is None:   # not advanced (finished between launch and provisional step)
+                continue
+            s.output_ids[-1] = int(tok)
+            s.ph_row = None
+            if id(s) in prefill:
+                self.bm.register_computed(s.block_table, s.all_ids[:s.num_computed], s.block_hashes)
+                if s.t_first_token is None:
+                    s.t_first_token = now
+                    if m is not None:
+                        m.llm_ttft.observe(now - s.t_arrival)
+                        m.llm_queue_wait.observe((s.t_scheduled or now) - s.t_arrival)
+            eos = (not s.params.ignore_eos) and self.tokenizer.is_eos(int(tok))
+            if eos or s.num_generated >= s.params.max_new_tokens:
+                if m is not None and s.t_first_token is not None and s.num_generated > 1:
+                    m.llm_tpot.observe((now - s.t_first_token) / (s.num_generated - 1))
+                self._finish(s, SeqStatus.FINISHED, "stop" if eos else "length")
+        self.scheduler.drop_finished()
+        self.steps += 1
+        if m is not None:
+            m.llm_step.labels("decode" if batch.is_decode else "prefill").observe(now - max(t_launch, self._t_done))
+            self._t_done = now
+
+    def _lookahead_step(self, prev, handle, t_prev: float) -> int:
+        """The in-flight `prev` cannot be followed by a same-rows decode chain: advance it
+        provisionally, schedule the next step from that state, queue it (its placeholder inputs
+        fixed up on the device), then read `prev` back and finalize it.  A step that cannot be queued
+        early (a decode batch above the largest graph bucket, ...) runs after the readback."""
+        self._provisional(prev)
+        batch, nh, t_nxt = None, None, 0.0
+        if self.scheduler.has_work():
+            self.scheduler.lookahead = True
+            try:
+                batch = self.scheduler.schedule()
+            finally:
+                self.scheduler.lookahead = False
+            if batch.seqs:
+                t_nxt = time.perf_counter()
+                if batch.is_decode:
+                    if self.runner.can_overlap(len(batch.seqs)):
+                        fix = [(i, s.ph_row) for i, s in enumerate(batch.seqs) if s.ph_row is not None]
+                        nh = self.runner.launch_decode_async(batch, fix=fix)
+                elif self.runner.can_overlap_prefill(len(batch.seqs)):
+                    nh = self.runner.launch_prefill_async(batch)
+                self.lookahead_steps += nh is not None
+        self._finalize(prev, self.runner.collect(handle), t_prev)
+        if nh is not None:
+            self._inflight = (batch, nh, t_nxt)
+        else:
+            self._inflight = None
+            if batch is not None and batch.seqs:   # placeholders are real now: run it synchronously
+                self._finish_step(batch, self.runner.execute(batch), t_nxt)
+        return len(prev.seqs)
 
     def _fail_all(self, err: BaseException) -> None:
         self._inflight = None

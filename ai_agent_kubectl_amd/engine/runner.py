@@ -27,6 +27,7 @@ from ..models.llama import AttnMeta, LlamaModel
 from ..parallel.comm import LocalComm
 from .safe_decode import mask_index_for
 from .scheduler import Batch
+from .sequence import PLACEHOLDER
 
 KIND_STOP, KIND_DECODE, KIND_PREFILL = 0, 1, 2
 HDR = 8
@@ -85,6 +86,15 @@ class ModelRunner:
         self.d_logits_idx = torch.arange(B, dtype=torch.int64, device=self.device)
         self.d_out = torch.zeros(B, dtype=torch.int32, device=self.device)
         self.h_out = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
+        # steps queued ahead of a readback (engine._lookahead_step): prefill / mixed staging in grown
+        # pinned buffers and token outputs, each double-buffered (a buffer is reused two launches
+        # later, when the step that used it has been read back), and the placeholder fixups of a
+        # decode step ([dst rows | src rows] of d_out)
+        self._h_pre: List[Optional[torch.Tensor]] = [None, None]
+        self._h_pouts = [torch.zeros(B, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self._pflip = 0
+        self._h_fix = [torch.zeros(2 * B, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self.d_fix = torch.zeros(2 * B, dtype=torch.int32, device=self.device)
         self.d_hdr = torch.zeros(HDR, dtype=torch.int32, device=self.device)
         self._h_hdrs = [torch.zeros(HDR, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         # TP decode overlap: rank 0 queues step t+1 (header + staging broadcast + graph) before
@@ -240,12 +250,19 @@ class ModelRunner:
     def can_overlap_prefill(self, B: int) -> bool:
         return self.tp_size == 1 and B <= self.bmax
 
+    def can_lookahead(self) -> bool:
+        """Steps can be scheduled and queued ahead of the in-flight step's readback (TP = 1: with TP
+        the staging broadcast would need the placeholder fixups on every rank)."""
+        return self.tp_size == 1
+
     @torch.inference_mode()
-    def launch_decode_async(self, batch: Batch, chained: bool = False):
+    def launch_decode_async(self, batch: Batch, chained: bool = False, fix: Optional[List[tuple]] = None):
         """Queue one decode step without waiting for it.  chained: `batch` is the step after the one
         in flight (same sequences, same row order): its input ids are copied on the device from the
         previous step's sampled tokens (with TP, on rank 0 before the staging broadcast, so the other
-        ranks receive them; every rank samples the same token).  Returns a handle for `collect`."""
+        ranks receive them; every rank samples the same token).  fix: (row, src) pairs of rows whose
+        input is a PLACEHOLDER: their ids are the in-flight step's sampled tokens d_out[src] (a step
+        scheduled ahead, engine._lookahead_step).  Returns a handle for `collect`."""
         B = len(batch.seqs)
         i = bisect.bisect_left(self.buckets, B)
         Bp = self.buckets[i] if i < len(self.buckets) else B
@@ -264,6 +281,14 @@ class ModelRunner:
         if chained:
             o = self._off["ids"]
             self.d_stage[o:o + B].copy_(self.d_out[:B])
+        if fix:
+            nf = len(fix)
+            hf = self._h_fix[k]
+            hf.numpy()[:2 * nf] = np.asarray(fix, dtype=np.int32).T.reshape(-1)
+            self.d_fix[:2 * nf].copy_(hf[:2 * nf], non_blocking=True)
+            o = self._off["ids"]
+            self.d_stage[o:o + Bp].index_copy_(0, self.d_fix[:nf].long(),
+                                               self.d_out.index_select(0, self.d_fix[nf:2 * nf].long()))
         self._launch_decode(Bp, n_copy)
         ho[:B].copy_(self.d_out[:B], non_blocking=True)
         ev = None
@@ -274,22 +299,46 @@ class ModelRunner:
 
     @torch.inference_mode()
     def launch_prefill_async(self, batch: Batch):
-        """Queue a prefill step without waiting for its tokens (TP = 1, every row a prompt, at most
-        `bmax` sequences): the sampled tokens are also left in `d_out`, in batch row order, so the
-        first decode step can be queued right behind it (`launch_decode_async(chained=True)`)
-        while the host applies this step's results.  Returns a handle for `collect`."""
+        """Queue a prefill or mixed step without waiting for its tokens (TP = 1, at most `bmax` rows):
+        the sampled tokens are also left in `d_out`, in batch row order, so the next step can be
+        queued right behind it with its inputs taken on the device (`launch_decode_async(chained=
+        True)` for the same rows, or the PLACEHOLDER fixups of a step scheduled ahead).  Rows whose
+        input is a PLACEHOLDER (this batch was scheduled ahead of the in-flight step's readback) get
+        it from `d_out` before the forward.  Returns a handle for `collect`."""
         t0 = time.perf_counter()
-        host = self._pack_prefill(batch, pad=True)
+        host, nf = self._pack_prefill(batch, pad=True, with_fix=True)
         T, S, max_q, nc = self.padded_tokens(batch.num_tokens), len(batch.seqs), max(batch.num_query), len(batch.copies)
-        buf = torch.from_numpy(host).to(self.device, non_blocking=False)
-        tok = self._run_prefill(buf, T, S, max_q, nc, 0, batch.num_tokens)
+        nd = S - len(batch.prefill_seqs) if self.split_mixed_attention else 0
+        buf = self._stage_prefill(host)
+        if nf:   # trailing [dst positions | src rows]
+            n = buf.shape[0]
+            buf[:T].index_copy_(0, buf[n - 2 * nf:n - nf].long(), self.d_out.index_select(0, buf[n - nf:].long()))
+            buf = buf[:n - 2 * nf]
+        tok = self._run_prefill(buf, T, S, max_q, nc, nd, batch.num_tokens)
         self.d_out[:S].copy_(tok)
-        self.h_out[:S].copy_(tok, non_blocking=True)
+        ho = self._h_pouts[self._pflip]
+        self._pflip ^= 1
+        ho[:S].copy_(tok, non_blocking=True)
         ev = None
         if self.device.type == "cuda":
             ev = torch.cuda.Event()
             ev.record()
-        return StepHandle(ev, self.h_out, S, t0, prefill_tokens=T)
+        return StepHandle(ev, ho, S, t0, prefill_tokens=T)
+
+    def _stage_prefill(self, host: np.ndarray) -> torch.Tensor:
+        """Packed prefill metadata -> device without a host sync: through one of two pinned buffers
+        (grown on demand; the one being refilled served the launch before last, already read back)."""
+        if self.device.type != "cuda":
+            return torch.from_numpy(host)
+        n = host.shape[0]
+        k = self._sflip = getattr(self, "_sflip", 0) ^ 1
+        hb = self._h_pre[k]
+        if hb is None or hb.numel() < n:
+            hb = torch.empty(max(n, 2 * (hb.numel() if hb is not None else 0), 1 << 16), dtype=torch.int32,
+                             pin_memory=True)
+            self._h_pre[k] = hb
+        hb.numpy()[:n] = host
+        return hb[:n].to(self.device, non_blocking=True)
 
     def collect(self, handle: "StepHandle") -> List[int]:
         ev, ho, B, t0 = handle.event, handle.host_out, handle.rows, handle.t0
@@ -328,16 +377,34 @@ class ModelRunner:
         q = self.prefill_pad
         return T if q <= 1 or T < self.prefill_pad_min else (T + q - 1) // q * q
 
-    def _pack_prefill(self, batch: Batch, pad: bool = False) -> np.ndarray:
+    def _pack_prefill(self, batch: Batch, pad: bool = False, with_fix: bool = False):
+        """Packed step metadata [ids | pos | slots | q_starts | ctx | mask | logits idx | block tables |
+        copies (src, dst) | fixups (dst, src)].  with_fix: also returns the number of PLACEHOLDER
+        fixups (flat id position, in-flight row) appended at the end (their ids are packed as the
+        placeholder and replaced on the device)."""
         S = len(batch.seqs)
         T = self.padded_tokens(batch.num_tokens) if pad else batch.num_tokens
         mb = self.max_blocks
         nc = len(batch.copies)
-        buf = np.zeros(3 * T + (S + 1) + 3 * S + S * mb + 2 * nc, dtype=np.int32)
-        if nc:   # trailing [src... | dst...] block-copy list (sub-block prefix reuse)
+        fix = []
+        if with_fix:
+            q0 = 0
+            for s, nq in zip(batch.seqs, batch.num_query):
+                # a placeholder is always the sequence's last token; the row covers it if it ends there
+                if s.ph_row is not None and s.num_computed + nq == s.total_len:
+                    fix.append((q0 + nq - 1, s.ph_row))
+                q0 += nq
+        nf = len(fix)
+        buf = np.zeros(3 * T + (S + 1) + 3 * S + S * mb + 2 * nc + 2 * nf, dtype=np.int32)
+        if nf:
+            fx = np.asarray(fix, dtype=np.int32)
+            buf[len(buf) - 2 * nf:len(buf) - nf] = fx[:, 0]
+            buf[len(buf) - nf:] = fx[:, 1]
+        if nc:   # [src... | dst...] block-copy list (sub-block prefix reuse), before the fixups
             cp = np.asarray(batch.copies, dtype=np.int32)
-            buf[len(buf) - 2 * nc:len(buf) - nc] = cp[:, 0]
-            buf[len(buf) - nc:] = cp[:, 1]
+            e = len(buf) - 2 * nf
+            buf[e - 2 * nc:e - nc] = cp[:, 0]
+            buf[e - nc:e] = cp[:, 1]
         ids, pos, slots = buf[:T], buf[T:2 * T], buf[2 * T:3 * T]
         slots[batch.num_tokens:] = -1          # padding rows (if any): no cache write
         o = 3 * T
@@ -379,7 +446,7 @@ class ModelRunner:
         pos[:n_real] = p
         bs = self.block_size
         slots[:n_real] = bt[seq_of, p // bs] * bs + p % bs
-        return buf
+        return (buf, nf) if with_fix else buf
 
     def _run_prefill(self, buf: torch.Tensor, T: int, S: int, max_q: int, nc: int = 0, nd: int = 0,
                      t_real: int = 0) -> torch.Tensor:

@@ -100,6 +100,9 @@ class Scheduler:
         self.chunked = chunked_prefill
         self.min_chunk = min_chunk          # a later row is chunked only if this much budget is left
         self.prefilling: List[Sequence] = []   # admitted, prompt partially computed (chunked)
+        # scheduling ahead of an in-flight step (engine._lookahead_step): sequences were advanced
+        # provisionally, so no preemption (a victim's placeholder token would be re-prefilled)
+        self.lookahead = False
 
     def add(self, seq: Sequence) -> None:
         if seq.total_len + seq.params.max_new_tokens > self.max_model_len:
@@ -137,7 +140,7 @@ class Scheduler:
             if c < rem:
                 partial.add(id(seq))
             budget -= c
-        n_busy = len(self.running) + len(self.prefilling)
+        n_busy = self._n_active() + len(self.prefilling)
         n_cont = len(admitted)     # continued chunk rows are already counted in n_busy
         while self.waiting and budget > 0 and n_busy + len(admitted) - n_cont < self.max_batch:
             seq = self.waiting[0]
@@ -172,6 +175,18 @@ class Scheduler:
                 partial.add(id(seq))
             budget -= c
         return admitted, nqs, partial
+
+    def _n_active(self) -> int:
+        """Running sequences still generating (a provisionally advanced one may already hold its
+        last token, to be finished when that step is read back)."""
+        return sum(1 for s in self.running if s.num_generated < s.params.max_new_tokens)
+
+    def drop_finished(self) -> None:
+        before = len(self.running)
+        self.running = [s for s in self.running if not s.finished]
+        if not self.running and before:
+            self._idle_since = time.perf_counter()
+            self._drained = before
 
     def gathering(self) -> bool:
         """Idle engine, requests still streaming in: hold the admission for a moment.  The window
@@ -211,7 +226,7 @@ class Scheduler:
             return False
         if not self.running:
             return not self.gathering()
-        if len(self.running) >= self.max_batch:
+        if self._n_active() >= self.max_batch:
             return False
         if self._holding():
             return False
@@ -228,11 +243,17 @@ class Scheduler:
             for seq in list(self.running):
                 if seq.status is not SeqStatus.RUNNING:
                     continue  # preempted below while serving an earlier row
+                if seq.num_generated >= seq.params.max_new_tokens:
+                    continue  # holds its last token (provisional): finished at that step's readback
+                ok = True
                 while True:
                     try:
                         self.bm.ensure_capacity(seq.block_table, seq.total_len)
                         break
                     except NoFreeBlocks:
+                        if self.lookahead:   # no preemption ahead of a readback: skip the row this step
+                            ok = False
+                            break
                         # preempt the newest running sequence (recomputed when re-admitted)
                         victim = self.running[-1]
                         self._preempt(victim)
@@ -240,7 +261,7 @@ class Scheduler:
                             decodes.remove(victim)
                         if victim is seq:
                             break
-                if seq.status is SeqStatus.RUNNING:
+                if ok and seq.status is SeqStatus.RUNNING:
                     decodes.append(seq)
         if admitted:
             seqs = decodes + admitted
@@ -270,8 +291,4 @@ class Scheduler:
                     self.running.append(s)
             elif s not in self.prefilling:
                 self.prefilling.append(s)
-        before = len(self.running)
-        self.running = [s for s in self.running if not s.finished]
-        if not self.running and before:
-            self._idle_since = time.perf_counter()
-            self._drained = before
+        self.drop_finished()

@@ -9,6 +9,11 @@ from typing import Callable, List, Optional
 
 _ids = itertools.count()
 
+# token id of an output whose value is still on the device: a step scheduled while the previous
+# one is in flight (engine._lookahead_step) appends it; the readback replaces it, and until then the
+# next step's packed inputs take that token from the device (runner fixups)
+PLACEHOLDER = -1
+
 
 class SeqStatus(enum.Enum):
     WAITING = 0
@@ -44,6 +49,7 @@ class Sequence:
     t_scheduled: Optional[float] = None     # first admission into a prefill step (queue wait ends)
     t_first_token: Optional[float] = None
     t_finish: Optional[float] = None
+    ph_row: Optional[int] = None            # row of the in-flight step whose token is the PLACEHOLDER
 
     def __post_init__(self):
         self.n_forced = len(self.forced_prefix)

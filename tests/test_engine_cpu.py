@@ -341,6 +341,54 @@ def test_overlapped_decode_matches_sync(tiny_engine):
     assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
 
 
+def test_lookahead_steps_match_sync(tiny_engine):
+    """Sequences of different lengths (rows leave the batch at different steps, EOS stops allowed)
+    and chunked prompts through the threaded engine with lookahead (each composition change
+    scheduled from a provisional advance of the in-flight step and queued before its readback, the
+    placeholder inputs fixed up on the device) sample the same tokens as without it."""
+    import threading
+    eng, be = tiny_engine
+    prompts = [be.prompt_ids(q) for q in ("list pods", "get svc -A", "top nodes", "describe pod web-1",
+                                          "logs api", "get deploy", "get services in namespace kube-system")]
+    lens = [3, 9, 5, 7, 2, 8, 6]
+
+    def run(lookahead, ignore_eos):
+        eng.lookahead = lookahead
+        eng.bm.reset_prefix_cache()
+        done, ev = {}, threading.Event()
+
+        def cb(seq):
+            done[seq.seq_id] = seq
+            if len(done) == len(prompts):
+                ev.set()
+
+        eng.start()
+        try:
+            seqs = [eng.submit(p, SamplingParams(max_new_tokens=n, ignore_eos=ignore_eos), cb,
+                               forced_prefix=be._forced) for p, n in zip(prompts, lens)]
+            assert ev.wait(60)
+        finally:
+            eng.shutdown()
+        return [list(s.output_ids) for s in seqs]
+
+    sch = eng.scheduler
+    saved = sch.max_batched_tokens, sch.min_chunk
+    sch.max_batched_tokens, sch.min_chunk = 40, 4
+    try:
+        n0 = eng.lookahead_steps
+        for ignore_eos in (True, False):
+            on, off = run(True, ignore_eos), run(False, ignore_eos)
+            assert on == off
+            assert all(-1 not in o for o in on)
+            if ignore_eos:
+                assert [len(o) - len(be._forced) for o in on] == lens
+        assert eng.lookahead_steps > n0
+    finally:
+        sch.max_batched_tokens, sch.min_chunk = saved
+        eng.lookahead = True
+    assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
+
+
 def test_chunked_prefill_matches_whole_prefill(tiny_engine):
     """Prompts prefilled in 24-token chunks (through the threaded engine: mixed chunk + decode
     steps, overlapped decode) sample the same tokens as one whole-prompt prefill."""
@@ -362,6 +410,7 @@ def test_chunked_prefill_matches_whole_prefill(tiny_engine):
         sch.max_batched_tokens, sch.min_chunk = saved
     assert min(len(p) for p in prompts) + len(be._forced) > 24   # every prompt really was chunked
     assert chunked == whole and threaded == whole
+    assert eng.lookahead_steps > 0
     assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
 
 
