@@ -56,6 +56,15 @@ class LLMEngine:
         # scheduled from a provisional advance of the in-flight step and queued before its readback
         self.lookahead = os.environ.get("KA_LOOKAHEAD", "1") == "1"
         self.lookahead_steps = 0
+        # ... but not earlier than needed: requests arriving while the in-flight step runs should
+        # still make it into the next one, so the lookahead waits until the in-flight step is
+        # expected to end within this margin (host-side schedule + pack + first launches), from
+        # running estimates of the step durations (decode: ms per step; prefill / mixed: a fixed part
+        # plus ms per token)
+        self.lookahead_margin_s = float(os.environ.get("KA_LOOKAHEAD_MARGIN_MS", "8")) / 1000.0
+        self._est_decode_s = 0.007
+        self._est_tok_s = 9e-6
+        self._est_fixed_s = 0.005
         self.idle_s = 0.0          # time the loop slept with no work (waiting for requests)
         self.step_t0: Optional[float] = None   # perf_counter at the start of the running step
         self.watchdog = None       # parallel/watchdog.py (TP/EP > 1, rank 0)
@@ -188,10 +197,23 @@ class LLMEngine:
         self.scheduler.on_step_done(batch)
         self.steps += 1
         m = self.metrics
-        if m is not None:   # a step's share of the pipeline: from its launch (or the previous
-            now = time.perf_counter()   # step's completion, when it was queued behind it) to its readback
+        # a step's share of the pipeline: from its launch (or the previous step's completion, when it
+        # was queued behind it) to its readback
+        now = time.perf_counter()
+        self._observe_step(batch, now - max(t_launch, self._t_done))
+        if m is not None:
             m.llm_step.labels("decode" if batch.is_decode else "prefill").observe(now - max(t_launch, self._t_done))
-            self._t_done = now
+        self._t_done = now
+
+    def _observe_step(self, batch, dur: float) -> None:
+        """Running step-duration estimates for the lookahead timing (EMA, weight 1/4)."""
+        if dur <= 0:
+            return
+        if batch.is_decode:
+            self._est_decode_s += 0.25 * (dur - self._est_decode_s)
+        elif batch.num_tokens >= 256:
+            per_tok = max(0.0, dur - self._est_fixed_s) / batch.num_tokens
+            self._est_tok_s += 0.25 * (per_tok - self._est_tok_s)
 
     def step(self) -> int:
         """Run one scheduler step; returns the number of sequences processed."""
@@ -292,15 +314,23 @@ class LLMEngine:
                 self._finish(s, SeqStatus.FINISHED, "stop" if eos else "length")
         self.scheduler.drop_finished()
         self.steps += 1
+        self._observe_step(batch, now - max(t_launch, self._t_done))
         if m is not None:
             m.llm_step.labels("decode" if batch.is_decode else "prefill").observe(now - max(t_launch, self._t_done))
-            self._t_done = now
+        self._t_done = now
 
     def _lookahead_step(self, prev, handle, t_prev: float) -> int:
         """The in-flight `prev` cannot be followed by a same-rows decode chain: advance it
         provisionally, schedule the next step from that state, queue it (its placeholder inputs
         fixed up on the device), then read `prev` back and finalize it.  A step that cannot be queued
         early (a decode batch above the largest graph bucket, ...) runs after the readback."""
+        start = max(t_prev, self._t_done)   # the device starts `prev` when the step before it is done
+        est = (self._est_decode_s if prev.is_decode
+               else self._est_fixed_s + self._est_tok_s * max(1, prev.num_tokens))
+        wait = start + est - self.lookahead_margin_s - time.perf_counter()
+        if wait > 0:
+            time.sleep(wait)     # arrivals meanwhile queue in the inbox and join the next step
+            self._drain_inbox()
         self._provisional(prev)
         batch, nh, t_nxt = None, None, 0.0
         if self.scheduler.has_work():
