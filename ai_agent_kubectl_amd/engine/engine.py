@@ -327,10 +327,13 @@ class LLMEngine:
         start = max(t_prev, self._t_done)   # the device starts `prev` when the step before it is done
         est = (self._est_decode_s if prev.is_decode
                else self._est_fixed_s + self._est_tok_s * max(1, prev.num_tokens))
-        wait = start + est - self.lookahead_margin_s - time.perf_counter()
-        if wait > 0:
-            time.sleep(wait)     # arrivals meanwhile queue in the inbox and join the next step
-            self._drain_inbox()
+        until = start + est - self.lookahead_margin_s
+        ev = handle.event
+        # arrivals meanwhile queue in the inbox and join the next step; stop waiting as soon as `prev`
+        # is done on the device (an estimate that runs long must not leave the GPU idle)
+        while ev is not None and time.perf_counter() < until and not ev.query():
+            time.sleep(min(0.0005, max(0.0, until - time.perf_counter())))
+        self._drain_inbox()
         self._provisional(prev)
         batch, nh, t_nxt = None, None, 0.0
         if self.scheduler.has_work():
