@@ -129,7 +129,7 @@ class Scheduler:
         admitted: List[Sequence] = []
         nqs: List[int] = []
         partial = set()
-        budget = self.max_batched_tokens - (len(self.running) if self.mix else 0)
+        budget = self.max_batched_tokens - (self._n_active() if self.mix else 0)
         for seq in self.prefilling:   # continue the chunked prompts (oldest first)
             rem = seq.total_len - seq.num_computed
             c = min(rem, budget)
