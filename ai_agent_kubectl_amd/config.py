@@ -119,7 +119,7 @@ class Settings:
     SAFE_DECODE: bool = True
     IGNORE_EOS: bool = False
     PREFIX_CACHING: bool = True
-    MAX_NUM_BATCHED_TOKENS: int = 4096
+    MAX_NUM_BATCHED_TOKENS: int = 0     # 0: per model (ModelConfig.default_step_tokens)
     FAULT_LLM_DELAY_MS: int = 0
     FAULT_LLM_ERROR: str = ""
     # --- multi-worker HTTP tier (serve.py) ---

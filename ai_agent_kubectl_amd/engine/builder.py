@@ -34,7 +34,7 @@ class EngineOptions:
     tp_size: int = 1
     ep_size: int = 1
     max_batch: int = 256
-    max_batched_tokens: int = 4096
+    max_batched_tokens: int = 0          # 0: the model's default_step_tokens()
     max_model_len: int = 8192      # Llama-3's context; long prompts prefill in chunks
     block_size: int = 16
     kv_cache_tokens: int = 1 << 18  # <= 0: every byte of the GPU_MEM_FRACTION budget
@@ -99,7 +99,8 @@ def build_engine(opts: EngineOptions, comm=None, metrics=None) -> LLMEngine:
                          max_model_len=opts.max_model_len, graph_buckets=opts.graph_buckets, mask_bits=masks,
                          comm=comm, tp_rank=opts.tp_rank, tp_size=opts.tp_size, ep_rank=par.ep_rank,
                          ep_size=ep_size, use_graphs=opts.use_graphs)
-    eng = LLMEngine(runner, tok, max_batch=opts.max_batch, max_batched_tokens=opts.max_batched_tokens,
+    step_tokens = opts.max_batched_tokens if opts.max_batched_tokens > 0 else cfg.default_step_tokens()
+    eng = LLMEngine(runner, tok, max_batch=opts.max_batch, max_batched_tokens=step_tokens,
                     max_model_len=opts.max_model_len, prefix_caching=opts.prefix_caching, metrics=metrics)
     eng.options = opts
     if comm is not None and opts.tp_size > 1:

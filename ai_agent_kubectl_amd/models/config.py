@@ -52,6 +52,15 @@ class ModelConfig:
         per_layer = attn + mlp + 2 * h
         return self.num_layers * per_layer + v * h * (1 if self.tie_embeddings else 2) + h
 
+    def default_step_tokens(self) -> int:
+        """Engine token budget per step when MAX_NUM_BATCHED_TOKENS is 0 (auto).  Each step streams
+        every weight once, so a step has a fixed cost that grows with the model: for an 8B model a
+        256-request wave's ~8k prompt tokens are best split over ~3 mixed steps that also carry the
+        running decodes (4096: 1243-1273 vs 1109-1122 req/s at 16384), while Mixtral-8x7B and
+        Llama-3-70B do better with the wave's prompt in one step (16384: 269 vs 252 and 102 vs 91
+        req/s; profiles/r2/budget/)."""
+        return 4096 if self.num_params() * 2 < (40 << 30) else 16384
+
     def kv_bytes_per_token(self, dtype_bytes: int = 2) -> int:
         return self.num_layers * 2 * self.kv_size * dtype_bytes
 

@@ -100,8 +100,8 @@ def parse_args(argv=None):
     ap.add_argument("--model", default=os.environ.get("BENCH_MODEL", "llama3-8b"))
     ap.add_argument("--max-new-tokens", type=int, default=16)
     ap.add_argument("--max-batched-tokens", type=int,
-                    default=int(os.environ.get("BENCH_MAX_BATCHED_TOKENS", 4096)),
-                    help="engine token budget per step (prefill chunks + decode rows)")
+                    default=int(os.environ.get("BENCH_MAX_BATCHED_TOKENS", 0)),
+                    help="engine token budget per step (prefill chunks + decode rows); 0: the model's default")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--in-process", action="store_true",
                     help="asgi transport: run the engine in this process (default: its own process on the GPU)")
