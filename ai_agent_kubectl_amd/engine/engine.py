@@ -329,6 +329,12 @@ class LLMEngine:
                else self._est_fixed_s + self._est_tok_s * max(1, prev.num_tokens))
         until = start + est - self.lookahead_margin_s
         ev = handle.event
+        if handle.progress is not None:
+            # an eager step marks its progress a few layers before its end: wait for that instead of
+            # the estimate (step sizes vary too much for one)
+            while not handle.progress.query() and not ev.query():
+                time.sleep(0.0003)
+            until = 0.0
         # arrivals meanwhile queue in the inbox and join the next step; stop waiting as soon as `prev`
         # is done on the device (an estimate that runs long must not leave the GPU idle)
         while ev is not None and time.perf_counter() < until and not ev.query():

@@ -41,6 +41,7 @@ class StepHandle(NamedTuple):
     rows: int
     t0: float                             # perf_counter at launch
     prefill_tokens: int = 0               # > 0: a prefill step (launch_prefill_async)
+    progress: Optional["torch.cuda.Event"] = None   # recorded KA_LOOKAHEAD_LAYERS layers before the end
 
 class ModelRunner:
     def __init__(self, cfg: ModelConfig, weights: Dict[str, torch.Tensor], device: torch.device,
@@ -54,6 +55,9 @@ class ModelRunner:
         self.split_mixed_attention = os.environ.get("KA_SPLIT_MIXED_ATTN", "1") == "1"
         self.prefill_pad = int(os.environ.get("KA_PREFILL_PAD", "256"))
         self.prefill_pad_min = int(os.environ.get("KA_PREFILL_PAD_MIN", "1024"))
+        # an async prefill / mixed step records a progress event this many layers before its end: the
+        # engine schedules the step after it once that event has passed (engine._lookahead_step)
+        self.lookahead_layers = int(os.environ.get("KA_LOOKAHEAD_LAYERS", "6"))
         self.tp_rank, self.tp_size = tp_rank, tp_size
         self.model = LlamaModel(cfg, weights, self.comm, tp_rank, tp_size, ep_rank, ep_size)
         self.block_size = block_size
@@ -314,7 +318,13 @@ class ModelRunner:
             n = buf.shape[0]
             buf[:T].index_copy_(0, buf[n - 2 * nf:n - nf].long(), self.d_out.index_select(0, buf[n - nf:].long()))
             buf = buf[:n - 2 * nf]
-        tok = self._run_prefill(buf, T, S, max_q, nc, nd, batch.num_tokens)
+        self.model.mark_layer = max(0, self.cfg.num_layers - self.lookahead_layers)
+        self.model.mark_event = None
+        try:
+            tok = self._run_prefill(buf, T, S, max_q, nc, nd, batch.num_tokens)
+        finally:
+            self.model.mark_layer = -1
+        progress, self.model.mark_event = self.model.mark_event, None
         self.d_out[:S].copy_(tok)
         ho = self._h_pouts[self._pflip]
         self._pflip ^= 1
@@ -323,7 +333,7 @@ class ModelRunner:
         if self.device.type == "cuda":
             ev = torch.cuda.Event()
             ev.record()
-        return StepHandle(ev, ho, S, t0, prefill_tokens=T)
+        return StepHandle(ev, ho, S, t0, prefill_tokens=T, progress=progress)
 
     def _stage_prefill(self, host: np.ndarray) -> torch.Tensor:
         """Packed prefill metadata -> device without a host sync: through one of two pinned buffers

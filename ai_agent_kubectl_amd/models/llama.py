@@ -68,6 +68,9 @@ class LlamaModel:
         # them in fp32): a separate switch so the two can be A/B'd independently
         self.bf16_qkv_partials = os.environ.get("KA_BF16_QKV_PARTIALS", "1") == "1"
         self.layers = [self._layer(i) for i in range(cfg.num_layers)]
+        # eager steps only: record `mark_event` when layer `mark_layer` starts (-1: never)
+        self.mark_layer = -1
+        self.mark_event = None
 
     def _layer(self, i):
         p = f"layers.{i}."
@@ -83,7 +86,11 @@ class LlamaModel:
         residual = None
         pending = False   # h holds this rank's partial of a row-parallel output (TP all-reduce due)
         T = input_ids.shape[0]
+        mark = self.mark_layer
         for li, L in enumerate(self.layers):
+            if li == mark and input_ids.is_cuda:   # progress marker (engine lookahead timing)
+                self.mark_event = torch.cuda.Event()
+                self.mark_event.record()
             if residual is None:
                 residual = h
                 x = ops.rmsnorm(h, L["ln1"], eps)
