@@ -57,7 +57,7 @@ class ModelRunner:
         self.prefill_pad_min = int(os.environ.get("KA_PREFILL_PAD_MIN", "1024"))
         # an async prefill / mixed step records a progress event this many layers before its end: the
         # engine schedules the step after it once that event has passed (engine._lookahead_step)
-        self.lookahead_layers = int(os.environ.get("KA_LOOKAHEAD_LAYERS", "6"))
+        self.lookahead_layers = int(os.environ.get("KA_LOOKAHEAD_LAYERS", "10"))
         self.tp_rank, self.tp_size = tp_rank, tp_size
         self.model = LlamaModel(cfg, weights, self.comm, tp_rank, tp_size, ep_rank, ep_size)
         self.block_size = block_size
