@@ -146,32 +146,10 @@ class LLMEngine:
                 logger.exception("request callback failed")
 
     def _apply(self, batch, tokens) -> None:
-        """Append sampled tokens, publish prefix blocks, finish sequences (EOS / max_new_tokens)."""
-        now = time.perf_counter()
-        m = self.metrics
-        prefill = {id(s) for s in batch.prefill_seqs}
-        partial = batch.partial
-        for s, nq, tok in zip(batch.seqs, batch.num_query, tokens):
-            if s.finished:
-                continue
-            was_prefill = id(s) in prefill
-            s.num_computed += nq
-            if id(s) in partial:   # a chunk of a long prompt: its KV is cached, nothing is sampled
-                self.bm.register_computed(s.block_table, s.all_ids[:s.num_computed], s.block_hashes)
-                continue
-            s.output_ids.append(int(tok))
-            if was_prefill:
-                self.bm.register_computed(s.block_table, s.all_ids[:s.num_computed], s.block_hashes)
-                if s.t_first_token is None:
-                    s.t_first_token = now
-                    if m is not None:
-                        m.llm_ttft.observe(now - s.t_arrival)
-                        m.llm_queue_wait.observe((s.t_scheduled or now) - s.t_arrival)
-            eos = (not s.params.ignore_eos) and self.tokenizer.is_eos(int(tok))
-            if eos or s.num_generated >= s.params.max_new_tokens:
-                if m is not None and s.t_first_token is not None and s.num_generated > 1:
-                    m.llm_tpot.observe((now - s.t_first_token) / (s.num_generated - 1))
-                self._finish(s, SeqStatus.FINISHED, "stop" if eos else "length")
+        """Append sampled tokens, publish prefix blocks, finish sequences (EOS / max_new_tokens): the
+        lookahead path's advance + finalize back to back."""
+        self._advance(batch)
+        self._settle(batch, tokens)
 
     def _chain(self, prev):
         """The decode step after `prev` (in flight, tokens not applied), or None when the batch
@@ -267,11 +245,10 @@ class LLMEngine:
                     m.rccl_allreduce_bytes.inc(nbytes - self._ar_bytes_seen)
                     self._ar_bytes_seen = nbytes
 
-    # ---- lookahead: the next step scheduled and queued before the in-flight one is read back ----
-    def _provisional(self, batch) -> None:
-        """Advance the sequences of the in-flight `batch` as if it had been read back: KV counts move
-        on and every sampling row gets a PLACEHOLDER token (its value is still on the device; the next
-        step's inputs take it from there)."""
+    # ---- applying a step: advance (at launch for lookahead, at readback otherwise), then settle ----
+    def _advance(self, batch) -> None:
+        """Move `batch`'s sequences past its step: KV counts advance and every sampling row gets a
+        PLACEHOLDER token (the sampled value is filled in by `_settle`)."""
         partial = batch.partial
         for row, (s, nq) in enumerate(zip(batch.seqs, batch.num_query)):
             if s.finished:
@@ -281,22 +258,21 @@ class LLMEngine:
                 continue
             s.output_ids.append(PLACEHOLDER)
             s.ph_row = row
-        self.scheduler.on_step_done(batch)
 
-    def _finalize(self, batch, tokens, t_launch: float) -> None:
-        """`_apply` for a batch `_provisional` advanced: placeholders get their sampled tokens, prefix
-        blocks are published, EOS / max_new_tokens finish sequences (a row the step queued ahead
-        computed for a sequence finished here is discarded at its own readback)."""
+    def _settle(self, batch, tokens) -> None:
+        """Placeholders of an advanced `batch` get their sampled tokens; prefix blocks are published;
+        EOS / max_new_tokens finish sequences (a row a lookahead step computed for a sequence
+        finished here is discarded at that step's own readback)."""
         now = time.perf_counter()
         m = self.metrics
         prefill = {id(s) for s in batch.prefill_seqs}
         for s, tok in zip(batch.seqs, tokens):
             if s.finished:
                 continue
-            if id(s) in batch.partial:
+            if id(s) in batch.partial:   # a chunk of a long prompt: its KV is cached, nothing sampled
                 self.bm.register_computed(s.block_table, s.all_ids[:s.num_computed], s.block_hashes)
                 continue
-            if s.ph_row is None:   # not advanced (finished between launch and provisional step)
+            if s.ph_row is None:   # not advanced (finished before the advance)
                 continue
             s.output_ids[-1] = int(tok)
             s.ph_row = None
@@ -312,11 +288,24 @@ class LLMEngine:
                 if m is not None and s.t_first_token is not None and s.num_generated > 1:
                     m.llm_tpot.observe((now - s.t_first_token) / (s.num_generated - 1))
                 self._finish(s, SeqStatus.FINISHED, "stop" if eos else "length")
+
+    # ---- lookahead: the next step scheduled and queued before the in-flight one is read back ----
+    def _provisional(self, batch) -> None:
+        """Advance the in-flight `batch` as if it had been read back (its tokens are still on the
+        device: the next step's inputs take them from there) and update the scheduler's sets."""
+        self._advance(batch)
+        self.scheduler.on_step_done(batch)
+
+    def _finalize(self, batch, tokens, t_launch: float) -> None:
+        """Readback of a `_provisional` batch: settle its tokens, then the step accounting."""
+        self._settle(batch, tokens)
         self.scheduler.drop_finished()
         self.steps += 1
+        now = time.perf_counter()
         self._observe_step(batch, now - max(t_launch, self._t_done))
-        if m is not None:
-            m.llm_step.labels("decode" if batch.is_decode else "prefill").observe(now - max(t_launch, self._t_done))
+        if self.metrics is not None:
+            self.metrics.llm_step.labels("decode" if batch.is_decode else "prefill").observe(
+                now - max(t_launch, self._t_done))
         self._t_done = now
 
     def _lookahead_step(self, prev, handle, t_prev: float) -> int:

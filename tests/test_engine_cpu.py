@@ -575,7 +575,7 @@ def test_scheduler_gather_is_short_for_steady_arrivals():
     while sch.gathering() and time.perf_counter() - t0 < 0.2:
         sch.add(_seq(10))              # an arrival every ~2 ms keeps the quiet gap from closing
         time.sleep(0.002)
-    assert time.perf_counter() - t0 < 0.05
+    assert time.perf_counter() - t0 < 0.08   # well short of gather_max_s (slack for a loaded host)
     sch2 = Scheduler(BlockManager(256, 16), max_batch=64, max_batched_tokens=4096, gather_max_s=0.1,
                      gather_quiet_s=0.005)
     sch2._idle_since, sch2._drained = time.perf_counter(), 64     # a 64-request wave just drained
