@@ -62,6 +62,7 @@ class LLMEngine:
         # running estimates of the step durations (decode: ms per step; prefill / mixed: a fixed part
         # plus ms per token)
         self.lookahead_margin_s = float(os.environ.get("KA_LOOKAHEAD_MARGIN_MS", "8")) / 1000.0
+        self.lookahead_poll_s = float(os.environ.get("KA_LOOKAHEAD_POLL_US", "300")) / 1e6
         self._est_decode_s = 0.007
         self._est_tok_s = 9e-6
         self._est_fixed_s = 0.005
@@ -321,8 +322,11 @@ class LLMEngine:
         if handle.progress is not None:
             # an eager step marks its progress a few layers before its end: wait for that instead of
             # the estimate (step sizes vary too much for one)
-            while not handle.progress.query() and not ev.query():
-                time.sleep(0.0003)
+            if self.lookahead_poll_s > 0:
+                while not handle.progress.query() and not ev.query():
+                    time.sleep(self.lookahead_poll_s)
+            else:
+                handle.progress.synchronize()
             until = 0.0
         # arrivals meanwhile queue in the inbox and join the next step; stop waiting as soon as `prev`
         # is done on the device (an estimate that runs long must not leave the GPU idle)
