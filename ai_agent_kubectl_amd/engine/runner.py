@@ -95,6 +95,7 @@ class ModelRunner:
         # later, when the step that used it has been read back), and the placeholder fixups of a
         # decode step ([dst rows | src rows] of d_out)
         self._h_pre: List[Optional[torch.Tensor]] = [None, None]
+        self._sflip = 0
         self._h_pouts = [torch.zeros(B, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         self._pflip = 0
         self._h_fix = [torch.zeros(2 * B, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
@@ -341,7 +342,7 @@ class ModelRunner:
         if self.device.type != "cuda":
             return torch.from_numpy(host)
         n = host.shape[0]
-        k = self._sflip = getattr(self, "_sflip", 0) ^ 1
+        k = self._sflip = self._sflip ^ 1
         hb = self._h_pre[k]
         if hb is None or hb.numel() < n:
             hb = torch.empty(max(n, 2 * (hb.numel() if hb is not None else 0), 1 << 16), dtype=torch.int32,
