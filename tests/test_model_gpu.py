@@ -163,6 +163,47 @@ def test_graph_decode_equals_eager():
     assert outs[0] == outs[1]
 
 
+def test_lookahead_matches_sync_gpu():
+    """Threaded engine on the GPU (hipGraph decode, chunked prompts, rows of different lengths):
+    with lookahead — steps queued ahead of the readback from pinned staging, placeholder inputs
+    gathered on the device from the in-flight step's samples, progress events — the tokens equal
+    those of the engine without it."""
+    import threading
+    eng = _engine("llama3-8b-2l", graphs=True)
+    be = EngineLLM(eng, max_new_tokens=12, ignore_eos=True)
+    prompts = [be.prompt_ids(q) for q in QUERIES]
+    lens = [3, 12, 6, 9, 2, 7]
+    sch = eng.scheduler
+    sch.max_batched_tokens, sch.min_chunk = 64, 8   # prompts prefilled in chunks, mixed steps
+
+    def run(lookahead):
+        eng.lookahead = lookahead
+        eng.bm.reset_prefix_cache()
+        done, ev = {}, threading.Event()
+
+        def cb(seq):
+            done[seq.seq_id] = seq
+            if len(done) == len(prompts):
+                ev.set()
+
+        eng.start()
+        try:
+            seqs = [eng.submit(p, SamplingParams(max_new_tokens=n, ignore_eos=True), cb, forced_prefix=be._forced)
+                    for p, n in zip(prompts, lens)]
+            assert ev.wait(120)
+        finally:
+            eng.shutdown()
+        return [list(s.output_ids) for s in seqs]
+
+    off = run(False)
+    n0 = eng.lookahead_steps
+    on = run(True)
+    assert eng.lookahead_steps > n0
+    assert on == off
+    assert [len(o) - len(be._forced) for o in on] == lens
+    assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
+
+
 def test_long_context_chunked_prefill_matches_whole():
     """A ~5k-token prompt (MAX_MODEL_LEN 8192) prefilled in 1024-token chunks over several mixed
     steps — each chunk's attention reads the previous chunks from the paged cache — against the
