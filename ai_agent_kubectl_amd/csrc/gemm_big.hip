@@ -1,0 +1,343 @@
+// gemm_big: the prefill / mixed-step projection GEMM (M > 512 token rows):
+//   Y[M, N] = X[M, K] * W[N, K]^T, bf16 in, fp32 accumulate, fused epilogues.
+//
+// Structure (one wave per SIMD, the register budget spent on the MFMA work — the shape rocBLAS' own
+// MT256x256x64 prefill kernel has in profiles/r2/pmc_gemm_r2.md: ~85 % MFMA busy, no barrier waits):
+//   * 256 x 256 output tile per 256-thread workgroup, BK = 64; wave w owns a 128 x 128 quadrant
+//     (W rows 128 * (w & 1), X rows 128 * (w >> 1)): 8 x 8 MFMA 16x16x32 tiles, 256 fp32
+//     accumulators per lane (the AGPR half of the 512-register file), so each k-step reads 16
+//     fragments (ds_read_b128) for 64 MFMAs — a quarter of the LDS traffic per MFMA of the 8-wave
+//     64 x 128-per-wave layout of gemm_mfma.hip's ping-pong kernel;
+//   * W is the MFMA A operand and X the B operand: a lane's four accumulators are four consecutive
+//     output columns (8-B bf16 stores), and the SwiGLU epilogue finds gate and up of one output in
+//     the same lane;
+//   * both operands staged HBM/L2 -> LDS by LDS-DMA (global_load_lds dwordx4), 2 buffers x 64 KB;
+//     the XOR swizzle slot = chunk ^ ((row >> 1) & 7) is applied to the per-lane global source and
+//     to the ds_read address (rule 21), conflict-free fragment reads;
+//   * two register fragment sets: the k-step's second half is read while the first half's 64 MFMAs
+//     run, and the next tile's first half while the second half's run.  ONE barrier per k-tile, and
+//     each tile's DMA is issued two half-steps (2 x 64 MFMAs) before the barrier that waits for it:
+//       phase A(t): read F1 <- (t, k 32..63)     | MFMA F0 | lgkmcnt(0), vmcnt(0) [tile t+1], barrier
+//       phase B(t): read F0 <- (t+1, k 0..31),  DMA tile t+2 -> buffer t&1 | MFMA F1
+//     (WAR: buffer t&1's last reads are F1 of phase A(t), retired before that barrier);
+//   * XCD-aware tile order (T1): the bijective round-robin remap, then GM m-tiles x all n-tiles
+//     super-rows so the panels of the tiles running together on one XCD are L2 hits.
+// Epilogues: bf16 store; SwiGLU over the un-interleaved [gate; up] weight (the tile's W rows are
+// gathered as alternating 16-row gate / up chunks by the DMA source addresses, so the [M, 2I]
+// gate_up output never exists); residual add (Y = X W^T + R, R may alias Y).
+#include "common.h"
+
+#include <utility>
+
+namespace gb {
+
+constexpr int BN = 256, BM = 256, BK = 64, NT = 256;
+#ifndef GB_SWZ_MASK
+#define GB_SWZ_MASK 7   // LDS XOR swizzle bits of the 16-B chunk index (7: conflict-free fragment reads)
+#endif
+constexpr int TILE_A = BN * BK * 2, TILE_B = BM * BK * 2;   // 32 KB each
+constexpr int STAGE = TILE_A + TILE_B, LDS = 2 * STAGE;       // 128 KB
+
+enum Epi : int { EPI_BF16 = 0, EPI_SWIGLU = 3, EPI_ADD = 4 };
+
+struct Args {
+  const bf16_t* X;   // [M, ldx]
+  const bf16_t* W;   // [N, K]  (SwiGLU: [2I, K], gate rows then up rows)
+  bf16_t* Y;         // [M, ldy]
+  const bf16_t* R;   // EPI_ADD: residual [M, ldy] (may be Y)
+  int M, N, K, ldx, ldy, tiles_m, tiles_n, gm;
+  int I;             // SwiGLU: the up rows start at W row I (N == 2I)
+};
+
+// Every instruction of the k-loop is an asm statement, so the program order written below IS the
+// issue order (hipcc may not hoist, sink or regroup volatile asm), and hipcc inserts no waits of its
+// own for these loads: the s_waitcnt / s_barrier statements below are the whole synchronisation.
+//  * ds_read_b128: fragment read (16-bit immediate offset);
+//  * LDS-DMA: buffer_load_dwordx4 ... offen lds through a buffer descriptor (wave-uniform base in
+//    SGPRs, k offset in soffset, one 32-bit VGPR offset per lane); M0 = the wave's LDS destination,
+//    saved and restored inside the statement (M0 is compiler-reserved);
+//  * MFMA with the accumulator pinned in place in the AGPR file ("+a"): the builtin form lets the
+//    register allocator rotate the 64 accumulators through VGPRs (~100 v_accvgpr moves per k-tile
+//    at this register pressure).  An MFMA's D read by anything but the next MFMA's C needs the wait
+//    states of mfma_drain() (hipcc pads nothing inside asm).
+// compile-time unrolled loop: f(std::integral_constant<int, 0>{}) ... f(..N-1): asm immediates
+// ("i" operands) need constants, which a #pragma-unrolled loop variable is not
+template <class F, int... S>
+KA_DEV void static_for_impl(F&& f, std::integer_sequence<int, S...>) {
+  (f(std::integral_constant<int, S>{}), ...);
+}
+template <int N, class F>
+KA_DEV void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int OFF>
+KA_DEV void ds_read16(bf16x8& dst, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
+}
+KA_DEV void dma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(r), "s"(lds_addr), "s"(soff)
+               : "memory");
+}
+KA_DEV void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+KA_DEV void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
+template <int N>
+KA_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+KA_DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+KA_DEV void block_sync() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// logical tile -> (m tile, n tile): XCD-contiguous (bijective), then GM m-tiles x all n-tiles
+KA_DEV void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int per = gm * tiles_n;
+  const int g = L / per, first = g * gm;
+  const int rows = min(gm, tiles_m - first);
+  const int in = L - g * per;
+  tm = first + in % rows;
+  tn = in / rows;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
+  char* const L = reinterpret_cast<char*>(lds);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = w & 1, wm = w >> 1;
+  int tm, tn;
+  tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tm, tn);
+  const int m0 = tm * BM;
+  const int nk = a.K / BK;
+
+  // DMA sources: wave-instruction j (< 8) of this wave fills staged rows (4j + w) * 8 .. + 8 (1 KB)
+  const int r8 = lane >> 3, slot = lane & 7;
+  uint32_t offA[8], offB[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int row = (4 * j + w) * 8 + r8;
+    const uint32_t ch = (uint32_t)(slot ^ (((row >> 1) & 7) & GB_SWZ_MASK)) * 8;
+    int wrow;
+    if constexpr (EPI == EPI_SWIGLU) {
+      // tile tn covers output columns [128 tn, 128 tn + 128): 16-row chunk c of the staged W tile is
+      // gate (c even) or up (c odd) of output columns 128 tn + 16 (c >> 1) + 0..15
+      wrow = 128 * tn + 16 * (row >> 5) + (row & 15) + ((row >> 4) & 1) * a.I;
+    } else {
+      wrow = min(tn * BN + row, a.N - 1);
+    }
+    offA[j] = ((uint32_t)wrow * (uint32_t)a.K + ch) * 2u;
+    offB[j] = ((uint32_t)min(m0 + row, a.M - 1) * (uint32_t)a.ldx + ch) * 2u;
+  }
+  const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(a.W), (short)0, (int)((uint32_t)a.N * (uint32_t)a.K * 2u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(a.X), (short)0, (int)((uint32_t)a.M * (uint32_t)a.ldx * 2u), 0x00020000);
+  // LDS byte address of the staging array (dynamic LDS: the only LDS object of this kernel)
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)lds;
+  const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)w * 1024u);
+  // DMA piece s (< 16) of a k-tile: W rows (s even) or X rows (s odd) group (4 (s >> 1) + w) * 8
+#define GB_DMA(S, BUF, T)                                                                            \
+  dma16(((S) & 1) ? rX : rW, ((S) & 1) ? offB[(S) >> 1] : offA[(S) >> 1], (uint32_t)(T) * (BK * 2), \
+        ldsw + (BUF) * STAGE + ((S) & 1) * TILE_A + ((S) >> 1) * 4096)
+
+  // fragment read bases (bytes, LDS address): [buffer][k half] of the A (W) and B (X) quadrants
+  const int r16 = lane & 15, grp = lane >> 4, sw = ((r16 >> 1) & 7) & GB_SWZ_MASK;
+  const uint32_t c0 = ((0 + grp) ^ sw) * 16, c1 = ((4 + grp) ^ sw) * 16;
+  const uint32_t rA = lds0 + (wn * 128 + r16) * 128, rB = lds0 + TILE_A + (wm * 128 + r16) * 128;
+  const uint32_t bA00 = rA + c0, bA01 = rA + c1, bA10 = rA + STAGE + c0, bA11 = rA + STAGE + c1;
+  const uint32_t bB00 = rB + c0, bB01 = rB + c1, bB10 = rB + STAGE + c0, bB11 = rB + STAGE + c1;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+
+  // read S of a fragment set: A fragment S >> 1 (S even) or B fragment S >> 1 (S odd)
+  auto rd = [&](auto sc, bf16x8* FA, bf16x8* FB, uint32_t ba, uint32_t bb) {
+    constexpr int S = decltype(sc)::value;
+    if constexpr (S & 1) ds_read16<(S >> 1) * 2048>(FB[S >> 1], bb);
+    else ds_read16<(S >> 1) * 2048>(FA[S >> 1], ba);
+  };
+  // MFMAs 4S .. 4S+3 of the 8 x 8 set
+  auto mma4 = [&](auto sc, const bf16x8* FA, const bf16x8* FB) {
+    constexpr int S = decltype(sc)::value;
+    static_for<4>([&](auto qc) {
+      constexpr int q = 4 * S + decltype(qc)::value;
+      mfma_acc(acc[q >> 3][q & 7], FA[q >> 3], FB[q & 7]);
+    });
+  };
+  // phase A of a tile in buffer BUF: its second k half into F1 while F0's MFMAs run; then every read
+  // of buffer BUF retired (WAR for the DMA that refills it) and the next tile landed (this wave's
+  // part; the barrier makes it every wave's)
+#ifndef GB_SPLIT_DMA
+#define GB_SPLIT_DMA 0
+#endif
+  // DMA pieces of tile T issued by phase A / phase B: with GB_SPLIT_DMA the 16 pieces of a tile are
+  // split 8 / 8 between the phase B that starts them and the next phase A (first 8 groups), so no
+  // phase carries more than 8 DMA issues beside its 16 reads and 64 MFMAs
+  constexpr int A_DMA = GB_SPLIT_DMA ? 8 : 0;
+  auto tile_or_oob = [&](int T) { return T < nk ? T : 0x4000000; };   // 0x4000000 * 128 B: past any range
+  auto phase_a = [&](auto bufc, int T) {
+    constexpr int BUF = decltype(bufc)::value;
+    const int tt = tile_or_oob(T);
+    static_for<16>([&](auto sc) {
+      constexpr int S = decltype(sc)::value;
+      rd(sc, fa1, fb1, BUF ? bA11 : bA01, BUF ? bB11 : bB01);
+      if constexpr (S < A_DMA) GB_DMA(16 - A_DMA + S, BUF ^ 1, tt);
+      mma4(sc, fa0, fb0);
+    });
+    wait_lgkm0();
+    wait_vm<0>();
+    block_sync();
+  };
+  // phase B: the next tile's first k half into F0, the DMA of tile T into buffer BUF, F1's MFMAs; F0
+  // retired at the end (covered by the 64 MFMAs).  Past the last tile the reads fetch stale LDS that
+  // no MFMA consumes and the DMA's k offset is out of the buffer's range (the bounds check turns it
+  // into a no-fetch zero fill of a buffer nothing reads again): no control flow in the k-loop.
+  auto phase_b = [&](auto bufc, int T) {
+    constexpr int BUF = decltype(bufc)::value;
+    const int tt = tile_or_oob(T);
+    static_for<16>([&](auto sc) {
+      constexpr int S = decltype(sc)::value;
+      rd(sc, fa0, fb0, BUF ? bA00 : bA10, BUF ? bB00 : bB10);
+      if constexpr (A_DMA == 0) GB_DMA(S, BUF, tt);
+      else if constexpr ((S & 1) == 0) GB_DMA(S >> 1, BUF, tt);
+      mma4(sc, fa1, fb1);
+    });
+    wait_lgkm0();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+
+  // prologue: tile 0 and the phase-B part of tile 1 in flight, wait for tile 0, read its first half
+  static_for<16>([&](auto sc) { GB_DMA(decltype(sc)::value, 0, 0); });
+  static_for<16 - A_DMA>([&](auto sc) { GB_DMA(decltype(sc)::value, 1, tile_or_oob(1)); });
+  wait_vm<16 - A_DMA>();
+  block_sync();
+  static_for<16>([&](auto sc) { rd(sc, fa0, fb0, bA00, bB00); });
+  wait_lgkm0();
+
+  // two tiles per trip so every buffer index is a compile-time constant (K % 128 == 0: no odd tail,
+  // no control flow in the loop but its back edge)
+  for (int t = 0; t < nk; t += 2) {
+    phase_a(I0{}, t + 1);
+    phase_b(I0{}, t + 2);
+    phase_a(I1{}, t + 2);
+    phase_b(I1{}, t + 3);
+  }
+  wait_vm<0>();   // the trailing out-of-range DMAs: nothing may land in LDS after the workgroup ends
+  mfma_drain();
+#undef GB_DMA
+
+  // epilogue.  acc[i][j][r] = C[n = 128 wn + 16 i + 4 grp + r][m = 128 wm + 16 j + r16] of the tile.
+  // The wave's quadrant is transposed through its own 32 KB of LDS (the staging buffers are free
+  // after the barrier below) into [m][n] rows, then stored as whole 16-B lanes: 4 rows x 256 B (SwiGLU:
+  // 8 rows x 128 B) per instruction instead of 8-B pieces scattered over 16 rows.
+#pragma unroll
+  for (int i = 0; i < 8; ++i)   // the asm MFMAs' results are read only after mfma_drain's wait states
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  block_sync();   // every wave is past its last (stale) fragment read of the staging buffers
+  char* const Q = L + w * 32768;
+  if constexpr (EPI == EPI_SWIGLU) {
+    // quadrant: 128 rows (m) x 64 output columns = 128 B per row, 16-B chunk index ^ (row & 7)
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const f32x4 g = acc[2 * p][j], u = acc[2 * p + 1][j];
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = g[r] / (1.f + __expf(-g[r])) * u[r];
+        const int row = 16 * j + r16, col = 16 * p + 4 * grp;   // col: bf16 index in the row
+        const int ch = (col >> 3) ^ (row & 7);
+        *reinterpret_cast<uint2*>(Q + row * 128 + ch * 16 + (col & 4) * 2) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+      }
+    const int rl = lane >> 3, cl = lane & 7;
+    const int ocol = 128 * tn + 64 * wn + 8 * cl;
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int row = 8 * it + rl, m = m0 + 128 * wm + row;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(Q + row * 128 + ((cl ^ (row & 7)) * 16));
+      if (m < a.M) *reinterpret_cast<u32x4*>(a.Y + (size_t)m * a.ldy + ocol) = v;
+    }
+  } else {
+    // quadrant: 128 rows (m) x 128 columns (n) = 256 B per row, 16-B chunk index ^ (row & 15)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const f32x4 v = acc[i][j];
+        const int row = 16 * j + r16, col = 16 * i + 4 * grp;
+        const int ch = (col >> 3) ^ (row & 15);
+        *reinterpret_cast<uint2*>(Q + row * 256 + ch * 16 + (col & 4) * 2) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    const int rl = lane >> 4, cl = lane & 15;
+    const int n = tn * BN + wn * 128 + 8 * cl;
+    if (n < a.N) {
+#pragma unroll
+      for (int it = 0; it < 32; ++it) {
+        const int row = 4 * it + rl, m = m0 + 128 * wm + row;
+        u32x4 v = *reinterpret_cast<const u32x4*>(Q + row * 256 + ((cl ^ (row & 15)) * 16));
+        if (m >= a.M) continue;
+        bf16_t* y = a.Y + (size_t)m * a.ldy + n;
+        if constexpr (EPI == EPI_ADD) {
+          const u32x4 rr = *reinterpret_cast<const u32x4*>(a.R + (size_t)m * a.ldy + n);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = pack2(lo_f(v[q]) + lo_f(rr[q]), hi_f(v[q]) + hi_f(rr[q]));
+        }
+        *reinterpret_cast<u32x4*>(y) = v;
+      }
+    }
+  }
+}
+
+template <int EPI>
+static int launch(const Args& a0, hipStream_t st) {
+  static bool attr = false;
+  auto kern = &gemm256_kernel<EPI>;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  Args a = a0;
+  a.tiles_m = (a.M + BM - 1) / BM;
+  a.tiles_n = EPI == EPI_SWIGLU ? a.I / 128 : (a.N + BN - 1) / BN;
+  hipLaunchKernelGGL(kern, dim3(a.tiles_m * a.tiles_n), dim3(NT), LDS, st, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace gb
+
+// Y = X W^T (+ R).  epi: 0 bf16 Y [M, ldy]; 3 SwiGLU: W = [gate; up] rows (N = 2I), Y [M, ldy] gets
+// silu(x gate^T) * (x up^T), I columns; 4: Y = X W^T + R (R [M, ldy], may alias Y).
+// Requirements: K % 128 == 0, N % 128 == 0 (SwiGLU: I % 128 == 0), 16-B aligned rows (ldx % 8 == 0).
+extern "C" int ka_gemm_big(void* Y, const void* R, const void* X, const void* W, int M, int N, int K, int ldx, int ldy,
+                           int epi, int gm, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K % 128 != 0 || N % 128 != 0 || ldx % 8 != 0 || ldy % 8 != 0) return (int)hipErrorInvalidValue;
+  gb::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), static_cast<bf16_t*>(Y),
+             static_cast<const bf16_t*>(R), M, N, K, ldx, ldy, 0, 0, gm > 0 ? gm : 8, N / 2};
+  switch (epi) {
+    case gb::EPI_BF16: return gb::launch<gb::EPI_BF16>(a, stream);
+    case gb::EPI_SWIGLU:
+      if (N % 256 != 0) return (int)hipErrorInvalidValue;
+      return gb::launch<gb::EPI_SWIGLU>(a, stream);
+    case gb::EPI_ADD:
+      if (R == nullptr) return (int)hipErrorInvalidValue;
+      return gb::launch<gb::EPI_ADD>(a, stream);
+  }
+  return (int)hipErrorInvalidValue;
+}

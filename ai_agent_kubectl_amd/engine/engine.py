@@ -356,8 +356,26 @@ class LLMEngine:
         else:
             self._inflight = None
             if batch is not None and batch.seqs:   # placeholders are real now: run it synchronously
-                self._finish_step(batch, self.runner.execute(batch), t_nxt)
+                # rows whose sequence `prev` just finished (EOS) were scheduled from the provisional
+                # state; `_finish` freed their block tables, so they must not reach the runner
+                batch = self._without_finished(batch)
+                if batch.seqs:
+                    self._finish_step(batch, self.runner.execute(batch), t_nxt)
+                else:
+                    self.scheduler.on_step_done(batch)
         return len(prev.seqs)
+
+    @staticmethod
+    def _without_finished(batch):
+        """`batch` minus the rows of finished sequences (same row order; chunk ids, block copies and the
+        step kind kept: copies only belong to newly admitted rows, which cannot have finished)."""
+        if not any(s.finished for s in batch.seqs):
+            return batch
+        from .scheduler import Batch
+        keep = [(s, nq) for s, nq in zip(batch.seqs, batch.num_query) if not s.finished]
+        return Batch([s for s, _ in keep], [nq for _, nq in keep], is_decode=batch.is_decode,
+                     prefill_seqs=[s for s in batch.prefill_seqs if not s.finished], copies=list(batch.copies),
+                     partial=batch.partial)
 
     def _fail_all(self, err: BaseException) -> None:
         self._inflight = None

@@ -233,6 +233,8 @@ class ModelRunner:
         o, mb = self._off, self.max_blocks
         B = len(batch.seqs)
         for i, s in enumerate(batch.seqs):
+            if not s.block_table:   # a freed (finished) sequence: its slots would alias block 0
+                raise RuntimeError(f"decode row {i} (seq {s.seq_id}) has no KV blocks")
             L = s.total_len + ahead
             pos = L - 1
             h[o["ids"] + i] = s.all_ids[-1] if not ahead else 0
@@ -443,6 +445,8 @@ class ModelRunner:
                 if n > lp:
                     toks.extend(s.output_ids[s.n_forced:s.n_forced + n - lp])
             tbl = s.block_table
+            if not tbl:   # a freed (finished) sequence: its slots would alias block 0
+                raise RuntimeError(f"prefill row {i} (seq {s.seq_id}) has no KV blocks")
             bt[i, :len(tbl)] = tbl
             mask[i] = mask_index_for(ng, s.params.safe_decode)
         n_real = int(nqs.sum())

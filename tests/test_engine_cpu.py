@@ -389,6 +389,55 @@ def test_lookahead_steps_match_sync(tiny_engine):
     assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
 
 
+def test_lookahead_sync_fallback_drops_finished_rows(tiny_engine):
+    """A step scheduled ahead that cannot be queued early (more rows than the largest graph bucket)
+    runs after the in-flight step's readback; rows whose sequence that readback finished (EOS) must
+    leave it before the runner packs it (their freed block tables would alias KV block 0).  Two
+    sequences decode in flight (bmax = 2), five more arrive, EOS stops are frequent (a patched
+    is_eos): the engine, stepped by hand, must sample what it samples with KA_LOOKAHEAD=0."""
+    from ai_agent_kubectl_amd.engine.engine import LLMEngine
+    eng, be = tiny_engine
+    prompts = [be.prompt_ids(q) for q in ("list pods", "get svc -A", "top nodes", "describe pod web-1",
+                                          "logs api", "get deploy", "get services in namespace kube-system")]
+    tok, r, sch = eng.tokenizer, eng.runner, eng.scheduler
+    orig_eos, saved = tok.is_eos, (r.bmax, sch.gather_max_s, sch.prefill_max_wait_s)
+    calls = {"n": 0}
+    orig_filter = LLMEngine._without_finished
+
+    def counting(batch):
+        calls["n"] += any(s.finished for s in batch.seqs)
+        return orig_filter(batch)
+
+    def run(lookahead, k):
+        eng.lookahead = lookahead
+        eng.bm.reset_prefix_cache()
+        seqs = [eng.submit(p, SamplingParams(max_new_tokens=9), None, forced_prefix=be._forced) for p in prompts[:2]]
+        for i in range(400):
+            if i == k:
+                seqs += [eng.submit(p, SamplingParams(max_new_tokens=9), None, forced_prefix=be._forced)
+                         for p in prompts[2:]]
+            eng.step()
+            if i >= k and all(s.finished for s in seqs) and eng._inflight is None:
+                break
+        assert all(s.finished for s in seqs) and eng.healthy
+        return [(list(s.output_ids), s.finish_reason) for s in seqs]
+
+    tok.is_eos = lambda t: orig_eos(t) or t % 5 == 2
+    r.bmax, sch.gather_max_s, sch.prefill_max_wait_s = 2, 0.0, 0.0
+    eng._without_finished = counting
+    try:
+        for k in range(1, 7):
+            on, off = run(True, k), run(False, k)
+            assert on == off, k
+        assert calls["n"] > 0   # the fallback really met rows finished by the readback
+    finally:
+        tok.is_eos = orig_eos
+        r.bmax, sch.gather_max_s, sch.prefill_max_wait_s = saved
+        del eng._without_finished
+        eng.lookahead = True
+    assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
+
+
 def test_chunked_prefill_matches_whole_prefill(tiny_engine):
     """Prompts prefilled in 24-token chunks (through the threaded engine: mixed chunk + decode
     steps, overlapped decode) sample the same tokens as one whole-prompt prefill."""
