@@ -7,8 +7,18 @@ through a thread-safe inbox and per-request callbacks (the asyncio side wraps th
 (`/root/reference/app.py:184`).
 
 Per step: drain inbox/aborts -> `Scheduler.schedule()` -> `ModelRunner.execute()` -> append tokens,
-publish completed prefix blocks, stop on EOS / max_new_tokens -> callbacks.  Failures inside a step
-fail every in-flight request (HTTP 500/503) and mark the engine unhealthy instead of hanging.
+publish completed prefix blocks, stop on EOS / max_new_tokens -> callbacks.
+
+Faults.  A step that raises fails every in-flight request (HTTP 503, the
+reference's degraded-mode status, `/root/reference/app.py:179-180`) instead of hanging, then:
+* recoverable (a host-side error, a transient allocation failure): the engine drops its transient
+  state (KV block tables were freed with the requests, the prefix cache is reset), checks that the
+  device still answers, and serves again — at most `max_recoveries` times per minute;
+* fatal (a one-shot TP collective timed out, a HIP fault, a TP group, or too many recoveries): the
+  engine stays unhealthy (`/ready` 503) and, with `exit_on_fatal` (serve.py / DP replicas), the
+  process exits non-zero so its supervisor restarts it — the reference relies on the same
+  process-level restart (`/root/reference/docker-compose.yml:14`, `restart: unless-stopped`).
+Fault injection: KA_FAULT_STEP=<n>[:fatal|:exit] raises in step n (tests, `FAULT_*` of §5.3).
 """
 from __future__ import annotations
 
@@ -18,14 +28,22 @@ import queue
 import sys
 import threading
 import time
-from typing import Callable, List, Optional
+from typing import Callable, Dict, List, Optional
 
 from .block_manager import make_block_manager
-from .runner import ModelRunner
+from .runner import CollectiveTimeout, ModelRunner
 from .scheduler import Scheduler
 from .sequence import PLACEHOLDER, SamplingParams, Sequence, SeqStatus
 
 logger = logging.getLogger("app.engine")
+
+EXIT_FATAL = 75   # process exit status after an unrecoverable engine fault (supervisors restart on it)
+_FATAL_MARKERS = ("hiperror", "hip error", "illegal memory access", "device-side assert", "launch failure",
+                  "unspecified launch", "gpu hang", "ecc error", "device lost")
+
+
+class InjectedFault(RuntimeError):
+    """KA_FAULT_STEP fault injection (recoverable unless `fatal`)."""
 
 
 class LLMEngine:
@@ -50,6 +68,9 @@ class LLMEngine:
         # overlapped decode: one decode step in flight while the host applies the previous one
         self.overlap = os.environ.get("KA_OVERLAP", "1") == "1"
         self._inflight = None
+        # every admitted, unfinished sequence (a step that raises may hold rows that are in none of
+        # the scheduler's sets yet: admitted by schedule(), added to `running` only at readback)
+        self._live: Dict[int, Sequence] = {}
         self.chained_steps = 0
         self.prefill_chains = 0    # decode steps queued behind a prefill before its readback
         # steps whose batch composition changes (admissions, finished rows, chunk continuations) are
@@ -71,6 +92,17 @@ class LLMEngine:
         self.watchdog = None       # parallel/watchdog.py (TP/EP > 1, rank 0)
         self._ar_bytes_seen = 0
         self._t_done = 0.0         # perf_counter of the last step readback (step-time metric)
+        # fault handling (module docstring)
+        self.exit_on_fatal = os.environ.get("KA_EXIT_ON_FATAL", "0") == "1"
+        self.max_recoveries = int(os.environ.get("KA_MAX_RECOVERIES_PER_MIN", "3"))
+        self.recoveries = 0
+        self.failures = 0
+        self._recovery_times: List[float] = []
+        self._exit = os._exit      # replaced in tests
+        spec = os.environ.get("KA_FAULT_STEP", "")
+        n, _, kind = spec.partition(":")
+        self.fault_step = int(n) if n.strip() else -1
+        self.fault_kind = kind or "error"
 
     def mark_unhealthy(self, reason: str) -> None:
         """Watchdog verdict (worker heartbeat lost / step stalled): new requests get 503."""
@@ -127,17 +159,20 @@ class LLMEngine:
                     continue
                 try:
                     self.scheduler.add(seq)
+                    self._live[seq.seq_id] = seq
                 except ValueError as e:
                     self._finish(seq, SeqStatus.ABORTED, "length", error=e)
             elif op == "abort" and not seq.finished:
                 self.scheduler.abort(seq)
                 seq.finish_reason = "abort"
+                self._live.pop(seq.seq_id, None)
 
     def _finish(self, seq: Sequence, status: SeqStatus, reason: str, error: Optional[BaseException] = None):
         seq.status = status
         seq.finish_reason = reason
         seq.error = error
         seq.t_finish = time.perf_counter()
+        self._live.pop(seq.seq_id, None)
         if seq.block_table:
             self.bm.free_table(seq.block_table)
         if seq.callback is not None:
@@ -197,6 +232,13 @@ class LLMEngine:
     def step(self) -> int:
         """Run one scheduler step; returns the number of sequences processed."""
         self._drain_inbox()
+        if self.fault_step >= 0 and self.steps >= self.fault_step and self.scheduler.has_work():
+            kind, self.fault_step = self.fault_kind, -1   # one shot
+            if kind == "exit":
+                self._exit(EXIT_FATAL)
+            if kind == "fatal":
+                raise CollectiveTimeout("injected collective timeout (KA_FAULT_STEP)")
+            raise InjectedFault("injected engine step fault (KA_FAULT_STEP)")
         if self._inflight is not None:
             prev, handle, t_prev = self._inflight
             nxt = self._chain(prev)
@@ -377,15 +419,45 @@ class LLMEngine:
                      prefill_seqs=[s for s in batch.prefill_seqs if not s.finished], copies=list(batch.copies),
                      partial=batch.partial)
 
+    def is_fatal(self, err: BaseException) -> bool:
+        if isinstance(err, CollectiveTimeout) or self.runner.tp_size > 1:
+            return True   # a TP group cannot be resynchronised from inside one rank
+        msg = repr(err).lower()
+        return any(m in msg for m in _FATAL_MARKERS)
+
+    def _recover(self, err: BaseException) -> bool:
+        """After `_fail_all`: drop transient state and serve again, unless the fault is fatal or
+        recoveries come too often.  Returns whether the engine is healthy again."""
+        now = time.monotonic()
+        self._recovery_times = [t for t in self._recovery_times if now - t < 60.0]
+        if self.is_fatal(err) or len(self._recovery_times) >= self.max_recoveries:
+            return False
+        try:
+            self._inflight = None
+            self.bm.reset_prefix_cache()    # a failed step may have left partly written KV behind
+            self.runner.health_check()
+        except Exception as e2:  # the device itself is gone
+            logger.error("engine recovery failed: %r", e2)
+            self.last_error = e2
+            return False
+        self._recovery_times.append(now)
+        self.recoveries += 1
+        self.healthy = True
+        logger.warning("engine recovered from %r (recovery %d)", err, self.recoveries)
+        return True
+
     def _fail_all(self, err: BaseException) -> None:
         self._inflight = None
         sch = self.scheduler
-        seqs = list(sch.running) + list(sch.prefilling) + list(sch.waiting)
+        seqs = list(sch.running) + list(sch.prefilling) + list(sch.waiting) + list(self._live.values())
         sch.running.clear()
         sch.prefilling.clear()
         sch.waiting.clear()
+        self._live.clear()
+        seen = set()
         for s in seqs:
-            if not s.finished:
+            if not s.finished and s.seq_id not in seen:
+                seen.add(s.seq_id)
                 self._finish(s, SeqStatus.ABORTED, "error", error=err)
 
     def _loop(self) -> None:
@@ -438,12 +510,18 @@ class LLMEngine:
                 self.step_t0 = None
                 if tprof is not None:
                     tprof(n)
-            except Exception as e:  # engine fault: fail in-flight requests, stay alive but unhealthy
+            except Exception as e:  # engine fault: fail in-flight requests, then recover or stop
                 logger.exception("engine step failed")
                 self.step_t0 = None
                 self.healthy = False
                 self.last_error = e
+                self.failures += 1
                 self._fail_all(e)
+                if not self._recover(e):
+                    logger.critical("unrecoverable engine fault: %r", e)
+                    if self.exit_on_fatal:
+                        logger.critical("exiting (status %d) for the supervisor to restart the engine", EXIT_FATAL)
+                        self._exit(EXIT_FATAL)
                 n = 0
             for hook in self.step_end_hooks:
                 hook()

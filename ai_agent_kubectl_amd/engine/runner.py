@@ -33,6 +33,13 @@ KIND_STOP, KIND_DECODE, KIND_PREFILL = 0, 1, 2
 HDR = 8
 
 
+class CollectiveTimeout(RuntimeError):
+    """A one-shot TP collective gave up waiting for a peer (csrc/allreduce.hip's bounded spin set its
+    error word): the step's reduced values are stale, so its tokens must not be used.  Fatal for
+    the process (the TP group's collective epochs are out of step): engine.py fails the in-flight
+    requests with 503 and marks the engine unhealthy / exits for the supervisor to restart it."""
+
+
 
 class StepHandle(NamedTuple):
     """A step queued on the device and not yet read back (`collect`)."""
@@ -42,6 +49,7 @@ class StepHandle(NamedTuple):
     t0: float                             # perf_counter at launch
     prefill_tokens: int = 0               # > 0: a prefill step (launch_prefill_async)
     progress: Optional["torch.cuda.Event"] = None   # recorded KA_LOOKAHEAD_LAYERS layers before the end
+    err_host: Optional[torch.Tensor] = None   # pinned copy of the one-shot collectives' error word
 
 class ModelRunner:
     def __init__(self, cfg: ModelConfig, weights: Dict[str, torch.Tensor], device: torch.device,
@@ -102,6 +110,11 @@ class ModelRunner:
         self.d_fix = torch.zeros(2 * B, dtype=torch.int32, device=self.device)
         self.d_hdr = torch.zeros(HDR, dtype=torch.int32, device=self.device)
         self._h_hdrs = [torch.zeros(HDR, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        # the one-shot TP collectives' error word rides back with every step's tokens (a pinned
+        # 4-byte copy behind them on the same stream: no extra synchronisation), one slot per launch
+        # parity like the token outputs
+        self._h_errs = [torch.zeros(1, dtype=torch.int32, pin_memory=pin) for _ in range(4)]
+        self._eflip = 0
         # TP decode overlap: rank 0 queues step t+1 (header + staging broadcast + graph) before
         # reading step t back.  Needs collectives that are stream-ordered on the device (RCCL):
         # with a host-synchronous transport (gloo) the step still works, it just does not overlap.
@@ -298,11 +311,12 @@ class ModelRunner:
                                                self.d_out.index_select(0, self.d_fix[nf:2 * nf].long()))
         self._launch_decode(Bp, n_copy)
         ho[:B].copy_(self.d_out[:B], non_blocking=True)
+        eh = self._copy_err()
         ev = None
         if self.device.type == "cuda":
             ev = torch.cuda.Event()
             ev.record()
-        return StepHandle(ev, ho, B, t0)
+        return StepHandle(ev, ho, B, t0, err_host=eh)
 
     @torch.inference_mode()
     def launch_prefill_async(self, batch: Batch):
@@ -332,11 +346,12 @@ class ModelRunner:
         ho = self._h_pouts[self._pflip]
         self._pflip ^= 1
         ho[:S].copy_(tok, non_blocking=True)
+        eh = self._copy_err()
         ev = None
         if self.device.type == "cuda":
             ev = torch.cuda.Event()
             ev.record()
-        return StepHandle(ev, ho, S, t0, prefill_tokens=T, progress=progress)
+        return StepHandle(ev, ho, S, t0, prefill_tokens=T, progress=progress, err_host=eh)
 
     def _stage_prefill(self, host: np.ndarray) -> torch.Tensor:
         """Packed prefill metadata -> device without a host sync: through one of two pinned buffers
@@ -353,6 +368,35 @@ class ModelRunner:
         hb.numpy()[:n] = host
         return hb[:n].to(self.device, non_blocking=True)
 
+    @torch.inference_mode()
+    def health_check(self) -> None:
+        """Raise if the device no longer answers: a tiny kernel through the stream and a sync."""
+        probe = self.d_out[:1] + 0
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        int(probe[0].item())
+
+    def _err_word(self) -> Optional[torch.Tensor]:
+        car = getattr(self.comm, "custom_ar", None)
+        return car.state[2:3] if car is not None else None
+
+    def _copy_err(self) -> Optional[torch.Tensor]:
+        """Queue the error word's readback behind the step just launched (None without one-shot
+        collectives)."""
+        src = self._err_word()
+        if src is None:
+            return None
+        h = self._h_errs[self._eflip]
+        self._eflip = (self._eflip + 1) % len(self._h_errs)
+        h.copy_(src, non_blocking=True)
+        return h
+
+    @staticmethod
+    def _check_err(h: Optional[torch.Tensor]) -> None:
+        if h is not None and int(h[0]):
+            raise CollectiveTimeout("one-shot TP collective: a peer never arrived (spin timeout); "
+                                    "the step's results are stale")
+
     def collect(self, handle: "StepHandle") -> List[int]:
         ev, ho, B, t0 = handle.event, handle.host_out, handle.rows, handle.t0
         if handle.prefill_tokens:   # launch_prefill_async
@@ -363,9 +407,11 @@ class ModelRunner:
             self.stats["prefill_tokens"] += handle.prefill_tokens
             self.stats["prefill_ms"] += (now - t0) * 1e3
             self._last_collect = now
+            self._check_err(handle.err_host)
             return ho[:B].tolist()
         if ev is not None:
             ev.synchronize()
+        self._check_err(handle.err_host)
         now = time.perf_counter()
         # wall time attributed to this step: from its launch (or the previous collect, if later)
         self.stats["decode_ms"] += (now - max(t0, getattr(self, "_last_collect", t0))) * 1e3
@@ -508,8 +554,10 @@ class ModelRunner:
             self.d_stage[:n_copy].copy_(self.h_stage[:n_copy], non_blocking=True)
             self._launch_decode(Bp, n_copy)
             self.h_out[:B].copy_(self.d_out[:B], non_blocking=True)
+            eh = self._copy_err()
             if self.device.type == "cuda":
                 torch.cuda.current_stream(self.device).synchronize()
+            self._check_err(eh)
             out = self.h_out[:B].tolist()
             self.stats["decode_steps"] += 1
             self.stats["decode_ms"] += (time.perf_counter() - t0) * 1e3
@@ -522,7 +570,9 @@ class ModelRunner:
         if self.tp_size > 1:
             self.comm.broadcast(buf, src=0)
         tok = self._run_prefill(buf, T, S, max_q, nc, nd, batch.num_tokens)
+        eh = self._copy_err()
         out = tok.cpu().tolist()
+        self._check_err(eh)
         self.stats["prefill_steps"] += 1
         self.stats["prefill_tokens"] += T
         self.stats["prefill_ms"] += (time.perf_counter() - t0) * 1e3
@@ -530,10 +580,15 @@ class ModelRunner:
 
     @torch.inference_mode()
     def worker_loop(self) -> None:
-        """Non-driver TP ranks: mirror every step of rank 0 until it broadcasts STOP."""
+        """Non-driver TP ranks: mirror every step of rank 0 until it broadcasts STOP.  A worker whose
+        one-shot collective timed out is out of step with the group: it raises (the process exits,
+        its heartbeat stops, rank 0's watchdog marks the engine unhealthy).  The error word of a step
+        is read after the next header arrives (that readback synchronises the stream anyway)."""
+        pending = None
         while True:
             self.comm.broadcast(self.d_hdr, src=0)
             kind, a, b, c, d, e, f, g = self.d_hdr[:8].tolist()
+            self._check_err(pending)
             if kind == KIND_STOP:
                 return
             if kind == KIND_DECODE:
@@ -542,6 +597,7 @@ class ModelRunner:
                 buf = torch.empty(d, dtype=torch.int32, device=self.device)
                 self.comm.broadcast(buf, src=0)
                 self._run_prefill(buf, a, b, c, e, f, g)
+            pending = self._copy_err()
 
     def stop_workers(self) -> None:
         self._bcast_header(KIND_STOP)

@@ -116,6 +116,7 @@ def _replica_main(idx: int, device: str, settings_dict: dict, req_conns, resp_qs
     the reply queue of API client c (one per API worker process)."""
     if not isinstance(req_conns, (list, tuple)):
         req_conns, resp_qs = [req_conns], [resp_qs]
+    os.environ.setdefault("KA_EXIT_ON_FATAL", "1")   # a fatal engine fault ends the replica: respawned
     import torch  # noqa: F401  (first CUDA use happens here, in the child)
 
     from ..config import Settings

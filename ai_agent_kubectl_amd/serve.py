@@ -23,6 +23,9 @@ def main(argv=None) -> int:
     from .config import Settings
 
     settings = Settings.from_env()
+    # a serving process exits after an unrecoverable engine fault so that its supervisor (docker's
+    # restart policy, torchrun, the DP supervisor) restarts it (engine/engine.py)
+    os.environ.setdefault("KA_EXIT_ON_FATAL", "1")
     ap = argparse.ArgumentParser(description="MI355X kubectl agent service")
     ap.add_argument("--host", default=settings.HOST)
     ap.add_argument("--port", type=int, default=settings.PORT)

@@ -7,14 +7,17 @@ exactly K*C timed completions, sync + barrier; the job value is total timed requ
 ranks elapsed (weak scaling: per-GPU work is fixed).
 
 Transports (`--transport`):
-  asgi  (default) the full ASGI app (Prometheus + rate-limit middleware, routing, auth, validation,
-        cache, JSON) driven in-process by a minimal ASGI client — no sockets; the engine runs in
-        its own process on the rank's GPU.
-  tcp   the production server over real sockets: `python -m ai_agent_kubectl_amd.serve` with
-        `--api-workers` uvicorn workers on one port (SO_REUSEPORT, shared cache + limiter,
-        parallel/workers.py) in front of the engine replica, and `--client-procs` load-generator
-        processes speaking HTTP/1.1 keep-alive.  This is what the reference's 354 req/s plumbing
-        floor (uvicorn over TCP) measures.
+  tcp   the production topology over real sockets: ONE `python -m ai_agent_kubectl_amd.serve` with
+        DP = N engine replicas (one process per GPU) behind `--api-workers` x N uvicorn workers on
+        one port (SO_REUSEPORT, one shared cache + limiter, parallel/workers.py), and
+        `--client-procs` load-generator processes per rank speaking HTTP/1.1 keep-alive.  This is
+        what the reference's 354 req/s plumbing floor (uvicorn over TCP) measures, so
+        the headline `value` and `vs_baseline` come from it.
+  asgi  the full ASGI app (Prometheus + rate-limit middleware, routing, auth, validation, cache,
+        JSON) driven in-process by a minimal ASGI client — no sockets; the engine runs in its own
+        process on the rank's GPU (one app + engine per rank).
+  both  (default) tcp for the headline, then asgi, then asgi with the prefix cache off; the last two
+        are reported in `detail.asgi` / `detail.prefix_cache_off`.
 
 Load (`--load`): `closed` (default) C clients per GPU, each sending its next distinct cache-miss
 query as soon as the previous reply arrives (BASELINE.md's concurrency-N method); `open` Poisson
@@ -25,7 +28,7 @@ arrivals at `--rate` req/s per GPU (latency under an arrival rate instead of a f
   python bench.py                                   # 1 GPU, defaults (driver form)
   python bench.py --gpus 8                          # spawns 8 ranks itself (torch.distributed.run)
   torchrun --nproc-per-node 8 bench.py --gpus 8     # driver form for N > 1
-  python bench.py --transport tcp --api-workers 2   # over real sockets
+  python bench.py --transport asgi                  # in-process transport only
 """
 import argparse
 import asyncio
@@ -105,9 +108,11 @@ def parse_args(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--in-process", action="store_true",
                     help="asgi transport: run the engine in this process (default: its own process on the GPU)")
-    ap.add_argument("--transport", choices=["asgi", "tcp"], default=os.environ.get("BENCH_TRANSPORT", "asgi"))
+    ap.add_argument("--transport", choices=["asgi", "tcp", "both"], default=os.environ.get("BENCH_TRANSPORT", "both"))
     ap.add_argument("--api-workers", type=int, default=int(os.environ.get("BENCH_API_WORKERS", 2)),
-                    help="tcp: uvicorn API worker processes sharing the port")
+                    help="tcp: uvicorn API worker processes sharing the port, per GPU")
+    ap.add_argument("--no-prefix-off-pass", action="store_true",
+                    help="both: skip the asgi pass with the prefix cache off")
     ap.add_argument("--client-procs", type=int, default=int(os.environ.get("BENCH_CLIENT_PROCS", 2)),
                     help="tcp: load-generator processes")
     ap.add_argument("--load", choices=["closed", "open"], default="closed")
@@ -262,9 +267,21 @@ def _client_proc(cid, nproc, args, rank, port, C, shared, out_q):
 
 
 # ---------------------------------------------------------------------------------------------
-def service_env(args, C, buckets, local, port, kubectl_dir):
-    env = dict(os.environ, LLM_BACKEND="engine", MODEL=args.model, DP="1", ENGINE_DEVICES=os.environ.get(
-        "BENCH_DEVICE", f"cuda:{local}"), WORKERS=str(args.api_workers), HOST="127.0.0.1", PORT=str(port),
+def bench_devices(world):
+    """Engine devices of the N replicas: cuda:0..N-1, or BENCH_DEVICE (one device for every replica,
+    e.g. `cpu` for the CPU test of this path, or a comma list)."""
+    dev = os.environ.get("BENCH_DEVICE", "")
+    if not dev:
+        return [f"cuda:{i}" for i in range(world)]
+    devs = [d.strip() for d in dev.split(",") if d.strip()]
+    return devs if len(devs) >= world else [devs[0]] * world
+
+
+def service_env(args, C, buckets, world, port, kubectl_dir):
+    """serve.py's environment: DP = world replicas (one per GPU), api_workers x world API workers."""
+    env = dict(os.environ, LLM_BACKEND="engine", MODEL=args.model, DP=str(world),
+        ENGINE_DEVICES=",".join(bench_devices(world)), WORKERS=str(args.api_workers * world), HOST="127.0.0.1",
+        PORT=str(port),
         RATE_LIMIT="100000000/minute", CACHE_MAXSIZE=str(cache_size(args)), LLM_TIMEOUT="600", LOG_LEVEL="WARNING",
         MAX_BATCH=str(max(C, 1)), MAX_NEW_TOKENS=str(args.max_new_tokens), IGNORE_EOS="0" if args.variable_len else "1",
         MAX_NUM_BATCHED_TOKENS=str(args.max_batched_tokens), HIPGRAPH_BUCKETS=",".join(str(b) for b in buckets),
@@ -272,6 +289,9 @@ def service_env(args, C, buckets, local, port, kubectl_dir):
         MAX_MODEL_LEN=os.environ.get("MAX_MODEL_LEN", "512"), PYTHONPATH=ROOT,
         PATH=kubectl_dir + os.pathsep + os.environ.get("PATH", ""))
     env.pop("API_AUTH_KEY", None)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
+              "MASTER_PORT", "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)   # the server is not a rank of this job
     if args.no_graphs:
         env["HIPGRAPH_BUCKETS"] = ""
     return env
@@ -301,19 +321,30 @@ async def scrape_engine_metrics(port):
 
 
 def run_tcp(args, rank, local, world, C, buckets, dist):
-    """tcp transport: the production server as a child process + client processes."""
+    """tcp transport: rank 0 starts ONE production server (DP = world replicas, shared cache and
+    limiter across its API workers, one port); every rank drives C closed-loop clients at it from
+    its own load-generator processes and times its own K*C completions."""
     import multiprocessing as mp
 
     kdir = tempfile.mkdtemp(prefix="ka_bench_bin_")
     with open(os.path.join(kdir, "kubectl"), "w") as f:
         f.write(FAKE_KUBECTL)
     os.chmod(os.path.join(kdir, "kubectl"), 0o755)
-    port = _free_port()
     t_build = time.perf_counter()
-    log_path = os.path.join(tempfile.gettempdir(), f"ka_bench_serve_{rank}_{os.getpid()}.log")
-    log = open(log_path, "w")
-    srv = subprocess.Popen([sys.executable, "-m", "ai_agent_kubectl_amd.serve"], env=service_env(
-        args, C, buckets, local, port, kdir), stdout=log, stderr=subprocess.STDOUT, start_new_session=True, cwd=kdir)
+    srv, log, log_path = None, None, None
+    if rank == 0:
+        port = _free_port()
+        log_path = os.path.join(tempfile.gettempdir(), f"ka_bench_serve_{os.getpid()}.log")
+        log = open(log_path, "w")
+        srv = subprocess.Popen([sys.executable, "-m", "ai_agent_kubectl_amd.serve"], env=service_env(
+            args, C, buckets, world, port, kdir), stdout=log, stderr=subprocess.STDOUT, start_new_session=True,
+            cwd=kdir)
+    else:
+        port = 0
+    if world > 1:
+        box = [port]
+        dist.broadcast_object_list(box, src=0)
+        port = box[0]
 
     async def health():
         conn = HttpConn("127.0.0.1", port)
@@ -324,34 +355,39 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
             conn.close()
 
     try:
-        deadline = time.time() + 1500
-        while True:
-            if srv.poll() is not None:
-                raise RuntimeError("server exited: " + open(log_path).read()[-3000:])
-            try:
-                if asyncio.run(health()):
-                    break
-            except OSError:
-                pass
-            if time.time() > deadline:
-                raise RuntimeError("server did not come up")
-            time.sleep(1.0)
-        # the first request of each API worker waits for the engine replica (start + autotune +
-        # hipGraph capture): one request per worker before timing anything
-        async def prime():
-            conns = [HttpConn("127.0.0.1", port) for _ in range(4 * args.api_workers)]
-            rs = await asyncio.gather(*[c.request("POST", "/kubectl-command", b'{"query":"prime %d %d"}' % (rank, j))
-                                        for j, c in enumerate(conns)])
-            if args.mix:   # hot queries for the hit class
-                rs += [await conns[0].request("POST", "/kubectl-command", b'{"query":' + json.dumps(
-                    hot_query(rank, j)).encode() + b"}") for j in range(32)]
-            for c in conns:
-                c.close()
-            return rs
-        rs = asyncio.run(prime())
-        bad = [r for r in rs if r[0] != 200]
-        if bad:
-            raise RuntimeError(f"priming failed: {bad[:2]}")
+        if rank == 0:
+            deadline = time.time() + 1500
+            while True:
+                if srv.poll() is not None:
+                    raise RuntimeError("server exited: " + open(log_path).read()[-3000:])
+                try:
+                    if asyncio.run(health()):
+                        break
+                except OSError:
+                    pass
+                if time.time() > deadline:
+                    raise RuntimeError("server did not come up")
+                time.sleep(1.0)
+
+            # the first request of each API worker waits for every engine replica (start + autotune
+            # + hipGraph capture): prime every worker before timing anything
+            async def prime():
+                conns = [HttpConn("127.0.0.1", port) for _ in range(4 * args.api_workers * world)]
+                rs = await asyncio.gather(*[c.request("POST", "/kubectl-command", b'{"query":"prime %d"}' % j)
+                                            for j, c in enumerate(conns)])
+                if args.mix:   # hot queries for the hit class, inserted through ONE worker: the other
+                    for r in range(world):   # workers' hits prove the cache is shared
+                        rs += [await conns[0].request("POST", "/kubectl-command", b'{"query":' + json.dumps(
+                            hot_query(r, j)).encode() + b"}") for j in range(32)]
+                for c in conns:
+                    c.close()
+                return rs
+            rs = asyncio.run(prime())
+            bad = [r for r in rs if r[0] != 200]
+            if bad:
+                raise RuntimeError(f"priming failed: {bad[:2]}")
+        if world > 1:
+            dist.barrier()
         t_build = time.perf_counter() - t_build
 
         ctx = mp.get_context("spawn")
@@ -367,7 +403,7 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
             time.sleep(0.005)
         if world > 1:
             dist.barrier()
-        m0 = asyncio.run(scrape_engine_metrics(port))
+        m0 = asyncio.run(scrape_engine_metrics(port)) if rank == 0 else {}
         with done.get_lock():
             done.value = 0
         phase.value = 1
@@ -377,7 +413,7 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
             time.sleep(0.001)
         elapsed = time.perf_counter() - t0
         phase.value = 2
-        m1 = asyncio.run(scrape_engine_metrics(port))
+        m1 = asyncio.run(scrape_engine_metrics(port)) if rank == 0 else {}
         if world > 1:
             dist.barrier()
         lat = {}
@@ -389,6 +425,8 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
                 lat.setdefault(k, []).extend(v)
         for p in procs:
             p.join(timeout=30)
+        if world > 1:
+            dist.barrier()   # every rank's clients are done before rank 0 stops the server
         if errors:
             raise RuntimeError("bad replies: %s" % errors[:3])
         d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1}
@@ -397,16 +435,17 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
               "queue_wait_ms_mean": round(d.get("qwait_sum", 0.0) * 1e3 / max(1.0, d.get("qwait_count", 0.0)), 2)}
         return elapsed, lat, st, t_build, None
     finally:
-        if srv.poll() is None:
-            os.killpg(srv.pid, 15)
-            try:
-                srv.wait(60)
-            except subprocess.TimeoutExpired:
-                os.killpg(srv.pid, 9)
-        log.close()
+        if srv is not None:
+            if srv.poll() is None:
+                os.killpg(srv.pid, 15)
+                try:
+                    srv.wait(60)
+                except subprocess.TimeoutExpired:
+                    os.killpg(srv.pid, 9)
+            log.close()
 
 
-def run_asgi(args, rank, local, world, C, buckets, dist):
+def run_asgi(args, rank, local, world, C, buckets, dist, prefix_caching=True):
     """asgi transport: the full app in this process, driven by a minimal in-process ASGI client."""
     import torch
 
@@ -422,7 +461,7 @@ def run_asgi(args, rank, local, world, C, buckets, dist):
                         LOG_LEVEL="WARNING",
                         LLM_BACKEND="engine", MODEL=args.model, MAX_BATCH=max(C, 1), MAX_NEW_TOKENS=args.max_new_tokens,
                         IGNORE_EOS=not args.variable_len, MAX_NUM_BATCHED_TOKENS=args.max_batched_tokens,
-                        HIPGRAPH_BUCKETS=",".join(str(b) for b in buckets))
+                        HIPGRAPH_BUCKETS=",".join(str(b) for b in buckets), PREFIX_CACHING=prefix_caching)
     os.environ.setdefault("KV_CACHE_TOKENS", str(max(65536, C * 528)))
     os.environ.setdefault("MAX_MODEL_LEN", "512")
     t_build = time.perf_counter()
@@ -431,8 +470,8 @@ def run_asgi(args, rank, local, world, C, buckets, dist):
         # GPU); this process runs the ASGI app + load generator, so HTTP handling and the GPU loop
         # never share a GIL.  Barriers use gloo; the device sync runs inside the engine process.
         from ai_agent_kubectl_amd.parallel.dp import DPRouterLLM
-        backend = DPRouterLLM(settings, 1, devices=[os.environ.get("BENCH_DEVICE", f"cuda:{local}")])
-        if world > 1:
+        backend = DPRouterLLM(settings, 1, devices=[bench_devices(world)[local]])
+        if world > 1 and not dist.is_initialized():
             dist.init_process_group("gloo")
         backend.wait_ready()
         if not any(r.up for r in backend.replicas):
@@ -441,12 +480,12 @@ def run_asgi(args, rank, local, world, C, buckets, dist):
     else:
         torch.cuda.set_device(local)
         dev = torch.device(f"cuda:{local}")
-        if world > 1:
+        if world > 1 and not dist.is_initialized():
             dist.init_process_group("nccl", device_id=dev)
         from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine
         from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM
         opts = EngineOptions(model=args.model, device=str(dev), max_batch=max(C, 1), graph_buckets=buckets,
-                             kv_cache_tokens=max(65536, C * 528), max_model_len=512,
+                             kv_cache_tokens=max(65536, C * 528), max_model_len=512, prefix_caching=prefix_caching,
                              use_graphs=not args.no_graphs, ignore_eos=not args.variable_len, max_batched_tokens=args.max_batched_tokens)
         eng = build_engine(opts)
         eng.runner.capture_graphs()
@@ -617,16 +656,44 @@ def main():
 
     import torch.distributed as dist
 
-    if args.transport == "tcp":
-        if world > 1:
-            dist.init_process_group("gloo")
-        elapsed, lat, st, t_build, extra = run_tcp(args, rank, local, world, C, buckets, dist)
-        reply, seq_len = None, prompt_len(args.model) + args.max_new_tokens
-    else:
-        elapsed, lat, st, t_build, extra = run_asgi(args, rank, local, world, C, buckets, dist)
-        reply, prompt = extra
-        seq_len = len(prompt) + args.max_new_tokens
+    if world > 1 and not (args.transport == "asgi" and args.in_process):
+        dist.init_process_group("gloo")   # barriers / gathers only (no rank touches a GPU itself)
+    passes = {"tcp": ["tcp"], "asgi": ["asgi"],
+              "both": ["tcp", "asgi"] + ([] if args.no_prefix_off_pass else ["asgi-prefix-off"])}[args.transport]
+    results = {}
+    for name in passes:
+        if name == "tcp":
+            r = run_tcp(args, rank, local, world, C, buckets, dist)
+            seq_len = prompt_len(args.model) + args.max_new_tokens
+        else:
+            r = run_asgi(args, rank, local, world, C, buckets, dist, prefix_caching=name == "asgi")
+            seq_len = len(r[4][1]) + args.max_new_tokens
+        results[name] = summarize(args, name, world, C, dist, r, seq_len)
+    if rank == 0:
+        head = results[passes[0]]
+        out = dict(head["out"])
+        detail = out["detail"]
+        for name in passes[1:]:
+            key = "asgi" if name == "asgi" else "prefix_cache_off"
+            detail[key] = results[name]["compact"]
+        for name in passes:
+            if name in ("tcp", "asgi"):
+                out[f"{name}_value"] = results[name]["out"]["value"]
+                out[f"{name}_p50_ms"] = results[name]["out"]["p50_ms"]
+        if "tcp" in results and "asgi" in results:
+            detail["tcp_vs_asgi"] = round(results["tcp"]["out"]["value"] / results["asgi"]["out"]["value"], 3)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
+
+def summarize(args, name, world, C, dist, r, seq_len):
+    """One pass's JSON (headline form) and compact form; elapsed is the max over ranks."""
+    elapsed, lat, st, t_build, extra = r
+    rank = int(os.environ.get("RANK", "0"))
+    transport = "tcp" if name == "tcp" else "asgi"
+    reply = extra[0] if extra else None
     n_req = C * args.steps
     allv = [v for k in ("miss", "hit", "exec") for v in lat.get(k, [])]
     p50 = statistics.median(allv) * 1e3 if allv else float("nan")
@@ -642,47 +709,52 @@ def main():
     def pct(v, q):
         return round(sorted(v)[int(q * (len(v) - 1))] * 1e3, 2) if v else None
 
-    if rank == 0:
-        detail = {"concurrency_per_gpu": C, "new_tokens": args.max_new_tokens, "transport": args.transport,
-                  "load": args.load + (f"@{args.rate}/s" if args.load == "open" else ""),
-                  "p99_ms": pct(allv, 0.99), "build_s": round(t_build, 1), "sample_reply": reply,
-                  "baseline": "BASELINE.md reference plumbing floor, cache-miss conc 32 = 354 req/s (uvicorn, TCP)"}
-        if args.transport == "tcp":
-            detail.update(api_workers=args.api_workers, client_procs=args.client_procs)
-        if args.mix:
-            detail["mix"] = {k: {"n": len(v), "p50_ms": pct(v, 0.5), "p99_ms": pct(v, 0.99)} for k, v in lat.items()}
-        if st and args.transport == "tcp":   # from the server's Prometheus histograms
-            detail.update({
-                "decode_steps": st["decode_steps"], "prefill_steps": st["prefill_steps"],
-                "decode_ms_per_step": round(st["decode_ms"] / max(1, st["decode_steps"]), 3),
-                "prefill_ms_per_step": round(st["prefill_ms"] / max(1, st["prefill_steps"]), 3),
-                "queue_wait_ms_mean": st["queue_wait_ms_mean"], "engine_stats_from": "/metrics"})
-        elif st:
-            detail.update({
-                "decode_steps": st.get("decode_steps"), "prefill_steps": st.get("prefill_steps"),
-                "decode_ms_per_step": round(st["decode_ms"] / max(1, st["decode_steps"]), 3),
-                "prefill_ms_per_step": round(st["prefill_ms"] / max(1, st["prefill_steps"]), 3),
-                "prefill_tokens": st.get("prefill_tokens"), "graph_replays": st.get("graph_replays"),
-                "prefix_cache_hit_rate": round(st.get("prefix_hits", 0) / max(1, st.get("prefix_queries", 0)), 3),
-                "sub_block_reused_tokens": st.get("partial_tokens", 0),
-                "overlapped_decode_steps": st.get("chained_steps", 0),
-                "engine_idle_ms_per_step": round(st.get("engine_idle_s", 0.0) * 1e3 / args.steps, 2),
-                "engine_process": not args.in_process})
-        out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "req/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": round(value / BASELINE_RPS, 3),
-            "dtype": "bf16", "data": "synthetic queries, random-init weights",
-            "config": {"model": "Llama-3-8B-Instruct" if args.model == "llama3-8b" else args.model,
-                       "global_batch": C * world, "seq_len": seq_len, "parallelism": f"dp{world}"},
-            "p50_ms": round(p50, 2), "detail": detail,
-        }
-        if args.mix:
-            out["config"]["mix"] = f"hit {args.hit_frac} exec {args.exec_frac} miss {1 - args.hit_frac - args.exec_frac}"
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    detail = {"concurrency_per_gpu": C, "new_tokens": args.max_new_tokens, "transport": transport,
+              "load": args.load + (f"@{args.rate}/s" if args.load == "open" else ""),
+              "p99_ms": pct(allv, 0.99), "build_s": round(t_build, 1), "sample_reply": reply,
+              "baseline": "BASELINE.md reference plumbing floor, cache-miss conc 32 = 354 req/s (uvicorn, TCP)"}
+    if transport == "tcp":
+        detail.update(topology=f"one server: DP={world} replicas, {args.api_workers * world} API workers, one port",
+                      api_workers=args.api_workers * world, client_procs_per_rank=args.client_procs)
+    if name == "asgi-prefix-off":
+        detail["prefix_caching"] = False
+    if args.mix:
+        detail["mix"] = {k: {"n": len(v), "p50_ms": pct(v, 0.5), "p99_ms": pct(v, 0.99)} for k, v in lat.items()}
+    if st and transport == "tcp":   # from the server's Prometheus histograms
+        detail.update({
+            "decode_steps": st["decode_steps"], "prefill_steps": st["prefill_steps"],
+            "decode_ms_per_step": round(st["decode_ms"] / max(1, st["decode_steps"]), 3),
+            "prefill_ms_per_step": round(st["prefill_ms"] / max(1, st["prefill_steps"]), 3),
+            "queue_wait_ms_mean": st["queue_wait_ms_mean"], "engine_stats_from": "/metrics"})
+    elif st:
+        detail.update({
+            "decode_steps": st.get("decode_steps"), "prefill_steps": st.get("prefill_steps"),
+            "decode_ms_per_step": round(st["decode_ms"] / max(1, st["decode_steps"]), 3),
+            "prefill_ms_per_step": round(st["prefill_ms"] / max(1, st["prefill_steps"]), 3),
+            "prefill_tokens": st.get("prefill_tokens"), "graph_replays": st.get("graph_replays"),
+            "prefix_cache_hit_rate": round(st.get("prefix_hits", 0) / max(1, st.get("prefix_queries", 0)), 3),
+            "sub_block_reused_tokens": st.get("partial_tokens", 0),
+            "overlapped_decode_steps": st.get("chained_steps", 0),
+            "engine_idle_ms_per_step": round(st.get("engine_idle_s", 0.0) * 1e3 / args.steps, 2),
+            "engine_process": not args.in_process})
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "req/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": round(value / BASELINE_RPS, 3),
+        "dtype": "bf16", "data": "synthetic queries, random-init weights",
+        "config": {"model": "Llama-3-8B-Instruct" if args.model == "llama3-8b" else args.model,
+                   "global_batch": C * world, "seq_len": seq_len, "parallelism": f"dp{world}"},
+        "p50_ms": round(p50, 2), "detail": detail,
+    }
+    if args.mix:
+        out["config"]["mix"] = f"hit {args.hit_frac} exec {args.exec_frac} miss {1 - args.hit_frac - args.exec_frac}"
+    compact = {"value": out["value"], "p50_ms": out["p50_ms"], "p99_ms": detail["p99_ms"],
+               "ms_per_step": out["ms_per_step"]}
+    for k in ("decode_ms_per_step", "prefill_ms_per_step", "prefill_steps", "decode_steps", "prefill_tokens",
+              "prefix_cache_hit_rate"):
+        if k in detail:
+            compact[k] = detail[k]
+    return {"out": out, "compact": compact}
 
 
 if __name__ == "__main__":

@@ -41,6 +41,13 @@ def _run(args, world, launcher="torchrun"):
 def test_bench_prints_one_json_line(world, launcher):
     out = _run([], world, launcher)
     assert KEYS <= set(out)
+    # default: the headline over TCP through ONE server (DP = world replicas, one port), then the
+    # in-process ASGI transport and an ASGI pass with the prefix cache off, in detail
+    d = out["detail"]
+    assert d["transport"] == "tcp" and f"DP={world} replicas" in d["topology"]
+    assert out["tcp_value"] == out["value"] and out["asgi_value"] == d["asgi"]["value"] > 0
+    assert d["prefix_cache_off"]["value"] > 0 and d["prefix_cache_off"]["prefix_cache_hit_rate"] == 0
+    assert d["tcp_vs_asgi"] > 0
     assert out["n_gpus"] == world and out["steps"] == 1 and out["warmup"] == 1
     assert out["higher_is_better"] is True and out["scaling"] == "weak" and out["unit"] == "req/s"
     assert out["value"] > 0 and out["ms_per_step"] > 0
@@ -56,6 +63,18 @@ def test_bench_gpus_must_match_world_size():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
                        text=True, timeout=120, env=env, cwd="/tmp")
     assert r.returncode != 0 and "does not match WORLD_SIZE" in r.stderr
+
+
+def test_bench_tcp_one_server_dp2_shared_cache():
+    """--gpus 2 --transport tcp --mix: ONE server with DP=2 engine replicas and 4 API workers on one
+    port (the deployed topology, parallel/workers.py); the hit class's queries were inserted
+    through one worker, and every hit answered by any worker must say from_cache=true (bench.py
+    reply_ok), so the cache is shared across workers."""
+    out = _run(["--transport", "tcp", "--mix", "--hit-frac", "0.5", "--exec-frac", "0.1"], 2)
+    d = out["detail"]
+    assert "DP=2 replicas, 4 API workers" in d["topology"] and out["n_gpus"] == 2
+    assert d["mix"]["hit"]["n"] > 0 and d["mix"]["miss"]["n"] > 0
+    assert out["value"] == pytest.approx(8 / (out["ms_per_step"] / 1e3), rel=0.02)
 
 
 def test_bench_tcp_transport():

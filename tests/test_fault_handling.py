@@ -1,0 +1,125 @@
+"""Engine fault handling: a failing step answers 503 for its in-flight requests, a
+recoverable fault leaves the engine serving again, a fatal one (a one-shot TP collective that timed
+out waiting for a peer, csrc/allreduce.hip's error word) never returns the step's stale tokens and
+stops the engine (exit for the supervisor).  The reference's only recovery is the container
+restart policy (`/root/reference/docker-compose.yml:14`)."""
+import asyncio
+
+import httpx
+import pytest
+import torch
+
+from ai_agent_kubectl_amd.engine.engine import EXIT_FATAL
+from ai_agent_kubectl_amd.engine.runner import CollectiveTimeout
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine
+    from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM
+    eng = build_engine(EngineOptions(model="tiny-llama", device="cpu", max_batch=8, graph_buckets=(1, 2, 4, 8),
+                                     kv_cache_tokens=8192, max_model_len=512))
+    return eng, EngineLLM(eng, max_new_tokens=6)
+
+
+def _app(be):
+    from ai_agent_kubectl_amd.api import create_app
+    from ai_agent_kubectl_amd.config import Settings
+    return create_app(Settings(RATE_LIMIT="100000/minute", CACHE_TTL=0), backend=be)
+
+
+async def _post_all(app, be, queries):
+    await be.start()
+    try:
+        async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://t") as c:
+            return await asyncio.gather(*[c.post("/kubectl-command", json={"query": q}) for q in queries])
+    finally:
+        await be.close()
+
+
+class _FakeOneShot:
+    """Stands in for parallel/custom_allreduce.OneShotAllReduce: only its state word matters here."""
+
+    def __init__(self, err: int):
+        self.state = torch.tensor([0, 0, err, 0], dtype=torch.int32)
+
+
+def test_recoverable_step_fault_fails_inflight_then_serves_again(tiny):
+    eng, be = tiny
+    app = _app(be)
+    eng.fault_step, eng.fault_kind = eng.steps, "error"
+    r0 = eng.recoveries
+    try:
+        rs = asyncio.run(_post_all(app, be, ["list pods", "get nodes", "top pods"]))
+        codes = [r.status_code for r in rs]
+        # the requests in the faulting step get 503; any admitted after the recovery are served
+        assert codes[0] == 503 and set(codes) <= {200, 503}, codes
+        assert "injected engine step fault" in rs[0].json()["detail"]
+        assert eng.healthy and eng.recoveries == r0 + 1
+        rs = asyncio.run(_post_all(app, be, ["list pods", "describe svc api"]))
+        assert [r.status_code for r in rs] == [200, 200]
+        assert all(r.json()["kubectl_command"].startswith("kubectl ") for r in rs)
+    finally:
+        eng.fault_step = -1
+        eng.healthy = True
+    assert all(eng.bm.ref_count(b) == 0 for b in range(eng.bm.num_blocks))
+
+
+def test_collective_timeout_is_503_never_200_and_fatal(tiny):
+    """The one-shot collectives' error word set (a peer never arrived) turns the step into a
+    CollectiveTimeout at readback: the requests get 503 (not the stale tokens with 200), the engine
+    stays unhealthy (/ready 503) and, with exit_on_fatal, exits with EXIT_FATAL."""
+    from fastapi.testclient import TestClient
+    eng, be = tiny
+    app = _app(be)
+    comm = eng.runner.comm
+    exits = []
+    saved_exit, saved_flag = eng._exit, eng.exit_on_fatal
+    comm.custom_ar = _FakeOneShot(err=1)
+    eng._exit, eng.exit_on_fatal = exits.append, True
+    try:
+        rs = asyncio.run(_post_all(app, be, ["list pods", "get svc"]))
+        assert [r.status_code for r in rs] == [503, 503]
+        assert "peer never arrived" in rs[0].json()["detail"]
+        assert not eng.healthy and isinstance(eng.last_error, CollectiveTimeout)
+        assert exits == [EXIT_FATAL]
+        with TestClient(app) as c:
+            assert c.get("/ready").status_code == 503
+            assert c.post("/kubectl-command", json={"query": "list all pods now"}).status_code == 503
+    finally:
+        del comm.custom_ar
+        eng._exit, eng.exit_on_fatal = saved_exit, saved_flag
+        eng.healthy, eng.last_error = True, None
+
+
+def test_error_word_clear_is_transparent(tiny):
+    """A zero error word changes nothing (the readback rides behind every step's tokens)."""
+    eng, be = tiny
+    from ai_agent_kubectl_amd.engine.sequence import SamplingParams
+    params = SamplingParams(max_new_tokens=5, ignore_eos=True)
+    ids = be.prompt_ids("list pods in prod")
+    eng.bm.reset_prefix_cache()
+    plain = eng.generate_blocking([ids], params, forced_prefix=be._forced)[0].output_ids
+    eng.runner.comm.custom_ar = _FakeOneShot(err=0)
+    try:
+        eng.bm.reset_prefix_cache()
+        with_word = eng.generate_blocking([ids], params, forced_prefix=be._forced)[0].output_ids
+    finally:
+        del eng.runner.comm.custom_ar
+    assert plain == with_word
+
+
+def test_repeated_faults_become_fatal(tiny):
+    eng, be = tiny
+    saved = eng.max_recoveries, list(eng._recovery_times)
+    eng.max_recoveries = 1
+    eng._recovery_times = []
+    try:
+        assert eng._recover(RuntimeError("transient")) and eng.healthy
+        assert not eng._recover(RuntimeError("transient again"))
+        assert eng.is_fatal(RuntimeError("HIP error: an illegal memory access was encountered"))
+        assert eng.is_fatal(CollectiveTimeout("x"))
+        assert not eng.is_fatal(RuntimeError("some host-side bug"))
+    finally:
+        eng.max_recoveries, eng._recovery_times = saved
+        eng.healthy = True
