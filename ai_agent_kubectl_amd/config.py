@@ -109,7 +109,7 @@ class Settings:
     WEIGHTS: str = "random:0"            # safetensors dir/file or random:<seed>
     TP: int = 1
     DP: int = 1
-    ENGINE_PROCESS: bool = True          # TP=1: run the engine in its own process (API keeps its GIL)
+    ENGINE_PROCESS: bool = True          # run the engine (a TP group) in its own process(es): the API keeps its GIL
     EP: int = 1
     MAX_BATCH: int = 256
     MAX_NEW_TOKENS: int = 24

@@ -53,9 +53,12 @@ def build_backend(settings, metrics=None) -> Optional[LLMBackend]:
         from .remote import OpenAIChatLLM
         return OpenAIChatLLM(settings)
     if kind == "engine":
-        if settings.DP > 1 or (settings.ENGINE_PROCESS and settings.TP == 1):
-            # engine replica process(es) behind this API process: HTTP handling and the GPU loop
-            # never contend for one GIL (SURVEY.md §7.3 hard part 6)
+        import os
+        under_torchrun = int(os.environ.get("WORLD_SIZE", "1")) > 1
+        if settings.DP > 1 or (settings.ENGINE_PROCESS and not under_torchrun):
+            # engine replica process(es) — each a TP group of TP devices — behind this API process:
+            # HTTP handling and the GPU loop never contend for one GIL (SURVEY.md §7.3 hard part 6).
+            # Under torchrun with TP > 1 this process is TP rank 0 itself (serve.py).
             from ..parallel.dp import DPRouterLLM
             return DPRouterLLM(settings, max(1, settings.DP))
         from .engine_backend import EngineLLM

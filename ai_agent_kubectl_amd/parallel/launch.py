@@ -28,7 +28,9 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> Tup
     if dist.is_initialized():
         return dist.get_rank(), dist.get_world_size(), local
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # KA_TP_BACKEND=gloo: several ranks on ONE GPU (tests on a 1-GPU box: RCCL refuses two ranks
+        # on one device; the decode collectives still run as the one-shot IPC kernels)
+        backend = os.environ.get("KA_TP_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     kw = {"backend": backend, "rank": rank, "world_size": world,
           "timeout": datetime.timedelta(seconds=timeout_s)}
     if backend == "nccl":

@@ -7,15 +7,16 @@ completes, and far below 8 GPUs' worth.  `serve.py` with WORKERS > 1 runs this s
   supervisor (no GPU use)
    ├─ shared-memory segment: response cache + rate-limit windows (shared_state.py), so
    │  `from_cache` (app.py:312-322) and 429 (app.py:298,368) stay global across workers
-   ├─ DP engine replicas, one process per device, each serving all W workers (dp.spawn_replicas)
+   ├─ DP engine replicas (dp.ReplicaSupervisor), each a TP group of TP devices, each serving all
+   │  W workers over its Unix socket; a replica that dies is respawned
    └─ W API workers: each binds HOST:PORT with SO_REUSEPORT (the kernel spreads connections),
       runs the full app (auth, validation, limiter, cache, Prometheus) under uvicorn and routes
       its misses to the least-loaded replica.  /metrics aggregates every worker
       (prometheus_client multiprocess mode: PROMETHEUS_MULTIPROC_DIR).
 
-The supervisor restarts nothing; a dead worker is logged and the rest keep serving (the kernel
-stops routing to a closed SO_REUSEPORT socket).  SIGTERM / SIGINT stop everything and remove the
-shared-memory segment and the metrics directory.
+A dead API worker is respawned too (its socket is re-bound with SO_REUSEPORT; the kernel stops
+routing to the dead one's).  SIGTERM / SIGINT stop everything and remove the shared-memory segment
+and the metrics directory.
 """
 from __future__ import annotations
 
@@ -58,7 +59,7 @@ def _api_worker(idx: int, settings_dict: dict, host: str, port: int, endpoints, 
     logging.basicConfig(level=settings.log_level, format="%(asctime)s - %(name)s - %(levelname)s - %(message)s")
     if endpoints is not None:
         from .dp import DPRouterLLM
-        backend = DPRouterLLM(settings, len(endpoints.senders), endpoints=endpoints)
+        backend = DPRouterLLM(settings, len(endpoints.addresses), endpoints=endpoints, client_id=idx)
     else:
         try:
             backend = build_backend(settings)
@@ -77,7 +78,7 @@ def run_workers(settings, host: str, port: int) -> int:
     import multiprocessing as mp
 
     from ..shared_state import SharedStore
-    from .dp import engine_devices, spawn_replicas
+    from .dp import ReplicaSupervisor
 
     W = max(1, int(settings.WORKERS))
     name = settings.SHARED_STATE or "/ka_state_%d" % os.getpid()
@@ -85,19 +86,22 @@ def run_workers(settings, host: str, port: int) -> int:
     metrics_dir = tempfile.mkdtemp(prefix="ka_prom_")
     sd = dataclasses.asdict(settings)
     sd["SHARED_STATE"] = store.name
-    endpoints = [None] * W
-    replicas = []
+    directory = None
+    sup = None
     if settings.LLM_BACKEND.lower() == "engine":
-        if settings.TP > 1:
-            raise SystemExit("WORKERS > 1 serves DP replicas (TP = 1); run TP > 1 with one API worker")
-        devices = engine_devices(settings, max(1, settings.DP))
-        replicas, endpoints = spawn_replicas(settings, devices, W)
-        log.info("DP replicas on %s serving %d API workers", ",".join(devices), W)
+        sup = ReplicaSupervisor(settings).start()
+        directory = sup.directory
+        log.info("DP=%d replicas (TP=%d each: %s) serving %d API workers", len(sup.specs), settings.TP,
+                 " | ".join(",".join(d) for d in sup.devices), W)
     ctx = mp.get_context("spawn")
-    workers = [ctx.Process(target=_api_worker, args=(i, sd, host, port, endpoints[i], metrics_dir), daemon=False)
-               for i in range(W)]
-    for p in workers:
+
+    def spawn_worker(i):
+        p = ctx.Process(target=_api_worker, args=(i, sd, host, port, directory, metrics_dir), daemon=False)
         p.start()
+        return p
+
+    workers = [spawn_worker(i) for i in range(W)]
+    restarts = [0] * W
     log.info("Started %d API workers on %s:%d (shared state %s)", W, host, port, store.name)
 
     stop = {"flag": False}
@@ -110,6 +114,11 @@ def run_workers(settings, host: str, port: int) -> int:
     rc = 0
     try:
         while not stop["flag"]:
+            for i, p in enumerate(workers):
+                if not p.is_alive() and not stop["flag"] and restarts[i] < 5:
+                    log.error("API worker %d exited (status %s): respawning", i, p.exitcode)
+                    restarts[i] += 1
+                    workers[i] = spawn_worker(i)
             if all(not p.is_alive() for p in workers):
                 rc = 1
                 break
@@ -122,10 +131,8 @@ def run_workers(settings, host: str, port: int) -> int:
             p.join(timeout=10)
             if p.is_alive():
                 p.kill()
-        for p in replicas:
-            p.join(timeout=10)   # replicas exit once every worker has disconnected
-            if p.is_alive():
-                p.terminate()
+        if sup is not None:
+            sup.stop()
         SharedStore.unlink(store.name)
         shutil.rmtree(metrics_dir, ignore_errors=True)
     return rc

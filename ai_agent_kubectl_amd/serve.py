@@ -4,11 +4,15 @@
     LLM_BACKEND=engine DP=8 python -m ai_agent_kubectl_amd.serve          # 8 replicas, 1 API process
     LLM_BACKEND=engine DP=8 WORKERS=8 python -m ai_agent_kubectl_amd.serve   # 8 replicas, 8 API workers
                                                                # (shared cache + limiter, parallel/workers.py)
+    LLM_BACKEND=engine DP=4 TP=2 WORKERS=4 python -m ai_agent_kubectl_amd.serve   # 4 replicas of 2 GPUs each
+    LLM_BACKEND=engine TP=8 MODEL=llama3-70b python -m ai_agent_kubectl_amd.serve          # one TP=8 replica
     LLM_BACKEND=engine TP=8 MODEL=llama3-70b torchrun --nproc-per-node 8 -m ai_agent_kubectl_amd.serve
 
 Settings come from the environment and `./.env` (same variables and defaults as the reference, plus
-the engine flags of SURVEY.md §5.6).  With TP > 1, rank 0 runs the API + scheduler and every other
-rank mirrors its steps in `ModelRunner.worker_loop()` (RCCL collectives inside each forward).
+the engine flags of SURVEY.md §5.6).  Engine replicas (parallel/dp.py) are TP groups: the replica
+process is TP rank 0 and spawns the other ranks.  Under torchrun (WORLD_SIZE = TP > 1) this process
+is rank 0 itself: it runs the API + scheduler and every other rank mirrors its steps in
+`ModelRunner.worker_loop()` (RCCL collectives inside each forward).
 HOST/PORT are honoured (the reference's Dockerfile ignored them, quirk Q10).
 """
 from __future__ import annotations
@@ -33,14 +37,16 @@ def main(argv=None) -> int:
     logging.basicConfig(level=settings.log_level, format="%(asctime)s - %(name)s - %(levelname)s - %(message)s")
     log = logging.getLogger("app")
 
-    if settings.LLM_BACKEND == "engine" and settings.TP > 1:
+    if settings.LLM_BACKEND == "engine" and settings.TP > 1 and int(os.environ.get("WORLD_SIZE", "1")) > 1:
         from .engine.builder import EngineOptions, build_engine
         from .parallel.launch import init_tp
 
         comm, rank = init_tp(settings.TP)
         if rank != 0:
             opts = EngineOptions.from_settings(settings)
-            opts.tp_rank, opts.device = rank, f"cuda:{os.environ.get('LOCAL_RANK', rank)}"
+            opts.tp_rank = rank
+            if opts.device.startswith("cuda"):
+                opts.device = f"cuda:{os.environ.get('LOCAL_RANK', rank)}"
             eng = build_engine(opts, comm=comm)
             eng.runner.capture_graphs()
             eng.runner.worker_loop()
