@@ -84,10 +84,18 @@ def build_engine(opts: EngineOptions, comm=None, metrics=None) -> LLMEngine:
     min_blocks = opts.max_model_len // opts.block_size + 1
     if dev.type == "cuda":
         free, _total = torch.cuda.mem_get_info(dev)
-        budget = int(free * opts.gpu_mem_fraction) - (4 << 30)   # headroom for activations / graphs
-        fit = min(budget // per_block, 1 << 20)   # (16M tokens: more than any batch here can hold)
+        # KA_GPU_MEM_SHARE: this engine's share of the device when several replicas / ranks are
+        # placed on one GPU (parallel/dp.py sets it), so they do not all size their pool from the
+        # same free-memory reading
+        share = float(os.environ.get("KA_GPU_MEM_SHARE", "1"))
+        budget = int(free * opts.gpu_mem_fraction * share) - int((4 << 30) * share)   # activations / graphs
+        fit = min(max(budget, 0) // per_block, 1 << 20)   # (16M tokens: more than any batch here can hold)
         want_blocks = max(opts.kv_cache_tokens // opts.block_size, min_blocks) if opts.kv_cache_tokens > 0 else fit
-        num_blocks = max(64, min(want_blocks, fit))
+        num_blocks = min(want_blocks, fit)
+        if num_blocks < min_blocks:
+            raise RuntimeError(f"KV pool of {num_blocks} blocks cannot hold one {opts.max_model_len}-token sequence "
+                               f"({min_blocks} blocks): {free / 2**30:.1f} GiB free x GPU_MEM_FRACTION "
+                               f"{opts.gpu_mem_fraction} x share {share:g}; lower MAX_MODEL_LEN or free the device")
     else:
         want = opts.kv_cache_tokens // opts.block_size if opts.kv_cache_tokens > 0 else 4096
         num_blocks = min(max(want, min_blocks), 4096)

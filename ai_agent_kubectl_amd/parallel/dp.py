@@ -121,6 +121,7 @@ class ReplicaSpec:
     address: str
     master_port: int = 0
     incarnation: int = 0        # 0 = first start, k = k-th respawn
+    mem_share: float = 1.0      # this replica's share of each of its GPUs (several replicas on one GPU)
 
     @property
     def tp(self) -> int:
@@ -173,6 +174,7 @@ def _tp_worker_main(spec: ReplicaSpec, rank: int, settings_dict: dict, parent: i
     """TP rank > 0 of a replica: mirror rank 0's steps until it stops (or dies)."""
     _exit_with_parent(parent)
     _tp_env(spec, rank)
+    os.environ["KA_GPU_MEM_SHARE"] = repr(spec.mem_share)
     dev = spec.devices[rank]
     from ..config import Settings
     from ..engine.builder import EngineOptions, build_engine
@@ -197,6 +199,7 @@ def _replica_main(spec: ReplicaSpec, settings_dict: dict, authkey: bytes, parent
     target = os.environ.get("KA_FAULT_REPLICA")
     if target is not None and (int(target) != spec.idx or spec.incarnation > 0):
         os.environ.pop("KA_FAULT_STEP", None)
+    os.environ["KA_GPU_MEM_SHARE"] = repr(spec.mem_share)
     dead_path = spec.address + ".dead"
     if os.path.exists(dead_path):
         os.unlink(dead_path)
@@ -377,8 +380,15 @@ class ReplicaSupervisor:
         sd = dataclasses.asdict(settings)
         sd.update(TP=1, DP=1)
         self.settings_dict = sd
+        # ranks sharing a GPU split its memory (tests put a DP x TP layout on one device)
+        per_dev: Dict[str, int] = {}
+        for d in self.devices:
+            for x in d:
+                per_dev[x] = per_dev.get(x, 0) + 1
         self.specs = [ReplicaSpec(i, list(d), os.path.join(self.run_dir, f"replica{i}.sock"),
-                                  _free_port() if len(d) > 1 else 0) for i, d in enumerate(self.devices)]
+                                  _free_port() if len(d) > 1 else 0,
+                                  mem_share=1.0 / max(per_dev[x] for x in d) if d[0] != "cpu" else 1.0)
+                      for i, d in enumerate(self.devices)]
         self.respawn = (os.environ.get("KA_REPLICA_RESPAWN", "1") == "1") if respawn is None else respawn
         self.max_restarts = max_restarts
         self.ctx = mp.get_context("spawn")

@@ -82,6 +82,7 @@ def run_workers(settings, host: str, port: int) -> int:
 
     W = max(1, int(settings.WORKERS))
     name = settings.SHARED_STATE or "/ka_state_%d" % os.getpid()
+    SharedStore.unlink(name)   # this supervisor owns the segment: never inherit an earlier run's cache
     store = SharedStore(name, settings.CACHE_MAXSIZE)   # created before any worker attaches
     metrics_dir = tempfile.mkdtemp(prefix="ka_prom_")
     sd = dataclasses.asdict(settings)

@@ -98,9 +98,10 @@ PYBIND11_MODULE(_native, m) {
            })
       .def("cache_len", &SharedState::cache_len)
       .def("cache_clear", &SharedState::cache_clear)
+      .def("debug_die_locked", &SharedState::debug_die_locked)
       .def("stats",
            [](SharedState& s) {
-             uint64_t o[6];
+             uint64_t o[7];
              s.stats(o);
              py::dict d;
              d["hits"] = o[0];
@@ -109,6 +110,7 @@ PYBIND11_MODULE(_native, m) {
              d["evictions"] = o[3];
              d["size"] = o[4];
              d["limiter_keys"] = o[5];
+             d["owner_deaths"] = o[6];
              return d;
            })
       .def("limiter_hit",

@@ -36,7 +36,7 @@ namespace ka {
 class SharedState {
  public:
   static constexpr uint64_t kMagic = 0x4b41535354415445ull;   // "KASSTATE"
-  static constexpr uint32_t kVersion = 1;
+  static constexpr uint32_t kVersion = 2;
 
   struct Header {
     uint64_t magic;
@@ -46,6 +46,7 @@ class SharedState {
     int32_t lru_head, lru_tail, free_head;   // LRU: head = least recently used
     uint32_t count;
     uint64_t hits, misses, sets, evictions, lim_used;
+    uint64_t owner_deaths;   // lock holders that died (each reset the segment)
   };
   struct Entry {
     uint64_t k0, k1;
@@ -114,7 +115,8 @@ class SharedState {
       }
       s.map(fd, (uint64_t)st.st_size);
       for (int i = 0; i < 2000 && __atomic_load_n(&s.h_->magic, __ATOMIC_ACQUIRE) != kMagic; ++i) usleep(1000);
-      if (s.h_->magic != kMagic || s.h_->version != kVersion || s.h_->total_bytes != (uint64_t)st.st_size)
+      if (s.h_->magic != kMagic || s.h_->version != kVersion || s.h_->total_bytes != (uint64_t)st.st_size ||
+          s.h_->value_max != value_max || s.h_->cache_cap != (cache_cap < 1 ? 1 : cache_cap))
         throw std::runtime_error("shared state " + name + " has an incompatible layout");
     }
     close(fd);
@@ -144,7 +146,7 @@ class SharedState {
   // ---- cache -------------------------------------------------------------------------------
   // get: live value -> true (and the entry becomes most recently used); expired / absent -> false
   bool cache_get(uint64_t k0, uint64_t k1, double now, std::string* out, bool count_stats = true) {
-    Lock l(h_);
+    Lock l(this);
     const int32_t e = find(k0, k1);
     if (e < 0 || !(now < entry(e)->expires)) {
       if (count_stats) h_->misses++;
@@ -161,7 +163,7 @@ class SharedState {
   // (nothing stored) when the value does not fit the slot.
   bool cache_set(uint64_t k0, uint64_t k1, const std::string& v, double now, double ttl, uint32_t maxsize) {
     if (v.size() > h_->value_max) return false;
-    Lock l(h_);
+    Lock l(this);
     purge_expired(now);
     if (maxsize > h_->cache_cap) maxsize = h_->cache_cap;
     int32_t e = find(k0, k1);
@@ -190,7 +192,7 @@ class SharedState {
   }
 
   bool cache_delete(uint64_t k0, uint64_t k1) {
-    Lock l(h_);
+    Lock l(this);
     const int32_t e = find(k0, k1);
     if (e < 0) return false;
     remove(e);
@@ -198,32 +200,40 @@ class SharedState {
   }
 
   uint32_t cache_len(double now) {
-    Lock l(h_);
+    Lock l(this);
     uint32_t n = 0;
     for (int32_t e = h_->lru_head; e >= 0; e = entry(e)->next) n += now < entry(e)->expires;
     return n;
   }
 
   void cache_clear() {
-    Lock l(h_);
+    Lock l(this);
     while (h_->lru_head >= 0) remove(h_->lru_head);
   }
 
-  void stats(uint64_t* out) {   // hits, misses, sets, evictions, count, limiter slots used
-    Lock l(h_);
+  // fault injection (tests): die holding the lock, half-way through a mutation
+  [[noreturn]] void debug_die_locked(int code) {
+    pthread_mutex_lock(&h_->mu);
+    h_->lru_head = 0;   // a dangling chain: what an interrupted relink leaves behind
+    _exit(code);
+  }
+
+  void stats(uint64_t* out) {   // hits, misses, sets, evictions, count, limiter slots used, owner deaths
+    Lock l(this);
     out[0] = h_->hits;
     out[1] = h_->misses;
     out[2] = h_->sets;
     out[3] = h_->evictions;
     out[4] = h_->count;
     out[5] = h_->lim_used;
+    out[6] = h_->owner_deaths;
   }
 
   // ---- fixed-window limiter (limits.FixedWindowRateLimiter.hit on a memory storage) -------------
   // The window starts at the first hit of the key and lasts `expiry` seconds; every hit counts
   // (also over the limit).  Returns true while count <= amount.
   bool limiter_hit(uint64_t k0, uint64_t k1, uint32_t amount, double expiry, double now) {
-    Lock l(h_);
+    Lock l(this);
     if (h_->lim_used * 4 >= (uint64_t)h_->lim_cap * 3) lim_rebuild(now);
     const uint32_t mask = h_->lim_cap - 1;
     uint32_t i = (uint32_t)(k0 ^ (k1 >> 17)) & mask;
@@ -261,7 +271,7 @@ class SharedState {
   }
 
   void limiter_reset() {
-    Lock l(h_);
+    Lock l(this);
     std::memset(static_cast<void*>(slot(0)), 0, (size_t)h_->lim_cap * sizeof(Slot));
     h_->lim_used = 0;
   }
@@ -269,10 +279,18 @@ class SharedState {
  private:
   struct Lock {
     Header* h;
-    explicit Lock(Header* hh) : h(hh) {
+    explicit Lock(SharedState* s) : h(s->h_) {
       const int rc = pthread_mutex_lock(&h->mu);
-      if (rc == EOWNERDEAD) pthread_mutex_consistent(&h->mu);   // a worker died holding it
-      else if (rc != 0) throw std::runtime_error("shared state lock failed");
+      if (rc == EOWNERDEAD) {
+        // a worker died holding the lock, possibly half-way through relinking the LRU / hash chains:
+        // nothing in the structures can be trusted, so start over (cache and limiter windows empty,
+        // what a restart of the reference's single process would leave) before making it consistent
+        s->reset_locked();
+        ++h->owner_deaths;
+        pthread_mutex_consistent(&h->mu);
+      } else if (rc != 0) {
+        throw std::runtime_error("shared state lock failed");
+      }
     }
     ~Lock() { pthread_mutex_unlock(&h->mu); }
   };

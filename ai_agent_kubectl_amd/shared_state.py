@@ -44,9 +44,19 @@ def shm_name(name: str) -> str:
 class SharedStore:
     """One named segment: `cache_capacity` cache entries + the limiter table."""
 
-    def __init__(self, name: str, cache_capacity: int, value_max: int = VALUE_MAX, limiter_keys: int = LIMITER_KEYS):
+    def __init__(self, name: str, cache_capacity: int, value_max: int = VALUE_MAX, limiter_keys: int = LIMITER_KEYS,
+                 recreate: bool = True):
+        """Create or attach.  A segment left behind by an earlier run with another layout (a changed
+        VALUE_MAX / capacity / version) is replaced instead of failing every worker (`recreate`)."""
         self.name = shm_name(name)
-        self._s = _native().SharedState(self.name, max(1, int(cache_capacity)), int(value_max), int(limiter_keys))
+        args = (self.name, max(1, int(cache_capacity)), int(value_max), int(limiter_keys))
+        try:
+            self._s = _native().SharedState(*args)
+        except RuntimeError as e:
+            if not recreate or "incompatible layout" not in str(e):
+                raise
+            self.unlink(self.name)
+            self._s = _native().SharedState(*args)
 
     @property
     def raw(self):

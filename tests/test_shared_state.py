@@ -143,3 +143,46 @@ def test_cross_process_cache_and_limiter(store_name):
         qb.put(None)
         pa.join(30)
         pb.join(30)
+
+
+def test_owner_death_resets_the_segment(tmp_path):
+    """A worker that dies holding the robust mutex half-way through a relink (EOWNERDEAD) must not
+    leave half-linked LRU / hash chains for the others: the next lock resets the segment."""
+    import multiprocessing as mp
+    from ai_agent_kubectl_amd.shared_state import SharedStore, SharedTTLCache
+    name = "/ka_test_owner_%d" % os.getpid()
+    SharedStore.unlink(name)
+    store = SharedStore(name, 8)
+    try:
+        cache = SharedTTLCache(store, 8, 300)
+        for i in range(5):
+            cache[f"k{i}"] = f"v{i}"
+        p = mp.get_context("fork").Process(target=lambda: SharedStore(name, 8).raw.debug_die_locked(7))
+        p.start()
+        p.join(30)
+        assert p.exitcode == 7
+        st = store.stats()
+        assert st["owner_deaths"] == 1 and st["size"] == 0
+        cache["again"] = "ok"
+        assert cache.get("again") == "ok" and cache.get("k1") is None
+    finally:
+        SharedStore.unlink(name)
+
+
+def test_incompatible_leftover_segment_is_recreated():
+    from ai_agent_kubectl_amd.shared_state import SharedStore, SharedTTLCache
+    name = "/ka_test_layout_%d" % os.getpid()
+    SharedStore.unlink(name)
+    old = SharedStore(name, 8, value_max=256)
+    try:
+        new = SharedStore(name, 8, value_max=512)   # an earlier run's layout: replaced, not an error
+        c = SharedTTLCache(new, 8, 300)
+        c["x"] = "y" * 400
+        assert c.get("x") == "y" * 400
+        with pytest.raises(RuntimeError):
+            SharedStore("/ka_test_layout_strict_%d" % os.getpid(), 8, value_max=256, recreate=False) and \
+                SharedStore("/ka_test_layout_strict_%d" % os.getpid(), 8, value_max=512, recreate=False)
+    finally:
+        del old
+        SharedStore.unlink(name)
+        SharedStore.unlink("/ka_test_layout_strict_%d" % os.getpid())
