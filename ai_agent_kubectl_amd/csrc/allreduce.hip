@@ -9,7 +9,7 @@
 // Block b of every rank owns the same element chunk b.  One call (epoch e = ctr + 1, half = e & 1):
 //   1. copy chunk b of the input into my half;  2. system-scope release, then store e into
 //   flags[b][me] of every peer;  3. wait until my flags[b][p] >= e for every p (acquire, bounded
-//   spin -> err instead of a hang);  4. sum chunk b over all ranks' halves in fp32, write the output;
+//   wait -> err instead of a hang, spin_wait);  4. sum chunk b over all ranks' halves in fp32, write the output;
 //   5. the last block to finish stores ctr = e.
 // The epoch lives in device memory, so the launch can be captured once in a hipGraph and replayed.
 // Halves alternate by epoch parity: a rank rewrites half h in call e + 2 only after every peer has
@@ -20,6 +20,27 @@
 
 #define AR_MAX_RANKS 8
 #define AR_MAX_BLOCKS 64
+
+// Bounded wait for a peer's flag: wall-clock bound (s_memrealtime, 100 MHz) of AR_SPIN_SECONDS — long
+// enough for the first steps' host-side skew between ranks (lazy kernel loading, eager prefill
+// setup), short of the engine's step watchdog — after which `err` is set instead of hanging the GPU;
+// once `err` is set every later wait gives up at once, so a dead peer costs one bound per process,
+// not one per collective.  The host reads `err` with every step (engine/runner.py) and never uses a
+// step that set it.
+#ifndef AR_SPIN_SECONDS
+#define AR_SPIN_SECONDS 20
+#endif
+KA_DEV void spin_wait(unsigned* f, unsigned epoch, int* err) {
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > (unsigned long long)AR_SPIN_SECONDS * 100000000ull) {
+      atomicExch(err, 1);   // a peer never arrived: report, never hang the GPU
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
 
 struct ArArgs {
   bf16_t* data[AR_MAX_RANKS];
@@ -47,14 +68,7 @@ __global__ __launch_bounds__(512) void allreduce_oneshot_kernel(ArArgs a, const 
     __hip_atomic_store(a.flags[p] + blockIdx.x * AR_MAX_RANKS + rank, epoch, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     unsigned* f = a.flags[rank] + blockIdx.x * AR_MAX_RANKS + p;
-    int spins = 0;
-    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      if (++spins > (1 << 22)) {   // ~1 s: a peer never arrived -> report, never hang the GPU
-        atomicExch(err, 1);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
+    spin_wait(f, epoch, err);
   }
   __syncthreads();
 
@@ -110,14 +124,7 @@ __global__ __launch_bounds__(512) void allgather_oneshot_kernel(ArArgs a, const 
     __hip_atomic_store(a.flags[p] + blockIdx.x * AR_MAX_RANKS + rank, epoch, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     unsigned* f = a.flags[rank] + blockIdx.x * AR_MAX_RANKS + p;
-    int spins = 0;
-    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      if (++spins > (1 << 22)) {
-        atomicExch(err, 1);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
+    spin_wait(f, epoch, err);
   }
   __syncthreads();
   for (int p = 0; p < world; ++p)
@@ -166,14 +173,7 @@ __global__ __launch_bounds__(512) void allreduce_rmsnorm_kernel(ArArgs a, const 
     __hip_atomic_store(a.flags[p] + blockIdx.x * AR_MAX_RANKS + rank, epoch, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     unsigned* f = a.flags[rank] + blockIdx.x * AR_MAX_RANKS + p;
-    int spins = 0;
-    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      if (++spins > (1 << 22)) {
-        atomicExch(err, 1);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
+    spin_wait(f, epoch, err);
   }
   __syncthreads();
 

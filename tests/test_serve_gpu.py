@@ -121,7 +121,7 @@ def test_serve_dp2_x_tp2_on_one_gpu(tmp_path):
         seen = []
         for q in ("list all pods in prod", "get nodes -o wide", "describe deployment api", "top pods"):
             st, body = _req(port, "POST", "/kubectl-command", {"query": q})
-            assert st == 200, body
+            assert st == 200, (body, (tmp_path / "serve.log").read_text()[-6000:])
             cmd = json.loads(body)["kubectl_command"]
             assert is_safe_kubectl_command(cmd), cmd
             seen.append(cmd)
