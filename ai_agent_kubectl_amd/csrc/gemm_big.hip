@@ -38,7 +38,7 @@ constexpr int BN = 256, BM = 256, BK = 64, NT = 256;
 constexpr int TILE_A = BN * BK * 2, TILE_B = BM * BK * 2;   // 32 KB each
 constexpr int STAGE = TILE_A + TILE_B;                        // 64 KB
 #ifndef GB_RING5
-#define GB_RING5 1   // 1: 5-slot ring of 32-deep stages (160 KB); 0: two 64-deep buffers (128 KB)
+#define GB_RING5 0  // 1: 5-slot ring of 32-deep stages (160 KB); 0: two 64-deep buffers (128 KB)
 #endif
 constexpr int R_TILE = BN * 32 * 2, R_STAGE = 2 * R_TILE, R_SLOTS = 5;   // ring: 16 KB per operand
 constexpr int LDS = GB_RING5 ? R_SLOTS * R_STAGE : 2 * STAGE;

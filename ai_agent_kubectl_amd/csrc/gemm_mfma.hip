@@ -1,5 +1,8 @@
-// gemm_mfma: the engine's projection GEMM for every M >= 48 (decode batches, mixed steps and
-// prefill):  Y[M, N] = X[M, K] * W[N, K]^T, bf16 in, fp32 accumulate, fused epilogues.
+// gemm_mfma: LDS-DMA ring MFMA GEMM family for decode batches and small mixed steps,
+// Y[M, N] = X[M, K] * W[N, K]^T, bf16 in, fp32 accumulate, fused epilogues.  It runs only where
+// the engine-start autotuner (ops/autotune.py) measured it fastest for an (M <= 512, N, K) shape;
+// larger M (prefill, big mixed steps) dispatches to hipBLASLt (ops.linear), and the grouped
+// variant serves MoE prefill (ops.grouped_linear).
 //
 // Design (cdna_hip_programming.md §5 "Canonical CDNA GEMM", T1, T2, "glds vs register staging"):
 //   * workgroup tile BN weight rows x BM activation rows, BK = 64; waves laid out WN x WM, each

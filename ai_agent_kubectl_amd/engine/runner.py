@@ -110,6 +110,7 @@ class ModelRunner:
         self.d_fix = torch.zeros(2 * B, dtype=torch.int32, device=self.device)
         self.d_hdr = torch.zeros(HDR, dtype=torch.int32, device=self.device)
         self._h_hdrs = [torch.zeros(HDR, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self._hflip = 0
         # the one-shot TP collectives' error word rides back with every step's tokens (a pinned
         # 4-byte copy behind them on the same stream: no extra synchronisation), one slot per launch
         # parity like the token outputs
@@ -268,12 +269,14 @@ class ModelRunner:
         return (self.tp_size == 1 or self.tp_overlap) and B <= self.bmax
 
     def can_overlap_prefill(self, B: int) -> bool:
-        return self.tp_size == 1 and B <= self.bmax
+        return (self.tp_size == 1 or self.tp_overlap) and B <= self.bmax
 
     def can_lookahead(self) -> bool:
-        """Steps can be scheduled and queued ahead of the in-flight step's readback (TP = 1: with TP
-        the staging broadcast would need the placeholder fixups on every rank)."""
-        return self.tp_size == 1
+        """Steps can be scheduled and queued ahead of the in-flight step's readback.  With TP, rank 0
+        applies the placeholder fixups on the device BEFORE the staging broadcast (every rank samples
+        the same tokens into its d_out, but only rank 0 knows the fixup list), so the other ranks
+        receive final inputs; needs stream-ordered collectives (tp_overlap) to actually overlap."""
+        return self.tp_size == 1 or self.tp_overlap
 
     @torch.inference_mode()
     def launch_decode_async(self, batch: Batch, chained: bool = False, fix: Optional[List[tuple]] = None):
@@ -292,11 +295,7 @@ class ModelRunner:
         hs, ho = self._h_stages[k], self._h_outs[k]
         self._pack_decode(batch, Bp, hs.numpy(), ahead=1 if chained else 0)
         n_copy = self._off["bt"] + Bp * self.max_blocks
-        if self.tp_size > 1:   # header from pinned memory: the copy stays asynchronous
-            hh = self._h_hdrs[k]
-            hh.numpy()[:3] = (KIND_DECODE, Bp, n_copy)
-            self.d_hdr.copy_(hh, non_blocking=True)
-            self.comm.broadcast(self.d_hdr, src=0)
+        self._bcast_header_async(KIND_DECODE, Bp, n_copy)
         self.d_stage[:n_copy].copy_(hs[:n_copy], non_blocking=True)
         if chained:
             o = self._off["ids"]
@@ -320,7 +319,8 @@ class ModelRunner:
 
     @torch.inference_mode()
     def launch_prefill_async(self, batch: Batch):
-        """Queue a prefill or mixed step without waiting for its tokens (TP = 1, at most `bmax` rows):
+        """Queue a prefill or mixed step without waiting for its tokens (at most `bmax` rows; with TP,
+        rank 0 broadcasts the header and the fixed-up metadata, stream-ordered):
         the sampled tokens are also left in `d_out`, in batch row order, so the next step can be
         queued right behind it with its inputs taken on the device (`launch_decode_async(chained=
         True)` for the same rows, or the PLACEHOLDER fixups of a step scheduled ahead).  Rows whose
@@ -335,6 +335,9 @@ class ModelRunner:
             n = buf.shape[0]
             buf[:T].index_copy_(0, buf[n - 2 * nf:n - nf].long(), self.d_out.index_select(0, buf[n - nf:].long()))
             buf = buf[:n - 2 * nf]
+        if self.tp_size > 1:   # the other ranks get the fixed-up metadata (worker_loop KIND_PREFILL)
+            self._bcast_header_async(KIND_PREFILL, T, S, max_q, buf.shape[0], nc, nd, batch.num_tokens)
+            self.comm.broadcast(buf, src=0)
         self.model.mark_layer = max(0, self.cfg.num_layers - self.lookahead_layers)
         self.model.mark_event = None
         try:
@@ -534,6 +537,20 @@ class ModelRunner:
         if self.tp_size == 1:
             return
         self.d_hdr.copy_(torch.tensor([kind, a, b, c, d, e, f, g], dtype=torch.int32))
+        self.comm.broadcast(self.d_hdr, src=0)
+
+    def _bcast_header_async(self, kind: int, *vals: int) -> None:
+        """The step header from pinned memory (the copy stays asynchronous on the stream); two
+        buffers: the one refilled here served the launch before last, which has been read back."""
+        if self.tp_size == 1:
+            return
+        hh = self._h_hdrs[self._hflip]
+        self._hflip ^= 1
+        h = hh.numpy()
+        h[:] = 0
+        h[0] = kind
+        h[1:1 + len(vals)] = vals
+        self.d_hdr.copy_(hh, non_blocking=True)
         self.comm.broadcast(self.d_hdr, src=0)
 
     @torch.inference_mode()
