@@ -172,6 +172,8 @@ def _tp_env(spec: ReplicaSpec, rank: int) -> None:
 
 def _tp_worker_main(spec: ReplicaSpec, rank: int, settings_dict: dict, parent: int) -> None:
     """TP rank > 0 of a replica: mirror rank 0's steps until it stops (or dies)."""
+    from ..utils.runtime import set_proc_name
+    set_proc_name(f"ka-tp-{spec.idx}.{rank}")
     _exit_with_parent(parent)
     _tp_env(spec, rank)
     os.environ["KA_GPU_MEM_SHARE"] = repr(spec.mem_share)
@@ -192,6 +194,8 @@ def _tp_worker_main(spec: ReplicaSpec, rank: int, settings_dict: dict, parent: i
 
 def _replica_main(spec: ReplicaSpec, settings_dict: dict, authkey: bytes, parent: int) -> None:
     """Entry point of one replica process (TP rank 0 of its group)."""
+    from ..utils.runtime import set_proc_name
+    set_proc_name(f"ka-replica-{spec.idx}")
     _exit_with_parent(parent)
     os.environ.setdefault("KA_EXIT_ON_FATAL", "1")   # a fatal engine fault ends the replica: respawned
     # fault injection (tests, SURVEY.md §5.3): KA_FAULT_STEP applies to replica KA_FAULT_REPLICA's

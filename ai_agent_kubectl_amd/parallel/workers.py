@@ -45,6 +45,8 @@ def bind_reuseport(host: str, port: int) -> socket.socket:
 
 def _api_worker(idx: int, settings_dict: dict, host: str, port: int, endpoints, metrics_dir: str) -> None:
     """One API worker process (spawned): the app + uvicorn on a SO_REUSEPORT socket."""
+    from ..utils.runtime import set_proc_name
+    set_proc_name(f"ka-api-{idx}")
     if metrics_dir:   # before prometheus_client is imported: multiprocess value storage
         os.environ["PROMETHEUS_MULTIPROC_DIR"] = metrics_dir
     import asyncio

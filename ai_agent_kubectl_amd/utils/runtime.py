@@ -77,3 +77,14 @@ def pin_process(cpus) -> None:
             os.sched_setaffinity(int(tid), cpus)
         except OSError:  # pragma: no cover - thread exited meanwhile
             pass
+
+
+def set_proc_name(name: str) -> None:
+    """Name this process (/proc/<pid>/comm, at most 15 bytes: `ps`, `top`, psutil.name()) so the
+    serving topology is readable from outside: ka-api-<i>, ka-replica-<i>, ka-tp-<i>.<r>."""
+    try:
+        import ctypes
+        libc = ctypes.CDLL(None, use_errno=True)
+        libc.prctl(15, ctypes.c_char_p(name.encode()[:15]), 0, 0, 0)   # PR_SET_NAME
+    except (OSError, AttributeError):
+        pass

@@ -320,6 +320,36 @@ async def scrape_engine_metrics(port):
     return out
 
 
+def cpu_snapshot(pids_by_role):
+    """CPU seconds (user + system) of every process of the server tree and of the load generators,
+    keyed by process name (serve.py names its processes ka-api-<i> / ka-replica-<i> / ka-tp-<i>.<r>)."""
+    import psutil
+    out = {}
+    for role, pid in pids_by_role:
+        try:
+            root = psutil.Process(pid)
+            procs = [root] + (root.children(recursive=True) if role == "server" else [])
+        except psutil.Error:
+            continue
+        for p in procs:
+            try:
+                t = p.cpu_times()
+                name = p.name() if role == "server" else f"client-{pid}"
+                out[(name, p.pid)] = t.user + t.system
+            except psutil.Error:
+                pass
+    return out
+
+
+def cpu_util(s0, s1, elapsed):
+    """Cores used per process over the timed region (1.0 = one core busy all the time)."""
+    util = {}
+    for key, v in s1.items():
+        name = key[0]
+        util[name] = round(util.get(name, 0.0) + (v - s0.get(key, v)) / max(elapsed, 1e-9), 3)
+    return dict(sorted(util.items(), key=lambda kv: -kv[1]))
+
+
 def run_tcp(args, rank, local, world, C, buckets, dist):
     """tcp transport: rank 0 starts ONE production server (DP = world replicas, shared cache and
     limiter across its API workers, one port); every rank drives C closed-loop clients at it from
@@ -404,6 +434,8 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
         if world > 1:
             dist.barrier()
         m0 = asyncio.run(scrape_engine_metrics(port)) if rank == 0 else {}
+        roles = ([("server", srv.pid)] if srv is not None else []) + [("client", p.pid) for p in procs]
+        c0 = cpu_snapshot(roles)
         with done.get_lock():
             done.value = 0
         phase.value = 1
@@ -412,6 +444,7 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
         while done.value < target:
             time.sleep(0.001)
         elapsed = time.perf_counter() - t0
+        c1 = cpu_snapshot(roles)
         phase.value = 2
         m1 = asyncio.run(scrape_engine_metrics(port)) if rank == 0 else {}
         if world > 1:
@@ -432,7 +465,8 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
         d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1}
         st = {"decode_steps": int(d.get("decode_count", 0)), "decode_ms": d.get("decode_sum", 0.0) * 1e3,
               "prefill_steps": int(d.get("prefill_count", 0)), "prefill_ms": d.get("prefill_sum", 0.0) * 1e3,
-              "queue_wait_ms_mean": round(d.get("qwait_sum", 0.0) * 1e3 / max(1.0, d.get("qwait_count", 0.0)), 2)}
+              "queue_wait_ms_mean": round(d.get("qwait_sum", 0.0) * 1e3 / max(1.0, d.get("qwait_count", 0.0)), 2),
+              "cpu_cores": cpu_util(c0, c1, elapsed)}
         return elapsed, lat, st, t_build, None
     finally:
         if srv is not None:
@@ -725,7 +759,8 @@ def summarize(args, name, world, C, dist, r, seq_len):
             "decode_steps": st["decode_steps"], "prefill_steps": st["prefill_steps"],
             "decode_ms_per_step": round(st["decode_ms"] / max(1, st["decode_steps"]), 3),
             "prefill_ms_per_step": round(st["prefill_ms"] / max(1, st["prefill_steps"]), 3),
-            "queue_wait_ms_mean": st["queue_wait_ms_mean"], "engine_stats_from": "/metrics"})
+            "queue_wait_ms_mean": st["queue_wait_ms_mean"], "engine_stats_from": "/metrics",
+            "cpu_cores": st.get("cpu_cores")})
     elif st:
         detail.update({
             "decode_steps": st.get("decode_steps"), "prefill_steps": st.get("prefill_steps"),
