@@ -43,7 +43,7 @@ constexpr int STAGE = TILE_A + TILE_B;                        // 64 KB
 constexpr int R_TILE = BN * 32 * 2, R_STAGE = 2 * R_TILE, R_SLOTS = 5;   // ring: 16 KB per operand
 constexpr int LDS = GB_RING5 ? R_SLOTS * R_STAGE : 2 * STAGE;
 
-enum Epi : int { EPI_BF16 = 0, EPI_SWIGLU = 3, EPI_ADD = 4 };
+enum Epi : int { EPI_BF16 = 0, EPI_SWIGLU = 3, EPI_ADD = 4, EPI_ARGMAX = 5 };
 
 struct Args {
   const bf16_t* X;   // [M, ldx]
@@ -52,6 +52,14 @@ struct Args {
   const bf16_t* R;   // EPI_ADD: residual [M, ldy] (may be Y)
   int M, N, K, ldx, ldy, tiles_m, tiles_n, gm;
   int I;             // SwiGLU: the up rows start at W row I (N == 2I)
+  // EPI_ARGMAX (the LM head + greedy SAFE_DECODE sampling): logits never leave the registers; each
+  // tile writes its per-row (max, lowest index) of the bf16-rounded, mask-allowed logits to
+  // part_val / part_idx [M][tiles_n] (argmax_finish_kernel picks the winner per row)
+  const uint32_t* mask_bits;   // [masks][mask_words], bit = global token id (nullptr: no mask)
+  const int* mask_idx;         // [M] mask row per output row, < 0 = unmasked
+  int mask_words, vocab_offset;
+  float* part_val;
+  int* part_idx;
 };
 
 // Every instruction of the k-loop is an asm statement, so the program order written below IS the
@@ -383,7 +391,66 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
   block_sync();   // every wave is past its last (stale) fragment read of the staging buffers
   char* const Q = L + w * 32768;
-  if constexpr (EPI == EPI_SWIGLU) {
+  if constexpr (EPI == EPI_ARGMAX) {
+    // lane (r16, grp) holds, for output row m = 128 wm + 16 j + r16, the 32 logits of columns
+    // n = 128 wn + 16 i + 4 grp + r (i < 8, r < 4).  Values are compared after bf16 rounding (what
+    // the unfused path's bf16 logits hold); i and r ascend, so strict '>' keeps the lowest index.
+    float* const Sv = reinterpret_cast<float*>(L);            // [4 waves][128 rows]
+    int* const Si = reinterpret_cast<int*>(L + 4 * 128 * 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + 128 * wm + 16 * j + r16;
+      const int mi = (a.mask_bits != nullptr && m < a.M) ? a.mask_idx[m] : -1;
+      const uint32_t* mrow = mi >= 0 ? a.mask_bits + (size_t)mi * a.mask_words : nullptr;
+      float best = -INFINITY;
+      int bidx = 0x7fffffff;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int n0 = tn * BN + 128 * wn + 16 * i + 4 * grp;
+        uint32_t bits = 0xfu;
+        if (mrow) {   // n0 + vocab_offset is a multiple of 4: the 4 bits share one mask word
+          const int gb = n0 + a.vocab_offset;
+          bits = (mrow[gb >> 5] >> (gb & 31)) & 0xfu;
+        }
+        if (n0 >= a.N) bits = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = lo_f(pack2(acc[i][j][r], 0.f));
+          if (((bits >> r) & 1u) && x > best) {
+            best = x;
+            bidx = n0 + r;
+          }
+        }
+      }
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {   // the 4 lanes of row r16 (grp 0..3)
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bidx, o, 64);
+        if (ob > best || (ob == best && oi < bidx)) {
+          best = ob;
+          bidx = oi;
+        }
+      }
+      if (grp == 0) {
+        Sv[w * 128 + 16 * j + r16] = best;
+        Si[w * 128 + 16 * j + r16] = bidx;
+      }
+    }
+    block_sync();
+    {   // thread t: tile row t = 128 wm' + rr, from waves 2 wm' (columns 0..127) and 2 wm' + 1
+      const int wm2 = tid >> 7, rr = tid & 127, m = m0 + tid;
+      float b0 = Sv[(2 * wm2) * 128 + rr], b1 = Sv[(2 * wm2 + 1) * 128 + rr];
+      int i0 = Si[(2 * wm2) * 128 + rr], i1 = Si[(2 * wm2 + 1) * 128 + rr];
+      if (b1 > b0 || (b1 == b0 && i1 < i0)) {
+        b0 = b1;
+        i0 = i1;
+      }
+      if (m < a.M) {
+        a.part_val[(size_t)m * a.tiles_n + tn] = b0;
+        a.part_idx[(size_t)m * a.tiles_n + tn] = i0;
+      }
+    }
+  } else if constexpr (EPI == EPI_SWIGLU) {
     // quadrant: 128 rows (m) x 64 output columns = 128 B per row, 16-B chunk index ^ (row & 7)
 #pragma unroll
     for (int p = 0; p < 4; ++p)
@@ -472,4 +539,30 @@ extern "C" int ka_gemm_big(void* Y, const void* R, const void* X, const void* W,
       return gb::launch<gb::EPI_ADD>(a, stream);
   }
   return (int)hipErrorInvalidValue;
+}
+
+extern "C" int ka_argmax_finish(int* out_idx, float* out_val, const float* part_val, const int* part_idx, int rows,
+                                int slices, int vocab_offset, hipStream_t stream);
+
+// Workspace bytes of ka_gemm_big_argmax: per-row, per-tile (max, index).
+extern "C" size_t ka_gemm_big_argmax_ws(int M, int N) { return (size_t)M * ((N + gb::BN - 1) / gb::BN) * 8; }
+
+// Fused LM head + greedy sampling: out_idx[m] = vocab_offset + argmax over allowed n of bf16(X W^T)[m, n]
+// (lowest index on ties; mask row mask_idx[m], < 0 or mask_bits == nullptr = all tokens allowed),
+// out_val[m] its value (for the vocab-parallel combine under TP).  The [M, N] logits are never written.
+extern "C" int ka_gemm_big_argmax(int* out_idx, float* out_val, const void* X, const void* W, int M, int N, int K,
+                                  int ldx, const uint32_t* mask_bits, const int* mask_idx, int mask_words,
+                                  int vocab_offset, void* workspace, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (K % 128 != 0 || N % 128 != 0 || ldx % 8 != 0 || vocab_offset % 4 != 0 || workspace == nullptr ||
+      (mask_bits != nullptr && mask_idx == nullptr))
+    return (int)hipErrorInvalidValue;
+  const int tiles_n = (N + gb::BN - 1) / gb::BN;
+  float* pv = static_cast<float*>(workspace);
+  int* pi = reinterpret_cast<int*>(pv + (size_t)M * tiles_n);
+  gb::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), nullptr, nullptr, M, N, K, ldx, 8, 0, 0,
+             8, N / 2, mask_bits, mask_idx, mask_words, vocab_offset, pv, pi};
+  int rc = gb::launch<gb::EPI_ARGMAX>(a, stream);
+  if (rc != 0) return rc;
+  return ka_argmax_finish(out_idx, out_val, pv, pi, M, tiles_n, vocab_offset, stream);
 }

@@ -113,6 +113,15 @@ __global__ __launch_bounds__(64) void argmax_finish_kernel(int* __restrict__ out
   }
 }
 
+// Per-slice (max, index) partials of another producer (the fused LM-head GEMM, gemm_big.hip) -> winner.
+extern "C" int ka_argmax_finish(int* out_idx, float* out_val, const float* part_val, const int* part_idx, int rows,
+                                int slices, int vocab_offset, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(argmax_finish_kernel, dim3(rows), dim3(64), 0, stream, out_idx, out_val, part_val, part_idx,
+                     slices, vocab_offset);
+  KA_CHECK_LAUNCH();
+}
+
 // slices > 1 needs a workspace of rows * slices floats + rows * slices ints (ka_argmax_slices).
 extern "C" int ka_argmax_slices(int rows, int vocab) {
   if (rows >= 128) return 1;

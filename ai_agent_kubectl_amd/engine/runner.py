@@ -14,6 +14,7 @@ inside it synchronising them.  Worker ranks sit in `worker_loop()`.
 from __future__ import annotations
 
 import bisect
+import logging
 import os
 import time
 from typing import Dict, List, NamedTuple, Optional
@@ -24,6 +25,8 @@ import torch
 from ..models.config import ModelConfig
 from .. import ops
 from ..models.llama import AttnMeta, LlamaModel
+
+logger = logging.getLogger("app.engine")
 from ..parallel.comm import LocalComm
 from .safe_decode import mask_index_for
 from .scheduler import Batch
@@ -186,6 +189,34 @@ class ModelRunner:
             save_plan(path, report, ctx_of)
         return report
 
+    @torch.inference_mode()
+    def tune_lm_head(self) -> dict:
+        """Per decode bucket: the fused LM head + masked argmax (csrc/gemm_big.hip) against the
+        GEMM plan's LM head + masked_argmax, on the model's own LM head and a SAFE_DECODE mask row;
+        fills ops.LM_HEAD_FUSED and the threshold for untimed row counts."""
+        m = self.model
+        lm = m.W["lm_head"]
+        if self.device.type != "cuda" or ops.LM_HEAD_MODE != "auto":
+            return {}
+        from ..ops.autotune import _time
+        K = lm.shape[1]
+        report = {}
+        for M in sorted(set(self.buckets)):
+            x = torch.randn(M, K, device=self.device, dtype=lm.dtype)
+            if not ops.lm_head_argmax_ok(x, lm, m.vocab_offset):
+                return {}
+            midx = (torch.zeros(M, dtype=torch.int32, device=self.device) if self.mask_bits is not None else None)
+            t_un = _time(lambda w: ops.masked_argmax(ops.linear(x, w), self.mask_bits, midx, m.vocab_offset), [lm])
+            t_fu = _time(lambda w: ops.lm_head_argmax(x, w, self.mask_bits, midx, m.vocab_offset), [lm])
+            ops.LM_HEAD_FUSED[M] = t_fu < t_un
+            report[M] = {"fused_us": round(t_fu, 1), "unfused_us": round(t_un, 1)}
+        wins = sorted(M for M, f in ops.LM_HEAD_FUSED.items() if f)
+        # untimed row counts: fused from the smallest bucket above which every timed bucket won
+        ops.LM_HEAD_FUSED_MIN_M = next((M for M in wins if all(ops.LM_HEAD_FUSED[b] for b in ops.LM_HEAD_FUSED
+                                                                  if b >= M)), 1 << 30)
+        logger.info("lm head plan: %s (fused from %d rows)", report, ops.LM_HEAD_FUSED_MIN_M)
+        return report
+
     def _attention_consumer(self, ctx: int = 128):
         """fn(qkv, M): decode_attention_rope over M synthetic sequences of `ctx` cached tokens in
         layer 0's cache (autotune runs before serving: the KV written here is never read)."""
@@ -213,6 +244,7 @@ class ModelRunner:
         t0 = time.perf_counter()
         if autotune:
             self.gemm_plan = self.autotune()
+            self.lm_head_plan = self.tune_lm_head()
         self.h_np[:] = 0
         o = self._off
         for name in ("slots",):

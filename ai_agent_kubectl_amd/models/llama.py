@@ -166,9 +166,15 @@ class LlamaModel:
 
     def sample(self, hidden_last: torch.Tensor, mask_bits: Optional[torch.Tensor],
                mask_idx: Optional[torch.Tensor]) -> torch.Tensor:
-        """Greedy (temperature 0, app.py:109) next tokens under the SAFE_DECODE mask: [S] int32."""
-        logits = self.logits(hidden_last)
-        idx, val = ops.masked_argmax(logits, mask_bits, mask_idx, vocab_offset=self.vocab_offset)
+        """Greedy (temperature 0, app.py:109) next tokens under the SAFE_DECODE mask: [S] int32.
+        Where it measured faster (ops.use_fused_lm_head), the LM head GEMM and the masked argmax are
+        one kernel and the logits are never written."""
+        lm = self.W["lm_head"]
+        if ops.use_fused_lm_head(hidden_last, lm, self.vocab_offset):
+            idx, val = ops.lm_head_argmax(hidden_last, lm, mask_bits, mask_idx, vocab_offset=self.vocab_offset)
+        else:
+            logits = self.logits(hidden_last)
+            idx, val = ops.masked_argmax(logits, mask_bits, mask_idx, vocab_offset=self.vocab_offset)
         if self.tp_size == 1:
             return idx
         vals = self.comm.all_gather(val)                       # [t, S]

@@ -244,6 +244,54 @@ def masked_argmax(logits: torch.Tensor, mask_bits: Optional[torch.Tensor], mask_
     return out_idx, out_val
 
 
+GB_BN = 256   # csrc/gemm_big.hip output tile (weight rows)
+
+
+def lm_head_argmax(x: torch.Tensor, w: torch.Tensor, mask_bits: Optional[torch.Tensor],
+                   mask_idx: Optional[torch.Tensor], vocab_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Fused LM head + greedy SAFE_DECODE sampling (csrc/gemm_big.hip EPI_ARGMAX): the [M, V] logits
+    are never written; each 256-token tile's per-row (max, lowest index) of the bf16-rounded allowed
+    logits goes to a small workspace and argmax_finish picks the winner.  Same result as
+    `masked_argmax(linear(x, w), ...)` (ties: lowest token id)."""
+    if _ref(x):
+        return ref.masked_argmax(ref.linear(x, w), mask_bits, mask_idx, vocab_offset)
+    lib = require()
+    M, K = x.shape
+    N = w.shape[0]
+    out_idx = torch.empty(M, dtype=torch.int32, device=x.device)
+    out_val = torch.empty(M, dtype=torch.float32, device=x.device)
+    ws = torch.empty(2 * M * ((N + GB_BN - 1) // GB_BN), dtype=torch.float32, device=x.device)
+    words = mask_bits.shape[1] if mask_bits is not None else 0
+    check(lib.ka_gemm_big_argmax(_p(out_idx), _p(out_val), _p(x), _p(w), M, N, K, x.stride(0), _p(mask_bits),
+                                 _p(mask_idx) if mask_bits is not None else None, words, int(vocab_offset),
+                                 _p(ws), _stream()), "gemm_big_argmax")
+    return out_idx, out_val
+
+
+def lm_head_argmax_ok(x: torch.Tensor, w: torch.Tensor, vocab_offset: int = 0) -> bool:
+    return (x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0 and x.shape[1] % 128 == 0
+            and w.shape[0] % 128 == 0 and w.is_contiguous() and vocab_offset % 4 == 0)
+
+
+# Fused LM head per row count M: filled at engine start by ModelRunner.tune_lm_head (timed against
+# the plan's GEMM + masked_argmax on the model's own LM head); row counts not timed (prefill / mixed
+# steps sample S rows) use the fused kernel from LM_HEAD_FUSED_MIN_M rows up.
+# KA_FUSED_LM_HEAD: auto (default) | 1 (always, where the shape allows) | 0 (never).
+LM_HEAD_MODE = os.environ.get("KA_FUSED_LM_HEAD", "auto")
+LM_HEAD_FUSED: dict = {}
+LM_HEAD_FUSED_MIN_M = 64
+
+
+def use_fused_lm_head(x: torch.Tensor, w: torch.Tensor, vocab_offset: int = 0) -> bool:
+    if _ref(x) or LM_HEAD_MODE == "0" or not lm_head_argmax_ok(x, w, vocab_offset):
+        return False
+    if LM_HEAD_MODE == "1":
+        return True
+    M = x.shape[0]
+    fused = LM_HEAD_FUSED.get(M)
+    return fused if fused is not None else M >= LM_HEAD_FUSED_MIN_M
+
+
 def moe_topk(router_logits: torch.Tensor, k: int):
     if _ref(router_logits):
         return ref.moe_topk(router_logits, k)

@@ -253,6 +253,51 @@ def test_masked_argmax_ties_lowest_index(B):
     assert idx.cpu().tolist() == [9000] * B and val.cpu().tolist() == [5.0] * B
 
 
+@pytest.mark.parametrize("M", [1, 7, 64, 200, 256, 300])
+@pytest.mark.parametrize("off", [0, 64128])
+def test_lm_head_argmax_vs_fp32(M, off):
+    """Fused LM head + masked argmax (csrc/gemm_big.hip EPI_ARGMAX): the chosen token is allowed by
+    the row's mask and its fp32 reference logit is the row's allowed maximum up to bf16 rounding;
+    vocab_offset = the second TP=2 shard's (the mask is indexed by the global token id)."""
+    import numpy as np
+    V, K = 64128, 4096
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(V, K, device=DEV) * 0.02).to(BF)
+    words = (V + off + 31) // 32
+    bits = torch.from_numpy(np.random.RandomState(1).randint(0, 2**32, size=(2, words), dtype=np.uint64)
+                            .astype(np.uint32).view(np.int32)).to(DEV)
+    midx = torch.tensor([0, 1, -1] * (M // 3 + 1), dtype=torch.int32, device=DEV)[:M]
+    idx, val = ops.lm_head_argmax(x, w, bits, midx, vocab_offset=off)
+    ref_logits = (x.float() @ w.float().t()).cpu()
+    allowed = torch.ones(M, V, dtype=torch.bool)
+    b = bits.cpu().view(torch.int32).numpy().view(np.uint32)
+    gid = np.arange(V) + off
+    for r in range(M):
+        mi = int(midx[r])
+        if mi >= 0:
+            allowed[r] = torch.from_numpy(((b[mi][gid >> 5] >> (gid & 31)) & 1).astype(bool))
+    masked = ref_logits.masked_fill(~allowed, float("-inf"))
+    best = masked.max(1).values
+    got = idx.cpu().long() - off
+    assert ((got >= 0) & (got < V)).all()
+    assert allowed.gather(1, got[:, None]).all()
+    chosen = ref_logits.gather(1, got[:, None]).squeeze(1)
+    assert ((best - chosen) <= 0.02 * best.abs().clamp(min=1.0)).all()
+    close(val, chosen, atol=0.05, rtol=0.02)
+
+
+def test_lm_head_argmax_ties_lowest_index():
+    """Equal maxima in different 256-token tiles and waves: the lowest token id wins."""
+    V, K, M = 128256, 4096, 130
+    v = torch.randn(K, device=DEV)
+    x = v.to(BF).expand(M, K).contiguous()
+    w = (torch.randn(V, K, device=DEV) * 0.001).to(BF)
+    for j in (70000, 300, 9000, 300 + 128):
+        w[j] = (v * 0.05).to(BF)
+    idx, _ = ops.lm_head_argmax(x, w, None, None)
+    assert idx.cpu().tolist() == [300] * M
+
+
 def test_moe_topk():
     lg = torch.randn(50, 8, device=DEV, dtype=BF)
     w1, i1 = ops.moe_topk(lg, 2)

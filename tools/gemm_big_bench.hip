@@ -3,10 +3,12 @@
 // in the same process, interleaved per round (cdna_hip_programming.md §5.4 rule 24).  No torch.
 //
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/gemm_big_bench.hip -lrocblas -o tools/gemm_big_bench
-//   tools/gemm_big_bench M,N,K,epi[,gm] ...     epi: 0 bf16, 3 SwiGLU (N = 2I), 4 residual add
+//   tools/gemm_big_bench M,N,K,epi[,gm] ...     epi: 0 bf16, 3 SwiGLU (N = 2I), 4 residual add,
+//                                               5 fused LM head + masked argmax (rocBLAS: GEMM only)
 //
 // Weights rotate over copies that exceed the 256 MB Infinity Cache unless GB_WARM=1.
 #include "../ai_agent_kubectl_amd/csrc/gemm_big.hip"
+#include "../ai_agent_kubectl_amd/csrc/sampling.hip"
 
 #include <rocblas/rocblas.h>
 
@@ -87,10 +89,30 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&R, (size_t)M * N * 2));
       hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, st, R, (size_t)M * N, 99u, 1.0f);
     }
+    // EPI 5: two mask rows (0: tokens n % 3 != 0, 1: all), row m uses m % 3 - 1 (-1 = unmasked)
+    const int words = (N + 31) / 32;
+    uint32_t* dmask = nullptr;
+    int *dmidx = nullptr, *didx = nullptr;
+    float* dval = nullptr;
+    void* ws = nullptr;
+    std::vector<uint32_t> hmask(2 * (size_t)words, 0xffffffffu);
+    std::vector<int> hmidx(M);
+    if (epi == 5) {
+      for (int n = 0; n < N; n += 3) hmask[n >> 5] &= ~(1u << (n & 31));
+      for (int m = 0; m < M; ++m) hmidx[m] = m % 3 - 1;
+      CK(hipMalloc(&dmask, hmask.size() * 4));
+      CK(hipMalloc(&dmidx, M * 4));
+      CK(hipMalloc(&didx, M * 4));
+      CK(hipMalloc(&dval, M * 4));
+      CK(hipMalloc(&ws, ka_gemm_big_argmax_ws(M, N)));
+      CK(hipMemcpy(dmask, hmask.data(), hmask.size() * 4, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dmidx, hmidx.data(), M * 4, hipMemcpyHostToDevice));
+    }
     CK(hipStreamSynchronize(st));
 
     auto mine = [&](int r) {
       const bf16_t* w = W + (size_t)(r % nrot) * N * K;
+      if (epi == 5) return ka_gemm_big_argmax(didx, dval, X, w, M, N, K, K, dmask, dmidx, words, 0, ws, st);
       return ka_gemm_big(Y, R, X, w, M, N, K, K, ldy, epi, gm, st);
     };
     auto blas = [&](int r) {
@@ -123,7 +145,22 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(ref.data(), dref, ref.size() * 4, hipMemcpyDeviceToHost));
     std::vector<uint16_t> got((size_t)ldy), rr((size_t)N);
     double err = 0, mr = 0;
-    for (int s = 0; s < S; ++s) {
+    if (epi == 5) {   // the chosen token is allowed and its reference logit is within tolerance of the max
+      std::vector<int> hidx(M);
+      CK(hipMemcpy(hidx.data(), didx, M * 4, hipMemcpyDeviceToHost));
+      for (int s = 0; s < S; ++s) {
+        const int m = rows[s], mi = hmidx[m];
+        auto ok = [&](int n) { return mi < 0 || ((hmask[(size_t)mi * words + (n >> 5)] >> (n & 31)) & 1u); };
+        double best = -1e30;
+        for (int n = 0; n < N; ++n)
+          if (ok(n)) best = std::max(best, (double)ref[(size_t)s * N + n]);
+        const int g = hidx[m];
+        const double d = (g >= 0 && g < N && ok(g)) ? best - ref[(size_t)s * N + g] : 1e30;
+        err = std::max(err, d);
+        mr = std::max(mr, std::fabs(best));
+      }
+    }
+    for (int s = 0; s < S && epi != 5; ++s) {
       CK(hipMemcpy(got.data(), Y + (size_t)rows[s] * ldy, ldy * 2, hipMemcpyDeviceToHost));
       if (R) CK(hipMemcpy(rr.data(), R + (size_t)rows[s] * N, N * 2, hipMemcpyDeviceToHost));
       for (int c = 0; c < ldy; ++c) {
@@ -173,6 +210,13 @@ int main(int argc, char** argv) {
     CK(hipFree(Y));
     CK(hipFree(Yb));
     if (R) CK(hipFree(R));
+    if (epi == 5) {
+      CK(hipFree(dmask));
+      CK(hipFree(dmidx));
+      CK(hipFree(didx));
+      CK(hipFree(dval));
+      CK(hipFree(ws));
+    }
   }
   rocblas_destroy_handle(rb);
   return bad;
