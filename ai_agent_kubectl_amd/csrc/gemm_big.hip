@@ -32,18 +32,11 @@
 namespace gb {
 
 constexpr int BN = 256, BM = 256, BK = 64, NT = 256;
-#ifndef GB_SWZ_MASK
-#define GB_SWZ_MASK 7   // LDS XOR swizzle bits of the 16-B chunk index (7: conflict-free fragment reads)
-#endif
 constexpr int TILE_A = BN * BK * 2, TILE_B = BM * BK * 2;   // 32 KB each
 constexpr int STAGE = TILE_A + TILE_B;                        // 64 KB
-#ifndef GB_RING5
-#define GB_RING5 0  // 1: 5-slot ring of 32-deep stages (160 KB); 0: two 64-deep buffers (128 KB)
-#endif
-constexpr int R_TILE = BN * 32 * 2, R_STAGE = 2 * R_TILE, R_SLOTS = 5;   // ring: 16 KB per operand
-constexpr int LDS = GB_RING5 ? R_SLOTS * R_STAGE : 2 * STAGE;
+constexpr int LDS = 2 * STAGE;   // two 64-deep buffers (a 5-slot ring of 32-deep stages measured slower)
 
-enum Epi : int { EPI_BF16 = 0, EPI_SWIGLU = 3, EPI_ADD = 4, EPI_ARGMAX = 5 };
+enum Epi : int { EPI_BF16 = 0, EPI_P32 = 1, EPI_P16 = 2, EPI_SWIGLU = 3, EPI_ADD = 4, EPI_ARGMAX = 5 };
 
 struct Args {
   const bf16_t* X;   // [M, ldx]
@@ -60,6 +53,10 @@ struct Args {
   int mask_words, vocab_offset;
   float* part_val;
   int* part_idx;
+  // split-K (EPI_P32 / EPI_P16): workgroup (tile, ks) sums k in [ks kp, (ks + 1) kp) into the partial
+  // slab P[ks] of [split][M][N] (fp32 / bf16), reduced by the consumer (ops.SplitK)
+  int split, kp;
+  void* P;
 };
 
 // Every instruction of the k-loop is an asm statement, so the program order written below IS the
@@ -88,18 +85,7 @@ template <int OFF>
 KA_DEV void ds_read16(bf16x8& dst, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
 }
-#ifndef GB_M0KEEP
-#define GB_M0KEEP 1
-#endif
 KA_DEV void dma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t lds_addr) {
-#if !GB_M0KEEP
-  // no M0 save / restore (diagnostic: the kernel issues no other M0 user)
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
-               :
-               : "v"(voff), "s"(r), "s"(lds_addr), "s"(soff)
-               : "memory");
-  return;
-#endif
   uint32_t keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
                "s_mov_b32 m0, %0"
@@ -120,10 +106,14 @@ KA_DEV void block_sync() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// logical tile -> (m tile, n tile): XCD-contiguous (bijective), then GM m-tiles x all n-tiles
-KA_DEV void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+// dispatch index -> logical index, XCD-contiguous (bijective over the grid: consecutive logical
+// indices run on one XCD and share its L2)
+KA_DEV int xcd_logical(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+// logical tile -> (m tile, n tile): GM m-tiles x all n-tiles super-rows
+KA_DEV void tile_of(int L, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
   const int per = gm * tiles_n;
   const int g = L / per, first = g * gm;
   const int rows = min(gm, tiles_m - first);
@@ -139,9 +129,17 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = w & 1, wm = w >> 1;
-  int tm, tn;
-  tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.gm, tm, tn);
+  int tm, tn, ks = 0;
+  {
+    int L = xcd_logical(blockIdx.x, gridDim.x);
+    if constexpr (EPI == EPI_P32 || EPI == EPI_P16) {   // the split slices of a tile on one XCD
+      ks = L % a.split;
+      L /= a.split;
+    }
+    tile_of(L, a.tiles_m, a.tiles_n, a.gm, tm, tn);
+  }
   const int m0 = tm * BM;
+  const uint32_t kb = (uint32_t)ks * (uint32_t)a.kp * 2u;   // byte offset of this slice's k range
 
   const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16_t*>(a.W), (short)0, (int)((uint32_t)a.N * (uint32_t)a.K * 2u), 0x00020000);
@@ -150,109 +148,14 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   // LDS byte address of the staging array (dynamic LDS: the only LDS object of this kernel)
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)lds;
   const int r16 = lane & 15, grp = lane >> 4;
-#if GB_RING5
-  // Ring of R_SLOTS 32-deep stages (A = W rows, B = X rows, 256 x 64 B each).  Stage t is consumed
-  // by phase t (64 MFMAs, fragment set t & 1); phase t also reads stage t + 1 into the other set and
-  // issues 8 DMA pieces (one per two MFMA groups) of stage t + 4 into the slot stage t - 1 vacated.
-  // Its end waits for stage t + 2 (issued in phase t - 2: ~2.5 phases of latency cover) with 16
-  // pieces left in flight, then one barrier.  Piece p of a stage: operand p & 1, rows
-  // (4 (p >> 1) + w) * 16 .. + 16 (1 KB = 16 rows x 64 B); 16-B chunk slot = ch ^ ((row >> 2) & 2).
-  const int nk = a.K / 32;
-  const int r4 = lane >> 2, q4 = lane & 3;
-  uint32_t offA[4], offB[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = (4 * j + w) * 16 + r4;
-    const uint32_t ch = (uint32_t)(q4 ^ ((row >> 2) & 2)) * 8;
-    int wrow;
-    if constexpr (EPI == EPI_SWIGLU) {
-      wrow = 128 * tn + 16 * (row >> 5) + (row & 15) + ((row >> 4) & 1) * a.I;
-    } else {
-      wrow = min(tn * BN + row, a.N - 1);
-    }
-    offA[j] = ((uint32_t)wrow * (uint32_t)a.K + ch) * 2u;
-    offB[j] = ((uint32_t)min(m0 + row, a.M - 1) * (uint32_t)a.ldx + ch) * 2u;
-  }
-  const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)w * 1024u);
-  auto stage_or_oob = [&](int T) { return T < nk ? T : 0x4000000; };   // 0x4000000 * 64 B: past any range
-  auto dma = [&](auto pc, int slot, int T) {
-    constexpr int P = decltype(pc)::value;
-    dma16((P & 1) ? rX : rW, (P & 1) ? offB[P >> 1] : offA[P >> 1], (uint32_t)T * 64u,
-          ldsw + (uint32_t)slot * R_STAGE + (P & 1) * R_TILE + (P >> 1) * 4096);
-  };
-  // fragment reads: row base + 16 i + r16, chunk grp ^ ((r16 >> 2) & 2) (the swizzle of a row depends
-  // only on row % 16)
-  const uint32_t cg = (uint32_t)(grp ^ ((r16 >> 2) & 2)) * 16;
-  const uint32_t rA = lds0 + (wn * 128 + r16) * 64 + cg, rB = lds0 + R_TILE + (wm * 128 + r16) * 64 + cg;
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
-
-  auto rd = [&](auto sc, bf16x8* FA, bf16x8* FB, uint32_t ba, uint32_t bb) {
-    constexpr int S = decltype(sc)::value;
-    if constexpr (S & 1) ds_read16<(S >> 1) * 1024>(FB[S >> 1], bb);
-    else ds_read16<(S >> 1) * 1024>(FA[S >> 1], ba);
-  };
-  auto mma4 = [&](auto sc, const bf16x8* FA, const bf16x8* FB) {
-    constexpr int S = decltype(sc)::value;
-    static_for<4>([&](auto qc) {
-      constexpr int q = 4 * S + decltype(qc)::value;
-      mfma_acc(acc[q >> 3][q & 7], FA[q >> 3], FB[q & 7]);
-    });
-  };
-  // phase t (fragment set FS computes, the other one is read): slots are runtime (t mod 5)
-  auto phase = [&](auto fsc, int t, int s_next, int s_dma) {
-    constexpr int FS = decltype(fsc)::value;
-    const uint32_t ba = rA + (uint32_t)s_next * R_STAGE, bb = rB + (uint32_t)s_next * R_STAGE;
-    const int td = stage_or_oob(t + 4);
-    static_for<16>([&](auto sc) {
-      constexpr int S = decltype(sc)::value;
-      if constexpr (FS == 0) rd(sc, fa1, fb1, ba, bb);
-      else rd(sc, fa0, fb0, ba, bb);
-      if constexpr ((S & 1) == 0) dma(std::integral_constant<int, (S >> 1)>{}, s_dma, td);
-      if constexpr (FS == 0) mma4(sc, fa0, fb0);
-      else mma4(sc, fa1, fb1);
-    });
-    wait_lgkm0();
-    wait_vm<16>();
-    block_sync();
-  };
-
-  // prologue: stages 0 .. 3 in flight; stages 0 and 1 landed; set 0 <- stage 0
-  static_for<8>([&](auto pc) { dma(pc, 0, 0); });
-  static_for<8>([&](auto pc) { dma(pc, 1, stage_or_oob(1)); });
-  static_for<8>([&](auto pc) { dma(pc, 2, stage_or_oob(2)); });
-  static_for<8>([&](auto pc) { dma(pc, 3, stage_or_oob(3)); });
-  wait_vm<16>();
-  block_sync();
-  static_for<16>([&](auto sc) { rd(sc, fa0, fb0, rA, rB); });
-  wait_lgkm0();
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  // K % 64 == 0: nk is even, two phases per trip (fragment sets are compile-time)
-  int s0 = 0;   // slot of stage t
-  for (int t = 0; t < nk; t += 2) {
-    const int s1 = s0 == 4 ? 0 : s0 + 1, s2 = s1 == 4 ? 0 : s1 + 1;
-    const int sm1 = s0 == 0 ? 4 : s0 - 1;   // slot of stage t - 1 == slot of stage t + 4
-    phase(I0{}, t, s1, sm1);
-    phase(I1{}, t + 1, s2, s0);
-    s0 = s2;
-  }
-  wait_vm<0>();   // the trailing out-of-range DMAs: nothing may land in LDS after the workgroup ends
-  mfma_drain();
-#else
-  const int nk = a.K / BK;
+  const int nk = (EPI == EPI_P32 || EPI == EPI_P16 ? a.kp : a.K) / BK;
   // DMA sources: wave-instruction j (< 8) of this wave fills staged rows (4j + w) * 8 .. + 8 (1 KB)
   const int r8 = lane >> 3, slot = lane & 7;
   uint32_t offA[8], offB[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int row = (4 * j + w) * 8 + r8;
-    const uint32_t ch = (uint32_t)(slot ^ (((row >> 1) & 7) & GB_SWZ_MASK)) * 8;
+    const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
     int wrow;
     if constexpr (EPI == EPI_SWIGLU) {
       // tile tn covers output columns [128 tn, 128 tn + 128): 16-row chunk c of the staged W tile is
@@ -261,8 +164,8 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     } else {
       wrow = min(tn * BN + row, a.N - 1);
     }
-    offA[j] = ((uint32_t)wrow * (uint32_t)a.K + ch) * 2u;
-    offB[j] = ((uint32_t)min(m0 + row, a.M - 1) * (uint32_t)a.ldx + ch) * 2u;
+    offA[j] = ((uint32_t)wrow * (uint32_t)a.K + ch) * 2u + kb;
+    offB[j] = ((uint32_t)min(m0 + row, a.M - 1) * (uint32_t)a.ldx + ch) * 2u + kb;
   }
   const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)w * 1024u);
   // DMA piece s (< 16) of a k-tile: W rows (s even) or X rows (s odd) group (4 (s >> 1) + w) * 8
@@ -271,7 +174,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
         ldsw + (BUF) * STAGE + ((S) & 1) * TILE_A + ((S) >> 1) * 4096)
 
   // fragment read bases (bytes, LDS address): [buffer][k half] of the A (W) and B (X) quadrants
-  const int sw = ((r16 >> 1) & 7) & GB_SWZ_MASK;
+  const int sw = (r16 >> 1) & 7;
   const uint32_t c0 = ((0 + grp) ^ sw) * 16, c1 = ((4 + grp) ^ sw) * 16;
   const uint32_t rA = lds0 + (wn * 128 + r16) * 128, rB = lds0 + TILE_A + (wm * 128 + r16) * 128;
   const uint32_t bA00 = rA + c0, bA01 = rA + c1, bA10 = rA + STAGE + c0, bA11 = rA + STAGE + c1;
@@ -301,58 +204,30 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   // phase A of a tile in buffer BUF: its second k half into F1 while F0's MFMAs run; then every read
   // of buffer BUF retired (WAR for the DMA that refills it) and the next tile landed (this wave's
   // part; the barrier makes it every wave's)
-#ifndef GB_SPLIT_DMA
-#define GB_SPLIT_DMA 0
-#endif
-  // DMA pieces of tile T issued by phase A / phase B: with GB_SPLIT_DMA the 16 pieces of a tile are
-  // split 8 / 8 between the phase B that starts them and the next phase A (first 8 groups), so no
-  // phase carries more than 8 DMA issues beside its 16 reads and 64 MFMAs
-  constexpr int A_DMA = GB_SPLIT_DMA ? 8 : 0;
-  auto tile_or_oob = [&](int T) { return T < nk ? T : 0x4000000; };   // 0x4000000 * 128 B: past any range
-#ifndef GB_ABL
-#define GB_ABL 0   // diagnostic ablations (wrong results): 1 no wait/barrier, 2 no DMA, 3 no fragment reads
-#endif
-  auto phase_a = [&](auto bufc, int T) {
+  // past the last tile: re-stage the last tile (L2-hot, never consumed) — the buffer range check
+  // does not cover soffset, so an out-of-range k offset would read past the operand
+  auto tile_or_oob = [&](int T) { return T < nk ? T : nk - 1; };
+  auto phase_a = [&](auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
-    const int tt = tile_or_oob(T);
     static_for<16>([&](auto sc) {
-      constexpr int S = decltype(sc)::value;
-      if constexpr (GB_ABL != 3) rd(sc, fa1, fb1, BUF ? bA11 : bA01, BUF ? bB11 : bB01);
-      if constexpr (S < A_DMA) GB_DMA(16 - A_DMA + S, BUF ^ 1, tt);
+      rd(sc, fa1, fb1, BUF ? bA11 : bA01, BUF ? bB11 : bB01);
       mma4(sc, fa0, fb0);
     });
     wait_lgkm0();
-    if constexpr (GB_ABL != 1) {
-      wait_vm<0>();
-      block_sync();
-    }
+    wait_vm<0>();
+    block_sync();
   };
-  // phase B: the next tile's first k half into F0, the DMA of tile T into buffer BUF, F1's MFMAs; F0
-  // retired at the end (covered by the 64 MFMAs).  Past the last tile the reads fetch stale LDS that
-  // no MFMA consumes and the DMA's k offset is out of the buffer's range (the bounds check turns it
-  // into a no-fetch zero fill of a buffer nothing reads again): no control flow in the k-loop.
+  // phase B: the next tile's first k half into F0, the DMA of tile T into buffer BUF (one 1-KB piece
+  // per MFMA group), F1's MFMAs; F0 retired at the end (covered by the 64 MFMAs).  Past the last
+  // tile the reads fetch LDS that no MFMA consumes and the DMA re-stages the last tile into a
+  // buffer nothing reads again: no control flow in the k-loop.
   auto phase_b = [&](auto bufc, int T) {
     constexpr int BUF = decltype(bufc)::value;
     const int tt = tile_or_oob(T);
-#ifndef GB_BPLACE
-#define GB_BPLACE 0   // phase-B DMA placement: 0 one per MFMA group, 1 two per group in the first half, 2 all first
-#endif
-    if constexpr (GB_BPLACE == 2 && A_DMA == 0) static_for<16>([&](auto sc) { GB_DMA(decltype(sc)::value, BUF, tt); });
     static_for<16>([&](auto sc) {
       constexpr int S = decltype(sc)::value;
-      if constexpr (GB_ABL != 3) rd(sc, fa0, fb0, BUF ? bA00 : bA10, BUF ? bB00 : bB10);
-      if constexpr (GB_ABL == 2) {
-      } else if constexpr (A_DMA == 0 && GB_BPLACE == 0) GB_DMA(S, BUF, tt);
-      else if constexpr (A_DMA == 0 && GB_BPLACE == 3) {
-        // wave-staggered: wave w issues piece S in group (S + 4 w) mod 16 (the four waves' DMA
-        // bursts do not line up on the TA); here group S issues piece (S - 4 w) mod 16
-        static_for<4>([&](auto wc) {
-          if (w == decltype(wc)::value) GB_DMA(((S + 16 - 4 * decltype(wc)::value) & 15), BUF, tt);
-        });
-      }
-      else if constexpr (A_DMA == 0 && GB_BPLACE == 1) {
-        if constexpr (S < 8) { GB_DMA(2 * S, BUF, tt); GB_DMA(2 * S + 1, BUF, tt); }
-      } else if constexpr (A_DMA != 0 && (S & 1) == 0) GB_DMA(S >> 1, BUF, tt);
+      rd(sc, fa0, fb0, BUF ? bA00 : bA10, BUF ? bB00 : bB10);
+      GB_DMA(S, BUF, tt);
       mma4(sc, fa1, fb1);
     });
     wait_lgkm0();
@@ -362,8 +237,8 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
 
   // prologue: tile 0 and the phase-B part of tile 1 in flight, wait for tile 0, read its first half
   static_for<16>([&](auto sc) { GB_DMA(decltype(sc)::value, 0, 0); });
-  static_for<16 - A_DMA>([&](auto sc) { GB_DMA(decltype(sc)::value, 1, tile_or_oob(1)); });
-  wait_vm<16 - A_DMA>();
+  static_for<16>([&](auto sc) { GB_DMA(decltype(sc)::value, 1, tile_or_oob(1)); });
+  wait_vm<16>();
   block_sync();
   static_for<16>([&](auto sc) { rd(sc, fa0, fb0, bA00, bB00); });
   wait_lgkm0();
@@ -371,16 +246,14 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   // two tiles per trip so every buffer index is a compile-time constant (K % 128 == 0: no odd tail,
   // no control flow in the loop but its back edge)
   for (int t = 0; t < nk; t += 2) {
-    phase_a(I0{}, t + 1);
+    phase_a(I0{});
     phase_b(I0{}, t + 2);
-    phase_a(I1{}, t + 2);
+    phase_a(I1{});
     phase_b(I1{}, t + 3);
   }
   wait_vm<0>();   // the trailing out-of-range DMAs: nothing may land in LDS after the workgroup ends
   mfma_drain();
 #undef GB_DMA
-
-#endif
   // epilogue.  acc[i][j][r] = C[n = 128 wn + 16 i + 4 grp + r][m = 128 wm + 16 j + r16] of the tile.
   // The wave's quadrant is transposed through its own 32 KB of LDS (the staging buffers are free
   // after the barrier below) into [m][n] rows, then stored as whole 16-B lanes: 4 rows x 256 B (SwiGLU:
@@ -389,6 +262,25 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   for (int i = 0; i < 8; ++i)   // the asm MFMAs' results are read only after mfma_drain's wait states
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  if constexpr (EPI == EPI_P32 || EPI == EPI_P16) {
+    // partial slab rows m, columns n .. n + 3 of the lane's accumulators: 16 B (fp32) / 8 B (bf16)
+    // per lane, the 4 lanes of a row contiguous
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + 128 * wm + 16 * j + r16;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int n = tn * BN + 128 * wn + 16 * i + 4 * grp;
+        if (n >= a.N) continue;
+        const size_t o = ((size_t)ks * a.M + m) * a.N + n;
+        const f32x4 v = acc[i][j];
+        if constexpr (EPI == EPI_P32) *reinterpret_cast<f32x4*>(static_cast<float*>(a.P) + o) = v;
+        else *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.P) + o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
+    return;
+  }
   block_sync();   // every wave is past its last (stale) fragment read of the staging buffers
   char* const Q = L + w * 32768;
   if constexpr (EPI == EPI_ARGMAX) {
@@ -436,6 +328,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
         Si[w * 128 + 16 * j + r16] = bidx;
       }
     }
+    wait_lgkm0();   // block_sync is a bare s_barrier: the other waves read these stores after it
     block_sync();
     {   // thread t: tile row t = 128 wm' + rr, from waves 2 wm' (columns 0..127) and 2 wm' + 1
       const int wm2 = tid >> 7, rr = tid & 127, m = m0 + tid;
@@ -514,7 +407,8 @@ static int launch(const Args& a0, hipStream_t st) {
   Args a = a0;
   a.tiles_m = (a.M + BM - 1) / BM;
   a.tiles_n = EPI == EPI_SWIGLU ? a.I / 128 : (a.N + BN - 1) / BN;
-  hipLaunchKernelGGL(kern, dim3(a.tiles_m * a.tiles_n), dim3(NT), LDS, st, a);
+  const int split = (EPI == EPI_P32 || EPI == EPI_P16) ? a.split : 1;
+  hipLaunchKernelGGL(kern, dim3(a.tiles_m * a.tiles_n * split), dim3(NT), LDS, st, a);
   return (int)hipGetLastError();
 }
 
@@ -539,6 +433,22 @@ extern "C" int ka_gemm_big(void* Y, const void* R, const void* X, const void* W,
       return gb::launch<gb::EPI_ADD>(a, stream);
   }
   return (int)hipErrorInvalidValue;
+}
+
+// Split-K partials: P[ks][M][N] = X[:, ks kp : (ks + 1) kp] W[:, same]^T with kp = K / split, fp32
+// (bf16_out = 0) or bf16 (1), for a consumer that fuses the reduction (ops.SplitK).
+// Requirements: K % (128 split) == 0, N % 128 == 0, ldx % 8 == 0.
+extern "C" int ka_gemm_big_splitk(void* P, const void* X, const void* W, int M, int N, int K, int ldx, int split,
+                                  int bf16_out, int gm, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (split < 1 || K % (128 * split) != 0 || N % 128 != 0 || ldx % 8 != 0 || P == nullptr)
+    return (int)hipErrorInvalidValue;
+  gb::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), nullptr, nullptr, M, N, K, ldx, 8, 0, 0,
+             gm > 0 ? gm : 8, N / 2};
+  a.split = split;
+  a.kp = K / split;
+  a.P = P;
+  return bf16_out ? gb::launch<gb::EPI_P16>(a, stream) : gb::launch<gb::EPI_P32>(a, stream);
 }
 
 extern "C" int ka_argmax_finish(int* out_idx, float* out_val, const float* part_val, const int* part_idx, int rows,

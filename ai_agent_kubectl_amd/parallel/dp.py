@@ -518,6 +518,18 @@ class DPRouterLLM(LLMBackend):
         self.owner = self.supervisor is not None
         self.authkey = endpoints.authkey
         self.replicas: List[_Replica] = [_Replica(i, a) for i, a in enumerate(endpoints.addresses)]
+        # several API workers in front of the same replicas (serve.py WORKERS > 1): least-loaded
+        # routing over every worker's in-flight counts, kept in the shared state's load table
+        # (each worker writes its own row); a single router balances on its own counts
+        self.loads = None
+        if not self.owner:
+            from ..shared_state import open_from_settings
+            try:
+                self.loads = open_from_settings(settings)
+            except Exception:   # pragma: no cover - no native runtime: local counts only
+                self.loads = None
+            if self.loads is not None:
+                self.loads.load_clear_worker(client_id)   # a respawned worker's row starts at zero
         # the reply-reader thread must get the GIL promptly while the event loop is busy
         sys.setswitchinterval(min(sys.getswitchinterval(), 0.001))
         self._pending: Dict[int, tuple] = {}
@@ -625,6 +637,7 @@ class DPRouterLLM(LLMBackend):
                     if ent is not None:
                         ent[2].inflight -= 1
                         by_loop.setdefault(ent[0], []).append((ent[1], payload))
+                self._publish_load(r)
             for loop, lst in by_loop.items():
                 loop.call_soon_threadsafe(_set_many, lst)
         elif kind == "ctl":
@@ -651,12 +664,29 @@ class DPRouterLLM(LLMBackend):
             for name in ("llm_batch_size", "llm_queue_depth", "llm_kv_blocks_used"):
                 getattr(m, name).set(sum(g.get(name, 0) for g in self._gauges.values()))
 
+    def _publish_load(self, r) -> None:
+        if self.loads is not None and isinstance(r, _Replica):
+            self.loads.load_set(self.client_id, r.idx, r.inflight)
+
+    def _pick(self, live: List["_Replica"]) -> "_Replica":
+        """Least-loaded live replica: over every API worker's in-flight requests when they share a
+        load table, else over this router's own."""
+        if self.loads is not None and len(self.replicas) > 1:
+            mask = 0
+            for r in live:
+                mask |= 1 << r.idx
+            i = self.loads.load_pick(len(self.replicas), mask)
+            if i >= 0:
+                return self.replicas[i]
+        return min(live, key=lambda r: r.inflight)
+
     def _fail_replica(self, r) -> None:
         with self._lock:
             dead = [(k, v) for k, v in self._pending.items() if v[2] is r]
             for k, _ in dead:
                 self._pending.pop(k)
             r.inflight = 0
+            self._publish_load(r)
         for _, (loop, fut, _) in dead:
             loop.call_soon_threadsafe(_set_exc, fut, LLMUnavailableError(f"replica {r.idx} died"))
 
@@ -738,13 +768,14 @@ class DPRouterLLM(LLMBackend):
         live = [r for r in self.replicas if r.up]
         if not live:
             raise LLMUnavailableError("no live DP replica")
-        rep = min(live, key=lambda r: r.inflight)
+        rep = self._pick(live)
         rid = next(self._ids)
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
         with self._lock:
             self._pending[rid] = (loop, fut, rep)
             rep.inflight += 1
+            self._publish_load(rep)
         self._send(rep, ("gen", rid, self.prompt_ids(query)), loop)
         try:
             out_ids, err, reason = await fut
@@ -756,6 +787,7 @@ class DPRouterLLM(LLMBackend):
             with self._lock:
                 if self._pending.pop(rid, None) is not None:
                     rep.inflight -= 1
+                    self._publish_load(rep)
             raise
         if err is not None:
             raise LLMUnavailableError(err) if reason == "error" else RuntimeError(err)

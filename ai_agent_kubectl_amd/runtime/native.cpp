@@ -120,5 +120,9 @@ PYBIND11_MODULE(_native, m) {
              py::gil_scoped_release rel;
              return s.limiter_hit(k0, k1, amount, expiry, now);
            })
-      .def("limiter_reset", &SharedState::limiter_reset);
+      .def("limiter_reset", &SharedState::limiter_reset)
+      .def("load_set", &SharedState::load_set)
+      .def("load_clear_worker", &SharedState::load_clear_worker)
+      .def("load_total", &SharedState::load_total)
+      .def("load_pick", &SharedState::load_pick);
 }

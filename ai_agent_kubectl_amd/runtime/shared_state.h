@@ -36,7 +36,11 @@ namespace ka {
 class SharedState {
  public:
   static constexpr uint64_t kMagic = 0x4b41535354415445ull;   // "KASSTATE"
-  static constexpr uint32_t kVersion = 2;
+  static constexpr uint32_t kVersion = 3;
+  // DP routing load table: in-flight requests per (API worker, engine replica).  Each worker writes
+  // only its own row (single writer, lock-free); a router picks the replica with the least total
+  // over all rows, so W workers balance N replicas as one router would.
+  static constexpr uint32_t kMaxWorkers = 64, kMaxReplicas = 64;
 
   struct Header {
     uint64_t magic;
@@ -47,6 +51,7 @@ class SharedState {
     uint32_t count;
     uint64_t hits, misses, sets, evictions, lim_used;
     uint64_t owner_deaths;   // lock holders that died (each reset the segment)
+    int64_t load[kMaxWorkers][kMaxReplicas];   // not covered by the mutex, not cleared by a reset
   };
   struct Entry {
     uint64_t k0, k1;
@@ -142,6 +147,36 @@ class SharedState {
   const std::string& name() const { return name_; }
   uint32_t cache_capacity() const { return h_->cache_cap; }
   uint32_t value_max() const { return h_->value_max; }
+
+  // ---- DP routing load -----------------------------------------------------------------------
+  void load_set(uint32_t worker, uint32_t replica, int64_t v) {
+    if (worker < kMaxWorkers && replica < kMaxReplicas) __atomic_store_n(&h_->load[worker][replica], v, __ATOMIC_RELAXED);
+  }
+  void load_clear_worker(uint32_t worker) {
+    if (worker >= kMaxWorkers) return;
+    for (uint32_t r = 0; r < kMaxReplicas; ++r) __atomic_store_n(&h_->load[worker][r], 0, __ATOMIC_RELAXED);
+  }
+  int64_t load_total(uint32_t replica) const {
+    int64_t t = 0;
+    if (replica >= kMaxReplicas) return 0;
+    for (uint32_t w = 0; w < kMaxWorkers; ++w) t += __atomic_load_n(&h_->load[w][replica], __ATOMIC_RELAXED);
+    return t;
+  }
+  // the live replica (bit r of live_mask) with the least total in-flight load; ties: lowest index.
+  // -1 when none is live.
+  int32_t load_pick(uint32_t n, uint64_t live_mask) const {
+    int32_t best = -1;
+    int64_t bl = 0;
+    for (uint32_t r = 0; r < n && r < kMaxReplicas; ++r) {
+      if (!((live_mask >> r) & 1u)) continue;
+      const int64_t t = load_total(r);
+      if (best < 0 || t < bl) {
+        best = (int32_t)r;
+        bl = t;
+      }
+    }
+    return best;
+  }
 
   // ---- cache -------------------------------------------------------------------------------
   // get: live value -> true (and the entry becomes most recently used); expired / absent -> false

@@ -65,6 +65,20 @@ class SharedStore:
     def stats(self) -> dict:
         return self._s.stats()
 
+    # DP routing load (parallel/dp.py): in-flight requests per (API worker, replica)
+    def load_set(self, worker: int, replica: int, value: int) -> None:
+        self._s.load_set(int(worker), int(replica), int(value))
+
+    def load_clear_worker(self, worker: int) -> None:
+        self._s.load_clear_worker(int(worker))
+
+    def load_total(self, replica: int) -> int:
+        return self._s.load_total(int(replica))
+
+    def load_pick(self, n: int, live_mask: int) -> int:
+        """Least-loaded live replica over every worker's in-flight counts (-1: none live)."""
+        return self._s.load_pick(int(n), int(live_mask))
+
     @staticmethod
     def unlink(name: str) -> None:
         """Remove the segment name (processes that still map it keep working)."""

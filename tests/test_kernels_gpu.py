@@ -282,7 +282,8 @@ def test_lm_head_argmax_vs_fp32(M, off):
     assert ((got >= 0) & (got < V)).all()
     assert allowed.gather(1, got[:, None]).all()
     chosen = ref_logits.gather(1, got[:, None]).squeeze(1)
-    assert ((best - chosen) <= 0.02 * best.abs().clamp(min=1.0)).all()
+    bad = ((best - chosen) > 0.02 * best.abs().clamp(min=1.0)).nonzero().flatten().tolist()
+    assert not bad, [(r, int(got[r]), float(chosen[r]), float(best[r]), int(masked[r].argmax())) for r in bad[:8]]
     close(val, chosen, atol=0.05, rtol=0.02)
 
 

@@ -4,7 +4,9 @@
 //
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/gemm_big_bench.hip -lrocblas -o tools/gemm_big_bench
 //   tools/gemm_big_bench M,N,K,epi[,gm] ...     epi: 0 bf16, 3 SwiGLU (N = 2I), 4 residual add,
-//                                               5 fused LM head + masked argmax (rocBLAS: GEMM only)
+//                                               5 fused LM head + masked argmax (rocBLAS: GEMM only),
+//                                               1 / 2 split-K fp32 / bf16 partials (the 5th field is the
+//                                               split; the consumer's reduction is not timed)
 //
 // Weights rotate over copies that exceed the 256 MB Infinity Cache unless GB_WARM=1.
 #include "../ai_agent_kubectl_amd/csrc/gemm_big.hip"
@@ -81,6 +83,10 @@ int main(int argc, char** argv) {
     bf16_t *X, *W, *Y, *Yb, *R = nullptr;
     CK(hipMalloc(&X, (size_t)M * K * 2));
     CK(hipMalloc(&W, wbytes * nrot));
+    const bool part = epi == 1 || epi == 2;
+    const int split = part ? gm : 1;
+    void* P = nullptr;
+    if (part) CK(hipMalloc(&P, (size_t)split * M * N * 4));
     CK(hipMalloc(&Y, (size_t)M * ldy * 2));
     CK(hipMalloc(&Yb, (size_t)M * N * 2));
     hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, st, X, (size_t)M * K, 1234u, 1.0f);
@@ -113,6 +119,7 @@ int main(int argc, char** argv) {
     auto mine = [&](int r) {
       const bf16_t* w = W + (size_t)(r % nrot) * N * K;
       if (epi == 5) return ka_gemm_big_argmax(didx, dval, X, w, M, N, K, K, dmask, dmidx, words, 0, ws, st);
+      if (part) return ka_gemm_big_splitk(P, X, w, M, N, K, K, split, epi == 2, 8, st);
       return ka_gemm_big(Y, R, X, w, M, N, K, K, ldy, epi, gm, st);
     };
     auto blas = [&](int r) {
@@ -160,7 +167,28 @@ int main(int argc, char** argv) {
         mr = std::max(mr, std::fabs(best));
       }
     }
-    for (int s = 0; s < S && epi != 5; ++s) {
+    if (part) {   // sum of the slices' partials
+      std::vector<float> pf((size_t)N);
+      std::vector<uint16_t> ph((size_t)N);
+      for (int s = 0; s < S; ++s) {
+        std::vector<double> sum((size_t)N, 0.0);
+        for (int k = 0; k < split; ++k) {
+          const size_t o = ((size_t)k * M + rows[s]) * N;
+          if (epi == 1) {
+            CK(hipMemcpy(pf.data(), static_cast<float*>(P) + o, N * 4, hipMemcpyDeviceToHost));
+            for (int c = 0; c < N; ++c) sum[c] += pf[c];
+          } else {
+            CK(hipMemcpy(ph.data(), static_cast<uint16_t*>(P) + o, N * 2, hipMemcpyDeviceToHost));
+            for (int c = 0; c < N; ++c) sum[c] += bf(ph[c]);
+          }
+        }
+        for (int c = 0; c < N; ++c) {
+          err = std::max(err, std::fabs(sum[c] - ref[(size_t)s * N + c]));
+          mr = std::max(mr, (double)std::fabs(ref[(size_t)s * N + c]));
+        }
+      }
+    }
+    for (int s = 0; s < S && epi != 5 && !part; ++s) {
       CK(hipMemcpy(got.data(), Y + (size_t)rows[s] * ldy, ldy * 2, hipMemcpyDeviceToHost));
       if (R) CK(hipMemcpy(rr.data(), R + (size_t)rows[s] * N, N * 2, hipMemcpyDeviceToHost));
       for (int c = 0; c < ldy; ++c) {
@@ -210,6 +238,7 @@ int main(int argc, char** argv) {
     CK(hipFree(Y));
     CK(hipFree(Yb));
     if (R) CK(hipFree(R));
+    if (P) CK(hipFree(P));
     if (epi == 5) {
       CK(hipFree(dmask));
       CK(hipFree(dmidx));
