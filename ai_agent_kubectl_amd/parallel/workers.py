@@ -33,8 +33,12 @@ log = logging.getLogger("app")
 
 
 def bind_reuseport(host: str, port: int) -> socket.socket:
+    """The worker's listening socket.  Created with proto=IPPROTO_TCP, as getaddrinfo's sockets are:
+    asyncio turns Nagle off (TCP_NODELAY) only on accepted sockets whose proto says TCP, and with
+    Nagle on, uvicorn's two writes per response (head, then body) wait for the client's delayed ACK
+    — +40 ms on every request (profiles/r3/README.md)."""
     fam = socket.AF_INET6 if ":" in host else socket.AF_INET
-    s = socket.socket(fam, socket.SOCK_STREAM)
+    s = socket.socket(fam, socket.SOCK_STREAM, socket.IPPROTO_TCP)
     s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
     s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
     s.bind((host, port))
