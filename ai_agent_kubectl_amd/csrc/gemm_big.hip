@@ -11,9 +11,15 @@
 //   * W is the MFMA A operand and X the B operand: a lane's four accumulators are four consecutive
 //     output columns (8-B bf16 stores), and the SwiGLU epilogue finds gate and up of one output in
 //     the same lane;
-//   * both operands staged HBM/L2 -> LDS by LDS-DMA (global_load_lds dwordx4), 2 buffers x 64 KB;
+//   * both operands staged HBM/L2 -> LDS by LDS-DMA (buffer_load dwordx4 ... lds), 2 buffers x 64 KB;
 //     the XOR swizzle slot = chunk ^ ((row >> 1) & 7) is applied to the per-lane global source and
-//     to the ds_read address (rule 21), conflict-free fragment reads;
+//     to the ds_read address (rule 21), conflict-free fragment reads.  A wave's 1-KB pieces of a
+//     k-tile are 4-KB contiguous groups written under one M0 value (the immediate offset selects the
+//     piece): 4 M0 writes per 16 pieces instead of 16, +6-7 % on every shape
+//     (profiles/r3/gemm_big/gb_m0_ab.log);
+//   * persistent: one workgroup per CU walks its tiles; the next tile's first two k-tiles are staged
+//     during the current tile's last two k-steps and the epilogue transposes through a separate
+//     32 KB of LDS, so it overlaps their landing (+0.5-1 %, gb_p_ab.log);
 //   * two register fragment sets: the k-step's second half is read while the first half's 64 MFMAs
 //     run, and the next tile's first half while the second half's run.  ONE barrier per k-tile, and
 //     each tile's DMA is issued two half-steps (2 x 64 MFMAs) before the barrier that waits for it:
@@ -22,12 +28,17 @@
 //     (WAR: buffer t&1's last reads are F1 of phase A(t), retired before that barrier);
 //   * XCD-aware tile order (T1): the bijective round-robin remap, then GM m-tiles x all n-tiles
 //     super-rows so the panels of the tiles running together on one XCD are L2 hits.
+// Measured at 0.90-0.92x rocBLAS's MT256x256x64 kernel on the plain shapes at M = 4096 and 0.96-0.98x
+// at M ~ 3000; the SwiGLU epilogue (no [M, 2I] write, no SiLU pass) makes gate_up + SiLU a net win,
+// which is what the engine dispatches (ops.linear_swiglu); the other prefill projections stay
+// hipBLASLt (profiles/r3/README.md).
 // Epilogues: bf16 store; SwiGLU over the un-interleaved [gate; up] weight (the tile's W rows are
 // gathered as alternating 16-row gate / up chunks by the DMA source addresses, so the [M, 2I]
 // gate_up output never exists); residual add (Y = X W^T + R, R may alias Y).
 #include "common.h"
 
 #include <utility>
+
 
 namespace gb {
 
@@ -64,8 +75,9 @@ struct Args {
 // own for these loads: the s_waitcnt / s_barrier statements below are the whole synchronisation.
 //  * ds_read_b128: fragment read (16-bit immediate offset);
 //  * LDS-DMA: buffer_load_dwordx4 ... offen lds through a buffer descriptor (wave-uniform base in
-//    SGPRs, k offset in soffset, one 32-bit VGPR offset per lane); M0 = the wave's LDS destination,
-//    saved and restored inside the statement (M0 is compiler-reserved);
+//    SGPRs, k offset in soffset, one 32-bit VGPR offset per lane); M0 = the LDS destination group,
+//    saved by a group's first piece and restored by its fourth (M0 is compiler-reserved; nothing
+//    hipcc emits between them uses it);
 //  * MFMA with the accumulator pinned in place in the AGPR file ("+a"): the builtin form lets the
 //    register allocator rotate the 64 accumulators through VGPRs (~100 v_accvgpr moves per k-tile
 //    at this register pressure).  An MFMA's D read by anything but the next MFMA's C needs the wait
@@ -85,13 +97,26 @@ template <int OFF>
 KA_DEV void ds_read16(bf16x8& dst, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
 }
-KA_DEV void dma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t lds_addr) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
-               "s_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(r), "s"(lds_addr), "s"(soff)
-               : "memory");
+// the same piece under a shared M0: piece P (< 4) of a 4-KB LDS group writes M0 + 1024 P (the immediate
+// offset applies to both the LDS destination and the global address, so the lane's global offset is
+// pre-biased by -1024 P); P == 0 saves M0 and points it at the group, P == 3 restores it
+template <int P>
+KA_DEV void dma16g(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t lds_addr, uint32_t& keep) {
+  if constexpr (P == 0)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(r), "s"(lds_addr), "s"(soff)
+                 : "memory");
+  else if constexpr (P == 3)
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:3072 lds\n\ts_mov_b32 m0, %3"
+                 :
+                 : "v"(voff), "s"(r), "s"(soff), "s"(keep)
+                 : "memory");
+  else
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:%3 lds"
+                 :
+                 : "v"(voff), "s"(r), "s"(soff), "i"(P * 1024)
+                 : "memory");
 }
 KA_DEV void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
@@ -129,49 +154,70 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = w & 1, wm = w >> 1;
-  int tm, tn, ks = 0;
-  {
-    int L = xcd_logical(blockIdx.x, gridDim.x);
-    if constexpr (EPI == EPI_P32 || EPI == EPI_P16) {   // the split slices of a tile on one XCD
-      ks = L % a.split;
-      L /= a.split;
+  constexpr bool SPLIT = EPI == EPI_P32 || EPI == EPI_P16;
+  // Persistent: workgroup b computes the output tiles of virtual dispatch ids b, b + G, b + 2G, ...
+  // (G = gridDim.x, a multiple of 8 whenever G < total), each mapped like a one-tile-per-workgroup
+  // grid of `total` workgroups would be: an id keeps its XCD (b mod 8), so the tiles running together
+  // on one XCD are still neighbours.  The next tile's first two k-tiles are staged during the last
+  // two k-steps of the current one, so the epilogue overlaps their landing.
+  const int total = a.tiles_m * a.tiles_n * (SPLIT ? a.split : 1);
+  auto decode = [&](int v, int& tm, int& tn, int& ks) {
+    int lg = xcd_logical(v, total);
+    ks = 0;
+    if constexpr (SPLIT) {   // the split slices of a tile on one XCD
+      ks = lg % a.split;
+      lg /= a.split;
     }
-    tile_of(L, a.tiles_m, a.tiles_n, a.gm, tm, tn);
-  }
-  const int m0 = tm * BM;
-  const uint32_t kb = (uint32_t)ks * (uint32_t)a.kp * 2u;   // byte offset of this slice's k range
+    tile_of(lg, a.tiles_m, a.tiles_n, a.gm, tm, tn);
+  };
+  int vb = blockIdx.x, tm, tn, ks;
+  decode(vb, tm, tn, ks);
 
+  // the descriptors start BIAS bytes before the operands, so the per-lane offsets (pre-biased by
+  // -1024 (j & 3) for the immediate offset of dma16g) never wrap; nothing below an operand is read
+  constexpr uint32_t BIAS = 3072;
   const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(a.W), (short)0, (int)((uint32_t)a.N * (uint32_t)a.K * 2u), 0x00020000);
+      const_cast<char*>(reinterpret_cast<const char*>(a.W)) - BIAS, (short)0,
+      (int)((uint32_t)a.N * (uint32_t)a.K * 2u + BIAS), 0x00020000);
   const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(a.X), (short)0, (int)((uint32_t)a.M * (uint32_t)a.ldx * 2u), 0x00020000);
+      const_cast<char*>(reinterpret_cast<const char*>(a.X)) - BIAS, (short)0,
+      (int)((uint32_t)a.M * (uint32_t)a.ldx * 2u + BIAS), 0x00020000);
   // LDS byte address of the staging array (dynamic LDS: the only LDS object of this kernel)
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)lds;
   const int r16 = lane & 15, grp = lane >> 4;
-  const int nk = (EPI == EPI_P32 || EPI == EPI_P16 ? a.kp : a.K) / BK;
-  // DMA sources: wave-instruction j (< 8) of this wave fills staged rows (4j + w) * 8 .. + 8 (1 KB)
+  const int nk = (SPLIT ? a.kp : a.K) / BK;
+  // DMA sources: wave-instruction j (< 8) of this wave fills staged rows 64 w + 8 j .. + 8 (1 KB) of
+  // the W and of the X tile, so a wave's pieces are contiguous 1-KB blocks (4 per M0 value)
   const int r8 = lane >> 3, slot = lane & 7;
   uint32_t offA[8], offB[8];
+  auto set_offsets = [&](int tm_, int tn_, int ks_) {
+    const int m0_ = tm_ * BM;
+    const uint32_t kb = (uint32_t)ks_ * (uint32_t)a.kp * 2u;   // byte offset of the slice's k range
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int row = (4 * j + w) * 8 + r8;
-    const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
-    int wrow;
-    if constexpr (EPI == EPI_SWIGLU) {
-      // tile tn covers output columns [128 tn, 128 tn + 128): 16-row chunk c of the staged W tile is
-      // gate (c even) or up (c odd) of output columns 128 tn + 16 (c >> 1) + 0..15
-      wrow = 128 * tn + 16 * (row >> 5) + (row & 15) + ((row >> 4) & 1) * a.I;
-    } else {
-      wrow = min(tn * BN + row, a.N - 1);
+    for (int j = 0; j < 8; ++j) {
+      const int row = 64 * w + 8 * j + r8;
+      const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
+      int wrow;
+      if constexpr (EPI == EPI_SWIGLU) {
+        // tile tn covers output columns [128 tn, 128 tn + 128): 16-row chunk c of the staged W tile
+        // is gate (c even) or up (c odd) of output columns 128 tn + 16 (c >> 1) + 0..15
+        wrow = 128 * tn_ + 16 * (row >> 5) + (row & 15) + ((row >> 4) & 1) * a.I;
+      } else {
+        wrow = min(tn_ * BN + row, a.N - 1);
+      }
+      offA[j] = ((uint32_t)wrow * (uint32_t)a.K + ch) * 2u + kb + BIAS - (uint32_t)(j & 3) * 1024u;
+      offB[j] = ((uint32_t)min(m0_ + row, a.M - 1) * (uint32_t)a.ldx + ch) * 2u + kb + BIAS -
+                (uint32_t)(j & 3) * 1024u;
     }
-    offA[j] = ((uint32_t)wrow * (uint32_t)a.K + ch) * 2u + kb;
-    offB[j] = ((uint32_t)min(m0 + row, a.M - 1) * (uint32_t)a.ldx + ch) * 2u + kb;
-  }
-  const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)w * 1024u);
-  // DMA piece s (< 16) of a k-tile: W rows (s even) or X rows (s odd) group (4 (s >> 1) + w) * 8
-#define GB_DMA(S, BUF, T)                                                                            \
-  dma16(((S) & 1) ? rX : rW, ((S) & 1) ? offB[(S) >> 1] : offA[(S) >> 1], (uint32_t)(T) * (BK * 2), \
-        ldsw + (BUF) * STAGE + ((S) & 1) * TILE_A + ((S) >> 1) * 4096)
+  };
+  set_offsets(tm, tn, ks);
+  // DMA piece s (< 16) of a k-tile: W (s < 8) or X (s >= 8) rows 64 w + 8 (s & 7) .. + 8; M0 is set
+  // once per 4 pieces (s & 3 == 0) and restored after the fourth
+  const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)w * 8192u);
+  uint32_t m0keep = 0;
+#define GB_DMA(S, BUF, T)                                                                                     \
+  dma16g<(S) & 3>(((S) >> 3) ? rX : rW, ((S) >> 3) ? offB[(S) & 7] : offA[(S) & 7], (uint32_t)(T) * (BK * 2), \
+                  ldsw + (BUF) * STAGE + ((S) >> 3) * TILE_A + (((S) >> 2) & 1) * 4096, m0keep)
 
   // fragment read bases (bytes, LDS address): [buffer][k half] of the A (W) and B (X) quadrants
   const int sw = (r16 >> 1) & 7;
@@ -181,10 +227,6 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   const uint32_t bB00 = rB + c0, bB01 = rB + c1, bB10 = rB + STAGE + c0, bB11 = rB + STAGE + c1;
 
   f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
 
   // read S of a fragment set: A fragment S >> 1 (S even) or B fragment S >> 1 (S odd)
@@ -201,12 +243,9 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
       mfma_acc(acc[q >> 3][q & 7], FA[q >> 3], FB[q & 7]);
     });
   };
-  // phase A of a tile in buffer BUF: its second k half into F1 while F0's MFMAs run; then every read
-  // of buffer BUF retired (WAR for the DMA that refills it) and the next tile landed (this wave's
-  // part; the barrier makes it every wave's)
-  // past the last tile: re-stage the last tile (L2-hot, never consumed) — the buffer range check
-  // does not cover soffset, so an out-of-range k offset would read past the operand
-  auto tile_or_oob = [&](int T) { return T < nk ? T : nk - 1; };
+  // phase A of a k-tile in buffer BUF: its second k half into F1 while F0's MFMAs run; then every
+  // read of buffer BUF retired (WAR for the DMA that refills it) and the next k-tile landed (this
+  // wave's part; the barrier makes it every wave's)
   auto phase_a = [&](auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
     static_for<16>([&](auto sc) {
@@ -217,17 +256,15 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     wait_vm<0>();
     block_sync();
   };
-  // phase B: the next tile's first k half into F0, the DMA of tile T into buffer BUF (one 1-KB piece
-  // per MFMA group), F1's MFMAs; F0 retired at the end (covered by the 64 MFMAs).  Past the last
-  // tile the reads fetch LDS that no MFMA consumes and the DMA re-stages the last tile into a
-  // buffer nothing reads again: no control flow in the k-loop.
+  // phase B: the next k-tile's first k half into F0, the DMA of k-tile T (of the tile the offsets
+  // describe) into buffer BUF (one 1-KB piece per MFMA group), F1's MFMAs; F0 retired at the end
+  // (covered by the 64 MFMAs).  In the last k-step the reads fetch LDS that no MFMA consumes.
   auto phase_b = [&](auto bufc, int T) {
     constexpr int BUF = decltype(bufc)::value;
-    const int tt = tile_or_oob(T);
     static_for<16>([&](auto sc) {
       constexpr int S = decltype(sc)::value;
       rd(sc, fa0, fb0, BUF ? bA00 : bA10, BUF ? bB00 : bB10);
-      GB_DMA(S, BUF, tt);
+      GB_DMA(S, BUF, T);
       mma4(sc, fa1, fb1);
     });
     wait_lgkm0();
@@ -235,165 +272,211 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
 
-  // prologue: tile 0 and the phase-B part of tile 1 in flight, wait for tile 0, read its first half
+  // prologue of the first tile: k-tiles 0 and 1 in flight
   static_for<16>([&](auto sc) { GB_DMA(decltype(sc)::value, 0, 0); });
-  static_for<16>([&](auto sc) { GB_DMA(decltype(sc)::value, 1, tile_or_oob(1)); });
-  wait_vm<16>();
-  block_sync();
-  static_for<16>([&](auto sc) { rd(sc, fa0, fb0, bA00, bB00); });
-  wait_lgkm0();
+  static_for<16>([&](auto sc) { GB_DMA(decltype(sc)::value, 1, 1); });
+  // epilogue scratch: 8 KB per wave past the two staging buffers (never a DMA target)
+  char* const Q = L + 2 * STAGE + w * 8192;
 
-  // two tiles per trip so every buffer index is a compile-time constant (K % 128 == 0: no odd tail,
-  // no control flow in the loop but its back edge)
-  for (int t = 0; t < nk; t += 2) {
-    phase_a(I0{});
-    phase_b(I0{}, t + 2);
-    phase_a(I1{});
-    phase_b(I1{}, t + 3);
-  }
-  wait_vm<0>();   // the trailing out-of-range DMAs: nothing may land in LDS after the workgroup ends
-  mfma_drain();
-#undef GB_DMA
-  // epilogue.  acc[i][j][r] = C[n = 128 wn + 16 i + 4 grp + r][m = 128 wm + 16 j + r16] of the tile.
-  // The wave's quadrant is transposed through its own 32 KB of LDS (the staging buffers are free
-  // after the barrier below) into [m][n] rows, then stored as whole 16-B lanes: 4 rows x 256 B (SwiGLU:
-  // 8 rows x 128 B) per instruction instead of 8-B pieces scattered over 16 rows.
-#pragma unroll
-  for (int i = 0; i < 8; ++i)   // the asm MFMAs' results are read only after mfma_drain's wait states
-#pragma unroll
-    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
-  if constexpr (EPI == EPI_P32 || EPI == EPI_P16) {
-    // partial slab rows m, columns n .. n + 3 of the lane's accumulators: 16 B (fp32) / 8 B (bf16)
-    // per lane, the 4 lanes of a row contiguous
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int m = m0 + 128 * wm + 16 * j + r16;
-      if (m >= a.M) continue;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int n = tn * BN + 128 * wn + 16 * i + 4 * grp;
-        if (n >= a.N) continue;
-        const size_t o = ((size_t)ks * a.M + m) * a.N + n;
-        const f32x4 v = acc[i][j];
-        if constexpr (EPI == EPI_P32) *reinterpret_cast<f32x4*>(static_cast<float*>(a.P) + o) = v;
-        else *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.P) + o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-      }
-    }
-    return;
-  }
-  block_sync();   // every wave is past its last (stale) fragment read of the staging buffers
-  char* const Q = L + w * 32768;
-  if constexpr (EPI == EPI_ARGMAX) {
-    // lane (r16, grp) holds, for output row m = 128 wm + 16 j + r16, the 32 logits of columns
-    // n = 128 wn + 16 i + 4 grp + r (i < 8, r < 4).  Values are compared after bf16 rounding (what
-    // the unfused path's bf16 logits hold); i and r ascend, so strict '>' keeps the lowest index.
-    float* const Sv = reinterpret_cast<float*>(L);            // [4 waves][128 rows]
-    int* const Si = reinterpret_cast<int*>(L + 4 * 128 * 4);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int m = m0 + 128 * wm + 16 * j + r16;
-      const int mi = (a.mask_bits != nullptr && m < a.M) ? a.mask_idx[m] : -1;
-      const uint32_t* mrow = mi >= 0 ? a.mask_bits + (size_t)mi * a.mask_words : nullptr;
-      float best = -INFINITY;
-      int bidx = 0x7fffffff;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int n0 = tn * BN + 128 * wn + 16 * i + 4 * grp;
-        uint32_t bits = 0xfu;
-        if (mrow) {   // n0 + vocab_offset is a multiple of 4: the 4 bits share one mask word
-          const int gb = n0 + a.vocab_offset;
-          bits = (mrow[gb >> 5] >> (gb & 31)) & 0xfu;
-        }
-        if (n0 >= a.N) bits = 0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float x = lo_f(pack2(acc[i][j][r], 0.f));
-          if (((bits >> r) & 1u) && x > best) {
-            best = x;
-            bidx = n0 + r;
-          }
-        }
-      }
-#pragma unroll
-      for (int o = 16; o < 64; o <<= 1) {   // the 4 lanes of row r16 (grp 0..3)
-        const float ob = __shfl_xor(best, o, 64);
-        const int oi = __shfl_xor(bidx, o, 64);
-        if (ob > best || (ob == best && oi < bidx)) {
-          best = ob;
-          bidx = oi;
-        }
-      }
-      if (grp == 0) {
-        Sv[w * 128 + 16 * j + r16] = best;
-        Si[w * 128 + 16 * j + r16] = bidx;
-      }
-    }
-    wait_lgkm0();   // block_sync is a bare s_barrier: the other waves read these stores after it
+  for (;;) {
+    const int nvb = vb + (int)gridDim.x;
+    const bool more = nvb < total;
+    int ntm = tm, ntn = tn, nks = ks;   // without a next tile: re-stage this one (never consumed)
+    if (more) decode(nvb, ntm, ntn, nks);
+    const int m0 = tm * BM;
+    // k-tile 0 landed: the 16 youngest vector-memory operations are k-tile 1's DMA or the previous
+    // tile's epilogue stores, everything older (k-tile 0) is done
+    wait_vm<16>();
     block_sync();
-    {   // thread t: tile row t = 128 wm' + rr, from waves 2 wm' (columns 0..127) and 2 wm' + 1
-      const int wm2 = tid >> 7, rr = tid & 127, m = m0 + tid;
-      float b0 = Sv[(2 * wm2) * 128 + rr], b1 = Sv[(2 * wm2 + 1) * 128 + rr];
-      int i0 = Si[(2 * wm2) * 128 + rr], i1 = Si[(2 * wm2 + 1) * 128 + rr];
-      if (b1 > b0 || (b1 == b0 && i1 < i0)) {
-        b0 = b1;
-        i0 = i1;
-      }
-      if (m < a.M) {
-        a.part_val[(size_t)m * a.tiles_n + tn] = b0;
-        a.part_idx[(size_t)m * a.tiles_n + tn] = i0;
-      }
-    }
-  } else if constexpr (EPI == EPI_SWIGLU) {
-    // quadrant: 128 rows (m) x 64 output columns = 128 B per row, 16-B chunk index ^ (row & 7)
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const f32x4 g = acc[2 * p][j], u = acc[2 * p + 1][j];
-        float o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = g[r] / (1.f + __expf(-g[r])) * u[r];
-        const int row = 16 * j + r16, col = 16 * p + 4 * grp;   // col: bf16 index in the row
-        const int ch = (col >> 3) ^ (row & 7);
-        *reinterpret_cast<uint2*>(Q + row * 128 + ch * 16 + (col & 4) * 2) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-      }
-    const int rl = lane >> 3, cl = lane & 7;
-    const int ocol = 128 * tn + 64 * wn + 8 * cl;
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int row = 8 * it + rl, m = m0 + 128 * wm + row;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(Q + row * 128 + ((cl ^ (row & 7)) * 16));
-      if (m < a.M) *reinterpret_cast<u32x4*>(a.Y + (size_t)m * a.ldy + ocol) = v;
-    }
-  } else {
-    // quadrant: 128 rows (m) x 128 columns (n) = 256 B per row, 16-B chunk index ^ (row & 15)
+    static_for<16>([&](auto sc) { rd(sc, fa0, fb0, bA00, bB00); });
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    wait_lgkm0();
+
+    // two k-tiles per trip so every buffer index is a compile-time constant (K % 128 == 0: no odd
+    // tail).  The last trip stages the next tile's k-tiles 0 and 1 (its offsets replace this
+    // tile's, whose last DMA was the previous trip's).
+    for (int t = 0; t < nk; t += 2) {
+      const bool last = t + 2 >= nk;
+      if (last) set_offsets(ntm, ntn, nks);
+      phase_a(I0{});
+      phase_b(I0{}, last ? 0 : t + 2);
+      phase_a(I1{});
+      phase_b(I1{}, last ? 1 : t + 3);
+      // the MFMA wait states inside the loop, before its exit: hipcc does not know the asm MFMAs'
+      // latency and may copy accumulators (v_accvgpr_mov) on the exit edge, which would read
+      // results still in flight (seen: the argmax epilogue's accumulators shuffled before a drain
+      // placed after the loop)
+      if (last) mfma_drain();
+    }
+    // epilogue.  acc[i][j][r] = C[n = 128 wn + 16 i + 4 grp + r][m = 128 wm + 16 j + r16] of the
+    // tile.  bf16 / SwiGLU: the wave's quadrant is transposed through its 8 KB of LDS in row passes
+    // into [m][n] rows and stored as whole 16-B lanes instead of 8-B pieces scattered over 16 rows.
+#pragma unroll
+    for (int i = 0; i < 8; ++i)   // the asm MFMAs' results are read only after mfma_drain's wait states
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+    if constexpr (SPLIT) {
+      // partial slab rows m, columns n .. n + 3 of the lane's accumulators: 16 B (fp32) / 8 B (bf16)
+      // per lane, the 4 lanes of a row contiguous
+#pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const f32x4 v = acc[i][j];
-        const int row = 16 * j + r16, col = 16 * i + 4 * grp;
-        const int ch = (col >> 3) ^ (row & 15);
-        *reinterpret_cast<uint2*>(Q + row * 256 + ch * 16 + (col & 4) * 2) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-      }
-    const int rl = lane >> 4, cl = lane & 15;
-    const int n = tn * BN + wn * 128 + 8 * cl;
-    if (n < a.N) {
-#pragma unroll
-      for (int it = 0; it < 32; ++it) {
-        const int row = 4 * it + rl, m = m0 + 128 * wm + row;
-        u32x4 v = *reinterpret_cast<const u32x4*>(Q + row * 256 + ((cl ^ (row & 15)) * 16));
+        const int m = m0 + 128 * wm + 16 * j + r16;
         if (m >= a.M) continue;
-        bf16_t* y = a.Y + (size_t)m * a.ldy + n;
-        if constexpr (EPI == EPI_ADD) {
-          const u32x4 rr = *reinterpret_cast<const u32x4*>(a.R + (size_t)m * a.ldy + n);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = pack2(lo_f(v[q]) + lo_f(rr[q]), hi_f(v[q]) + hi_f(rr[q]));
+        for (int i = 0; i < 8; ++i) {
+          const int n = tn * BN + 128 * wn + 16 * i + 4 * grp;
+          if (n >= a.N) continue;
+          const size_t o = ((size_t)ks * a.M + m) * a.N + n;
+          const f32x4 v = acc[i][j];
+          if constexpr (EPI == EPI_P32) *reinterpret_cast<f32x4*>(static_cast<float*>(a.P) + o) = v;
+          else *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.P) + o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         }
-        *reinterpret_cast<u32x4*>(y) = v;
+      }
+    } else if constexpr (EPI == EPI_ARGMAX) {
+      // lane (r16, grp) holds, for output row m = 128 wm + 16 j + r16, the 32 logits of columns
+      // n = 128 wn + 16 i + 4 grp + r (i < 8, r < 4).  Values are compared after bf16 rounding (what
+      // the unfused path's bf16 logits hold); i and r ascend, so strict '>' keeps the lowest index.
+      float* const Sv = reinterpret_cast<float*>(L + 2 * STAGE);            // [4 waves][128 rows]
+      int* const Si = reinterpret_cast<int*>(L + 2 * STAGE + 4 * 128 * 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = m0 + 128 * wm + 16 * j + r16;
+        const int mi = (a.mask_bits != nullptr && m < a.M) ? a.mask_idx[m] : -1;
+        const uint32_t* mrow = mi >= 0 ? a.mask_bits + (size_t)mi * a.mask_words : nullptr;
+        float best = -INFINITY;
+        int bidx = 0x7fffffff;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int n0 = tn * BN + 128 * wn + 16 * i + 4 * grp;
+          uint32_t bits = 0xfu;
+          if (mrow) {   // n0 + vocab_offset is a multiple of 4: the 4 bits share one mask word
+            const int gb = n0 + a.vocab_offset;
+            bits = (mrow[gb >> 5] >> (gb & 31)) & 0xfu;
+          }
+          if (n0 >= a.N) bits = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = lo_f(pack2(acc[i][j][r], 0.f));
+            if (((bits >> r) & 1u) && x > best) {
+              best = x;
+              bidx = n0 + r;
+            }
+          }
+        }
+#pragma unroll
+        for (int o = 16; o < 64; o <<= 1) {   // the 4 lanes of row r16 (grp 0..3)
+          const float ob = __shfl_xor(best, o, 64);
+          const int oi = __shfl_xor(bidx, o, 64);
+          if (ob > best || (ob == best && oi < bidx)) {
+            best = ob;
+            bidx = oi;
+          }
+        }
+        if (grp == 0) {
+          Sv[w * 128 + 16 * j + r16] = best;
+          Si[w * 128 + 16 * j + r16] = bidx;
+        }
+      }
+      wait_lgkm0();   // block_sync is a bare s_barrier: the other waves read these stores after it
+      block_sync();
+      {   // thread t: tile row t = 128 wm' + rr, from waves 2 wm' (columns 0..127) and 2 wm' + 1
+        const int wm2 = tid >> 7, rr = tid & 127, m = m0 + tid;
+        float b0 = Sv[(2 * wm2) * 128 + rr], b1 = Sv[(2 * wm2 + 1) * 128 + rr];
+        int i0 = Si[(2 * wm2) * 128 + rr], i1 = Si[(2 * wm2 + 1) * 128 + rr];
+        if (b1 > b0 || (b1 == b0 && i1 < i0)) {
+          b0 = b1;
+          i0 = i1;
+        }
+        if (m < a.M) {
+          a.part_val[(size_t)m * a.tiles_n + tn] = b0;
+          a.part_idx[(size_t)m * a.tiles_n + tn] = i0;
+        }
+      }
+      // the next tile's epilogue rewrites Sv / Si only after its k-loop's barriers
+    } else if constexpr (EPI == EPI_SWIGLU) {
+      // quadrant: 128 rows (m) x 64 output columns = 128 B per row, in 2 passes of 64 rows;
+      // 16-B chunk index ^ (row & 7)
+      const int rl = lane >> 3, cl = lane & 7;
+      const int ocol = 128 * tn + 64 * wn + 8 * cl;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const f32x4 g = acc[2 * pp][4 * p + jj], u = acc[2 * pp + 1][4 * p + jj];
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = g[r] / (1.f + __expf(-g[r])) * u[r];
+            const int row = 16 * jj + r16, col = 16 * pp + 4 * grp;   // col: bf16 index in the row
+            const int ch = (col >> 3) ^ (row & 7);
+            *reinterpret_cast<uint2*>(Q + row * 128 + ch * 16 + (col & 4) * 2) =
+                make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+          }
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int row = 8 * it + rl, m = m0 + 128 * wm + 64 * p + row;
+          const u32x4 v = *reinterpret_cast<const u32x4*>(Q + row * 128 + ((cl ^ (row & 7)) * 16));
+          if (m < a.M) *reinterpret_cast<u32x4*>(a.Y + (size_t)m * a.ldy + ocol) = v;
+        }
+      }
+    } else {
+      // quadrant: 128 rows (m) x 128 columns (n) = 256 B per row, in 4 passes of 32 rows; 16-B chunk
+      // index ^ (row & 15)
+      const int rl = lane >> 4, cl = lane & 15;
+      const int n = tn * BN + wn * 128 + 8 * cl;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const f32x4 v = acc[i][2 * p + jj];
+            const int row = 16 * jj + r16, col = 16 * i + 4 * grp;
+            const int ch = (col >> 3) ^ (row & 15);
+            *reinterpret_cast<uint2*>(Q + row * 256 + ch * 16 + (col & 4) * 2) =
+                make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          }
+        if (n < a.N) {
+#pragma unroll
+          for (int it = 0; it < 8; ++it) {
+            const int row = 4 * it + rl, m = m0 + 128 * wm + 32 * p + row;
+            u32x4 v = *reinterpret_cast<const u32x4*>(Q + row * 256 + ((cl ^ (row & 15)) * 16));
+            if (m >= a.M) continue;
+            bf16_t* y = a.Y + (size_t)m * a.ldy + n;
+            if constexpr (EPI == EPI_ADD) {
+              const u32x4 rr = *reinterpret_cast<const u32x4*>(a.R + (size_t)m * a.ldy + n);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] = pack2(lo_f(v[q]) + lo_f(rr[q]), hi_f(v[q]) + hi_f(rr[q]));
+            }
+            *reinterpret_cast<u32x4*>(y) = v;
+          }
+        }
       }
     }
+    if (!more) break;
+    vb = nvb;
+    tm = ntm;
+    tn = ntn;
+    ks = nks;
   }
+  wait_vm<0>();   // the trailing re-stage DMA: nothing may land in LDS after the workgroup ends
+#undef GB_DMA
+}
+
+constexpr int LDS_TOTAL = LDS + 4 * 8192;   // staging buffers + the epilogue scratch (160 KB)
+
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
 }
 
 template <int EPI>
@@ -401,14 +484,19 @@ static int launch(const Args& a0, hipStream_t st) {
   static bool attr = false;
   auto kern = &gemm256_kernel<EPI>;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_TOTAL);
     attr = true;
   }
   Args a = a0;
   a.tiles_m = (a.M + BM - 1) / BM;
   a.tiles_n = EPI == EPI_SWIGLU ? a.I / 128 : (a.N + BN - 1) / BN;
   const int split = (EPI == EPI_P32 || EPI == EPI_P16) ? a.split : 1;
-  hipLaunchKernelGGL(kern, dim3(a.tiles_m * a.tiles_n * split), dim3(NT), LDS, st, a);
+  const int total = a.tiles_m * a.tiles_n * split;
+  // one workgroup per CU (the LDS allows no more); a persistent grid is a multiple of 8 (XCDs)
+  const int cus = num_cus() & ~7;
+  const int grid = total <= cus ? total : cus;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS_TOTAL, st, a);
   return (int)hipGetLastError();
 }
 

@@ -122,6 +122,10 @@ class LlamaModel:
             combined = False
             if cfg.is_moe:
                 h, combined = moe_forward(x, L, cfg, self.ep_rank, self.ep_size, meta.is_decode, self.comm)
+            elif ops.use_prefill_swiglu(x, L["w13"]):
+                # prefill / mixed steps: gate_up with the SwiGLU epilogue (no [T, 2I] intermediate)
+                h = ops.linear(ops.linear_swiglu(x, L["w13"]), L["w2"], defer_reduce=fuse,
+                               bf16_partials=self.bf16_partials)
             else:
                 # batch <= 4: SiLU·mul computed inside the down GEMV's X staging (ops.swiglu_linear)
                 h = ops.swiglu_linear(ops.linear(x, L["w13"], defer_reduce=True), L["w2"], defer_reduce=fuse,

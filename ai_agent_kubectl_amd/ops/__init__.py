@@ -365,6 +365,46 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
     return y
 
 
+# Prefill / mixed-step gate_up with the SwiGLU epilogue (csrc/gemm_big.hip EPI_SWIGLU): the [M, 2I]
+# gate_up output never exists and the separate SiLU·mul pass goes away.  M >= PREFILL_SWIGLU_MIN_M
+# rows (profiles/r3/gemm_big: 565 us vs hipBLASLt 550 us + SiLU·mul at M = 2944, 691 vs 620 + 122
+# at M = 4096, Llama-3-8B).  KA_PREFILL_SWIGLU=0 restores hipBLASLt + silu_mul.
+PREFILL_SWIGLU = os.environ.get("KA_PREFILL_SWIGLU", "1") == "1"
+PREFILL_SWIGLU_MIN_M = int(os.environ.get("KA_PREFILL_SWIGLU_MIN_M", "1024"))
+GB_EPI_SWIGLU = 3
+
+
+def swiglu_gemm_ok(x: torch.Tensor, w13: torch.Tensor) -> bool:
+    """Shapes csrc/gemm_big.hip's SwiGLU epilogue takes: K % 128, I % 128, 16-B aligned rows."""
+    M, K = x.shape
+    N = w13.shape[0]
+    return (x.stride(1) == 1 and x.stride(0) % 8 == 0 and K % 128 == 0 and N % 256 == 0
+            and w13.is_contiguous() and w13.shape[1] == K)
+
+
+def use_prefill_swiglu(x: torch.Tensor, w13: torch.Tensor) -> bool:
+    return (PREFILL_SWIGLU and not _ref(x) and x.shape[0] >= PREFILL_SWIGLU_MIN_M
+            and x.shape[0] > TILE_MAX_M and swiglu_gemm_ok(x, w13))
+
+
+def linear_swiglu(x: torch.Tensor, w13: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(x @ gate.T) * (x @ up.T) for w13 = [gate; up] ([2I, K]): [M, I] bf16.  GPU: one
+    gemm_big launch (256 x 256 tiles whose W rows alternate 16-row gate / up chunks, so each lane
+    holds gate and up of the same outputs); CPU: the fp32 reference."""
+    if _ref(x):
+        return ref.silu_mul(ref.linear(x, w13))
+    if not swiglu_gemm_ok(x, w13):
+        raise ValueError(f"gemm_big SwiGLU needs K % 128 == 0, 2I % 256 == 0, aligned rows: {tuple(x.shape)} "
+                         f"x {tuple(w13.shape)}")
+    lib = require()
+    M, K = x.shape
+    N = w13.shape[0]
+    out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device) if out is None else out
+    check(lib.ka_gemm_big(_p(out), None, _p(x), _p(w13), M, N, K, x.stride(0), out.stride(0), GB_EPI_SWIGLU, 0,
+                          _stream()), "gemm_big_swiglu")
+    return out
+
+
 GEMV_SWIGLU_MAX_M = 4   # csrc/gemm_skinny.hip GEMV_MAX_M
 
 

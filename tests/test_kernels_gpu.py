@@ -299,6 +299,27 @@ def test_lm_head_argmax_ties_lowest_index():
     assert idx.cpu().tolist() == [300] * M
 
 
+@pytest.mark.parametrize("M,I,K", [(1024, 14336, 4096), (2944, 1792, 4096), (777, 512, 256), (4096, 3584, 4096)])
+def test_prefill_swiglu_gemm_vs_fp32(M, I, K):
+    """Prefill gate_up with the SwiGLU epilogue (csrc/gemm_big.hip EPI_SWIGLU) against the fp32
+    silu(x gate^T) * (x up^T): full Llama-3-8B I, the TP=8 shard (1792), a ragged M tail."""
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w13 = (torch.randn(2 * I, K, device=DEV) / math.sqrt(K)).to(BF)
+    y = ops.linear_swiglu(x, w13)
+    assert y.shape == (M, I)
+    g = x.float() @ w13[:I].float().t()
+    u = x.float() @ w13[I:].float().t()
+    close(y, torch.nn.functional.silu(g) * u, atol=2e-2, rtol=2e-2)
+
+
+def test_prefill_swiglu_used_by_model_path():
+    """The model's MLP takes the fused kernel for prefill-sized steps (ops.use_prefill_swiglu)."""
+    x = torch.randn(max(ops.PREFILL_SWIGLU_MIN_M, ops.TILE_MAX_M + 1), 4096, device=DEV, dtype=BF)
+    w13 = torch.zeros(2 * 14336, 4096, device=DEV, dtype=BF)
+    assert ops.use_prefill_swiglu(x, w13) == ops.PREFILL_SWIGLU
+    assert not ops.use_prefill_swiglu(x[:256], w13)
+
+
 def test_moe_topk():
     lg = torch.randn(50, 8, device=DEV, dtype=BF)
     w1, i1 = ops.moe_topk(lg, 2)
