@@ -477,3 +477,26 @@ extern "C" int ka_kv_block_copy(void* k_cache, void* v_cache, const void* src, c
                      layer_stride, block_elems);
   KA_CHECK_LAUNCH();
 }
+
+// ---- weight prefetch into the Infinity Cache (MALL) ----
+// Reads [p, p + bytes) once with 16-B loads and discards it (the XOR of what was read is stored only
+// if it equals a value no read produces in practice, so the loads stay live): run on a side stream
+// beside a kernel that leaves most CUs idle (batch-1 decode attention, RMSNorm), it turns the next
+// GEMV's weight stream into MALL hits.  Read-only, no output.
+__global__ __launch_bounds__(256) void prefetch_kernel(const u32x4* __restrict__ p, size_t n16, uint32_t* sink) {
+  uint32_t acc = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
+    const u32x4 v = p[i];
+    acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+  }
+  if (acc == 0x9e3779b9u && sink != nullptr) *sink = acc;
+}
+
+extern "C" int ka_prefetch(const void* p, long bytes, int blocks, void* sink, hipStream_t stream) {
+  if (bytes <= 0) return 0;
+  const size_t n16 = (size_t)bytes / 16;
+  const int grid = blocks > 0 ? blocks : (int)std::min<size_t>(1024, (n16 + 255) / 256);
+  hipLaunchKernelGGL(prefetch_kernel, dim3(grid), dim3(256), 0, stream, static_cast<const u32x4*>(p), n16,
+                     static_cast<uint32_t*>(sink));
+  return (int)hipGetLastError();
+}

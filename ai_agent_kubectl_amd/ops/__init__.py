@@ -213,6 +213,18 @@ def silu_mul(gu, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     return out
 
 
+def prefetch(t: torch.Tensor, nbytes: int = 0, blocks: int = 0) -> None:
+    """Read the first `nbytes` (default: all) of `t` once and discard them: pulls a weight into the
+    Infinity Cache ahead of the kernel that streams it (csrc/elementwise.hip prefetch_kernel).  No-op
+    on CPU tensors."""
+    if _ref(t):
+        return
+    lib = require()
+    n = t.numel() * t.element_size()
+    n = min(n, nbytes) if nbytes > 0 else n
+    check(lib.ka_prefetch(_p(t), n, int(blocks), None, _stream()), "prefetch")
+
+
 def embedding(ids: torch.Tensor, table: torch.Tensor, vocab_offset: int = 0,
               out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if _ref(table):

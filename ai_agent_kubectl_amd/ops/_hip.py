@@ -44,6 +44,7 @@ _SIGS = {
     "ka_rope_kv_splitk": [P, P, P, P, I, P, P, P, I, I, I, I, I, P],
     "ka_silu_mul_splitk": [P, P, I, I, I, P],
     "ka_kv_block_copy": [P, P, P, P, I, I, ctypes.c_long, ctypes.c_long, P],
+    "ka_prefetch": [P, ctypes.c_long, I, P, P],
     "ka_gemm_mfma": [P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "ka_gemm_mfma_grouped": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
     "ka_gemm_big": [P, P, P, P, I, I, I, I, I, I, I, P],
