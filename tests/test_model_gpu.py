@@ -146,6 +146,73 @@ def test_decode_chain_vs_fp32_reference(B):
     assert errs[True] <= 2 * errs[False] + 0.05, errs
 
 
+@pytest.mark.parametrize("B", [1, 4, 64])
+def test_decode_trajectory_independent_fp32_kv(B):
+    """An independent fp32 trajectory: the reference KV cache is written only by the fp32
+    reference path, from the prefill on (prefix caching off, so no block is shared), and both paths
+    are fed the tokens the HIP path samples (teacher forcing keeps them aligned) for 24 decode steps.
+    Unlike test_decode_chain_vs_fp32_reference (which re-bases the reference on the HIP path's cache
+    every step) this sees KV drift accumulate: every step's logits stay within bf16 tolerance of
+    the fp32 trajectory and the error of the last 8 steps is not a growing multiple of the first 8's."""
+    from ai_agent_kubectl_amd.engine.sequence import Sequence
+    from ai_agent_kubectl_amd.models.llama import AttnMeta
+    eng = _engine("llama3-8b-2l", graphs=False, buckets=(1, 4, 64), max_batch=64, kv_cache_tokens=32768,
+                  prefix_caching=False, max_batched_tokens=16384)
+    be = EngineLLM(eng, max_new_tokens=40, ignore_eos=True)
+    params = SamplingParams(max_new_tokens=40, ignore_eos=True)
+    sch, r = eng.scheduler, eng.runner
+    sch.prefill_max_wait_s = 0.0
+    sch.gather_max_s = 0.0
+    sch.hold_steps = 0
+    m = r.model
+    kc_ref, vc_ref = torch.zeros_like(r.k_cache), torch.zeros_like(r.v_cache)
+    errs, coss = [], []
+    with torch.inference_mode():
+        for i in range(B):
+            sch.add(Sequence(prompt_ids=be.prompt_ids(QUERIES[i % len(QUERIES)] + f" #{i}"), params=params))
+        b = sch.schedule()
+        assert not b.is_decode and len(b.seqs) == B and not b.copies
+        host = torch.from_numpy(r._pack_prefill(b)).cuda()
+        T, S, mb = b.num_tokens, B, r.max_blocks
+        o = 3 * T
+        meta = AttnMeta(positions=host[T:2 * T], slot_mapping=host[2 * T:3 * T],
+                        block_tables=host[o + 4 * S + 1:o + 4 * S + 1 + S * mb].view(S, mb),
+                        ctx_lens=host[o + S + 1:o + 2 * S + 1], logits_indices=host[o + 3 * S + 1:o + 4 * S + 1].long(),
+                        is_decode=False, q_starts=host[o:o + S + 1], max_q_len=max(b.num_query))
+        mask = host[o + 2 * S + 1:o + 3 * S + 1]
+        h = m.forward(host[:T], meta, r.k_cache, r.v_cache)
+        with ops.force_reference():
+            h_ref = m.forward(host[:T], meta, kc_ref, vc_ref)
+        coss.append(torch.nn.functional.cosine_similarity(m.logits(h).float(), m.logits(h_ref).float(), dim=-1).min().item())
+        tok = m.sample(h, r.mask_bits, mask if r.mask_bits is not None else None).tolist()
+        eng._apply(b, tok)
+        sch.on_step_done(b)
+        for step in range(24):
+            batch = sch.schedule()
+            assert batch.is_decode and len(batch.seqs) == B
+            r._pack_decode(batch, B)
+            n = r._off["bt"] + B * r.max_blocks
+            r.d_stage[:n].copy_(r.h_stage[:n])
+            meta = AttnMeta(positions=r._view("pos", B), slot_mapping=r._view("slots", B),
+                            block_tables=r._view("bt", B), ctx_lens=r._view("ctx", B),
+                            logits_indices=r.d_logits_idx[:B], is_decode=True)
+            ids = r._view("ids", B)
+            h = m.forward(ids, meta, r.k_cache, r.v_cache)
+            lg = m.logits(h).float()[:B]
+            with ops.force_reference():
+                lg_ref = m.logits(m.forward(ids, meta, kc_ref, vc_ref)).float()[:B]
+            errs.append((lg - lg_ref).abs().max().item())
+            coss.append(torch.nn.functional.cosine_similarity(lg, lg_ref, dim=-1).min().item())
+            mask = r._view("mask", B) if r.mask_bits is not None else None
+            eng._apply(batch, m.sample(h, r.mask_bits, mask)[:B].tolist())
+            sch.on_step_done(batch)
+    print(f"B={B}: logits cosine min {min(coss):.5f}; max |logit - fp32 trajectory| first 8 steps "
+          f"{max(errs[:8]):.4f}, last 8 {max(errs[-8:]):.4f}")
+    assert min(coss) > 0.99, coss
+    assert max(errs) < 0.3, errs
+    assert max(errs[-8:]) <= 2 * max(errs[:8]) + 0.05, errs
+
+
 def test_graph_decode_equals_eager():
     params = SamplingParams(max_new_tokens=12, ignore_eos=True)
     outs = []
