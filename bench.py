@@ -730,14 +730,22 @@ def summarize(args, name, world, C, dist, r, seq_len):
     reply = extra[0] if extra else None
     n_req = C * args.steps
     allv = [v for k in ("miss", "hit", "exec") for v in lat.get(k, [])]
-    p50 = statistics.median(allv) * 1e3 if allv else float("nan")
     if world > 1:
+        # the slowest rank's elapsed time; p50 / p99 over every rank's latencies merged (per-class
+        # lists too), so both percentiles describe the same population
         import torch
-        t = torch.tensor([elapsed, p50], dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         gathered = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(gathered, t)
         elapsed = max(g[0].item() for g in gathered)
-        p50 = statistics.median([g[1].item() for g in gathered])
+        lats = [None] * world
+        dist.all_gather_object(lats, {k: list(v) for k, v in lat.items()})
+        lat = {}
+        for d in lats:
+            for k, v in d.items():
+                lat.setdefault(k, []).extend(v)
+        allv = [v for k in ("miss", "hit", "exec") for v in lat.get(k, [])]
+    p50 = statistics.median(allv) * 1e3 if allv else float("nan")
     value = n_req * world / elapsed
 
     def pct(v, q):
