@@ -134,9 +134,12 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
 #pragma unroll
     for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(vp + (size_t)n * 16 * KBS);
   };
+#ifndef KA_ATTN_EARLY_V
+#define KA_ATTN_EARLY_V 0
+#endif
   if (wave < nchunks) {
     load_k(wave);
-    if constexpr (!FUSED) load_v(wave);   // fused: V after the prologue (128-VGPR budget)
+    if constexpr (!FUSED || KA_ATTN_EARLY_V) load_v(wave);   // fused: V after the prologue (128-VGPR budget)
   }
 
   if constexpr (FUSED) {
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
     __syncthreads();
   }
 
-  if constexpr (FUSED) {
+  if constexpr (FUSED && !KA_ATTN_EARLY_V) {
     if (wave < nchunks) load_v(wave);
   }
   bf16x8 qf[4];
