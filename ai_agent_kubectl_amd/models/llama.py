@@ -68,6 +68,11 @@ class LlamaModel:
         # them in fp32): a separate switch so the two can be A/B'd independently
         self.bf16_qkv_partials = os.environ.get("KA_BF16_QKV_PARTIALS", "1") == "1"
         self.layers = [self._layer(i) for i in range(cfg.num_layers)]
+        # prefill / mixed steps: the last layer's rows other than each sequence's last token feed
+        # nothing (only the last rows reach the final norm and the LM head), so after that layer's
+        # QKV + RoPE + KV append (which every row needs for later steps) it continues on the S
+        # last-token rows only: attention as S one-query rows, O-proj, norm and MLP on S rows
+        self.prune_last_layer = os.environ.get("KA_PRUNE_LAST_LAYER", "1") == "1"
         # eager steps only: record `mark_event` when layer `mark_layer` starts (-1: never)
         self.mark_layer = -1
         self.mark_event = None
@@ -87,6 +92,8 @@ class LlamaModel:
         pending = False   # h holds this rank's partial of a row-parallel output (TP all-reduce due)
         T = input_ids.shape[0]
         mark = self.mark_layer
+        last_li = len(self.layers) - 1
+        pruned = False   # rows cut down to the sequences' last tokens (last layer, prefill / mixed)
         for li, L in enumerate(self.layers):
             if li == mark and input_ids.is_cuda:   # progress marker (engine lookahead timing)
                 self.mark_event = torch.cuda.Event()
@@ -110,14 +117,24 @@ class LlamaModel:
             else:
                 q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, k_cache[li],
                                       v_cache[li], self.hq, self.hkv, self.D)
-                a = self._attention(q, meta, k_cache[li], v_cache[li])
-            if 0 < meta.num_tokens < T and not meta.is_decode:
+                if li == last_li and not meta.is_decode and self.prune_last_layer:
+                    # every sequence's last token as a one-query decode row over its whole context
+                    # (this step's keys were just appended); the residual stream follows those rows
+                    idx = meta.logits_indices
+                    a = ops.attention_decode(q.index_select(0, idx), k_cache[li], v_cache[li], meta.block_tables,
+                                             meta.ctx_lens, self.scale)
+                    residual = residual.index_select(0, idx)
+                    pruned = True
+                else:
+                    a = self._attention(q, meta, k_cache[li], v_cache[li])
+            if 0 < meta.num_tokens < T and not meta.is_decode and not pruned:
                 a[meta.num_tokens:].zero_()   # padding rows: no sequence's attention writes them
             # TP = 1: the projections feeding a norm leave their split-K partials to the fused
             # reduce + residual + RMSNorm kernel (ops.SplitK); with TP the row-parallel output is
             # bf16 and the all-reduce is fused with that norm (comm.all_reduce_rmsnorm, A1)
             fuse = self._local_comm
-            h = ops.linear(a.view(T, self.hq * self.D), L["wo"], defer_reduce=fuse, bf16_partials=self.bf16_partials)
+            h = ops.linear(a.reshape(a.shape[0], self.hq * self.D), L["wo"], defer_reduce=fuse,
+                           bf16_partials=self.bf16_partials)
             x = self._reduce_norm(h, L["ln2"], eps, residual, True)
             combined = False
             if cfg.is_moe:
@@ -135,6 +152,8 @@ class LlamaModel:
             return self._reduce_norm(h, self.W["norm"], eps, residual, pending)
         if pending and not self._local_comm:
             self.comm.all_reduce(h)
+        if pruned:   # h and residual already hold only the sequences' last rows
+            return ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
         if isinstance(h, ops.SplitK):
             x = ops.rmsnorm(h, self.W["norm"], eps, residual=residual)
             return x.index_select(0, meta.logits_indices)

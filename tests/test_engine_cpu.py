@@ -815,3 +815,59 @@ def test_gemm_plan_file_roundtrip(tmp_path):
     finally:
         ops.GEMM_PLAN.clear()
         ops.GEMM_PLAN.update(saved)
+
+
+def test_last_layer_pruning_matches_full(tiny_engine):
+    """Prefill / mixed steps continue the last layer on each sequence's last row only (after the
+    QKV + RoPE + KV append every row needs): the same tokens as computing every row, in whole
+    prefills, staggered mixed steps and padded steps."""
+    from tests.engine_helpers import run_staggered
+    eng, be = tiny_engine
+    model = eng.runner.model
+    params = SamplingParams(max_new_tokens=6, ignore_eos=True)
+    prompts = [be.prompt_ids(q) for q in ("list pods", "get nodes -o wide", "describe svc api", "top pods")]
+    outs = {}
+    for prune in (False, True):
+        model.prune_last_layer = prune
+        eng.bm.reset_prefix_cache()
+        try:
+            whole = [s.output_ids for s in eng.generate_blocking(prompts, params, forced_prefix=be._forced)]
+            eng.bm.reset_prefix_cache()
+            mixed = run_staggered(eng, prompts, params, be._forced)
+        finally:
+            model.prune_last_layer = True
+        outs[prune] = (whole, mixed)
+    assert outs[True] == outs[False]
+
+
+def test_last_layer_pruning_hidden_matches():
+    """Model level: the final hidden rows of a prefill step with and without pruning agree to fp32
+    rounding (the pruned path's attention runs as one-query decode rows)."""
+    import numpy as np
+    from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine
+    from ai_agent_kubectl_amd.engine.scheduler import Batch
+    from ai_agent_kubectl_amd.engine.sequence import Sequence
+    from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM
+    from ai_agent_kubectl_amd.models.llama import AttnMeta
+    eng = build_engine(EngineOptions(model="tiny-llama", device="cpu", max_batch=8, use_graphs=False,
+                                     kv_cache_tokens=4096, max_model_len=512))
+    be = EngineLLM(eng, max_new_tokens=4)
+    r = eng.runner
+    seqs = [Sequence(prompt_ids=be.prompt_ids(q), params=be.params) for q in ("list pods", "scale web to 3")]
+    for s in seqs:
+        s.block_table, _, s.block_hashes = eng.bm.allocate_prompt(s.all_ids)
+    batch = Batch(seqs, [s.total_len for s in seqs], is_decode=False, prefill_seqs=seqs)
+    host = torch.from_numpy(r._pack_prefill(batch).astype(np.int32))
+    T, S, mb = batch.num_tokens, len(seqs), r.max_blocks
+    o = 3 * T
+    meta = AttnMeta(positions=host[T:2 * T], slot_mapping=host[2 * T:3 * T],
+                    block_tables=host[o + 4 * S + 1:o + 4 * S + 1 + S * mb].view(S, mb),
+                    ctx_lens=host[o + S + 1:o + 2 * S + 1], logits_indices=host[o + 3 * S + 1:o + 4 * S + 1].long(),
+                    is_decode=False, q_starts=host[o:o + S + 1], max_q_len=max(batch.num_query))
+    hs = {}
+    for prune in (False, True):
+        r.model.prune_last_layer = prune
+        hs[prune] = r.model.forward(host[:T], meta, r.k_cache, r.v_cache).float()
+    r.model.prune_last_layer = True
+    assert hs[True].shape == hs[False].shape == (S, r.model.W["embed"].shape[1])
+    torch.testing.assert_close(hs[True], hs[False], atol=2e-2, rtol=2e-2)
