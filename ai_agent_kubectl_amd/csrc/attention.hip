@@ -134,12 +134,11 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
 #pragma unroll
     for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(vp + (size_t)n * 16 * KBS);
   };
-#ifndef KA_ATTN_EARLY_V
-#define KA_ATTN_EARLY_V 0
-#endif
   if (wave < nchunks) {
     load_k(wave);
-    if constexpr (!FUSED || KA_ATTN_EARLY_V) load_v(wave);   // fused: V after the prologue (128-VGPR budget)
+    // fused: V after the prologue (issuing it here too measured 24.3 vs 23.4 us at B = 256,
+    // 9.9 vs 10.4 at B = 1: profiles/r3/decode_attn_early_v/)
+    if constexpr (!FUSED) load_v(wave);
   }
 
   if constexpr (FUSED) {
@@ -193,7 +192,7 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
     __syncthreads();
   }
 
-  if constexpr (FUSED && !KA_ATTN_EARLY_V) {
+  if constexpr (FUSED) {
     if (wave < nchunks) load_v(wave);
   }
   bf16x8 qf[4];

@@ -269,34 +269,40 @@ __global__ __launch_bounds__(256) void rope_kv_window_kernel(bf16_t* __restrict_
   const int t0 = blockIdx.x * W;
   const int nt = min(W, tokens - t0);
   const int qkv_stride = (hq + 2 * hkv) * d;
-  // ---- q / k rotation: (hq + hkv) heads x 16 items of 4 rotary pairs per token ----
-  const int per_tok = (hq + hkv) * 16;
-  for (int it = threadIdx.x; it < nt * per_tok; it += 256) {
-    const int j = it / per_tok, r = it % per_tok;
+  // ---- q / k rotation: (hq + hkv) heads x 8 items of 8 rotary pairs per token, 16-B loads and
+  // stores; unrolled so each thread keeps several items' loads in flight (the window grid is small:
+  // ~2 workgroups per CU at an 8k-token step, so memory-level parallelism comes from the thread) ----
+  const int per_tok = (hq + hkv) * 8;
+  const int n_items = nt * per_tok;
+#pragma unroll 4
+  for (int it = threadIdx.x; it < n_items; it += 256) {
+    const int j = it / per_tok, r = it - j * per_tok;
     const int t = t0 + j;
-    const int h = r >> 4, i = (r & 15) * 4;
+    const int h = r >> 3, i = (r & 7) * 8;
     const bf16_t* row = qkv + (size_t)t * qkv_stride;
     const float* prow = Pq ? Pq + (size_t)t * qkv_stride : nullptr;
     const int slot = slot_mapping[t];
     if (h >= hq && slot < 0) continue;
     const float* cs = cos_sin + (size_t)positions[t] * d;
-    const uint2 a = ld4(row, prow, split, pstride, (size_t)h * d + i);
-    const uint2 b = ld4(row, prow, split, pstride, (size_t)h * d + i + half);
-    const float4 c = *reinterpret_cast<const float4*>(cs + i);
-    const float4 sn = *reinterpret_cast<const float4*>(cs + half + i);
-    const float x1[4] = {lo_f(a.x), hi_f(a.x), lo_f(a.y), hi_f(a.y)};
-    const float x2[4] = {lo_f(b.x), hi_f(b.x), lo_f(b.y), hi_f(b.y)};
-    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
-    float o1[4], o2[4];
+    const uint4 a = ld8(row, prow, split, pstride, (size_t)h * d + i);
+    const uint4 b = ld8(row, prow, split, pstride, (size_t)h * d + i + half);
+    const float4 c0 = *reinterpret_cast<const float4*>(cs + i), c1 = *reinterpret_cast<const float4*>(cs + i + 4);
+    const float4 s0 = *reinterpret_cast<const float4*>(cs + half + i);
+    const float4 s1 = *reinterpret_cast<const float4*>(cs + half + i + 4);
+    const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {b.x, b.y, b.z, b.w};
+    const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    uint32_t o1[4], o2[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      o1[k] = x1[k] * cc[k] - x2[k] * ss[k];
-      o2[k] = x2[k] * cc[k] + x1[k] * ss[k];
+      const float xa0 = lo_f(aw[k]), xa1 = hi_f(aw[k]), xb0 = lo_f(bw[k]), xb1 = hi_f(bw[k]);
+      o1[k] = pack2(xa0 * cc[2 * k] - xb0 * ss[2 * k], xa1 * cc[2 * k + 1] - xb1 * ss[2 * k + 1]);
+      o2[k] = pack2(xb0 * cc[2 * k] + xa0 * ss[2 * k], xb1 * cc[2 * k + 1] + xa1 * ss[2 * k + 1]);
     }
     bf16_t* dst = h < hq ? q_out + ((size_t)t * hq + h) * d
                          : k_cache + (((size_t)(slot / bs) * hkv + (h - hq)) * bs + slot % bs) * d;
-    *reinterpret_cast<uint2*>(dst + i) = make_uint2(pack2(o1[0], o1[1]), pack2(o1[2], o1[3]));
-    *reinterpret_cast<uint2*>(dst + i + half) = make_uint2(pack2(o2[0], o2[1]), pack2(o2[2], o2[3]));
+    *reinterpret_cast<uint4*>(dst + i) = make_uint4(o1[0], o1[1], o1[2], o1[3]);
+    *reinterpret_cast<uint4*>(dst + i + half) = make_uint4(o2[0], o2[1], o2[2], o2[3]);
   }
   // ---- V: per kv head, 16 tokens x 128 dims through LDS ----
   const int lj = threadIdx.x & 15;                  // store phase: lane -> token
