@@ -86,8 +86,12 @@ __device__ __forceinline__ uint2 dq_ld4(const DecodeFuse& f, size_t off) {
   return make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
 }
 
-template <bool FUSED>
-__global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
+// NW = waves per workgroup.  4: wave w takes the 32-token chunks w, w + 4, ... (one chunk each at
+// the serving context); 2: chunks w, w + 2, ... with half the LDS (8 workgroups per CU instead of
+// 4), so a B = 256 step's 2048 (kv head, sequence) workgroups run in ONE round of the chip instead
+// of two — chosen on the host when B * hkv exceeds what one round of 4-wave workgroups holds.
+template <bool FUSED, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
                                                            const bf16_t* __restrict__ k_cache,
                                                            const bf16_t* __restrict__ v_cache,
                                                            const int* __restrict__ block_tables, int max_blocks,
@@ -100,13 +104,15 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
   // fused: the chunk loop covers the cached tokens only; the new one is merged from LDS
   const int ctx = ctx_lens[b] - (FUSED ? 1 : 0);
 
-  __shared__ __attribute__((aligned(16))) float smem[4 * 16 * 2 + 4 * 16 * (HD + 4)];
-  __shared__ __attribute__((aligned(16))) bf16_t p_lds[4][16 * PSTR];
+  __shared__ __attribute__((aligned(16))) float smem[NW * 16 * 2 + NW * 16 * (HD + 4)];
+  // per-wave P scratch; fused: first the staging of the G rotated q rows + k ((G + 1) x 128 bf16,
+  // which the host guarantees fits: G + 1 <= NW * 16 * PSTR / 128)
+  __shared__ __attribute__((aligned(16))) bf16_t p_lds[NW][16 * PSTR];
   // fused: new token's value and per-row score (the rotated q rows and k are staged in p_lds)
   __shared__ __attribute__((aligned(16))) float new_lds[FUSED ? HD / 2 + 16 : 4];
-  float* sm = smem;                 // [4][16]
-  float* sl = smem + 64;            // [4][16]
-  float* so = smem + 128;           // [4][16][HD+4]
+  float* sm = smem;                 // [NW][16]
+  float* sl = smem + NW * 16;       // [NW][16]
+  float* so = smem + NW * 32;       // [NW][16][HD+4]
 
   // The wave's first 32-token chunk of K and V is fetched before anything else: those loads
   // depend only on the block table, so their HBM latency overlaps the fused prologue's (split-K
@@ -149,7 +155,7 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
     const int slot = fz.slot_mapping[b];   // -1: padding row (no cache write, empty output)
     const int blk = slot >= 0 ? slot / KBS : 0, off = slot >= 0 ? slot % KBS : 0;
     // (G query heads + 1 key head) x 16 items of 4 rotary pairs
-    for (int it = threadIdx.x; it < (G + 1) * 16; it += 256) {
+    for (int it = threadIdx.x; it < (G + 1) * 16; it += 64 * NW) {
       const int hh = it >> 4, i = (it & 15) * 4;
       const size_t col0 = hh < G ? (size_t)(h * G + hh) * HD : (size_t)(hq + h) * HD;
       const uint2 a = dq_ld4(fz, rowoff + col0 + i);
@@ -237,9 +243,9 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
   for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   bf16_t* pw = p_lds[wave];
-  for (int c = wave; c < nchunks; c += 4) {
+  for (int c = wave; c < nchunks; c += NW) {
     const int t0 = c * 32;
-    if (c != wave) load_k(c);   // later chunks (contexts > 128 tokens): fetched in the loop
+    if (c != wave) load_k(c);   // later chunks (contexts > 32 NW tokens): fetched in the loop
     // ---- S = Q K^T for the two 16-token halves ----
     f32x4 s[2];
 #pragma unroll
@@ -277,7 +283,7 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // P scratch reads done before next chunk's writes
   }
 
-  // ---- merge the 4 waves ----
+  // ---- merge the NW waves ----
   if (col == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -291,12 +297,11 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
     for (int r = 0; r < 4; ++r) so[(wave * 16 + 4 * grp + r) * (HD + 4) + n * 16 + col] = o[n][r];
   }
   __syncthreads();
-  const int row = threadIdx.x >> 4;          // 16 rows
-  const int d0 = (threadIdx.x & 15) * 8;     // 8 dims per thread
-  if (row < G) {
+  const int d0 = (threadIdx.x & 15) * 8;     // 8 dims per thread, 4 NW rows per pass
+  for (int row = threadIdx.x >> 4; row < G; row += 4 * NW) {
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[w * 16 + row]);
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, sm[w * 16 + row]);
     float s_new = -INFINITY;
     if constexpr (FUSED) {
       s_new = new_lds[HD / 2 + row];
@@ -306,7 +311,7 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
     float den = 0.f;
     if (M != -INFINITY) {
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < NW; ++w) {
         const float e = exp2f(sm[w * 16 + row] - M);
         den += e * sl[w * 16 + row];
         const float* src = so + (w * 16 + row) * (HD + 4) + d0;
@@ -333,16 +338,35 @@ __global__ __launch_bounds__(256, 4) void paged_decode_kernel(bf16_t* __restrict
 }
 
 
+// 2-wave workgroups once the grid exceeds one round of 4-wave ones (4 per CU by LDS and VGPRs):
+// KA_DECODE_NW2_MIN_WGS (default 4 x CUs = 1024; 0 = never).  The fused prologue stages G + 1 rows
+// of 128 in the 2-wave P scratch: G <= 9.
+static bool decode_two_waves(int batch, int hq, int hkv) {
+  static int min_wgs = -1;
+  if (min_wgs < 0) {
+    const char* e = getenv("KA_DECODE_NW2_MIN_WGS");
+    int cus = 256, dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    min_wgs = e ? atoi(e) : 4 * cus;
+  }
+  const int G = hq / hkv;
+  return min_wgs > 0 && (long)batch * hkv > min_wgs && (G + 1) * HD <= 2 * 16 * PSTR;
+}
+
 extern "C" int ka_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache,
                                const int* block_tables, int max_blocks, const int* ctx_lens, int batch, int hq,
                                int hkv, int head_dim, int block_size, float scale, hipStream_t stream) {
   if (batch <= 0) return 0;
   if (head_dim != HD || block_size != KBS || hq % hkv != 0 || hq / hkv > 16) return (int)hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(paged_decode_kernel<false>, dim3(hkv, batch), dim3(256), 0, stream, static_cast<bf16_t*>(out),
-                     static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
-                     static_cast<const bf16_t*>(v_cache), block_tables, max_blocks, ctx_lens, hq, hkv, scale_log2,
-                     DecodeFuse{});
+  auto args = [&](auto kern, int nw) {
+    hipLaunchKernelGGL(kern, dim3(hkv, batch), dim3(64 * nw), 0, stream, static_cast<bf16_t*>(out),
+                       static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
+                       static_cast<const bf16_t*>(v_cache), block_tables, max_blocks, ctx_lens, hq, hkv, scale_log2,
+                       DecodeFuse{});
+  };
+  if (decode_two_waves(batch, hq, hkv)) args(paged_decode_kernel<false, 2>, 2);
+  else args(paged_decode_kernel<false, 4>, 4);
   KA_CHECK_LAUNCH();
 }
 
@@ -361,9 +385,13 @@ extern "C" int ka_paged_decode_rope(void* out, const void* qkv, const float* P, 
   const float scale_log2 = scale * 1.4426950408889634f;
   DecodeFuse fz{static_cast<const bf16_t*>(qkv), P, split, p_bf16, (size_t)batch * (hq + 2 * hkv) * HD, positions,
                 cos_sin, slot_mapping, static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache)};
-  hipLaunchKernelGGL(paged_decode_kernel<true>, dim3(hkv, batch), dim3(256), 0, stream, static_cast<bf16_t*>(out),
-                     nullptr, static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), block_tables,
-                     max_blocks, ctx_lens, hq, hkv, scale_log2, fz);
+  auto args = [&](auto kern, int nw) {
+    hipLaunchKernelGGL(kern, dim3(hkv, batch), dim3(64 * nw), 0, stream, static_cast<bf16_t*>(out), nullptr,
+                       static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), block_tables,
+                       max_blocks, ctx_lens, hq, hkv, scale_log2, fz);
+  };
+  if (decode_two_waves(batch, hq, hkv)) args(paged_decode_kernel<true, 2>, 2);
+  else args(paged_decode_kernel<true, 4>, 4);
   KA_CHECK_LAUNCH();
 }
 

@@ -97,12 +97,13 @@ def test_paged_decode(hq, hkv, ctx_lens):
     close(ops.attention_decode(q, kc, vc, bt, ctx, scale), ref.attention_decode(q, kc, vc, bt, ctx, scale), atol=2e-2)
 
 
-def test_paged_decode_large_batch_mixed_lengths():
-    """80 sequences of mixed lengths, a padding row (ctx 0 -> zeros) and a 1000-token context whose
-    chunks each wave walks in several passes."""
+@pytest.mark.parametrize("S,hq", [(80, 32), (160, 32), (160, 64)])
+def test_paged_decode_large_batch_mixed_lengths(S, hq):
+    """S sequences of mixed lengths, a padding row (ctx 0 -> zeros) and a 1000-token context whose
+    chunks each wave walks in several passes; S * hkv > 1024 takes the 2-wave workgroups."""
     import random
     rng = random.Random(0)
-    S, hq, hkv = 80, 32, 8
+    hkv = 8
     ctx_lens = [rng.randint(1, 300) for _ in range(S)]
     ctx_lens[5] = 0
     ctx_lens[7] = 1000
@@ -127,14 +128,15 @@ def test_paged_decode_padding_rows_zero():
     assert out[1].abs().max().item() == 0
 
 
-@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (4, 1)])
+@pytest.mark.parametrize("hq,hkv,reps", [(32, 8, 1), (64, 8, 1), (4, 1, 1), (32, 8, 23), (64, 8, 23)])
 @pytest.mark.parametrize("split", [0, 1, 4, -1, -4])
-def test_decode_attention_rope_fused(hq, hkv, split):
+def test_decode_attention_rope_fused(hq, hkv, reps, split):
     """RoPE + KV append + paged decode in one kernel == rope_kv_write then attention_decode (fp32
     torch references), on bf16 qkv and on split-K partials; cache contents identical to the
-    unfused kernels'; a padding row (slot -1, ctx 0) writes nothing and returns zeros."""
-    d, nb = 128, 400
-    ctx_lens = [1, 2, 17, 100, 129, 33, 0]
+    unfused kernels'; a padding row (slot -1, ctx 0) writes nothing and returns zeros.  reps = 23:
+    161 rows x 8 kv heads > 1024 workgroups, the 2-wave variant."""
+    d, nb = 128, 400 * reps
+    ctx_lens = [1, 2, 17, 100, 129, 33] * reps + [0]
     S = len(ctx_lens)
     bt = _tables(S, ctx_lens, nb, 16)
     ctx = torch.tensor(ctx_lens, dtype=torch.int32, device=DEV)
