@@ -20,12 +20,16 @@
 //   * persistent: one workgroup per CU walks its tiles; the next tile's first two k-tiles are staged
 //     during the current tile's last two k-steps and the epilogue transposes through a separate
 //     32 KB of LDS, so it overlaps their landing (+0.5-1 %, gb_p_ab.log);
-//   * two register fragment sets: the k-step's second half is read while the first half's 64 MFMAs
-//     run, and the next tile's first half while the second half's run.  ONE barrier per k-tile, and
-//     each tile's DMA is issued two half-steps (2 x 64 MFMAs) before the barrier that waits for it:
-//       phase A(t): read F1 <- (t, k 32..63)     | MFMA F0 | lgkmcnt(0), vmcnt(0) [tile t+1], barrier
-//       phase B(t): read F0 <- (t+1, k 0..31),  DMA tile t+2 -> buffer t&1 | MFMA F1
-//     (WAR: buffer t&1's last reads are F1 of phase A(t), retired before that barrier);
+//   * two register fragment sets (F0 = k 0..31, F1 = k 32..63 of a k-tile) and two barriers per
+//     k-tile, with the fragment reads and the LDS-DMA pieces in separate windows of the 128-MFMA
+//     stream (the order hipBLASLt's gfx950 MT256x256x64 DirectToLds kernel uses; +1-2 % over a
+//     single-barrier loop whose second half carried reads and DMA together, and the fused LM head
+//     at M = 256 297 -> 260 us, profiles/r3/gemm_big/gbs_ab.log):
+//       MFMA F0(t) 0-15 | read F1(t) <- buffer t&1
+//       lgkmcnt(0), barrier          (every wave's reads of buffer t&1 done)
+//       MFMA F0(t) 16-63, F1(t) 0-47 | 16 DMA pieces of k-tile t+2 -> buffer t&1, one per 6 MFMAs
+//       vmcnt(16), barrier           (k-tile t+1, staged one k-tile earlier, landed)
+//       MFMA F1(t) 48-63 | read F0(t+1) <- buffer (t+1)&1;
 //   * XCD-aware tile order (T1): the bijective round-robin remap, then GM m-tiles x all n-tiles
 //     super-rows so the panels of the tiles running together on one XCD are L2 hits.
 // Measured at 0.90-0.92x rocBLAS's MT256x256x64 kernel on the plain shapes at M = 4096 and 0.96-0.98x
@@ -243,29 +247,41 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
       mfma_acc(acc[q >> 3][q & 7], FA[q >> 3], FB[q & 7]);
     });
   };
-  // phase A of a k-tile in buffer BUF: its second k half into F1 while F0's MFMAs run; then every
-  // read of buffer BUF retired (WAR for the DMA that refills it) and the next k-tile landed (this
-  // wave's part; the barrier makes it every wave's)
-  auto phase_a = [&](auto bufc) {
+  // one 64-deep k-tile per call as 32 groups of 4 MFMAs (groups 0-15 on F0, 16-31 on
+  // F1), the fragment reads and the LDS-DMA pieces in separate windows of the MFMA stream (the
+  // order hipBLASLt's MT256x256x64 DirectToLds kernel uses on gfx950; it measured faster than a
+  // window carrying both):
+  //   groups 0-3:   F1(t) <- buffer BUF, 4 reads before each group
+  //   lgkmcnt(0) + barrier #1: every wave's reads of buffer BUF are done (F0(t) was read at the end
+  //                 of the previous call)
+  //   groups 4-27:  the 16 pieces of k-tile T into buffer BUF, 2 of every 3 groups (1 per 6 MFMAs)
+  //   vmcnt(16) + barrier #2: the k-tile staged one call earlier has landed in buffer BUF ^ 1
+  //   groups 28-31: F0(t + 1) <- buffer BUF ^ 1, 4 reads before each (F0(t) retired at group 15)
+  auto iter = [&](auto bufc, int T) {
     constexpr int BUF = decltype(bufc)::value;
-    static_for<16>([&](auto sc) {
-      rd(sc, fa1, fb1, BUF ? bA11 : bA01, BUF ? bB11 : bB01);
-      mma4(sc, fa0, fb0);
-    });
-    wait_lgkm0();
-    wait_vm<0>();
-    block_sync();
-  };
-  // phase B: the next k-tile's first k half into F0, the DMA of k-tile T (of the tile the offsets
-  // describe) into buffer BUF (one 1-KB piece per MFMA group), F1's MFMAs; F0 retired at the end
-  // (covered by the 64 MFMAs).  In the last k-step the reads fetch LDS that no MFMA consumes.
-  auto phase_b = [&](auto bufc, int T) {
-    constexpr int BUF = decltype(bufc)::value;
-    static_for<16>([&](auto sc) {
-      constexpr int S = decltype(sc)::value;
-      rd(sc, fa0, fb0, BUF ? bA00 : bA10, BUF ? bB00 : bB10);
-      GB_DMA(S, BUF, T);
-      mma4(sc, fa1, fb1);
+    static_for<32>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      if constexpr (g < 4)
+        static_for<4>([&](auto rc) {
+          rd(std::integral_constant<int, 4 * g + decltype(rc)::value>{}, fa1, fb1, BUF ? bA11 : bA01,
+             BUF ? bB11 : bB01);
+        });
+      if constexpr (g == 4) {
+        wait_lgkm0();
+        block_sync();
+      }
+      if constexpr (g >= 4 && g < 28 && (g - 4) % 3 != 2) GB_DMA(((g - 4) / 3) * 2 + (g - 4) % 3, BUF, T);
+      if constexpr (g == 28) {
+        wait_vm<16>();
+        block_sync();
+      }
+      if constexpr (g >= 28)
+        static_for<4>([&](auto rc) {
+          rd(std::integral_constant<int, 4 * (g - 28) + decltype(rc)::value>{}, fa0, fb0, BUF ? bA00 : bA10,
+             BUF ? bB00 : bB10);
+        });
+      if constexpr (g < 16) mma4(std::integral_constant<int, g>{}, fa0, fb0);
+      else mma4(std::integral_constant<int, g - 16>{}, fa1, fb1);
     });
     wait_lgkm0();
   };
@@ -285,7 +301,9 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     if (more) decode(nvb, ntm, ntn, nks);
     const int m0 = tm * BM;
     // k-tile 0 landed: the 16 youngest vector-memory operations are k-tile 1's DMA or the previous
-    // tile's epilogue stores, everything older (k-tile 0) is done
+    // tile's epilogue stores, everything older (k-tile 0) is done.  (The previous tile's last call
+    // already read these fragments; reading them again here keeps F0 dead across the epilogue,
+    // which would otherwise spill.)
     wait_vm<16>();
     block_sync();
     static_for<16>([&](auto sc) { rd(sc, fa0, fb0, bA00, bB00); });
@@ -301,10 +319,8 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     for (int t = 0; t < nk; t += 2) {
       const bool last = t + 2 >= nk;
       if (last) set_offsets(ntm, ntn, nks);
-      phase_a(I0{});
-      phase_b(I0{}, last ? 0 : t + 2);
-      phase_a(I1{});
-      phase_b(I1{}, last ? 1 : t + 3);
+      iter(I0{}, last ? 0 : t + 2);
+      iter(I1{}, last ? 1 : t + 3);
       // the MFMA wait states inside the loop, before its exit: hipcc does not know the asm MFMAs'
       // latency and may copy accumulators (v_accvgpr_mov) on the exit edge, which would read
       // results still in flight (seen: the argmax epilogue's accumulators shuffled before a drain
