@@ -29,7 +29,10 @@
 //       lgkmcnt(0), barrier          (every wave's reads of buffer t&1 done)
 //       MFMA F0(t) 16-63, F1(t) 0-47 | 16 DMA pieces of k-tile t+2 -> buffer t&1, one per 6 MFMAs
 //       vmcnt(16), barrier           (k-tile t+1, staged one k-tile earlier, landed)
-//       MFMA F1(t) 48-63 | read F0(t+1) <- buffer (t+1)&1;
+//       MFMA F1(t) 48-63 | read F0(t+1) <- buffer (t+1)&1, waited for per fragment row by the
+//                          next k-tile's first MFMAs;
+//     one fragment read per MFMA in the read windows and the counted waits: another 1-2 %
+//     (gb_rp_ab.log, gb_cw_ab.log);
 //   * XCD-aware tile order (T1): the bijective round-robin remap, then GM m-tiles x all n-tiles
 //     super-rows so the panels of the tiles running together on one XCD are L2 hits.
 // Measured at 0.90-0.92x rocBLAS's MT256x256x64 kernel on the plain shapes at M = 4096 and 0.96-0.98x
@@ -129,6 +132,8 @@ KA_DEV void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "mem
 template <int N>
 KA_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 KA_DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+template <int N>
+KA_DEV void wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory"); }
 KA_DEV void block_sync() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_barrier" ::: "memory");
@@ -261,11 +266,26 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     constexpr int BUF = decltype(bufc)::value;
     static_for<32>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
-      if constexpr (g < 4)
-        static_for<4>([&](auto rc) {
-          rd(std::integral_constant<int, 4 * g + decltype(rc)::value>{}, fa1, fb1, BUF ? bA11 : bA01,
-             BUF ? bB11 : bB01);
+      if constexpr (g < 4 || g >= 28) {   // read windows: one fragment read before each MFMA
+        static_for<4>([&](auto qc) {
+          constexpr int qq = decltype(qc)::value;
+          if constexpr (g < 4)
+            rd(std::integral_constant<int, 4 * g + qq>{}, fa1, fb1, BUF ? bA11 : bA01, BUF ? bB11 : bB01);
+          else   // B0..B7 first, then A0..A7: row 0 of the next call needs A0 and every B
+            rd(std::integral_constant<int, (4 * (g - 28) + qq) < 8 ? 2 * (4 * (g - 28) + qq) + 1
+                                                                   : 2 * (4 * (g - 28) + qq - 8)>{},
+               fa0, fb0, BUF ? bA00 : bA10, BUF ? bB00 : bB10);
+          constexpr int q = 4 * (g & 15) + qq;
+          // the previous call's F0 reads are waited for here, per A fragment: row 0 (A0, all B)
+          // before MFMA 0 (A1..A7 and this call's first read may still be in flight), row 1 (A1)
+          // before MFMA 8; rows 2.. are covered by barrier #1's lgkmcnt(0).  No copy of a fragment
+          // register sits between (checked in the disassembly: the loop has no v_mov)
+          if constexpr (q == 0) wait_lgkm<8>();
+          if constexpr (q == 8) wait_lgkm<15>();
+          if constexpr (g < 16) mfma_acc(acc[q >> 3][q & 7], fa0[q >> 3], fb0[q & 7]);
+          else mfma_acc(acc[q >> 3][q & 7], fa1[q >> 3], fb1[q & 7]);
         });
+      }
       if constexpr (g == 4) {
         wait_lgkm0();
         block_sync();
@@ -275,15 +295,12 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
         wait_vm<16>();
         block_sync();
       }
-      if constexpr (g >= 28)
-        static_for<4>([&](auto rc) {
-          rd(std::integral_constant<int, 4 * (g - 28) + decltype(rc)::value>{}, fa0, fb0, BUF ? bA00 : bA10,
-             BUF ? bB00 : bB10);
-        });
-      if constexpr (g < 16) mma4(std::integral_constant<int, g>{}, fa0, fb0);
-      else mma4(std::integral_constant<int, g - 16>{}, fa1, fb1);
+      if constexpr (g >= 4 && g < 28) {
+        if constexpr (g < 16) mma4(std::integral_constant<int, g>{}, fa0, fb0);
+        else mma4(std::integral_constant<int, g - 16>{}, fa1, fb1);
+      }
     });
-    wait_lgkm0();
+    // (no lgkmcnt wait here: the next call waits per fragment; the tile's last call waits below)
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -325,7 +342,10 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
       // latency and may copy accumulators (v_accvgpr_mov) on the exit edge, which would read
       // results still in flight (seen: the argmax epilogue's accumulators shuffled before a drain
       // placed after the loop)
-      if (last) mfma_drain();
+      if (last) {
+        mfma_drain();
+        wait_lgkm0();   // the last call's F0 reads land before the epilogue may reuse those registers
+      }
     }
     // epilogue.  acc[i][j][r] = C[n = 128 wn + 16 i + 4 grp + r][m = 128 wm + 16 j + r16] of the
     // tile.  bf16 / SwiGLU: the wave's quadrant is transposed through its 8 KB of LDS in row passes
