@@ -110,17 +110,17 @@ KA_DEV void ds_read16(bf16x8& dst, uint32_t addr) {
 template <int P>
 KA_DEV void dma16g(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t lds_addr, uint32_t& keep) {
   if constexpr (P == 0)
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offenlds"
                  : "=&s"(keep)
                  : "v"(voff), "s"(r), "s"(lds_addr), "s"(soff)
                  : "memory");
   else if constexpr (P == 3)
-    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:3072 lds\n\ts_mov_b32 m0, %3"
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:3072lds\n\ts_mov_b32 m0, %3"
                  :
                  : "v"(voff), "s"(r), "s"(soff), "s"(keep)
                  : "memory");
   else
-    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:%3 lds"
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:%3lds"
                  :
                  : "v"(voff), "s"(r), "s"(soff), "i"(P * 1024)
                  : "memory");
@@ -266,14 +266,16 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     constexpr int BUF = decltype(bufc)::value;
     static_for<32>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
-      if constexpr (g < 4 || g >= 28) {   // read windows: one fragment read before each MFMA
+      constexpr int RW = 28;               // F0(t+1) read window: groups 28-31 (starting it one
+                                           // group earlier measured the same, gb_sc_ab.log rw27)
+      if constexpr (g < 4 || (g >= RW && g < RW + 4)) {   // read windows: one fragment read before each MFMA
         static_for<4>([&](auto qc) {
           constexpr int qq = decltype(qc)::value;
           if constexpr (g < 4)
             rd(std::integral_constant<int, 4 * g + qq>{}, fa1, fb1, BUF ? bA11 : bA01, BUF ? bB11 : bB01);
           else   // B0..B7 first, then A0..A7: row 0 of the next call needs A0 and every B
-            rd(std::integral_constant<int, (4 * (g - 28) + qq) < 8 ? 2 * (4 * (g - 28) + qq) + 1
-                                                                   : 2 * (4 * (g - 28) + qq - 8)>{},
+            rd(std::integral_constant<int, (4 * (g - RW) + qq) < 8 ? 2 * (4 * (g - RW) + qq) + 1
+                                                                   : 2 * (4 * (g - RW) + qq - 8)>{},
                fa0, fb0, BUF ? bA00 : bA10, BUF ? bB00 : bB10);
           constexpr int q = 4 * (g & 15) + qq;
           // the previous call's F0 reads are waited for here, per A fragment: row 0 (A0, all B)
@@ -290,12 +292,12 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
         wait_lgkm0();
         block_sync();
       }
-      if constexpr (g >= 4 && g < 28 && (g - 4) % 3 != 2) GB_DMA(((g - 4) / 3) * 2 + (g - 4) % 3, BUF, T);
-      if constexpr (g == 28) {
+      if constexpr (g >= 4 && g < RW && (g - 4) % 3 != 2) GB_DMA(((g - 4) / 3) * 2 + (g - 4) % 3, BUF, T);
+      if constexpr (g == RW) {
         wait_vm<16>();
         block_sync();
       }
-      if constexpr (g >= 4 && g < 28) {
+      if constexpr (g >= 4 && !(g >= RW && g < RW + 4)) {
         if constexpr (g < 16) mma4(std::integral_constant<int, g>{}, fa0, fb0);
         else mma4(std::integral_constant<int, g - 16>{}, fa1, fb1);
       }
