@@ -110,17 +110,17 @@ KA_DEV void ds_read16(bf16x8& dst, uint32_t addr) {
 template <int P>
 KA_DEV void dma16g(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t lds_addr, uint32_t& keep) {
   if constexpr (P == 0)
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offenlds"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds"
                  : "=&s"(keep)
                  : "v"(voff), "s"(r), "s"(lds_addr), "s"(soff)
                  : "memory");
   else if constexpr (P == 3)
-    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:3072lds\n\ts_mov_b32 m0, %3"
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:3072 lds\n\ts_mov_b32 m0, %3"
                  :
                  : "v"(voff), "s"(r), "s"(soff), "s"(keep)
                  : "memory");
   else
-    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:%3lds"
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:%3 lds"
                  :
                  : "v"(voff), "s"(r), "s"(soff), "i"(P * 1024)
                  : "memory");
