@@ -306,6 +306,26 @@ def test_prefix_cache_hit_matches_cold():
     assert warm.output_ids == cold.output_ids
 
 
+def test_last_layer_pruning_hidden_matches_full_gpu():
+    """Prefill with the last layer continued on the last-token rows only (one-query HIP decode
+    attention over the just-appended keys, then O / norm / MLP on S rows) gives the final hidden rows
+    of the full forward (prefill attention over every row) to bf16 tolerance; on a ~1.3k-token step
+    the gate_up of the other layers takes the gemm_big SwiGLU path."""
+    eng = _engine("llama3-8b-2l", graphs=False, max_batch=64, kv_cache_tokens=32768,
+                  prefix_caching=False, max_batched_tokens=16384)
+    be = EngineLLM(eng, max_new_tokens=4)
+    m = eng.runner.model
+    queries = [q + f" #{i}" for i in range(12) for q in QUERIES[:1]]
+    hs = {}
+    with torch.inference_mode():
+        for prune in (False, True):
+            m.prune_last_layer = prune
+            hs[prune] = _prefill_hidden(eng, be, queries).float()
+    m.prune_last_layer = True
+    assert hs[True].shape == hs[False].shape == (len(queries), m.W["embed"].shape[1])
+    torch.testing.assert_close(hs[True], hs[False], atol=0.05, rtol=0.05)
+
+
 def test_mixed_step_split_attention_hidden_matches_unsplit():
     """One real mixed step (2 decode rows + 1 prompt): the forward with decode rows through the
     decode kernel equals the forward with every row through the varlen prefill kernel (hidden
