@@ -87,6 +87,9 @@ struct Args {
   const int* lists;
   int lstride, src_div, groups;
   int wnt;   // 1: weight DMAs non-temporal (aux = 2) so the streamed weights do not evict X from L2
+  // EPI_SWIGLU over a [gate; up] weight (up rows from row swi = I, N = 2I) instead of one whose rows
+  // are interleaved in 16-row chunks: the DMA sources gather the interleaved order (0: interleaved)
+  int swi;
 };
 
 // logical tile -> (m tile, n tile): XCD-contiguous, then GM m-tiles x all n-tiles super-rows
@@ -170,7 +173,12 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   for (int j = 0; j < C::GA; ++j) {
     const int row = (j * C::NW + wave) * RPI + rl;
     const int ch = swz<C::KT>(row, slot);
-    offA[j] = (uint32_t)(min(n0 + row, a.N - 1) * (uint32_t)a.K + kb + ch * 8) * 2u;
+    int wr = min(n0 + row, a.N - 1);
+    if (EPI == EPI_SWIGLU && a.swi > 0) {   // interleaved row ri: 16-row chunk ri >> 4 of gate (even) / up (odd)
+      const int ri = wr;
+      wr = ((ri >> 5) << 4) + (ri & 15) + ((ri >> 4) & 1) * a.swi;
+    }
+    offA[j] = (uint32_t)(wr * (uint32_t)a.K + kb + ch * 8) * 2u;
   }
 #pragma unroll
   for (int j = 0; j < C::GB; ++j) {
@@ -671,6 +679,21 @@ extern "C" int ka_gemm_mfma(void* Y, void* P, const void* X, const void* W, int 
     case gm::EPI_SWIGLU: return gm::dispatch<gm::EPI_SWIGLU>(cfg, a, split, stream);
   }
   return (int)hipErrorInvalidValue;
+}
+
+// Y [M, ldy] = silu(X gate^T) * (X up^T) for W = [gate; up] ([2I, K], the model's gate_up layout):
+// the decode-size gate_up with its SiLU·mul epilogue (no [M, 2I] output, no separate SiLU kernel).
+// Requirements: K % 64 == 0, I % 16 == 0, ldx % 8 == 0; cfg one of GM_CFGS (not 19).
+extern "C" int ka_gemm_mfma_swiglu(void* Y, const void* X, const void* W, int M, int I, int K, int ldx, int ldy,
+                                   int cfg, hipStream_t stream) {
+  if (M <= 0 || I <= 0) return 0;
+  if (K % 64 != 0 || I % 16 != 0 || ldx % 8 != 0 || cfg == 19 || ka_gm_bn(cfg) < 0)
+    return (int)hipErrorInvalidValue;
+  gm::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), Y, nullptr, M, 2 * I, K, ldx, ldy, K,
+             0, 0, 8};
+  a.wnt = M <= 512;
+  a.swi = I;
+  return gm::dispatch<gm::EPI_SWIGLU>(cfg, a, 1, stream);
 }
 
 // Grouped (MoE expert) GEMM with device-side routing, no host read of the counts:

@@ -217,6 +217,36 @@ class ModelRunner:
         logger.info("lm head plan: %s (fused from %d rows)", report, ops.LM_HEAD_FUSED_MIN_M)
         return report
 
+    @torch.inference_mode()
+    def tune_swiglu(self) -> dict:
+        """Per decode bucket: gate_up with the ring kernel's SwiGLU epilogue (ops.linear_gm_swiglu,
+        each configuration) against the GEMM plan's gate_up + SiLU·mul, on the model's own w13
+        rotated over layers; fills ops.DECODE_SWIGLU_CFG with the winners."""
+        m = self.model
+        ops.DECODE_SWIGLU_CFG.clear()
+        if self.device.type != "cuda" or ops.DECODE_SWIGLU == "0" or getattr(m.cfg, "is_moe", False):
+            return {}
+        ws = [L["w13"] for L in m.layers if L.get("w13") is not None and L["w13"].dim() == 2][:8]
+        if not ws:
+            return {}
+        from ..ops.autotune import _time
+        report = {}
+        for M in sorted(set(self.buckets)):
+            x = torch.randn(M, ws[0].shape[1], device=self.device, dtype=ws[0].dtype)
+            if not ops.decode_swiglu_ok(x, ws[0]):
+                continue
+            t_un = _time(lambda w: ops.silu_mul(ops.linear(x, w, defer_reduce=True)), ws)
+            best = (0, t_un)
+            for cfg in ops.DECODE_SWIGLU_CFGS:
+                t = _time(lambda w: ops.linear_gm_swiglu(x, w, cfg), ws)
+                if t < best[1]:
+                    best = (cfg, t)
+            if best[0]:
+                ops.DECODE_SWIGLU_CFG[M] = best[0]
+            report[M] = {"cfg": best[0], "fused_us": round(best[1], 1), "unfused_us": round(t_un, 1)}
+        logger.info("decode swiglu plan: %s", report)
+        return report
+
     def _attention_consumer(self, ctx: int = 128):
         """fn(qkv, M): decode_attention_rope over M synthetic sequences of `ctx` cached tokens in
         layer 0's cache (autotune runs before serving: the KV written here is never read)."""
@@ -245,6 +275,7 @@ class ModelRunner:
         if autotune:
             self.gemm_plan = self.autotune()
             self.lm_head_plan = self.tune_lm_head()
+            self.swiglu_plan = self.tune_swiglu()
         self.h_np[:] = 0
         o = self._off
         for name in ("slots",):

@@ -143,6 +143,10 @@ class LlamaModel:
                 # prefill / mixed steps: gate_up with the SwiGLU epilogue (no [T, 2I] intermediate)
                 h = ops.linear(ops.linear_swiglu(x, L["w13"]), L["w2"], defer_reduce=fuse,
                                bf16_partials=self.bf16_partials)
+            elif sw := ops.decode_swiglu_cfg(x, L["w13"]):
+                # decode buckets where the ring kernel's SwiGLU epilogue won (ModelRunner.tune_swiglu)
+                h = ops.linear(ops.linear_gm_swiglu(x, L["w13"], sw), L["w2"], defer_reduce=fuse,
+                               bf16_partials=self.bf16_partials)
             else:
                 # batch <= 4: SiLU·mul computed inside the down GEMV's X staging (ops.swiglu_linear)
                 h = ops.swiglu_linear(ops.linear(x, L["w13"], defer_reduce=True), L["w2"], defer_reduce=fuse,

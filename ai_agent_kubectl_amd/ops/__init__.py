@@ -417,6 +417,29 @@ def linear_swiglu(x: torch.Tensor, w13: torch.Tensor, out: Optional[torch.Tensor
     return out
 
 
+# Decode gate_up with the SwiGLU epilogue in the csrc/gemm_mfma.hip ring kernel, per decode bucket
+# M -> configuration: filled at engine start by ModelRunner.tune_swiglu where it beats the GEMM plan's
+# gate_up + SiLU·mul (profiles/r3/decode_swiglu: 72.9 vs 77.4 us at M = 256, 51.9 vs 58.4 at 128,
+# Llama-3-8B).  KA_DECODE_SWIGLU=0 disables it.
+DECODE_SWIGLU = os.environ.get("KA_DECODE_SWIGLU", "auto")
+DECODE_SWIGLU_CFG: dict = {}
+DECODE_SWIGLU_CFGS = (2, 3, 4, 5, 12)
+
+
+def decode_swiglu_ok(x: torch.Tensor, w13: torch.Tensor) -> bool:
+    M, K = x.shape
+    return (x.is_contiguous() and w13.is_contiguous() and w13.shape[1] == K and K % 64 == 0
+            and w13.shape[0] % 32 == 0 and 32 <= M <= TILE_MAX_M)
+
+
+def decode_swiglu_cfg(x: torch.Tensor, w13: torch.Tensor) -> int:
+    """The gemm_mfma configuration for this decode gate_up + SwiGLU, 0 for the unfused path."""
+    if DECODE_SWIGLU == "0" or _ref(x):
+        return 0
+    cfg = DECODE_SWIGLU_CFG.get(x.shape[0], 0)
+    return cfg if cfg and decode_swiglu_ok(x, w13) else 0
+
+
 GEMV_SWIGLU_MAX_M = 4   # csrc/gemm_skinny.hip GEMV_MAX_M
 
 
@@ -491,6 +514,20 @@ def linear_gm(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, defer_
     check(lib.ka_gemm_mfma(_p(y), _p(ws), _p(x), _p(w), M, N, K, x.stride(0), N, split, cfg, GM_EPI_P32, 0, st),
           "gemm_mfma")
     return y
+
+
+def linear_gm_swiglu(x: torch.Tensor, w13: torch.Tensor, cfg: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(x @ gate.T) * (x @ up.T) for w13 = [gate; up] through csrc/gemm_mfma.hip configuration
+    `cfg` with the SwiGLU epilogue (the DMA sources gather gate / up in 16-row chunks): [M, I] bf16."""
+    M, K = x.shape
+    I = w13.shape[0] // 2
+    if _ref(x):
+        return ref.silu_mul(ref.linear(x, w13))
+    lib = require()
+    out = torch.empty((M, I), dtype=x.dtype, device=x.device) if out is None else out
+    check(lib.ka_gemm_mfma_swiglu(_p(out), _p(x), _p(w13), M, I, K, x.stride(0), out.stride(0), int(cfg), _stream()),
+          "gemm_mfma_swiglu")
+    return out
 
 
 def linear_grouped(x: torch.Tensor, w: torch.Tensor, counts: torch.Tensor, lists: torch.Tensor, rows: int,

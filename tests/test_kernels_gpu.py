@@ -322,6 +322,37 @@ def test_prefill_swiglu_used_by_model_path():
     assert not ops.use_prefill_swiglu(x[:256], w13)
 
 
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5, 12])
+@pytest.mark.parametrize("M,I", [(32, 14336), (100, 1792), (256, 14336), (300, 1792), (512, 1792)])
+def test_decode_swiglu_gemm_vs_fp32(M, I, cfg):
+    """Decode gate_up with the gemm_mfma SwiGLU epilogue over the model's [gate; up] weight (the
+    weight DMAs gather 16-row gate / up chunks) against fp32 silu(x gate^T) * (x up^T)."""
+    K = 4096
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w13 = (torch.randn(2 * I, K, device=DEV) / math.sqrt(K)).to(BF)
+    y = ops.linear_gm_swiglu(x, w13, cfg)
+    assert y.shape == (M, I)
+    g = x.float() @ w13[:I].float().t()
+    u = x.float() @ w13[I:].float().t()
+    close(y, torch.nn.functional.silu(g) * u, atol=2e-2, rtol=2e-2)
+
+
+def test_decode_swiglu_plan_dispatch():
+    """ops.decode_swiglu_cfg follows the per-bucket plan and the shape rules."""
+    x = torch.randn(256, 4096, device=DEV, dtype=BF)
+    w13 = torch.zeros(2 * 14336, 4096, device=DEV, dtype=BF)
+    saved = dict(ops.DECODE_SWIGLU_CFG)
+    try:
+        ops.DECODE_SWIGLU_CFG.clear()
+        assert ops.decode_swiglu_cfg(x, w13) == 0
+        ops.DECODE_SWIGLU_CFG[256] = 2
+        assert ops.decode_swiglu_cfg(x, w13) == (0 if ops.DECODE_SWIGLU == "0" else 2)
+        assert ops.decode_swiglu_cfg(x[:128], w13) == 0
+    finally:
+        ops.DECODE_SWIGLU_CFG.clear()
+        ops.DECODE_SWIGLU_CFG.update(saved)
+
+
 def test_moe_topk():
     lg = torch.randn(50, 8, device=DEV, dtype=BF)
     w1, i1 = ops.moe_topk(lg, 2)

@@ -14,6 +14,23 @@ def test_linear_swiglu_cpu_is_reference():
     assert not ops.use_prefill_swiglu(x, w13)   # CPU tensors never take the HIP path
 
 
+def test_linear_gm_swiglu_cpu_is_reference():
+    torch.manual_seed(0)
+    x = torch.randn(40, 256, dtype=torch.bfloat16)
+    w13 = (torch.randn(2 * 64, 256) / 16).to(torch.bfloat16)
+    torch.testing.assert_close(ops.linear_gm_swiglu(x, w13, 2).float(), ref.silu_mul(ref.linear(x, w13)).float())
+    saved = dict(ops.DECODE_SWIGLU_CFG)
+    ops.DECODE_SWIGLU_CFG[40] = 2
+    try:
+        assert ops.decode_swiglu_cfg(x, w13) == 0   # CPU tensors never take the HIP path
+    finally:
+        ops.DECODE_SWIGLU_CFG.clear()
+        ops.DECODE_SWIGLU_CFG.update(saved)
+    assert ops.decode_swiglu_ok(x, w13)
+    assert not ops.decode_swiglu_ok(x[:16], w13)                       # M < 32: GEMV / skinny paths
+    assert not ops.decode_swiglu_ok(x, torch.zeros(2 * 56, 256, dtype=torch.bfloat16))   # I % 16
+
+
 def test_swiglu_gemm_shape_rules():
     x = torch.zeros(2048, 4096, dtype=torch.bfloat16)
     assert ops.swiglu_gemm_ok(x, torch.zeros(2 * 14336, 4096, dtype=torch.bfloat16))
