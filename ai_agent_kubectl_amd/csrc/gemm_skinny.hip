@@ -271,6 +271,146 @@ extern "C" void ka_splitk_reduce_launch(bf16_t* Y, const float* P, int split, lo
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((int)blocks), dim3(256), 0, stream, Y, P, split, mn);
 }
 
+// Row-streaming GEMV for M <= 4: each wave owns RW consecutive weight rows, i.e. one contiguous
+// RW x klen block of W, and streams it 1 KB per load instruction (64 lanes x 16 B along K) through
+// a RING-deep register ring; the dot products run on v_dot2c_f32_bf16 against the workgroup's
+// LDS-staged X slice, and each finished row is summed across the wave (xor shuffles).  Against
+// gemv_ring_kernel (16 rows x 128 B per load, MFMA with one live row) this issues HBM-friendly
+// sequential streams and lets the grid be sized by rows per wave instead of 64-row tiles.
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+KA_DEV float dot8(uint4 w, uint4 x, float acc) {
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, w.x), __builtin_bit_cast(bf16x2v, x.x), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, w.y), __builtin_bit_cast(bf16x2v, x.y), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, w.z), __builtin_bit_cast(bf16x2v, x.z), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, w.w), __builtin_bit_cast(bf16x2v, x.w), acc, false);
+  return acc;
+}
+
+template <bool NT>
+KA_DEV uint4 ld_w16(const bf16_t* p) {
+  if constexpr (NT) return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p)));
+  else return *reinterpret_cast<const uint4*>(p);
+}
+
+template <int MR, int RING, bool SWIGLU, bool NT = false>
+__global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                        bf16_t* __restrict__ Y, float* __restrict__ P, int M, int N,
+                                                        int K, int kps, int RW) {
+  extern __shared__ __attribute__((aligned(16))) uint4 xsr[];   // [MR][klen / 8]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int split = blockIdx.y;
+  const int k_begin = split * kps;
+  const int klen = min(K, k_begin + kps) - k_begin;
+  const int KC = klen >> 9;          // 512-element chunks per row
+  const int pr = klen >> 3;          // 16-B pieces per X row
+  const int r0 = (blockIdx.x * 4 + wave) * RW;
+  const int nrows = max(0, min(RW, N - r0));
+  const int total = nrows * KC;      // loads of this wave (wave-uniform)
+
+  // weight stream: load i covers row i / KC, chunk i % KC; past the end the pointer stays on the
+  // last chunk (L2 re-reads) so the ring's wait counts stay static
+  const bf16_t* lp = W + (size_t)min(r0, N - 1) * K + k_begin + lane * 8;
+  int lc = 0, issued = 0;
+  const int row_skip = K - klen;
+  uint4 w[RING];
+#pragma unroll
+  for (int r = 0; r < RING; ++r) {
+    w[r] = ld_w16<NT>(lp);
+    if (issued + 1 < total) {
+      lp += 512;
+      if (++lc == KC) { lc = 0; lp += row_skip; }
+    }
+    ++issued;
+  }
+  for (int p = tid; p < MR * pr; p += 256) {
+    const int m = p / pr, pc = p - m * pr;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (m < M) {
+      if constexpr (SWIGLU) {
+        const bf16_t* g = X + (size_t)m * 2 * K + k_begin + pc * 8;
+        v = __builtin_bit_cast(uint4, swiglu8(*reinterpret_cast<const u32x4*>(g), *reinterpret_cast<const u32x4*>(g + K)));
+      } else {
+        v = *reinterpret_cast<const uint4*>(X + (size_t)m * K + k_begin + pc * 8);
+      }
+    }
+    xsr[p] = v;
+  }
+  __syncthreads();
+
+  float acc[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) acc[m] = 0.f;
+  int cc = 0, crow = r0;
+  for (int base = 0; base < total; base += RING) {
+#pragma unroll
+    for (int r = 0; r < RING; ++r) {
+      if (base + r < total) {
+#pragma unroll
+        for (int m = 0; m < MR; ++m) acc[m] = dot8(w[r], xsr[m * pr + cc * 64 + lane], acc[m]);
+        if (++cc == KC) {
+          cc = 0;
+#pragma unroll
+          for (int m = 0; m < MR; ++m) {
+            float v = acc[m];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+            acc[m] = 0.f;
+            if (lane == m && m < M) {
+              if (P) P[((size_t)split * M + m) * N + crow] = v;
+              else Y[(size_t)m * N + crow] = f2bf(v);
+            }
+          }
+          ++crow;
+        }
+      }
+      w[r] = ld_w16<NT>(lp);
+      if (issued + 1 < total) {
+        lp += 512;
+        if (++lc == KC) { lc = 0; lp += row_skip; }
+      }
+      ++issued;
+    }
+  }
+}
+
+// M <= 4 GEMV / SwiGLU-down through gemv_rows_kernel: `rw` weight rows per wave, K split `split` ways
+// (`swiglu` = flags, below)
+// (K % (512 * split) == 0); P (split > 1) receives fp32 partials (Y == nullptr: left for a fused
+// consumer, else reduced into Y).  Returns hipErrorInvalidValue for shapes it does not take.
+extern "C" int ka_gemv_rows(void* Y, const void* X, const void* W, void* workspace, int M, int N, int K, int split,
+                            int rw, int swiglu, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > 4 || split < 1 || rw < 1 || K % (512 * split) != 0) return (int)hipErrorInvalidValue;
+  const int kps = K / split;
+  const int mr = M == 1 ? 1 : M == 2 ? 2 : 4;
+  const size_t lds = (size_t)mr * kps * 2;
+  if (lds > 65536) return (int)hipErrorInvalidValue;
+  auto* x = static_cast<const bf16_t*>(X);
+  auto* w = static_cast<const bf16_t*>(W);
+  auto* y = static_cast<bf16_t*>(Y);
+  float* p = split > 1 ? static_cast<float*>(workspace) : nullptr;
+  dim3 grid((N + 4 * rw - 1) / (4 * rw), split);
+  // flags bit 0: SwiGLU X staging; bit 1: 16-deep ring (measurement only); bit 2: non-temporal
+  // weight loads (the engine's setting: profiles/r3/gemv_rows)
+  const int var = swiglu >> 1;
+  const bool sw = swiglu & 1;
+#define KA_ROWS_LAUNCH(MRV, SW, RG, NTV) \
+  hipLaunchKernelGGL((gemv_rows_kernel<MRV, RG, SW, NTV>), grid, dim3(256), lds, stream, x, w, y, p, M, N, K, kps, rw)
+#define KA_ROWS_MR(SW, RG, NTV) \
+  do { if (mr == 1) KA_ROWS_LAUNCH(1, SW, RG, NTV); else if (mr == 2) KA_ROWS_LAUNCH(2, SW, RG, NTV); \
+       else KA_ROWS_LAUNCH(4, SW, RG, NTV); } while (0)
+#define KA_ROWS_VAR(SW) \
+  do { if (var == 0) KA_ROWS_MR(SW, 8, false); else if (var == 1) KA_ROWS_MR(SW, 16, false); \
+       else if (var == 2) KA_ROWS_MR(SW, 8, true); else KA_ROWS_MR(SW, 16, true); } while (0)
+  if (sw) KA_ROWS_VAR(true);
+  else KA_ROWS_VAR(false);
+#undef KA_ROWS_VAR
+#undef KA_ROWS_MR
+#undef KA_ROWS_LAUNCH
+  if (split > 1 && y != nullptr) ka_splitk_reduce_launch(y, p, split, (long)M * N, stream);
+  KA_CHECK_LAUNCH();
+}
+
 template <int MT>
 static void launch_mt(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int split, int kps,
                       hipStream_t stream) {

@@ -360,6 +360,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
             return torch.nn.functional.linear(x, w)
         elif plan[0] == "gm":
             return linear_gm(x, w, plan[2], plan[1], defer_reduce, bf16_partials)
+        elif plan[0] == "rows":
+            return linear_rows(x, w, plan[1], plan[2], defer_reduce)
         else:
             split = plan[1]
     if M > SKINNY_MAX_M:
@@ -440,6 +442,40 @@ def decode_swiglu_cfg(x: torch.Tensor, w13: torch.Tensor) -> int:
     return cfg if cfg and decode_swiglu_ok(x, w13) else 0
 
 
+# Row-streaming GEMV (csrc/gemm_skinny.hip gemv_rows_kernel) for M <= 4: each wave streams a
+# contiguous block of weight rows 1 KB per load, non-temporal (profiles/r3/gemv_rows: Llama-3-8B
+# batch 1 gate_up 46.8 -> 38.6 us, down with SwiGLU staging 24.1 -> 21.8, QKV 13.3 -> 12.1, LM head
+# 201 -> 164).  Planned per shape by ops.autotune ("rows", split, rows per wave).
+ROWS_MAX_M = 4
+ROWS_NT = 4                     # ka_gemv_rows flag: non-temporal weight loads
+ROWS_SWIGLU = os.environ.get("KA_GEMV_ROWS_SWIGLU", "1") == "1"
+ROWS_SWIGLU_SPLIT, ROWS_SWIGLU_RW = 4, 4
+
+
+def rows_ok(M: int, K: int, split: int) -> bool:
+    mr = 1 if M == 1 else 2 if M == 2 else 4
+    return M <= ROWS_MAX_M and split >= 1 and K % (512 * split) == 0 and mr * (K // split) * 2 <= 65536
+
+
+def linear_rows(x: torch.Tensor, w: torch.Tensor, split: int, rw: int, defer_reduce: bool = False):
+    """y = x @ w.T for M <= 4 through the row-streaming GEMV (`rw` weight rows per wave, K split
+    `split` ways); split > 1 with defer_reduce returns the fp32 partials as a `SplitK`."""
+    M, K = x.shape
+    N = w.shape[0]
+    if _ref(x):
+        return ref.linear(x, w)
+    if not rows_ok(M, K, split) or not x.is_contiguous():
+        raise ValueError(f"gemv_rows needs M <= 4, K % (512*split) == 0: M={M} K={K} split={split}")
+    lib = require()
+    ws = torch.empty((split, M, N), dtype=torch.float32, device=x.device) if split > 1 else None
+    if defer_reduce and split > 1:
+        check(lib.ka_gemv_rows(None, _p(x), _p(w), _p(ws), M, N, K, split, rw, ROWS_NT, _stream()), "gemv_rows")
+        return SplitK(ws, split)
+    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    check(lib.ka_gemv_rows(_p(y), _p(x), _p(w), _p(ws), M, N, K, split, rw, ROWS_NT, _stream()), "gemv_rows")
+    return y
+
+
 GEMV_SWIGLU_MAX_M = 4   # csrc/gemm_skinny.hip GEMV_MAX_M
 
 
@@ -458,6 +494,18 @@ def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, bf16_partials
     M, I2 = gu.shape
     I = I2 // 2
     N = w.shape[0]
+    if ROWS_SWIGLU and rows_ok(M, I, ROWS_SWIGLU_SPLIT):
+        lib = require()
+        sp = ROWS_SWIGLU_SPLIT
+        ws = torch.empty((sp, M, N), dtype=torch.float32, device=gu.device)
+        if defer_reduce:
+            check(lib.ka_gemv_rows(None, _p(gu), _p(w), _p(ws), M, N, I, sp, ROWS_SWIGLU_RW, ROWS_NT | 1, _stream()),
+                  "gemv_rows_swiglu")
+            return SplitK(ws, sp)
+        y = torch.empty((M, N), dtype=gu.dtype, device=gu.device)
+        check(lib.ka_gemv_rows(_p(y), _p(gu), _p(w), _p(ws), M, N, I, sp, ROWS_SWIGLU_RW, ROWS_NT | 1, _stream()),
+              "gemv_rows_swiglu")
+        return y
     if M <= GEMV_SWIGLU_MAX_M and I % 64 == 0 and N % 4 == 0:
         lib = require()
         split = skinny_split(M, N, I, 256)

@@ -46,6 +46,7 @@ _SIGS = {
     "ka_kv_block_copy": [P, P, P, P, I, I, ctypes.c_long, ctypes.c_long, P],
     "ka_prefetch": [P, ctypes.c_long, I, P, P],
     "ka_gemm_mfma": [P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "ka_gemv_rows": [P, P, P, P, I, I, I, I, I, I, P],
     "ka_gemm_mfma_swiglu": [P, P, P, I, I, I, I, I, I, P],
     "ka_gemm_mfma_grouped": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
     "ka_gemm_big": [P, P, P, P, I, I, I, I, I, I, I, P],

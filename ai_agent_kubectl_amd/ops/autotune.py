@@ -13,7 +13,8 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from . import GEMM_PLAN, SKINNY_MAX_M, TILE_MAX_M, gm_shape, linear, linear_gm, rmsnorm, skinny_split
+from . import (GEMM_PLAN, SKINNY_MAX_M, TILE_MAX_M, gm_shape, linear, linear_gm, linear_rows, rmsnorm, rows_ok,
+               skinny_split)
 
 logger = logging.getLogger("app.engine")
 
@@ -209,6 +210,13 @@ def _tune(groups, Ms, norm_fed=frozenset(), bf16_partials: bool = True, consumer
                     t = _time(lambda w: norm(linear(x, w, split=sp, defer_reduce=fed)), ws)
                     if t < best[3]:
                         best = ("skinny", sp, 0, t)
+            for sp in (1, 2, 4):   # row-streaming GEMV (M <= 4): split x rows per wave
+                if not rows_ok(M, K, sp):
+                    continue
+                for rw in (1, 2, 4, 8):
+                    t = _time(lambda w: norm(linear_rows(x, w, sp, rw, defer_reduce=fed)), ws)
+                    if t < best[3]:
+                        best = ("rows", sp, rw, t)
             for cfg, sp in gm_candidates(M, N, K):
                 t = _time(lambda w: norm(linear_gm(x, w, cfg, sp, defer_reduce=fed, bf16_partials=bf16)), ws)
                 if t < best[3]:

@@ -32,8 +32,10 @@ threading.Thread(target=_heartbeat, daemon=True).start()
 COPY_TO = os.environ.get("PLAN_COPY_TO")   # e.g. gpurun_out/tuned: a copy after every model
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512)
+if os.environ.get("PLAN_BUCKETS"):   # re-tune (and re-write) only these buckets, e.g. "1,2,4"
+    BUCKETS = tuple(int(b) for b in os.environ["PLAN_BUCKETS"].split(","))
 for model in sys.argv[1:] or ["llama3-8b"]:
-    eng = build_engine(EngineOptions(model=model, device="cuda", max_batch=512, graph_buckets=BUCKETS,
+    eng = build_engine(EngineOptions(model=model, device="cuda", max_batch=max(BUCKETS), graph_buckets=BUCKETS,
                                      kv_cache_tokens=65536, max_model_len=512))
     rep = eng.runner.autotune()
     print(model, len(rep), "plan entries", flush=True)

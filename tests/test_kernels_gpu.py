@@ -322,6 +322,35 @@ def test_prefill_swiglu_used_by_model_path():
     assert not ops.use_prefill_swiglu(x[:256], w13)
 
 
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,K,split,rw", [(6144, 4096, 2, 8), (4100, 4096, 1, 4), (28672, 4096, 1, 4),
+                                          (1000, 14336, 4, 2), (300, 2048, 4, 1)])
+def test_gemv_rows_vs_fp32(M, N, K, split, rw):
+    """Row-streaming GEMV (csrc/gemm_skinny.hip gemv_rows_kernel): bf16 output and deferred fp32
+    partials against fp32 x @ w^T, ragged N (rows past N in the last wave)."""
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(BF)
+    want = x.float() @ w.float().t()
+    close(ops.linear_rows(x, w, split, rw), want, atol=2e-2, rtol=2e-2)
+    if split > 1:
+        p = ops.linear_rows(x, w, split, rw, defer_reduce=True)
+        assert isinstance(p, ops.SplitK)
+        close(p.P.sum(0), want, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 4])
+def test_gemv_rows_swiglu_down_vs_fp32(M):
+    """Batch-1..4 down projection with SiLU·mul in the row-streaming GEMV's X staging."""
+    I, N = 14336, 4096
+    gu = torch.randn(M, 2 * I, device=DEV, dtype=BF)
+    w = (torch.randn(N, I, device=DEV) / math.sqrt(I)).to(BF)
+    act = torch.nn.functional.silu(gu[:, :I].float()) * gu[:, I:].float()
+    want = act @ w.float().t()
+    close(ops.swiglu_linear(gu, w), want, atol=3e-2, rtol=3e-2)
+    p = ops.swiglu_linear(gu, w, defer_reduce=True)
+    close(p.P.sum(0) if isinstance(p, ops.SplitK) else p.float(), want, atol=3e-2, rtol=3e-2)
+
+
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5, 12])
 @pytest.mark.parametrize("M,I", [(32, 14336), (100, 1792), (256, 14336), (300, 1792), (512, 1792)])
 def test_decode_swiglu_gemm_vs_fp32(M, I, cfg):
@@ -610,9 +639,11 @@ def test_gemv_swiglu_fused_is_exact(M, N, I):
     then the same GEMV at the same split (bitwise), and close to the fp32 reference."""
     gu = torch.randn(M, 2 * I, device=DEV, dtype=BF)
     w = (torch.randn(N, I, device=DEV) * 0.02).to(BF)
-    split = ops.skinny_split(M, N, I, 256)
     got = ops.swiglu_linear(gu, w)
-    want = ops.linear(ops.silu_mul(gu), w, split=split)
+    if ops.ROWS_SWIGLU and ops.rows_ok(M, I, ops.ROWS_SWIGLU_SPLIT):   # row-streaming GEMV
+        want = ops.linear_rows(ops.silu_mul(gu), w, ops.ROWS_SWIGLU_SPLIT, ops.ROWS_SWIGLU_RW)
+    else:
+        want = ops.linear(ops.silu_mul(gu), w, split=ops.skinny_split(M, N, I, 256))
     assert torch.equal(got, want)
     parts = ops.swiglu_linear(gu, w, defer_reduce=True)
     if isinstance(parts, ops.SplitK):

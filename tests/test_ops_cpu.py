@@ -31,6 +31,16 @@ def test_linear_gm_swiglu_cpu_is_reference():
     assert not ops.decode_swiglu_ok(x, torch.zeros(2 * 56, 256, dtype=torch.bfloat16))   # I % 16
 
 
+def test_gemv_rows_rules_and_cpu_reference():
+    assert ops.rows_ok(1, 4096, 1) and ops.rows_ok(4, 14336, 4) and ops.rows_ok(1, 14336, 1)
+    assert not ops.rows_ok(5, 4096, 1)            # M > 4: tiled kernels
+    assert not ops.rows_ok(4, 14336, 1)           # X slice over the 64 KB LDS budget
+    assert not ops.rows_ok(1, 4096, 3)            # K % (512 * split)
+    x = torch.randn(2, 1024, dtype=torch.bfloat16)
+    w = (torch.randn(96, 1024) / 32).to(torch.bfloat16)
+    torch.testing.assert_close(ops.linear_rows(x, w, 2, 4).float(), ref.linear(x, w).float())
+
+
 def test_swiglu_gemm_shape_rules():
     x = torch.zeros(2048, 4096, dtype=torch.bfloat16)
     assert ops.swiglu_gemm_ok(x, torch.zeros(2 * 14336, 4096, dtype=torch.bfloat16))
