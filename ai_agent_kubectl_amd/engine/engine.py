@@ -14,9 +14,10 @@ reference's degraded-mode status, `/root/reference/app.py:179-180`) instead of h
 * recoverable (a host-side error, a transient allocation failure): the engine drops its transient
   state (KV block tables were freed with the requests, the prefix cache is reset), checks that the
   device still answers, and serves again — at most `max_recoveries` times per minute;
-* fatal (a one-shot TP collective timed out, a HIP fault, a TP group, or too many recoveries): the
-  engine stays unhealthy (`/ready` 503) and, with `exit_on_fatal` (serve.py / DP replicas), the
-  process exits non-zero so its supervisor restarts it — the reference relies on the same
+* fatal (a one-shot TP collective timed out, a HIP fault, a TP group, too many recoveries, or the
+  TP watchdog's verdict: a lost worker rank / a stalled step, `mark_unhealthy`): the engine stays
+  unhealthy (`/ready` 503, new requests rejected) and, with `exit_on_fatal` (serve.py / DP
+  replicas), the process exits non-zero so its supervisor restarts it — the reference relies on the same
   process-level restart (`/root/reference/docker-compose.yml:14`, `restart: unless-stopped`).
 Fault injection: KA_FAULT_STEP=<n>[:fatal|:exit] raises in step n (tests, `FAULT_*` of §5.3).
 """
@@ -105,9 +106,29 @@ class LLMEngine:
         self.fault_kind = kind or "error"
 
     def mark_unhealthy(self, reason: str) -> None:
-        """Watchdog verdict (worker heartbeat lost / step stalled): new requests get 503."""
+        """Watchdog verdict (worker heartbeat lost / step stalled): new requests get 503.
+
+        A lost TP worker or a stalled step is fatal: rank 0 is typically blocked inside a collective
+        that only the process-group timeout (minutes) would end.  With `exit_on_fatal` (serve.py, DP
+        replicas) the in-flight requests are failed (503) and the process exits with EXIT_FATAL
+        right away, so its supervisor respawns the whole TP group; the clients of a DP replica also
+        see its sockets close and fail whatever was routed to it."""
         self.healthy = False
         self.last_error = RuntimeError(reason)
+        if not self.exit_on_fatal:
+            return
+        logger.critical("fatal engine fault (%s): exiting (status %d) for the supervisor to restart the engine",
+                        reason, EXIT_FATAL)
+        try:
+            # the engine thread may be blocked mid-step: fail what is tracked and push the replies out
+            # best-effort (this process ends next either way)
+            self._fail_all(self.last_error)
+            for hook in self.step_end_hooks:
+                hook()
+        except Exception:  # pragma: no cover - racing the blocked engine thread
+            logger.exception("failing in-flight requests before the fatal exit")
+        finally:
+            self._exit(EXIT_FATAL)
 
     # ------------------------------------------------------------------------------------------
     def start(self) -> None:

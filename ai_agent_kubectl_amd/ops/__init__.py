@@ -327,8 +327,10 @@ def skinny_split(M: int, N: int, K: int, target_wgs: int = 0) -> int:
     return split
 
 
-# (M, N, K) -> ("skinny", split) | ("gm", split, cfg) | ("blas", 0); filled by ops.autotune at
-# engine start for the decode batch buckets.
+# (M, N, K) -> ("skinny", split) | ("gm", split, cfg) | ("rows", split, rows per wave) | ("blas", 0);
+# filled by ops.autotune at engine start for the decode batch buckets.  PLAN_CHOICES is the set
+# `linear` dispatches on (tests and the autotuner check plans against it).
+PLAN_CHOICES = ("skinny", "gm", "rows", "blas")
 GEMM_PLAN: dict = {}
 TILE_MAX_M = 512      # largest M the autotuner plans for (decode buckets and small mixed steps)
 

@@ -317,6 +317,7 @@ def _replica_main(spec: ReplicaSpec, settings_dict: dict, authkey: bytes, parent
     eng.step_end_hooks.append(flush)
 
     live: Dict[tuple, object] = {}
+    told_healthy: Dict[int, bool] = {}     # connection id -> the health last pushed to that client
     while True:
         with conns_lock:
             items = list(conns.items())
@@ -324,6 +325,13 @@ def _replica_main(spec: ReplicaSpec, settings_dict: dict, authkey: bytes, parent
             new_conn.wait(0.5)
             new_conn.clear()
             continue
+        # engine health changes (watchdog verdict, recoveries exhausted without exit_on_fatal) are
+        # pushed to every client, which then routes around this replica while it is unhealthy
+        healthy = bool(eng.healthy)
+        for k, _ in items:
+            if told_healthy.get(k, True) != healthy:
+                told_healthy[k] = healthy
+                send(k, ("health", spec.idx, healthy))
         ready = _wait([c for _, c in items], timeout=0.2)
         by_conn = {id(c): k for k, c in items}
         for c in ready:
@@ -336,6 +344,7 @@ def _replica_main(spec: ReplicaSpec, settings_dict: dict, authkey: bytes, parent
                 with conns_lock:
                     conns.pop(k, None)
                     send_locks.pop(k, None)
+                told_healthy.pop(k, None)
                 for key in [key for key in live if key[0] == k]:
                     eng.abort(live.pop(key))
                 continue
@@ -343,6 +352,11 @@ def _replica_main(spec: ReplicaSpec, settings_dict: dict, authkey: bytes, parent
             for op, rid, payload in msgs:
                 key = (k, rid)
                 if op == "gen":
+                    if not eng.healthy:   # an unhealthy engine takes no work: the client answers 503
+                        send(k, ("done_batch", spec.idx,
+                                 ([(rid, ([], repr(RuntimeError(f"engine unhealthy: {eng.last_error}")), "error"))],
+                                  None)))
+                        continue
                     seq = eng.submit(payload, params, lambda sq, key=key: done(sq, key), forced_prefix=forced)
                     live[key] = seq
                 elif op == "abort":
@@ -472,6 +486,7 @@ class _Replica:
     conn: object = None
     inflight: int = 0
     up: bool = False
+    healthy: bool = True                  # the replica's engine health, pushed by the replica
     failed: Optional[str] = None          # startup failure reported by the replica (.dead file)
     outbox: list = dataclasses.field(default_factory=list)
     flush_scheduled: bool = False
@@ -619,6 +634,7 @@ class DPRouterLLM(LLMBackend):
                 self.reconnects += 1
                 logger.warning("DP replica %d is back", r.idx)
             r.up = True
+            r.healthy = True   # a (re)started replica reports a change of health itself
             r.cpus = list(b or [])
             if len(self.replicas) == 1 and r.cpus and self.owner:
                 # one replica (a bench rank, or DP=1 serving): the API process joins its engine on
@@ -645,6 +661,10 @@ class DPRouterLLM(LLMBackend):
                 ent = self._pending.pop(a, None)
             if ent is not None:
                 ent[0].call_soon_threadsafe(_set, ent[1], b)
+        elif kind == "health":
+            if r.healthy != bool(b):
+                logger.error("DP replica %d reports its engine %s", r.idx, "healthy" if b else "UNHEALTHY")
+            r.healthy = bool(b)
 
     def attach_metrics(self, metrics) -> None:
         self._metrics = metrics
@@ -681,13 +701,14 @@ class DPRouterLLM(LLMBackend):
         return min(live, key=lambda r: r.inflight)
 
     def _fail_replica(self, r) -> None:
+        """Fail every pending request and control op routed to `r` (503)."""
         with self._lock:
             dead = [(k, v) for k, v in self._pending.items() if v[2] is r]
             for k, _ in dead:
                 self._pending.pop(k)
             r.inflight = 0
             self._publish_load(r)
-        for _, (loop, fut, _) in dead:
+        for _, (loop, fut, *_rest) in dead:
             loop.call_soon_threadsafe(_set_exc, fut, LLMUnavailableError(f"replica {r.idx} died"))
 
     def wait_ready(self, timeout: Optional[float] = None) -> bool:
@@ -713,7 +734,7 @@ class DPRouterLLM(LLMBackend):
             await loop.run_in_executor(None, self.supervisor.stop)
 
     def healthy(self) -> bool:
-        return any(r.up for r in self.replicas)
+        return any(r.up and r.healthy for r in self.replicas)
 
     def stats(self):
         return {f"replica{r.idx}_inflight": r.inflight for r in self.replicas}
@@ -752,8 +773,15 @@ class DPRouterLLM(LLMBackend):
             rid = next(self._ids)
             fut = loop.create_future()
             with self._lock:
-                self._pending[rid] = (loop, fut, _Dummy())
-            r.put((op, rid, None))
+                # registered with the real replica, so its death fails the op (_fail_replica); the
+                # "ctl" reply pops it without touching the request in-flight counts
+                self._pending[rid] = (loop, fut, r, "ctl")
+            try:
+                r.put((op, rid, None))
+            except (OSError, ValueError) as e:
+                with self._lock:
+                    self._pending.pop(rid, None)
+                fut.set_exception(LLMUnavailableError(f"replica {r.idx} unreachable: {e}"))
             futs.append(fut)
         return list(await asyncio.gather(*futs))
 
@@ -765,7 +793,7 @@ class DPRouterLLM(LLMBackend):
     async def generate(self, query: str) -> str:
         if not self._ready.is_set():
             await self.start()
-        live = [r for r in self.replicas if r.up]
+        live = [r for r in self.replicas if r.up and r.healthy]
         if not live:
             raise LLMUnavailableError("no live DP replica")
         rep = self._pick(live)
@@ -792,10 +820,6 @@ class DPRouterLLM(LLMBackend):
         if err is not None:
             raise LLMUnavailableError(err) if reason == "error" else RuntimeError(err)
         return self.tok.decode([t for t in out_ids if not self.tok.is_eos(t)])
-
-
-class _Dummy:
-    inflight = 0
 
 
 def _set_many(lst):

@@ -31,6 +31,8 @@ import time
 
 log = logging.getLogger("app")
 
+MAX_WORKERS = 64   # rows of the shared load table (runtime/shared_state.h kMaxWorkers)
+
 
 def bind_reuseport(host: str, port: int) -> socket.socket:
     """The worker's listening socket.  Created with proto=IPPROTO_TCP, as getaddrinfo's sockets are:
@@ -87,9 +89,11 @@ def run_workers(settings, host: str, port: int) -> int:
     from .dp import ReplicaSupervisor
 
     W = max(1, int(settings.WORKERS))
+    if W > MAX_WORKERS:   # the shared load table has one row per worker (runtime/shared_state.h)
+        raise ValueError(f"WORKERS={W} exceeds the shared state's {MAX_WORKERS} worker rows")
     name = settings.SHARED_STATE or "/ka_state_%d" % os.getpid()
     SharedStore.unlink(name)   # this supervisor owns the segment: never inherit an earlier run's cache
-    store = SharedStore(name, settings.CACHE_MAXSIZE)   # created before any worker attaches
+    store = SharedStore(name, settings.CACHE_MAXSIZE, recreate=True)   # created before any worker attaches
     metrics_dir = tempfile.mkdtemp(prefix="ka_prom_")
     sd = dataclasses.asdict(settings)
     sd["SHARED_STATE"] = store.name
@@ -109,6 +113,7 @@ def run_workers(settings, host: str, port: int) -> int:
 
     workers = [spawn_worker(i) for i in range(W)]
     restarts = [0] * W
+    gone = set()   # workers that stay down (restart cap reached / stopping)
     log.info("Started %d API workers on %s:%d (shared state %s)", W, host, port, store.name)
 
     stop = {"flag": False}
@@ -122,10 +127,16 @@ def run_workers(settings, host: str, port: int) -> int:
     try:
         while not stop["flag"]:
             for i, p in enumerate(workers):
-                if not p.is_alive() and not stop["flag"] and restarts[i] < 5:
+                if p.is_alive() or i in gone:
+                    continue
+                # a dead worker's in-flight counts must not skew everyone else's routing
+                store.load_clear_worker(i)
+                if not stop["flag"] and restarts[i] < 5:
                     log.error("API worker %d exited (status %s): respawning", i, p.exitcode)
                     restarts[i] += 1
                     workers[i] = spawn_worker(i)
+                else:
+                    gone.add(i)
             if all(not p.is_alive() for p in workers):
                 rc = 1
                 break

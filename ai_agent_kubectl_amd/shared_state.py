@@ -158,7 +158,10 @@ class SharedFixedWindowLimiter(FixedWindowLimiter):
 
 
 def open_from_settings(settings) -> Optional[SharedStore]:
+    """Attach to the segment the supervisor created (serve.py / parallel/workers.run_workers owns it
+    and replaces stale layouts itself).  An attaching worker never recreates it: a layout mismatch
+    fails loudly instead of silently unlinking the live segment and serving from a private one."""
     name = getattr(settings, "SHARED_STATE", "") or ""
     if not name:
         return None
-    return SharedStore(name, settings.CACHE_MAXSIZE)
+    return SharedStore(name, settings.CACHE_MAXSIZE, recreate=False)

@@ -123,3 +123,26 @@ def test_repeated_faults_become_fatal(tiny):
     finally:
         eng.max_recoveries, eng._recovery_times = saved
         eng.healthy = True
+
+
+def test_watchdog_verdict_with_exit_on_fatal_fails_inflight_and_exits():
+    """engine.mark_unhealthy (the TP watchdog's callback) with exit_on_fatal: in-flight requests are
+    failed with the verdict and the process exits with EXIT_FATAL (no minutes-long collective wait)."""
+    from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine
+    from ai_agent_kubectl_amd.engine.sequence import SamplingParams
+    eng = build_engine(EngineOptions(model="tiny-llama", device="cpu", max_batch=4, graph_buckets=(1, 2, 4),
+                                     kv_cache_tokens=4096, max_model_len=256))
+    exits, done, flushed = [], [], []
+    eng._exit = exits.append
+    eng.exit_on_fatal = True
+    eng.step_end_hooks.append(lambda: flushed.append(1))
+    seq = eng.submit([5, 6, 7], SamplingParams(max_new_tokens=4), done.append)
+    eng._drain_inbox()                       # admitted, not yet stepped (the engine thread is "blocked")
+    eng.mark_unhealthy("TP/EP worker rank 1 heartbeat lost")
+    assert exits == [EXIT_FATAL] and not eng.healthy
+    assert done == [seq] and seq.finish_reason == "error" and "heartbeat lost" in str(seq.error)
+    assert flushed
+    eng2_exits = []
+    eng.exit_on_fatal, eng._exit = False, eng2_exits.append
+    eng.mark_unhealthy("again")              # without exit_on_fatal: only unhealthy
+    assert eng2_exits == []

@@ -489,12 +489,12 @@ def test_gemm_mfma_bf16_partials_into_rmsnorm(cfg):
 
 
 def test_gemm_autotune_plan_dispatch():
-    """tune_linear fills GEMM_PLAN for every bucket (skinny / gm / blas) and ops.linear follows it."""
+    """tune_linear fills GEMM_PLAN for every bucket (one of ops.PLAN_CHOICES) and ops.linear follows it."""
     from ai_agent_kubectl_amd.ops.autotune import tune_linear
     ws = [(torch.randn(6144, 4096, device=DEV) * 0.02).to(BF) for _ in range(3)]
     rep = tune_linear({(6144, 4096): ws}, [1, 64, 256, 320])
     assert set(k[0] for k in rep) == {1, 64, 256, 320}
-    assert all(v["choice"] in ("skinny", "gm", "blas") for v in rep.values())
+    assert all(v["choice"] in ops.PLAN_CHOICES for v in rep.values())
     for M in (1, 64, 256, 320):
         x = torch.randn(M, 4096, device=DEV, dtype=BF)
         close(ops.linear(x, ws[0]), x.float() @ ws[0].float().t(), atol=3e-2, rtol=2e-2)
