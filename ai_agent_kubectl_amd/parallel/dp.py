@@ -168,6 +168,9 @@ def _tp_env(spec: ReplicaSpec, rank: int) -> None:
     local = dev.split(":")[1] if dev.startswith("cuda") and ":" in dev else "0"
     os.environ.update(RANK=str(rank), LOCAL_RANK=local, WORLD_SIZE=str(spec.tp), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(spec.master_port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    # the group's rank 0 hosts its own store on MASTER_PORT: a torchrun agent store inherited from a
+    # launcher (TORCHELASTIC_USE_AGENT_STORE) would make it wait for a server that never comes
+    os.environ.pop("TORCHELASTIC_USE_AGENT_STORE", None)
 
 
 def _tp_worker_main(spec: ReplicaSpec, rank: int, settings_dict: dict, parent: int) -> None:

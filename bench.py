@@ -29,6 +29,8 @@ arrivals at `--rate` req/s per GPU (latency under an arrival rate instead of a f
   python bench.py --gpus 8                          # spawns 8 ranks itself (torch.distributed.run)
   torchrun --nproc-per-node 8 bench.py --gpus 8     # driver form for N > 1
   python bench.py --transport asgi                  # in-process transport only
+  python bench.py --gpus 8 --tp 8 --model llama3-70b --concurrency 8   # config #3: one TP=8 replica
+  python bench.py --gpus 8 --tp 8 --model mixtral-8x7b                 # config #4: EP=8 (experts over TP)
 """
 import argparse
 import asyncio
@@ -49,6 +51,8 @@ METRIC = "requests/sec + p50 e2e latency, /kubectl-command Llama-3-8B 1/2/4/8 GP
 # reference app.py, cache-miss /kubectl-command at concurrency 32 = 354 req/s
 # (plumbing floor with an instant stub LLM over TCP; the reference publishes no OpenAI-backed number).
 BASELINE_RPS = 354.0
+MODEL_NAMES = {"llama3-8b": "Llama-3-8B-Instruct", "llama3-70b": "Llama-3-70B-Instruct",
+               "mixtral-8x7b": "Mixtral-8x7B-Instruct"}
 
 VERBS = ["list", "show", "get", "display", "find"]
 RES = ["pods", "services", "deployments", "nodes", "configmaps", "secrets", "jobs", "ingresses", "events",
@@ -124,7 +128,28 @@ def parse_args(argv=None):
                     help="closed loop: client start times spread uniformly over this many seconds")
     ap.add_argument("--variable-len", action="store_true",
                     help="EOS-terminated replies (IGNORE_EOS=0) instead of exactly --max-new-tokens")
-    return ap.parse_args(argv)
+    ap.add_argument("--tp", type=int, default=int(os.environ.get("BENCH_TP", 1)),
+                    help="tensor-parallel degree of each engine replica (BASELINE configs #3 / #4: "
+                         "--model llama3-70b --tp 8, --model mixtral-8x7b --tp 8 = EP 8); the server runs "
+                         "DP = gpus / tp replicas, each a TP group of consecutive GPUs (tcp transport)")
+    args = ap.parse_args(argv)
+    if args.tp < 1 or args.gpus % args.tp:
+        ap.error(f"--tp {args.tp} must divide --gpus {args.gpus}")
+    if args.tp > 1 and args.transport != "tcp":
+        # a TP group spans several ranks' GPUs: only the one-server tcp topology (serve.py with
+        # DP x TP) places it; the per-rank in-process asgi transport has one GPU per rank
+        args.transport = "tcp"
+    return args
+
+
+def parallelism(args, world: int) -> str:
+    """config.parallelism: dp{N} (one replica per GPU), dp{d}tp{t} for tensor-parallel replicas, or
+    dp{d}ep{t} for a MoE model (experts sharded over the tensor-parallel group: EP = TP)."""
+    if args.tp == 1:
+        return f"dp{world}"
+    from ai_agent_kubectl_amd.models.config import get_config
+    kind = "ep" if get_config(args.model).is_moe else "tp"
+    return f"dp{world // args.tp}{kind}{args.tp}"
 
 
 # ---------------------------------------------------------------------------------------------
@@ -278,20 +303,28 @@ def bench_devices(world):
 
 
 def service_env(args, C, buckets, world, port, kubectl_dir):
-    """serve.py's environment: DP = world replicas (one per GPU), api_workers x world API workers."""
-    env = dict(os.environ, LLM_BACKEND="engine", MODEL=args.model, DP=str(world),
+    """serve.py's environment: DP = world / tp replicas (each a TP group of tp consecutive GPUs, one
+    process per GPU), api_workers x world API workers.  A replica serves the C clients of each of its
+    tp GPUs' ranks: batch up to C x tp."""
+    tp = args.tp
+    rb = max(C, 1) * tp
+    env = dict(os.environ, LLM_BACKEND="engine", MODEL=args.model, DP=str(world // tp), TP=str(tp),
         ENGINE_DEVICES=",".join(bench_devices(world)), WORKERS=str(args.api_workers * world), HOST="127.0.0.1",
         PORT=str(port),
         RATE_LIMIT="100000000/minute", CACHE_MAXSIZE=str(cache_size(args)), LLM_TIMEOUT="600", LOG_LEVEL="WARNING",
-        MAX_BATCH=str(max(C, 1)), MAX_NEW_TOKENS=str(args.max_new_tokens), IGNORE_EOS="0" if args.variable_len else "1",
+        MAX_BATCH=str(rb), MAX_NEW_TOKENS=str(args.max_new_tokens), IGNORE_EOS="0" if args.variable_len else "1",
         MAX_NUM_BATCHED_TOKENS=str(args.max_batched_tokens), HIPGRAPH_BUCKETS=",".join(str(b) for b in buckets),
-        KV_CACHE_TOKENS=os.environ.get("KV_CACHE_TOKENS", str(max(65536, C * 528))),
+        KV_CACHE_TOKENS=os.environ.get("KV_CACHE_TOKENS", str(max(65536, rb * 528))),
         MAX_MODEL_LEN=os.environ.get("MAX_MODEL_LEN", "512"), PYTHONPATH=ROOT,
         PATH=kubectl_dir + os.pathsep + os.environ.get("PATH", ""))
     env.pop("API_AUTH_KEY", None)
-    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
-              "MASTER_PORT", "TORCHELASTIC_RUN_ID"):
-        env.pop(k, None)   # the server is not a rank of this job
+    for k in list(env):
+        # the server is not a rank of this job: none of torchrun's variables may leak into it (with
+        # TORCHELASTIC_USE_AGENT_STORE a TP replica's rank 0 would wait for an agent store that does
+        # not exist instead of hosting its group's rendezvous)
+        if k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                 "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT") or k.startswith("TORCHELASTIC_"):
+            env.pop(k, None)
     if args.no_graphs:
         env["HIPGRAPH_BUCKETS"] = ""
     return env
@@ -683,10 +716,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     C = args.concurrency
+    rb = max(C, 1) * args.tp   # a replica's largest batch (tp ranks' clients)
     buckets = tuple(b for b in (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512)
-                    if b <= max(C, 1))
-    if C not in buckets:
-        buckets = tuple(sorted(set(buckets) | {C}))
+                    if b <= rb)
+    if rb not in buckets and rb <= 512:
+        buckets = tuple(sorted(set(buckets) | {rb}))
 
     import torch.distributed as dist
 
@@ -756,7 +790,9 @@ def summarize(args, name, world, C, dist, r, seq_len):
               "p99_ms": pct(allv, 0.99), "build_s": round(t_build, 1), "sample_reply": reply,
               "baseline": "BASELINE.md reference plumbing floor, cache-miss conc 32 = 354 req/s (uvicorn, TCP)"}
     if transport == "tcp":
-        detail.update(topology=f"one server: DP={world} replicas, {args.api_workers * world} API workers, one port",
+        tp = f" of TP={args.tp}" if args.tp > 1 else ""
+        detail.update(topology=f"one server: DP={world // args.tp} replicas{tp}, {args.api_workers * world} API "
+                               f"workers, one port",
                       api_workers=args.api_workers * world, client_procs_per_rank=args.client_procs)
     if name == "asgi-prefix-off":
         detail["prefix_caching"] = False
@@ -785,8 +821,8 @@ def summarize(args, name, world, C, dist, r, seq_len):
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": round(value / BASELINE_RPS, 3),
         "dtype": "bf16", "data": "synthetic queries, random-init weights",
-        "config": {"model": "Llama-3-8B-Instruct" if args.model == "llama3-8b" else args.model,
-                   "global_batch": C * world, "seq_len": seq_len, "parallelism": f"dp{world}"},
+        "config": {"model": MODEL_NAMES.get(args.model, args.model),
+                   "global_batch": C * world, "seq_len": seq_len, "parallelism": parallelism(args, world)},
         "p50_ms": round(p50, 2), "detail": detail,
     }
     if args.mix:

@@ -97,3 +97,29 @@ def test_bench_open_loop_mixed_stream():
     mix = out["detail"]["mix"]
     assert out["detail"]["load"].startswith("open")
     assert sum(v["n"] for k, v in mix.items() if k != "scrape") >= 4
+
+
+def test_bench_tp_replicas_over_tcp():
+    """--gpus 2 --tp 2 (BASELINE configs #3 / #4 path): ONE server with DP = 1 replica that is a TP = 2
+    group (its rank 0 spawns the TP worker rank; gloo on the CPU), both ranks' clients talk to it over
+    TCP; `parallelism` says dp1tp2 and the value is still the whole-job aggregate."""
+    out = _run(["--tp", "2"], 2)
+    d = out["detail"]
+    assert d["transport"] == "tcp" and "DP=1 replicas of TP=2" in d["topology"]
+    assert out["config"]["parallelism"] == "dp1tp2" and out["n_gpus"] == 2
+    assert out["config"]["global_batch"] == 8
+    assert out["value"] == pytest.approx(8 / (out["ms_per_step"] / 1e3), rel=0.02)
+    assert d["decode_steps"] > 0 and d["prefill_steps"] > 0
+
+
+def test_bench_parallelism_labels():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.parallelism(bench.parse_args(["--gpus", "8", "--tp", "8", "--model", "llama3-70b"]), 8) == "dp1tp8"
+    assert bench.parallelism(bench.parse_args(["--gpus", "8", "--tp", "8", "--model", "mixtral-8x7b"]), 8) == "dp1ep8"
+    assert bench.parallelism(bench.parse_args(["--gpus", "8", "--tp", "2"]), 8) == "dp4tp2"
+    assert bench.parallelism(bench.parse_args(["--gpus", "4"]), 4) == "dp4"
+    a = bench.parse_args(["--gpus", "4", "--tp", "2", "--transport", "both"])
+    assert a.transport == "tcp"
+    with pytest.raises(SystemExit):
+        bench.parse_args(["--gpus", "4", "--tp", "3"])

@@ -108,3 +108,18 @@ def test_serve_dp2_x_tp2_two_workers(tmp_path):
         _check_service(port)
     finally:
         _stop(p, log)
+
+
+@pytest.mark.slow
+def test_serve_tp8_70b_head_geometry(tmp_path):
+    """serve.py with TP = 8 on the CPU (gloo): one replica whose rank 0 spawns 7 TP worker ranks, at
+    the Llama-3-70B head layout (64 q / 8 kv heads, one KV head per rank) with small layers."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "ai_agent_kubectl_amd.serve"]
+    env = _env(port, TP="8", DP="1", ENGINE_DEVICES="cpu")
+    env["MODEL"] = "llama3-70b-tiny"
+    p, log = _serve(cmd, env, tmp_path, port, deadline_s=600)
+    try:
+        _check_service(port)
+    finally:
+        _stop(p, log)
