@@ -80,6 +80,17 @@ struct Args {
   // slab P[ks] of [split][M][N] (fp32 / bf16), reduced by the consumer (ops.SplitK)
   int split, kp;
   void* P;
+  // split tail (EPI_BF16 / SWIGLU / ADD): units [0, full) are whole tiles (full = a multiple of the
+  // persistent grid); the tail_tiles tiles after them would leave most CUs idle in a last partial
+  // round, so each is cut into tail_s K-slices run by different workgroups of ONE XCD.  Every wave
+  // of a slice publishes its fp32 quadrant (stores, the wave's own vmcnt(0), an agent-scope release),
+  // then adds to its quadrant's arrival counter; the wave whose add returns
+  // tail_s - 1 acquires at agent scope, sums the slices and runs the epilogue — no wait on other
+  // workgroups — and resets the counter for the next launch.
+  int full, tail_s, tail_tiles, span;
+  float* slab;   // [tail tile][tail_s slices][4 waves][64 accumulators][64 lanes] f32x4
+  int* cnt;      // [tail tile][4 waves][arrivals, spare]
+  int* err;      // reserved error word (0)
 };
 
 // Every instruction of the k-loop is an asm statement, so the program order written below IS the
@@ -161,6 +172,97 @@ KA_DEV void tile_of(int L, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
   tn = in / rows;
 }
 
+// 16-B store / load of the tail hand-off.  KA_GB_TAIL_MODE 0: plain accesses ordered by agent-scope
+// release / acquire fences; 1: sc1 (write-through) asm stores + the same fences; 2: sc1 asm stores and
+// loads, no fence (MI355X_MICROARCH.md hand-off table, row 1).  hipcc does not pad the
+// VMEM-store-data / VALU-write hazard around asm it cannot see, so the asm stores carry their own
+// wait states (without them a few lanes' data were corrupted: profiles/r4/gemm_big_tail/).
+#ifndef KA_GB_TAIL_MODE
+#define KA_GB_TAIL_MODE 2   // measured fastest, and exact in every test (profiles/r4/gemm_big_tail/)
+#endif
+template <int N>
+KA_DEV void st_slab8(float* p, const f32x4 (&v)[8], const int (&q)[8]) {
+#if KA_GB_TAIL_MODE == 0
+#pragma unroll
+  for (int e = 0; e < 8; ++e) *reinterpret_cast<f32x4*>(p + q[e] * 256) = v[e];
+#else
+  asm volatile(
+      "global_store_dwordx4 %0, %8, off sc1\n\tglobal_store_dwordx4 %1, %9, off sc1\n\t"
+      "global_store_dwordx4 %2, %10, off sc1\n\tglobal_store_dwordx4 %3, %11, off sc1\n\t"
+      "global_store_dwordx4 %4, %12, off sc1\n\tglobal_store_dwordx4 %5, %13, off sc1\n\t"
+      "global_store_dwordx4 %6, %14, off sc1\n\tglobal_store_dwordx4 %7, %15, off sc1\n\ts_nop 4" ::"v"(p + q[0] * 256),
+      "v"(p + q[1] * 256), "v"(p + q[2] * 256), "v"(p + q[3] * 256), "v"(p + q[4] * 256), "v"(p + q[5] * 256),
+      "v"(p + q[6] * 256), "v"(p + q[7] * 256), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]),
+      "v"(v[6]), "v"(v[7])
+      : "memory");
+#endif
+}
+KA_DEV void ld_slab8(f32x4 (&t)[8], const float* p, const int (&q)[8]) {
+#if KA_GB_TAIL_MODE == 2
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(t[e]) : "v"(p + q[e] * 256) : "memory");
+  // the loads' registers are operands of the wait, so no use is scheduled above it
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
+               "+v"(t[7])::"memory");
+#else
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = *reinterpret_cast<const f32x4*>(p + q[e] * 256);
+#endif
+}
+
+// Tail slice hand-off of one wave's 128 x 128 quadrant (Args.full .. comment): every slice publishes
+// its fp32 quadrant to slot k of the tile's slab (the epilogue's mode 1, tail_store8), waits for its
+// own stores, then takes an arrival ticket; the slice whose ticket is the last one (all others have
+// published before arriving) runs the epilogue on the sum of the slots (mode 2, tail_fetch8) and
+// resets the counter for the next launch.  The accumulators are read at ONE place of the epilogue
+// (a second read, or summing into them, made hipcc move the whole tile into VGPRs and spill).
+KA_DEV bool tail_ticket(const Args& a, int tt, int w, int lane) {
+  // release at agent scope: this wave's slab stores are done and written back past its XCD's L2
+  // before its ticket (the slices of a tile are meant to share an XCD for speed, but placement is
+  // only observed, never promised).  The asm wait after the fence: MI355X_MICROARCH.md 'Compiler hazard'.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if KA_GB_TAIL_MODE != 2
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  int* const c = a.cnt + (tt * 4 + w) * 2;
+  int old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __builtin_amdgcn_readfirstlane(old);
+  if (old != a.tail_s - 1) return false;
+  if (lane == 0) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // tile complete
+#if KA_GB_TAIL_MODE != 2
+  // acquire at agent scope before this wave reads the other slices' slabs
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  return true;
+}
+
+KA_DEV float* tail_slot(const Args& a, int tt, int k, int w, int lane) {
+  return a.slab + ((((size_t)tt * a.tail_s + k) * 4 + w) * 64) * 256 + lane * 4;
+}
+
+// this slice's accumulators q[e] -> its slot
+KA_DEV void tail_store8(const Args& a, int tt, int k, int w, int lane, const int (&q)[8], const f32x4 (&v)[8]) {
+  st_slab8<8>(tail_slot(a, tt, k, w, lane), v, q);
+}
+
+// v[e] = sum over the tile's ts slots of accumulator q[e] of this lane (after tail_ticket's acquire)
+KA_DEV void tail_fetch8(const Args& a, int tt, int w, int lane, const int (&q)[8], f32x4 (&v)[8]) {
+  const int ts = a.tail_s;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < ts; ++k) {
+    const float* const p = tail_slot(a, tt, k, w, lane);
+    f32x4 t[8];
+    ld_slab8(t, p, q);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t[e];
+  }
+}
+
 template <int EPI>
 __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
@@ -174,18 +276,47 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   // grid of `total` workgroups would be: an id keeps its XCD (b mod 8), so the tiles running together
   // on one XCD are still neighbours.  The next tile's first two k-tiles are staged during the last
   // two k-steps of the current one, so the epilogue overlaps their landing.
-  const int total = a.tiles_m * a.tiles_n * (SPLIT ? a.split : 1);
-  auto decode = [&](int v, int& tm, int& tn, int& ks) {
-    int lg = xcd_logical(v, total);
-    ks = 0;
+  constexpr bool TAILOK = EPI == EPI_BF16 || EPI == EPI_SWIGLU || EPI == EPI_ADD;
+  const int total = SPLIT ? a.tiles_m * a.tiles_n * a.split : (TAILOK ? a.full + a.span : a.tiles_m * a.tiles_n);
+  const int nkt = a.K / BK;
+  // unit v -> tile (tm, tn), k-tiles [kt0, kt0 + nk), tail tile index tt (-1: a whole tile / split-K slice);
+  // false for the holes of the last tail group (tail_tiles not a multiple of 8)
+  auto decode = [&](int v, int& tm, int& tn, int& kt0, int& nk, int& tt, int& tk) -> bool {
+    tt = -1;
+    tk = 0;
     if constexpr (SPLIT) {   // the split slices of a tile on one XCD
-      ks = lg % a.split;
+      int lg = xcd_logical(v, total);
+      const int ks = lg % a.split;
       lg /= a.split;
+      tile_of(lg, a.tiles_m, a.tiles_n, a.gm, tm, tn);
+      kt0 = ks * (a.kp / BK);
+      nk = a.kp / BK;
+      return true;
     }
-    tile_of(lg, a.tiles_m, a.tiles_n, a.gm, tm, tn);
+    if (!TAILOK || v < a.full) {
+      tile_of(xcd_logical(v, TAILOK ? a.full : total), a.tiles_m, a.tiles_n, a.gm, tm, tn);
+      kt0 = 0;
+      nk = nkt;
+      return true;
+    }
+    // tail: groups of 8 tiles x tail_s slices; slice k of tile 8 g + l is unit 8 (g tail_s + k) + l, so
+    // a tile's slices share v mod 8, i.e. one XCD (their slab hand-off stays in its L2)
+    const int u = v - a.full, ts = a.tail_s;
+    const int g = u / (8 * ts), r = u - g * 8 * ts, k = r >> 3;
+    tt = g * 8 + (r & 7);
+    tk = k;
+    if (tt >= a.tail_tiles) return false;
+    tile_of(a.full + tt, a.tiles_m, a.tiles_n, a.gm, tm, tn);
+    const int trips = nkt >> 1;   // the k-loop runs two k-tiles per trip
+    const int t0 = k * trips / ts, t1 = (k + 1) * trips / ts;
+    kt0 = 2 * t0;
+    nk = 2 * (t1 - t0);
+    return true;
   };
-  int vb = blockIdx.x, tm, tn, ks;
-  decode(vb, tm, tn, ks);
+  const int G = (int)gridDim.x;
+  int vb = blockIdx.x, tm = 0, tn = 0, kt0 = 0, nku = nkt, tt = -1, tslice = 0;
+  while (vb < total && !decode(vb, tm, tn, kt0, nku, tt, tslice)) vb += G;
+  if (vb >= total) return;   // only holes for this workgroup: nothing staged, nothing to wait for
 
   // the descriptors start BIAS bytes before the operands, so the per-lane offsets (pre-biased by
   // -1024 (j & 3) for the immediate offset of dma16g) never wrap; nothing below an operand is read
@@ -199,14 +330,13 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   // LDS byte address of the staging array (dynamic LDS: the only LDS object of this kernel)
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)lds;
   const int r16 = lane & 15, grp = lane >> 4;
-  const int nk = (SPLIT ? a.kp : a.K) / BK;
   // DMA sources: wave-instruction j (< 8) of this wave fills staged rows 64 w + 8 j .. + 8 (1 KB) of
   // the W and of the X tile, so a wave's pieces are contiguous 1-KB blocks (4 per M0 value)
   const int r8 = lane >> 3, slot = lane & 7;
   uint32_t offA[8], offB[8];
-  auto set_offsets = [&](int tm_, int tn_, int ks_) {
+  auto set_offsets = [&](int tm_, int tn_, int kt0_) {
     const int m0_ = tm_ * BM;
-    const uint32_t kb = (uint32_t)ks_ * (uint32_t)a.kp * 2u;   // byte offset of the slice's k range
+    const uint32_t kb = (uint32_t)kt0_ * (uint32_t)(BK * 2);   // byte offset of the unit's k range
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int row = 64 * w + 8 * j + r8;
@@ -224,7 +354,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
                 (uint32_t)(j & 3) * 1024u;
     }
   };
-  set_offsets(tm, tn, ks);
+  set_offsets(tm, tn, kt0);
   // DMA piece s (< 16) of a k-tile: W (s < 8) or X (s >= 8) rows 64 w + 8 (s & 7) .. + 8; M0 is set
   // once per 4 pieces (s & 3 == 0) and restored after the fourth
   const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)w * 8192u);
@@ -319,10 +449,15 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   char* const Q = L + 2 * STAGE + w * 8192;
 
   for (;;) {
-    const int nvb = vb + (int)gridDim.x;
+    int nvb = vb + G, ntm = tm, ntn = tn, nkt0 = kt0, nnk = nku, ntt = tt, ntk = tslice;
+    while (nvb < total && !decode(nvb, ntm, ntn, nkt0, nnk, ntt, ntk)) nvb += G;
     const bool more = nvb < total;
-    int ntm = tm, ntn = tn, nks = ks;   // without a next tile: re-stage this one (never consumed)
-    if (more) decode(nvb, ntm, ntn, nks);
+    if (!more) {   // without a next unit: re-stage this one (never consumed)
+      ntm = tm;
+      ntn = tn;
+      nkt0 = kt0;
+    }
+    const int nk = nku;
     const int m0 = tm * BM;
     // k-tile 0 landed: the 16 youngest vector-memory operations are k-tile 1's DMA or the previous
     // tile's epilogue stores, everything older (k-tile 0) is done.  (The previous tile's last call
@@ -342,7 +477,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     // tile's, whose last DMA was the previous trip's).
     for (int t = 0; t < nk; t += 2) {
       const bool last = t + 2 >= nk;
-      if (last) set_offsets(ntm, ntn, nks);
+      if (last) set_offsets(ntm, ntn, nkt0);
       iter(I0{}, last ? 0 : t + 2);
       iter(I1{}, last ? 1 : t + 3);
       // the MFMA wait states inside the loop, before its exit: hipcc does not know the asm MFMAs'
@@ -361,150 +496,197 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     for (int i = 0; i < 8; ++i)   // the asm MFMAs' results are read only after mfma_drain's wait states
 #pragma unroll
       for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
-    if constexpr (SPLIT) {
-      // partial slab rows m, columns n .. n + 3 of the lane's accumulators: 16 B (fp32) / 8 B (bf16)
-      // per lane, the 4 lanes of a row contiguous
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int m = m0 + 128 * wm + 16 * j + r16;
-        if (m >= a.M) continue;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int n = tn * BN + 128 * wn + 16 * i + 4 * grp;
-          if (n >= a.N) continue;
-          const size_t o = ((size_t)ks * a.M + m) * a.N + n;
-          const f32x4 v = acc[i][j];
-          if constexpr (EPI == EPI_P32) *reinterpret_cast<f32x4*>(static_cast<float*>(a.P) + o) = v;
-          else *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.P) + o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        }
-      }
-    } else if constexpr (EPI == EPI_ARGMAX) {
-      // lane (r16, grp) holds, for output row m = 128 wm + 16 j + r16, the 32 logits of columns
-      // n = 128 wn + 16 i + 4 grp + r (i < 8, r < 4).  Values are compared after bf16 rounding (what
-      // the unfused path's bf16 logits hold); i and r ascend, so strict '>' keeps the lowest index.
-      float* const Sv = reinterpret_cast<float*>(L + 2 * STAGE);            // [4 waves][128 rows]
-      int* const Si = reinterpret_cast<int*>(L + 2 * STAGE + 4 * 128 * 4);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int m = m0 + 128 * wm + 16 * j + r16;
-        const int mi = (a.mask_bits != nullptr && m < a.M) ? a.mask_idx[m] : -1;
-        const uint32_t* mrow = mi >= 0 ? a.mask_bits + (size_t)mi * a.mask_words : nullptr;
-        float best = -INFINITY;
-        int bidx = 0x7fffffff;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int n0 = tn * BN + 128 * wn + 16 * i + 4 * grp;
-          uint32_t bits = 0xfu;
-          if (mrow) {   // n0 + vocab_offset is a multiple of 4: the 4 bits share one mask word
-            const int gb = n0 + a.vocab_offset;
-            bits = (mrow[gb >> 5] >> (gb & 31)) & 0xfu;
+    // the epilogue of a whole tile / split-K slice / the last-arriving tail slice (a lambda called from
+    // two branches: merging the tail combine's accumulators back into one path made hipcc keep the
+    // whole tile in VGPRs and spill)
+    // mode 0: the output of a whole tile / split-K slice; 1: publish this tail slice; 2: the output of
+    // the last tail slice from the sum of the published slices
+    auto epilogue = [&](int mode) {
+      if constexpr (SPLIT) {
+        // partial slab rows m, columns n .. n + 3 of the lane's accumulators: 16 B (fp32) / 8 B (bf16)
+        // per lane, the 4 lanes of a row contiguous
+  #pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int m = m0 + 128 * wm + 16 * j + r16;
+          if (m >= a.M) continue;
+  #pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int n = tn * BN + 128 * wn + 16 * i + 4 * grp;
+            if (n >= a.N) continue;
+            const size_t o = ((size_t)(kt0 / (a.kp / BK)) * a.M + m) * a.N + n;
+            const f32x4 v = acc[i][j];
+            if constexpr (EPI == EPI_P32) *reinterpret_cast<f32x4*>(static_cast<float*>(a.P) + o) = v;
+            else *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.P) + o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
           }
-          if (n0 >= a.N) bits = 0;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float x = lo_f(pack2(acc[i][j][r], 0.f));
-            if (((bits >> r) & 1u) && x > best) {
-              best = x;
-              bidx = n0 + r;
+        }
+      } else if constexpr (EPI == EPI_ARGMAX) {
+        // lane (r16, grp) holds, for output row m = 128 wm + 16 j + r16, the 32 logits of columns
+        // n = 128 wn + 16 i + 4 grp + r (i < 8, r < 4).  Values are compared after bf16 rounding (what
+        // the unfused path's bf16 logits hold); i and r ascend, so strict '>' keeps the lowest index.
+        float* const Sv = reinterpret_cast<float*>(L + 2 * STAGE);            // [4 waves][128 rows]
+        int* const Si = reinterpret_cast<int*>(L + 2 * STAGE + 4 * 128 * 4);
+  #pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int m = m0 + 128 * wm + 16 * j + r16;
+          const int mi = (a.mask_bits != nullptr && m < a.M) ? a.mask_idx[m] : -1;
+          const uint32_t* mrow = mi >= 0 ? a.mask_bits + (size_t)mi * a.mask_words : nullptr;
+          float best = -INFINITY;
+          int bidx = 0x7fffffff;
+  #pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int n0 = tn * BN + 128 * wn + 16 * i + 4 * grp;
+            uint32_t bits = 0xfu;
+            if (mrow) {   // n0 + vocab_offset is a multiple of 4: the 4 bits share one mask word
+              const int gb = n0 + a.vocab_offset;
+              bits = (mrow[gb >> 5] >> (gb & 31)) & 0xfu;
+            }
+            if (n0 >= a.N) bits = 0;
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float x = lo_f(pack2(acc[i][j][r], 0.f));
+              if (((bits >> r) & 1u) && x > best) {
+                best = x;
+                bidx = n0 + r;
+              }
             }
           }
-        }
-#pragma unroll
-        for (int o = 16; o < 64; o <<= 1) {   // the 4 lanes of row r16 (grp 0..3)
-          const float ob = __shfl_xor(best, o, 64);
-          const int oi = __shfl_xor(bidx, o, 64);
-          if (ob > best || (ob == best && oi < bidx)) {
-            best = ob;
-            bidx = oi;
+  #pragma unroll
+          for (int o = 16; o < 64; o <<= 1) {   // the 4 lanes of row r16 (grp 0..3)
+            const float ob = __shfl_xor(best, o, 64);
+            const int oi = __shfl_xor(bidx, o, 64);
+            if (ob > best || (ob == best && oi < bidx)) {
+              best = ob;
+              bidx = oi;
+            }
+          }
+          if (grp == 0) {
+            Sv[w * 128 + 16 * j + r16] = best;
+            Si[w * 128 + 16 * j + r16] = bidx;
           }
         }
-        if (grp == 0) {
-          Sv[w * 128 + 16 * j + r16] = best;
-          Si[w * 128 + 16 * j + r16] = bidx;
-        }
-      }
-      wait_lgkm0();   // block_sync is a bare s_barrier: the other waves read these stores after it
-      block_sync();
-      {   // thread t: tile row t = 128 wm' + rr, from waves 2 wm' (columns 0..127) and 2 wm' + 1
-        const int wm2 = tid >> 7, rr = tid & 127, m = m0 + tid;
-        float b0 = Sv[(2 * wm2) * 128 + rr], b1 = Sv[(2 * wm2 + 1) * 128 + rr];
-        int i0 = Si[(2 * wm2) * 128 + rr], i1 = Si[(2 * wm2 + 1) * 128 + rr];
-        if (b1 > b0 || (b1 == b0 && i1 < i0)) {
-          b0 = b1;
-          i0 = i1;
-        }
-        if (m < a.M) {
-          a.part_val[(size_t)m * a.tiles_n + tn] = b0;
-          a.part_idx[(size_t)m * a.tiles_n + tn] = i0;
-        }
-      }
-      // the next tile's epilogue rewrites Sv / Si only after its k-loop's barriers
-    } else if constexpr (EPI == EPI_SWIGLU) {
-      // quadrant: 128 rows (m) x 64 output columns = 128 B per row, in 2 passes of 64 rows;
-      // 16-B chunk index ^ (row & 7)
-      const int rl = lane >> 3, cl = lane & 7;
-      const int ocol = 128 * tn + 64 * wn + 8 * cl;
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            const f32x4 g = acc[2 * pp][4 * p + jj], u = acc[2 * pp + 1][4 * p + jj];
-            float o[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = g[r] / (1.f + __expf(-g[r])) * u[r];
-            const int row = 16 * jj + r16, col = 16 * pp + 4 * grp;   // col: bf16 index in the row
-            const int ch = (col >> 3) ^ (row & 7);
-            *reinterpret_cast<uint2*>(Q + row * 128 + ch * 16 + (col & 4) * 2) =
-                make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+        wait_lgkm0();   // block_sync is a bare s_barrier: the other waves read these stores after it
+        block_sync();
+        {   // thread t: tile row t = 128 wm' + rr, from waves 2 wm' (columns 0..127) and 2 wm' + 1
+          const int wm2 = tid >> 7, rr = tid & 127, m = m0 + tid;
+          float b0 = Sv[(2 * wm2) * 128 + rr], b1 = Sv[(2 * wm2 + 1) * 128 + rr];
+          int i0 = Si[(2 * wm2) * 128 + rr], i1 = Si[(2 * wm2 + 1) * 128 + rr];
+          if (b1 > b0 || (b1 == b0 && i1 < i0)) {
+            b0 = b1;
+            i0 = i1;
           }
-#pragma unroll
-        for (int it = 0; it < 8; ++it) {
-          const int row = 8 * it + rl, m = m0 + 128 * wm + 64 * p + row;
-          const u32x4 v = *reinterpret_cast<const u32x4*>(Q + row * 128 + ((cl ^ (row & 7)) * 16));
-          if (m < a.M) *reinterpret_cast<u32x4*>(a.Y + (size_t)m * a.ldy + ocol) = v;
-        }
-      }
-    } else {
-      // quadrant: 128 rows (m) x 128 columns (n) = 256 B per row, in 4 passes of 32 rows; 16-B chunk
-      // index ^ (row & 15)
-      const int rl = lane >> 4, cl = lane & 15;
-      const int n = tn * BN + wn * 128 + 8 * cl;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) {
-            const f32x4 v = acc[i][2 * p + jj];
-            const int row = 16 * jj + r16, col = 16 * i + 4 * grp;
-            const int ch = (col >> 3) ^ (row & 15);
-            *reinterpret_cast<uint2*>(Q + row * 256 + ch * 16 + (col & 4) * 2) =
-                make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          if (m < a.M) {
+            a.part_val[(size_t)m * a.tiles_n + tn] = b0;
+            a.part_idx[(size_t)m * a.tiles_n + tn] = i0;
           }
-        if (n < a.N) {
-#pragma unroll
+        }
+        // the next tile's epilogue rewrites Sv / Si only after its k-loop's barriers
+      } else if constexpr (EPI == EPI_SWIGLU) {
+        // quadrant: 128 rows (m) x 64 output columns = 128 B per row, in 2 passes of 64 rows;
+        // 16-B chunk index ^ (row & 7).  Groups of 8: v[2 jj] = gate, v[2 jj + 1] = up of column group pp
+        const int rl = lane >> 3, cl = lane & 7;
+        const int ocol = 128 * tn + 64 * wn + 8 * cl;
+        static_for<2>([&](auto pc) {
+          constexpr int p = decltype(pc)::value;
+          static_for<4>([&](auto ppc) {
+            constexpr int pp = decltype(ppc)::value;
+            f32x4 v[8];
+            const int q[8] = {16 * pp + 4 * p, 16 * pp + 8 + 4 * p, 16 * pp + 4 * p + 1, 16 * pp + 8 + 4 * p + 1,
+                              16 * pp + 4 * p + 2, 16 * pp + 8 + 4 * p + 2, 16 * pp + 4 * p + 3, 16 * pp + 8 + 4 * p + 3};
+            if (mode == 2) {
+              tail_fetch8(a, tt, w, lane, q, v);
+            } else {
+              static_for<4>([&](auto jc) {
+                constexpr int jj = decltype(jc)::value;
+                v[2 * jj] = acc[2 * pp][4 * p + jj];
+                v[2 * jj + 1] = acc[2 * pp + 1][4 * p + jj];
+              });
+              if (mode == 1) {
+                tail_store8(a, tt, tslice, w, lane, q, v);
+                return;
+              }
+            }
+  #pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const f32x4 g = v[2 * jj], u = v[2 * jj + 1];
+              float o[4];
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = g[r] / (1.f + __expf(-g[r])) * u[r];
+              const int row = 16 * jj + r16, col = 16 * pp + 4 * grp;   // col: bf16 index in the row
+              const int ch = (col >> 3) ^ (row & 7);
+              *reinterpret_cast<uint2*>(Q + row * 128 + ch * 16 + (col & 4) * 2) =
+                  make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+            }
+          });
+          if (mode == 1) return;
+  #pragma unroll
           for (int it = 0; it < 8; ++it) {
-            const int row = 4 * it + rl, m = m0 + 128 * wm + 32 * p + row;
-            u32x4 v = *reinterpret_cast<const u32x4*>(Q + row * 256 + ((cl ^ (row & 15)) * 16));
-            if (m >= a.M) continue;
-            bf16_t* y = a.Y + (size_t)m * a.ldy + n;
-            if constexpr (EPI == EPI_ADD) {
-              const u32x4 rr = *reinterpret_cast<const u32x4*>(a.R + (size_t)m * a.ldy + n);
-#pragma unroll
-              for (int q = 0; q < 4; ++q) v[q] = pack2(lo_f(v[q]) + lo_f(rr[q]), hi_f(v[q]) + hi_f(rr[q]));
-            }
-            *reinterpret_cast<u32x4*>(y) = v;
+            const int row = 8 * it + rl, m = m0 + 128 * wm + 64 * p + row;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(Q + row * 128 + ((cl ^ (row & 7)) * 16));
+            if (m < a.M) *reinterpret_cast<u32x4*>(a.Y + (size_t)m * a.ldy + ocol) = v;
           }
-        }
+        });
+      } else {
+        // quadrant: 128 rows (m) x 128 columns (n) = 256 B per row, in 4 passes of 32 rows; 16-B chunk
+        // index ^ (row & 15)
+        const int rl = lane >> 4, cl = lane & 15;
+        const int n = tn * BN + wn * 128 + 8 * cl;
+        static_for<4>([&](auto pc) {
+          constexpr int p = decltype(pc)::value;
+          static_for<2>([&](auto jc) {   // groups of 8: accumulator column 2 p + jj, all i
+            constexpr int jj = decltype(jc)::value;
+            f32x4 v8[8];
+            const int q[8] = {2 * p + jj, 8 + 2 * p + jj, 16 + 2 * p + jj, 24 + 2 * p + jj,
+                              32 + 2 * p + jj, 40 + 2 * p + jj, 48 + 2 * p + jj, 56 + 2 * p + jj};
+            if (mode == 2) {
+              tail_fetch8(a, tt, w, lane, q, v8);
+            } else {
+              static_for<8>([&](auto ic) { v8[decltype(ic)::value] = acc[decltype(ic)::value][2 * p + jj]; });
+              if (mode == 1) {
+                tail_store8(a, tt, tslice, w, lane, q, v8);
+                return;
+              }
+            }
+  #pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const f32x4 v = v8[i];
+              const int row = 16 * jj + r16, col = 16 * i + 4 * grp;
+              const int ch = (col >> 3) ^ (row & 15);
+              *reinterpret_cast<uint2*>(Q + row * 256 + ch * 16 + (col & 4) * 2) =
+                  make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+            }
+          });
+          if (mode != 1 && n < a.N) {
+  #pragma unroll
+            for (int it = 0; it < 8; ++it) {
+              const int row = 4 * it + rl, m = m0 + 128 * wm + 32 * p + row;
+              u32x4 v = *reinterpret_cast<const u32x4*>(Q + row * 256 + ((cl ^ (row & 15)) * 16));
+              if (m >= a.M) continue;
+              bf16_t* y = a.Y + (size_t)m * a.ldy + n;
+              if constexpr (EPI == EPI_ADD) {
+                const u32x4 rr = *reinterpret_cast<const u32x4*>(a.R + (size_t)m * a.ldy + n);
+  #pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = pack2(lo_f(v[q]) + lo_f(rr[q]), hi_f(v[q]) + hi_f(rr[q]));
+              }
+              *reinterpret_cast<u32x4*>(y) = v;
+            }
+          }
+        });
       }
-    }
+    };
+    // the accumulators are read at one call site (see tail_ticket): a tail slice publishes them (mode
+    // 1); the last one to arrive then stores the output from the published slices (mode 2, which
+    // reads no accumulator)
+    const int mode = (TAILOK && tt >= 0) ? 1 : 0;
+    epilogue(mode);
+    if (TAILOK && mode == 1 && tail_ticket(a, tt, w, lane)) epilogue(2);
     if (!more) break;
     vb = nvb;
     tm = ntm;
     tn = ntn;
-    ks = nks;
+    kt0 = nkt0;
+    nku = nnk;
+    tt = ntt;
+    tslice = ntk;
   }
   wait_vm<0>();   // the trailing re-stage DMA: nothing may land in LDS after the workgroup ends
 #undef GB_DMA
@@ -522,8 +704,42 @@ static int num_cus() {
   return n;
 }
 
+// Workspace of the split tail: [err + pad 256 B][counters: TAIL_MAX_TILES x 4 waves x 2][slabs]
+constexpr int TAIL_MAX_TILES = 1024;
+constexpr size_t TAIL_HDR = 256 + (size_t)TAIL_MAX_TILES * 8 * 4;
+constexpr size_t TAIL_SLAB = (size_t)BM * BN * 4;   // one tile's fp32 accumulators (4 quadrants)
+
+// The tail split for T tiles on G persistent workgroups, in k-tile times: the tail's last round
+// takes ceil(span / G) slices of ~nkt / s k-tiles; each slice publishes its fp32 tile and the last
+// arriving one reads all s back (XCD-local L2) before its epilogue.
+// Returns s (1: no split) and sets full / tail tiles.
+static int choose_tail(int T, int G, int nkt, size_t ws_bytes, int& full, int& tail) {
+  full = T;
+  tail = 0;
+  const int rem = T % G;
+  if (rem == 0 || ws_bytes < TAIL_HDR) return 1;
+  const int trips = nkt / 2;
+  double best = (double)nkt;   // s = 1: one more round of whole tiles
+  int bs = 1;
+  for (int s = 2; s <= 8 && s <= trips; ++s) {
+    if (TAIL_HDR + (size_t)rem * s * TAIL_SLAB > ws_bytes || rem > TAIL_MAX_TILES) break;
+    const int span = (rem + 7) / 8 * 8 * s;
+    // + publishing the quadrant (~1.5 k-tile times) + the last slice reading s slabs (~1.8 each)
+    const double t = (double)((span + G - 1) / G) * (double)((trips + s - 1) / s) * 2.0 + 1.5 + 1.8 * s;
+    if (t < best * 0.95) {   // a clear win only: the hand-off's cost model is coarse
+      best = t;
+      bs = s;
+    }
+  }
+  if (bs > 1) {
+    full = T - rem;
+    tail = rem;
+  }
+  return bs;
+}
+
 template <int EPI>
-static int launch(const Args& a0, hipStream_t st) {
+static int launch(const Args& a0, hipStream_t st, void* ws = nullptr, size_t ws_bytes = 0) {
   static bool attr = false;
   auto kern = &gemm256_kernel<EPI>;
   if (!attr) {
@@ -535,9 +751,25 @@ static int launch(const Args& a0, hipStream_t st) {
   a.tiles_m = (a.M + BM - 1) / BM;
   a.tiles_n = EPI == EPI_SWIGLU ? a.I / 128 : (a.N + BN - 1) / BN;
   const int split = (EPI == EPI_P32 || EPI == EPI_P16) ? a.split : 1;
-  const int total = a.tiles_m * a.tiles_n * split;
+  const int tiles = a.tiles_m * a.tiles_n;
   // one workgroup per CU (the LDS allows no more); a persistent grid is a multiple of 8 (XCDs)
   const int cus = num_cus() & ~7;
+  int total = tiles * split;
+  a.full = tiles;
+  a.tail_s = 1;
+  a.tail_tiles = 0;
+  a.span = 0;
+  if (EPI == EPI_BF16 || EPI == EPI_SWIGLU || EPI == EPI_ADD) {
+    a.tail_s = choose_tail(tiles, cus, a.K / BK, ws ? ws_bytes : 0, a.full, a.tail_tiles);
+    if (a.tail_s > 1) {
+      char* base = static_cast<char*>(ws);
+      a.err = reinterpret_cast<int*>(base);
+      a.cnt = reinterpret_cast<int*>(base + 256);
+      a.slab = reinterpret_cast<float*>(base + TAIL_HDR);
+      a.span = (a.tail_tiles + 7) / 8 * 8 * a.tail_s;
+      total = a.full + a.span;
+    }
+  }
   const int grid = total <= cus ? total : cus;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS_TOTAL, st, a);
   return (int)hipGetLastError();
@@ -548,22 +780,44 @@ static int launch(const Args& a0, hipStream_t st) {
 // Y = X W^T (+ R).  epi: 0 bf16 Y [M, ldy]; 3 SwiGLU: W = [gate; up] rows (N = 2I), Y [M, ldy] gets
 // silu(x gate^T) * (x up^T), I columns; 4: Y = X W^T + R (R [M, ldy], may alias Y).
 // Requirements: K % 128 == 0, N % 128 == 0 (SwiGLU: I % 128 == 0), 16-B aligned rows (ldx % 8 == 0).
+// ws (optional, zero-filled once, ka_gemm_big_ws_bytes): the split tail's counters and slabs; the
+// kernel leaves the counters zeroed again.  nullptr: no split tail.
 extern "C" int ka_gemm_big(void* Y, const void* R, const void* X, const void* W, int M, int N, int K, int ldx, int ldy,
-                           int epi, int gm, hipStream_t stream) {
+                           int epi, int gm, void* ws, size_t ws_bytes, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 128 != 0 || N % 128 != 0 || ldx % 8 != 0 || ldy % 8 != 0) return (int)hipErrorInvalidValue;
   gb::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), static_cast<bf16_t*>(Y),
              static_cast<const bf16_t*>(R), M, N, K, ldx, ldy, 0, 0, gm > 0 ? gm : 8, N / 2};
   switch (epi) {
-    case gb::EPI_BF16: return gb::launch<gb::EPI_BF16>(a, stream);
+    case gb::EPI_BF16: return gb::launch<gb::EPI_BF16>(a, stream, ws, ws_bytes);
     case gb::EPI_SWIGLU:
       if (N % 256 != 0) return (int)hipErrorInvalidValue;
-      return gb::launch<gb::EPI_SWIGLU>(a, stream);
+      return gb::launch<gb::EPI_SWIGLU>(a, stream, ws, ws_bytes);
     case gb::EPI_ADD:
       if (R == nullptr) return (int)hipErrorInvalidValue;
-      return gb::launch<gb::EPI_ADD>(a, stream);
+      return gb::launch<gb::EPI_ADD>(a, stream, ws, ws_bytes);
   }
   return (int)hipErrorInvalidValue;
+}
+
+// Workspace bytes of ka_gemm_big's split tail: 512 tile slabs (128 MB; choose_tail keeps tail tiles x
+// slices within the workspace it is given).
+extern "C" size_t ka_gemm_big_ws_bytes() { return gb::TAIL_HDR + (size_t)512 * gb::TAIL_SLAB; }
+
+// The split that ka_gemm_big would use (tests / diagnostics): tail_s, and the whole / tail tile counts.
+extern "C" int ka_gemm_big_plan(int M, int N, int epi, int K, size_t ws_bytes, int* full, int* tail) {
+  const int tm = (M + gb::BM - 1) / gb::BM, tn = epi == gb::EPI_SWIGLU ? N / 256 : (N + gb::BN - 1) / gb::BN;
+  return gb::choose_tail(tm * tn, gb::num_cus() & ~7, K / gb::BK, ws_bytes, *full, *tail);
+}
+
+// Error word of the split tail (a slice that waited ~0.1 s for the others); cleared by the read.
+extern "C" int ka_gemm_big_err(void* ws, hipStream_t stream) {
+  int v = 0;
+  if (ws == nullptr) return 0;
+  (void)hipMemcpyAsync(&v, ws, 4, hipMemcpyDeviceToHost, stream);
+  (void)hipStreamSynchronize(stream);
+  if (v) (void)hipMemsetAsync(ws, 0, 4, stream);
+  return v;
 }
 
 // Split-K partials: P[ks][M][N] = X[:, ks kp : (ks + 1) kp] W[:, same]^T with kp = K / split, fp32

@@ -271,7 +271,7 @@ extern "C" void ka_splitk_reduce_launch(bf16_t* Y, const float* P, int split, lo
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((int)blocks), dim3(256), 0, stream, Y, P, split, mn);
 }
 
-// Row-streaming GEMV for M <= 4: each wave owns RW consecutive weight rows, i.e. one contiguous
+// Row-streaming GEMV for M <= 16: each wave owns RW consecutive weight rows, i.e. one contiguous
 // RW x klen block of W, and streams it 1 KB per load instruction (64 lanes x 16 B along K) through
 // a RING-deep register ring; the dot products run on v_dot2c_f32_bf16 against the workgroup's
 // LDS-staged X slice, and each finished row is summed across the wave (xor shuffles).  Against
@@ -373,16 +373,18 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const bf16_t* __restrict
   }
 }
 
-// M <= 4 GEMV / SwiGLU-down through gemv_rows_kernel: `rw` weight rows per wave, K split `split` ways
+// M <= 16 GEMV / SwiGLU-down through gemv_rows_kernel: `rw` weight rows per wave, K split `split` ways
 // (`swiglu` = flags, below)
 // (K % (512 * split) == 0); P (split > 1) receives fp32 partials (Y == nullptr: left for a fused
 // consumer, else reduced into Y).  Returns hipErrorInvalidValue for shapes it does not take.
 extern "C" int ka_gemv_rows(void* Y, const void* X, const void* W, void* workspace, int M, int N, int K, int split,
                             int rw, int swiglu, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (M > 4 || split < 1 || rw < 1 || K % (512 * split) != 0) return (int)hipErrorInvalidValue;
+  if (M > 16 || split < 1 || rw < 1 || K % (512 * split) != 0) return (int)hipErrorInvalidValue;
   const int kps = K / split;
-  const int mr = M == 1 ? 1 : M == 2 ? 2 : 4;
+  // X rows staged per workgroup: the next power of two >= M (8 / 16: the decode buckets above batch 4,
+  // where the weight stream still sets the time and hipBLASLt's tiles do not reach the HBM rate)
+  const int mr = M == 1 ? 1 : M == 2 ? 2 : M <= 4 ? 4 : M <= 8 ? 8 : 16;
   const size_t lds = (size_t)mr * kps * 2;
   if (lds > 65536) return (int)hipErrorInvalidValue;
   auto* x = static_cast<const bf16_t*>(X);
@@ -398,7 +400,8 @@ extern "C" int ka_gemv_rows(void* Y, const void* X, const void* W, void* workspa
   hipLaunchKernelGGL((gemv_rows_kernel<MRV, RG, SW, NTV>), grid, dim3(256), lds, stream, x, w, y, p, M, N, K, kps, rw)
 #define KA_ROWS_MR(SW, RG, NTV) \
   do { if (mr == 1) KA_ROWS_LAUNCH(1, SW, RG, NTV); else if (mr == 2) KA_ROWS_LAUNCH(2, SW, RG, NTV); \
-       else KA_ROWS_LAUNCH(4, SW, RG, NTV); } while (0)
+       else if (mr == 4) KA_ROWS_LAUNCH(4, SW, RG, NTV); else if (mr == 8) KA_ROWS_LAUNCH(8, SW, RG, NTV); \
+       else KA_ROWS_LAUNCH(16, SW, RG, NTV); } while (0)
 #define KA_ROWS_VAR(SW) \
   do { if (var == 0) KA_ROWS_MR(SW, 8, false); else if (var == 1) KA_ROWS_MR(SW, 16, false); \
        else if (var == 2) KA_ROWS_MR(SW, 8, true); else KA_ROWS_MR(SW, 16, true); } while (0)

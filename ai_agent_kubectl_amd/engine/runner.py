@@ -198,18 +198,30 @@ class ModelRunner:
         lm = m.W["lm_head"]
         if self.device.type != "cuda" or ops.LM_HEAD_MODE != "auto":
             return {}
-        from ..ops.autotune import _time
+        from ..ops.autotune import _time, load_section, plan_mode, save_section
         K = lm.shape[1]
         report = {}
+        # persisted with the GEMM plan (ops/tuned/gemm_plan_mi355x.json, section lm_head): the same
+        # decision on every box and run unless KA_GEMM_PLAN=tune / write re-times it
+        mode, path = plan_mode()
+        key = lambda M: f"{M},{lm.shape[0]},{K},{int(self.mask_bits is not None)}"   # noqa: E731
+        saved = load_section(path, "lm_head") if mode == "file" else {}
         for M in sorted(set(self.buckets)):
             x = torch.randn(M, K, device=self.device, dtype=lm.dtype)
             if not ops.lm_head_argmax_ok(x, lm, m.vocab_offset):
                 return {}
-            midx = (torch.zeros(M, dtype=torch.int32, device=self.device) if self.mask_bits is not None else None)
-            t_un = _time(lambda w: ops.masked_argmax(ops.linear(x, w), self.mask_bits, midx, m.vocab_offset), [lm])
-            t_fu = _time(lambda w: ops.lm_head_argmax(x, w, self.mask_bits, midx, m.vocab_offset), [lm])
-            ops.LM_HEAD_FUSED[M] = t_fu < t_un
-            report[M] = {"fused_us": round(t_fu, 1), "unfused_us": round(t_un, 1)}
+            if key(M) in saved:
+                fused, t_fu, t_un = saved[key(M)]
+            else:
+                midx = (torch.zeros(M, dtype=torch.int32, device=self.device) if self.mask_bits is not None else None)
+                t_un = _time(lambda w: ops.masked_argmax(ops.linear(x, w), self.mask_bits, midx, m.vocab_offset), [lm])
+                t_fu = _time(lambda w: ops.lm_head_argmax(x, w, self.mask_bits, midx, m.vocab_offset), [lm])
+                fused = t_fu < t_un
+            ops.LM_HEAD_FUSED[M] = bool(fused)
+            report[M] = {"fused_us": round(t_fu, 1), "unfused_us": round(t_un, 1), "fused": bool(fused)}
+        if mode == "write":
+            save_section(path, "lm_head", {key(M): [r["fused"], r["fused_us"], r["unfused_us"]]
+                                          for M, r in report.items()})
         wins = sorted(M for M, f in ops.LM_HEAD_FUSED.items() if f)
         # untimed row counts: fused from the smallest bucket above which every timed bucket won
         ops.LM_HEAD_FUSED_MIN_M = next((M for M in wins if all(ops.LM_HEAD_FUSED[b] for b in ops.LM_HEAD_FUSED
@@ -229,21 +241,31 @@ class ModelRunner:
         ws = [L["w13"] for L in m.layers if L.get("w13") is not None and L["w13"].dim() == 2][:8]
         if not ws:
             return {}
-        from ..ops.autotune import _time
+        from ..ops.autotune import _time, load_section, plan_mode, save_section
         report = {}
+        mode, path = plan_mode()   # persisted like the GEMM plan (section decode_swiglu)
+        key = lambda M: f"{M},{ws[0].shape[0]},{ws[0].shape[1]}"   # noqa: E731
+        saved = load_section(path, "decode_swiglu") if mode == "file" else {}
         for M in sorted(set(self.buckets)):
             x = torch.randn(M, ws[0].shape[1], device=self.device, dtype=ws[0].dtype)
             if not ops.decode_swiglu_ok(x, ws[0]):
                 continue
-            t_un = _time(lambda w: ops.silu_mul(ops.linear(x, w, defer_reduce=True)), ws)
-            best = (0, t_un)
-            for cfg in ops.DECODE_SWIGLU_CFGS:
-                t = _time(lambda w: ops.linear_gm_swiglu(x, w, cfg), ws)
-                if t < best[1]:
-                    best = (cfg, t)
+            if key(M) in saved:
+                cfg, t_fu, t_un = saved[key(M)]
+                best = (int(cfg), t_fu)
+            else:
+                t_un = _time(lambda w: ops.silu_mul(ops.linear(x, w, defer_reduce=True)), ws)
+                best = (0, t_un)
+                for cfg in ops.DECODE_SWIGLU_CFGS:
+                    t = _time(lambda w: ops.linear_gm_swiglu(x, w, cfg), ws)
+                    if t < best[1]:
+                        best = (cfg, t)
             if best[0]:
                 ops.DECODE_SWIGLU_CFG[M] = best[0]
             report[M] = {"cfg": best[0], "fused_us": round(best[1], 1), "unfused_us": round(t_un, 1)}
+        if mode == "write":
+            save_section(path, "decode_swiglu", {key(M): [r["cfg"], r["fused_us"], r["unfused_us"]]
+                                                for M, r in report.items()})
         logger.info("decode swiglu plan: %s", report)
         return report
 
@@ -272,6 +294,8 @@ class ModelRunner:
         if not self.use_graphs:
             return 0.0
         t0 = time.perf_counter()
+        if self.device.type == "cuda":
+            ops.gemm_big_ws(self.device)   # allocated (and zeroed) outside any capture
         if autotune:
             self.gemm_plan = self.autotune()
             self.lm_head_plan = self.tune_lm_head()

@@ -339,8 +339,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
            bf16_partials: bool = False):
     """y = x @ w.T (w is [out, in]).  Decode-sized M goes to the hand-written weight-streaming
     kernel (M <= 256, csrc/gemm_skinny.hip), the LDS-DMA MFMA kernel (M <= 512, csrc/gemm_mfma.hip)
-    or hipBLASLt, whichever the autotuned plan measured fastest for this (M, N, K); other shapes
-    (prefill) go to hipBLASLt via F.linear.
+    or hipBLASLt, whichever the autotuned plan measured fastest for this (M, N, K); prefill / mixed
+    steps (M > 512) go to csrc/gemm_big.hip (`linear_big`, KA_PREFILL_GEMM) where the shape allows,
+    else hipBLASLt via F.linear.
     defer_reduce: when the chosen kernel splits K, return its partials as a `SplitK` for a consumer
     that fuses the reduction instead of running the reduce kernel.
     bf16_partials: with defer_reduce, a gemm_mfma plan stores those partials as bf16
@@ -351,6 +352,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
     N = w.shape[0]
     if _ref(x):
         return ref.linear(x, w)
+    if M > TILE_MAX_M and use_big_gemm(x, w):
+        return linear_big(x, w)
     if M > TILE_MAX_M or K % 64 != 0 or N % 4 != 0 or not x.is_contiguous():
         return torch.nn.functional.linear(x, w)
     if not split:
@@ -382,11 +385,20 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
 
 
 # Prefill / mixed-step gate_up with the SwiGLU epilogue (csrc/gemm_big.hip EPI_SWIGLU): the [M, 2I]
-# gate_up output never exists and the separate SiLU·mul pass goes away.  M >= PREFILL_SWIGLU_MIN_M
+# gate_up output never exists and the separate SiLU·mul pass goes away.  Every M > TILE_MAX_M (513+)
 # rows (profiles/r3/gemm_big: 565 us vs hipBLASLt 550 us + SiLU·mul at M = 2944, 691 vs 620 + 122
-# at M = 4096, Llama-3-8B).  KA_PREFILL_SWIGLU=0 restores hipBLASLt + silu_mul.
+# at M = 4096, Llama-3-8B; the split tail of round 4 takes the short last round of tiles at smaller
+# M).  KA_PREFILL_SWIGLU=0 restores hipBLASLt + silu_mul.
 PREFILL_SWIGLU = os.environ.get("KA_PREFILL_SWIGLU", "1") == "1"
-PREFILL_SWIGLU_MIN_M = int(os.environ.get("KA_PREFILL_SWIGLU_MIN_M", "1024"))
+PREFILL_SWIGLU_MIN_M = int(os.environ.get("KA_PREFILL_SWIGLU_MIN_M", "513"))
+# Prefill / mixed-step QKV, O and down projections (M > TILE_MAX_M): KA_PREFILL_GEMM=big runs them on
+# csrc/gemm_big.hip with the split tail; the default stays hipBLASLt (F.linear), which measured
+# faster on these plain shapes (gemm_big 0.79-0.92x rocBLAS at M = 2944-4096: profiles/r4/gemm_big_tail/).
+PREFILL_GEMM = os.environ.get("KA_PREFILL_GEMM", "blas")
+
+
+def use_big_gemm(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return PREFILL_GEMM == "big" and not _ref(x) and x.shape[0] > TILE_MAX_M and big_gemm_ok(x, w)
 GB_EPI_SWIGLU = 3
 
 
@@ -416,9 +428,56 @@ def linear_swiglu(x: torch.Tensor, w13: torch.Tensor, out: Optional[torch.Tensor
     M, K = x.shape
     N = w13.shape[0]
     out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device) if out is None else out
+    ws = gemm_big_ws(x.device)
     check(lib.ka_gemm_big(_p(out), None, _p(x), _p(w13), M, N, K, x.stride(0), out.stride(0), GB_EPI_SWIGLU, 0,
-                          _stream()), "gemm_big_swiglu")
+                          _p(ws), ws.numel() if ws is not None else 0, _stream()), "gemm_big_swiglu")
     return out
+
+
+# csrc/gemm_big.hip split tail: a zero-filled workspace per device (counters + fp32 slabs; the kernel
+# leaves the counters zeroed).  KA_GEMM_BIG_TAIL=0: no split tail.
+GEMM_BIG_TAIL = os.environ.get("KA_GEMM_BIG_TAIL", "1") == "1"
+_GB_WS: dict = {}
+
+
+def gemm_big_ws(device) -> Optional[torch.Tensor]:
+    if not GEMM_BIG_TAIL:
+        return None
+    ws = _GB_WS.get(device)
+    if ws is None:
+        ws = _GB_WS[device] = torch.zeros(int(require().ka_gemm_big_ws_bytes()), dtype=torch.uint8, device=device)
+    return ws
+
+
+def gemm_big_err(device) -> int:
+    """The split tail's error word (a slice that waited ~0.1 s for the others; 0 in a correct run),
+    cleared by the read.  Synchronises the stream."""
+    ws = _GB_WS.get(device)
+    return 0 if ws is None else int(require().ka_gemm_big_err(_p(ws), _stream()))
+
+
+def linear_big(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ w.T through csrc/gemm_big.hip (prefill / mixed-step projections, M > TILE_MAX_M):
+    256 x 256 tiles, one workgroup per CU, the partial last round split over K (split tail)."""
+    if _ref(x):
+        return ref.linear(x, w)
+    if not big_gemm_ok(x, w):
+        raise ValueError(f"gemm_big needs K % 128 == 0, N % 128 == 0, aligned rows: {tuple(x.shape)} x {tuple(w.shape)}")
+    lib = require()
+    M, K = x.shape
+    N = w.shape[0]
+    out = torch.empty((M, N), dtype=x.dtype, device=x.device) if out is None else out
+    ws = gemm_big_ws(x.device)
+    check(lib.ka_gemm_big(_p(out), None, _p(x), _p(w), M, N, K, x.stride(0), out.stride(0), 0, 0, _p(ws),
+                          ws.numel() if ws is not None else 0, _stream()), "gemm_big")
+    return out
+
+
+def big_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    M, K = x.shape
+    N = w.shape[0]
+    return (x.stride(1) == 1 and x.stride(0) % 8 == 0 and K % 128 == 0 and N % 128 == 0 and w.is_contiguous()
+            and w.shape[1] == K)
 
 
 # Decode gate_up with the SwiGLU epilogue in the csrc/gemm_mfma.hip ring kernel, per decode bucket
@@ -448,26 +507,30 @@ def decode_swiglu_cfg(x: torch.Tensor, w13: torch.Tensor) -> int:
 # contiguous block of weight rows 1 KB per load, non-temporal (profiles/r3/gemv_rows: Llama-3-8B
 # batch 1 gate_up 46.8 -> 38.6 us, down with SwiGLU staging 24.1 -> 21.8, QKV 13.3 -> 12.1, LM head
 # 201 -> 164).  Planned per shape by ops.autotune ("rows", split, rows per wave).
-ROWS_MAX_M = 4
+ROWS_MAX_M = 16                 # csrc/gemm_skinny.hip stages up to 16 X rows per workgroup
 ROWS_NT = 4                     # ka_gemv_rows flag: non-temporal weight loads
 ROWS_SWIGLU = os.environ.get("KA_GEMV_ROWS_SWIGLU", "1") == "1"
 ROWS_SWIGLU_SPLIT, ROWS_SWIGLU_RW = 4, 4
 
 
+def rows_mr(M: int) -> int:
+    return 1 if M == 1 else 2 if M == 2 else 4 if M <= 4 else 8 if M <= 8 else 16
+
+
 def rows_ok(M: int, K: int, split: int) -> bool:
-    mr = 1 if M == 1 else 2 if M == 2 else 4
-    return M <= ROWS_MAX_M and split >= 1 and K % (512 * split) == 0 and mr * (K // split) * 2 <= 65536
+    return (M <= ROWS_MAX_M and split >= 1 and K % (512 * split) == 0
+            and rows_mr(M) * (K // split) * 2 <= 65536)
 
 
 def linear_rows(x: torch.Tensor, w: torch.Tensor, split: int, rw: int, defer_reduce: bool = False):
-    """y = x @ w.T for M <= 4 through the row-streaming GEMV (`rw` weight rows per wave, K split
+    """y = x @ w.T for M <= 16 through the row-streaming GEMV (`rw` weight rows per wave, K split
     `split` ways); split > 1 with defer_reduce returns the fp32 partials as a `SplitK`."""
     M, K = x.shape
     N = w.shape[0]
     if _ref(x):
         return ref.linear(x, w)
     if not rows_ok(M, K, split) or not x.is_contiguous():
-        raise ValueError(f"gemv_rows needs M <= 4, K % (512*split) == 0: M={M} K={K} split={split}")
+        raise ValueError(f"gemv_rows needs M <= 16, K % (512*split) == 0: M={M} K={K} split={split}")
     lib = require()
     ws = torch.empty((split, M, N), dtype=torch.float32, device=x.device) if split > 1 else None
     if defer_reduce and split > 1:

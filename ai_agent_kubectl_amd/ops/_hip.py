@@ -27,6 +27,8 @@ P = ctypes.c_void_p
 I = ctypes.c_int
 F = ctypes.c_float
 
+_RESTYPES = {"ka_gemm_big_ws_bytes": ctypes.c_size_t}
+
 _SIGS = {
     "ka_rmsnorm": [P, P, P, P, I, I, F, P],
     "ka_rope_kv": [P, P, P, P, P, P, P, I, I, I, I, I, P],
@@ -49,7 +51,10 @@ _SIGS = {
     "ka_gemv_rows": [P, P, P, P, I, I, I, I, I, I, P],
     "ka_gemm_mfma_swiglu": [P, P, P, I, I, I, I, I, I, P],
     "ka_gemm_mfma_grouped": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
-    "ka_gemm_big": [P, P, P, P, I, I, I, I, I, I, I, P],
+    "ka_gemm_big": [P, P, P, P, I, I, I, I, I, I, I, P, ctypes.c_size_t, P],
+    "ka_gemm_big_ws_bytes": [],
+    "ka_gemm_big_plan": [I, I, I, I, ctypes.c_size_t, P, P],
+    "ka_gemm_big_err": [P, P],
     "ka_gemm_big_argmax": [P, P, P, P, I, I, I, I, P, P, I, I, P, P],
     "ka_argmax_finish": [P, P, P, P, I, I, I, P],
     "ka_gm_bn": [I],
@@ -87,7 +92,7 @@ def load(path: str = LIB_PATH) -> Optional[ctypes.CDLL]:
             if fn is None:
                 continue
             fn.argtypes = argtypes
-            fn.restype = ctypes.c_int
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
         _lib = lib
         return _lib
 

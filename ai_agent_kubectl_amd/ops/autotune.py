@@ -19,6 +19,7 @@ from . import (GEMM_PLAN, SKINNY_MAX_M, TILE_MAX_M, gm_shape, linear, linear_gm,
 logger = logging.getLogger("app.engine")
 
 
+import os
 import os as _os
 
 # TunableOp results for the decode GEMM shapes on MI355X (ROCm 7.x); loaded at start, extended
@@ -95,6 +96,39 @@ def save_plan(path: str, report: Dict, ctx_of: Dict[Tuple[int, int], str]) -> No
     data["note"] = "ops/autotune.py: [choice, split, cfg, us, hipBLASLt us] per M,N,K,consumer"
     with open(path, "w") as f:
         json.dump(data, f, indent=0, sort_keys=True)
+
+
+def load_section(path: str, section: str) -> Dict[str, list]:
+    """Entries of another persisted engine-start decision (`lm_head`, `decode_swiglu`) in the plan file."""
+    import json
+    try:
+        with open(path) as f:
+            return dict(json.load(f).get(section, {}))
+    except (OSError, ValueError):
+        return {}
+
+
+def save_section(path: str, section: str, entries: Dict[str, list]) -> None:
+    import json
+    try:
+        with open(path) as f:
+            data = json.load(f)
+    except (OSError, ValueError):
+        data = {}
+    data.setdefault(section, {}).update(entries)
+    with open(path, "w") as f:
+        json.dump(data, f, indent=0, sort_keys=True)
+
+
+def plan_mode() -> Tuple[str, str]:
+    """(KA_GEMM_PLAN, plan file): `file` (load, tune what is missing), `tune` or `write`."""
+    return os.environ.get("KA_GEMM_PLAN", "file"), os.environ.get("KA_GEMM_PLAN_FILE", DEFAULT_PLAN_FILE)
+
+
+# A hipBLASLt plan is kept only when it beats the best hand-written candidate by more than this
+# fraction: within it the hand-written kernel is taken (no vendor kernel in the captured decode
+# graphs, and one library's heuristics fewer between boxes).  KA_PLAN_BLAS_MARGIN=0: fastest wins.
+BLAS_MARGIN = float(os.environ.get("KA_PLAN_BLAS_MARGIN", "0.03"))
 
 
 def _tunableop_begin() -> bool:
@@ -203,7 +237,7 @@ def _tune(groups, Ms, norm_fed=frozenset(), bf16_partials: bool = True, consumer
                 norm = (lambda h: h)
             GEMM_PLAN.pop((M, N, K), None)
             t_blas = _time(lambda w: norm(torch.nn.functional.linear(x, w)), ws)
-            best = ("blas", 0, 0, t_blas)
+            best = ("blas", 0, 0, float("inf"))   # the best hand-written candidate
             if M <= SKINNY_MAX_M and K % 64 == 0 and N % 4 == 0:
                 cands = sorted({skinny_split(M, N, K, t) for t in (256, 512, 1024, 2048)})
                 for sp in cands:
@@ -221,6 +255,8 @@ def _tune(groups, Ms, norm_fed=frozenset(), bf16_partials: bool = True, consumer
                 t = _time(lambda w: norm(linear_gm(x, w, cfg, sp, defer_reduce=fed, bf16_partials=bf16)), ws)
                 if t < best[3]:
                     best = ("gm", sp, cfg, t)
+            if best[3] > t_blas * (1.0 + BLAS_MARGIN):
+                best = ("blas", 0, 0, t_blas)
             GEMM_PLAN[(M, N, K)] = (best[0], best[1], best[2])
             report[(M, N, K)] = {"choice": best[0], "split": best[1], "cfg": best[2], "us": round(best[3], 1),
                                  "blas_us": round(t_blas, 1),

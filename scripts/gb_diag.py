@@ -23,7 +23,9 @@ def gb(x, w, epi=0):
     M, K = x.shape
     N = w.shape[0]
     y = torch.empty(M, N // 2 if epi == 3 else N, device=dev, dtype=BF)
+    ws = ops.gemm_big_ws(x.device)
     _hip.check(lib.ka_gemm_big(y.data_ptr(), None, x.data_ptr(), w.data_ptr(), M, N, K, K, y.shape[1], epi, 0,
+                               ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0,
                                ops._stream()), "gemm_big")
     return y
 

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round-4 HEAD profile, one gpurun call: driver-form bench, rocprofv3 kernel stats of a short bench,
+# phase profiles at C = 256 and C = 1.  Every GPU step has its own limit; the first failure ends it.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-r4b}
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $OUT/bench_default.log 2>&1 &&
+rm -rf /tmp/ka_prof && (cd /tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d /tmp/ka_prof -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --transport tcp > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1) &&
+mkdir -p $OUT/prof && find /tmp/ka_prof -name "*stats.csv" -exec cp {} $OUT/prof/ \; &&
+timeout -k 10 400 python scripts/phase_profile.py --concurrency 256 > $OUT/phase_c256.log 2>&1 &&
+timeout -k 10 400 python scripts/phase_profile.py --concurrency 1 > $OUT/phase_c1.log 2>&1
+rc=$?
+echo "exit=$rc"
+tail -3 $OUT/*.log
+exit $rc

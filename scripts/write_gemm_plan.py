@@ -39,6 +39,9 @@ for model in sys.argv[1:] or ["llama3-8b"]:
                                      kv_cache_tokens=65536, max_model_len=512))
     rep = eng.runner.autotune()
     print(model, len(rep), "plan entries", flush=True)
+    # the engine-start decisions persisted next to the plan (sections lm_head / decode_swiglu)
+    print("lm_head:", eng.runner.tune_lm_head(), flush=True)
+    print("decode_swiglu:", eng.runner.tune_swiglu(), flush=True)
     if COPY_TO:
         os.makedirs(COPY_TO, exist_ok=True)
         shutil.copy(DEFAULT_PLAN_FILE, COPY_TO)

@@ -322,12 +322,15 @@ def test_prefill_swiglu_used_by_model_path():
     assert not ops.use_prefill_swiglu(x[:256], w13)
 
 
-@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 5, 8, 12, 16])
 @pytest.mark.parametrize("N,K,split,rw", [(6144, 4096, 2, 8), (4100, 4096, 1, 4), (28672, 4096, 1, 4),
-                                          (1000, 14336, 4, 2), (300, 2048, 4, 1)])
+                                          (1000, 14336, 4, 2), (300, 2048, 4, 1), (128256, 4096, 2, 4)])
 def test_gemv_rows_vs_fp32(M, N, K, split, rw):
     """Row-streaming GEMV (csrc/gemm_skinny.hip gemv_rows_kernel): bf16 output and deferred fp32
-    partials against fp32 x @ w^T, ragged N (rows past N in the last wave)."""
+    partials against fp32 x @ w^T, ragged N (rows past N in the last wave); M 5..16 stage 8 / 16 X
+    rows (decode buckets 8 and 16)."""
+    if not ops.rows_ok(M, K, split):
+        pytest.skip("X slice over the LDS budget for this split")
     x = torch.randn(M, K, device=DEV, dtype=BF)
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(BF)
     want = x.float() @ w.float().t()
@@ -338,7 +341,7 @@ def test_gemv_rows_vs_fp32(M, N, K, split, rw):
         close(p.P.sum(0), want, atol=1e-3, rtol=1e-3)
 
 
-@pytest.mark.parametrize("M", [1, 4])
+@pytest.mark.parametrize("M", [1, 4, 8])
 def test_gemv_rows_swiglu_down_vs_fp32(M):
     """Batch-1..4 down projection with SiLU·mul in the row-streaming GEMV's X staging."""
     I, N = 14336, 4096
@@ -690,3 +693,53 @@ def test_gemm_mfma_swiglu_epilogue(M):
         _hip.check(lib.ka_gemm_mfma(y.data_ptr(), None, x.data_ptr(), w13i.data_ptr(), M, 2 * I, K, K, I, 1, cfg,
                                     ops.GM_EPI_SWIGLU, 0, ops._stream()), "gemm_mfma swiglu")
         close(y, want, atol=3e-2, rtol=3e-2)
+
+
+# ---- csrc/gemm_big.hip split tail (prefill projections: the partial last round of 256 x 256 tiles is
+# cut into K slices that hand their fp32 tiles to the last-arriving slice of the same XCD) ----
+def _gb_plan(M, N, K, epi):
+    full, tail = torch.zeros(1, dtype=torch.int32), torch.zeros(1, dtype=torch.int32)
+    ws = ops.gemm_big_ws(torch.device(DEV))
+    s = _hip.require().ka_gemm_big_plan(M, N, epi, K, ws.numel(), full.data_ptr(), tail.data_ptr())
+    return s, int(full), int(tail)
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 6144, 4096), (2944, 6144, 4096), (777, 6144, 4096), (4096, 4096, 4096),
+                                   (2900, 4096, 14336), (513, 1024, 512)])
+def test_gemm_big_linear_split_tail_vs_fp32(M, N, K):
+    """ops.linear_big (EPI_BF16) over shapes whose last round of tiles is split over K and over shapes
+    that need no split; full matrices against the fp32 reference, the counters left at zero (the
+    next launch of another shape reuses them) and the tail error word clear."""
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(BF)
+    want = x.float() @ w.float().t()
+    for _ in range(2):   # the second launch runs on counters the first one reset
+        got = ops.linear_big(x, w)
+        close(got, want, atol=3e-2, rtol=2e-2)
+    ws = ops.gemm_big_ws(torch.device(DEV))
+    assert int(ws[256:256 + 1024 * 32].view(torch.int32).abs().sum()) == 0
+    assert ops.gemm_big_err(torch.device(DEV)) == 0
+
+
+def test_gemm_big_split_tail_plans():
+    """The shapes the bench's mixed steps produce get a split tail where the last round is short."""
+    s, full, tail = _gb_plan(4096, 6144, 4096, 0)      # QKV: 384 tiles = 256 + 128
+    assert s > 1 and full == 256 and tail == 128
+    s, full, tail = _gb_plan(2944, 28672, 4096, 3)     # gate_up + SwiGLU: 12 x 112 = 1344 = 5 x 256 + 64
+    assert s > 1 and full == 1280 and tail == 64
+    assert _gb_plan(4096, 4096, 4096, 0)[0] == 1       # O: exactly one round
+
+
+@pytest.mark.parametrize("M", [2944, 1100, 4096])
+def test_gemm_big_swiglu_split_tail_vs_fp32(M):
+    """gate_up + SwiGLU epilogue with the split tail: silu(x g^T) * (x u^T) vs fp32 (the sum of the
+    slices goes through the nonlinearity, so a lost or doubled slice shows)."""
+    H, I = 4096, 14336
+    x = torch.randn(M, H, device=DEV, dtype=BF)
+    w13 = (torch.randn(2 * I, H, device=DEV) / math.sqrt(H)).to(BF)
+    g = x.float() @ w13[:I].float().t()
+    u = x.float() @ w13[I:].float().t()
+    want = torch.nn.functional.silu(g) * u
+    got = ops.linear_swiglu(x, w13)
+    close(got, want, atol=3e-2, rtol=3e-2)
+    assert ops.gemm_big_err(torch.device(DEV)) == 0

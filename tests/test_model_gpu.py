@@ -71,7 +71,40 @@ def test_llama_forward_hip_vs_reference():
     torch.testing.assert_close(h_hip.float(), h_ref.float(), atol=0.1, rtol=0.05)
 
 
-@pytest.mark.parametrize("B", [1, 4, 256])
+def test_llama_forward_hip_vs_reference_large_prefill():
+    """A prefill step of >= 1024 rows — the shape class of the bench's mixed steps — through the
+    prefill kernels the engine dispatches there (csrc/gemm_big.hip: QKV / O / down with the split
+    tail, gate_up with the SwiGLU epilogue; the 16-token RoPE + KV window kernel; the varlen
+    prefill attention) vs the same weights through the fp32 torch references."""
+    eng = _engine("llama3-8b-2l", graphs=False, max_batch=16, kv_cache_tokens=32768)
+    be = EngineLLM(eng, max_new_tokens=8)
+    queries = [f"{q} in namespace team-{i} sorted by creation time" for i, q in enumerate(QUERIES * 2)]
+    n_rows = sum(len(be.prompt_ids(q)) for q in queries)
+    assert n_rows >= 1024, n_rows
+    x = torch.zeros(n_rows, 4096, device="cuda", dtype=torch.bfloat16)
+    assert ops.use_prefill_swiglu(x, eng.runner.model.layers[0]["w13"])
+    assert ops.big_gemm_ok(x, eng.runner.model.layers[0]["wqkv"])
+    with torch.inference_mode():
+        h_hip = _prefill_hidden(eng, be, queries)
+        with ops.force_reference():
+            h_ref = _prefill_hidden(eng, be, queries)
+        lg_hip = eng.runner.model.logits(h_hip).float()
+        lg_ref = eng.runner.model.logits(h_ref).float()
+    cos = torch.nn.functional.cosine_similarity(lg_hip, lg_ref, dim=-1)
+    assert cos.min().item() > 0.995, cos
+    torch.testing.assert_close(h_hip.float(), h_ref.float(), atol=0.1, rtol=0.05)
+    # the same step with QKV / O / down on gemm_big as well (KA_PREFILL_GEMM=big)
+    saved, ops.PREFILL_GEMM = ops.PREFILL_GEMM, "big"
+    try:
+        assert ops.use_big_gemm(x, eng.runner.model.layers[0]["wqkv"])
+        with torch.inference_mode():
+            h_big = _prefill_hidden(eng, be, queries)
+    finally:
+        ops.PREFILL_GEMM = saved
+    torch.testing.assert_close(h_big.float(), h_ref.float(), atol=0.1, rtol=0.05)
+
+
+@pytest.mark.parametrize("B", [1, 4, 8, 16, 256])
 def test_decode_chain_vs_fp32_reference(B):
     """The real decode chain — autotuned GEMM plan (gemm_mfma kernels at M = 256 with bf16 split-K
     partials reduced inside the fused RoPE + KV-append + attention kernel and inside the fused
@@ -83,7 +116,7 @@ def test_decode_chain_vs_fp32_reference(B):
     partials are compared against."""
     from ai_agent_kubectl_amd.engine.sequence import Sequence
     from ai_agent_kubectl_amd.models.llama import AttnMeta
-    eng = _engine("llama3-8b-2l", graphs=True, buckets=(1, 4, 256), max_batch=256, kv_cache_tokens=65536)
+    eng = _engine("llama3-8b-2l", graphs=True, buckets=(1, 4, 8, 16, 256), max_batch=256, kv_cache_tokens=65536)
     be = EngineLLM(eng, max_new_tokens=40, ignore_eos=True)
     params = SamplingParams(max_new_tokens=40, ignore_eos=True)
     sch, r = eng.scheduler, eng.runner

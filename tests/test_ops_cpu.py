@@ -33,7 +33,9 @@ def test_linear_gm_swiglu_cpu_is_reference():
 
 def test_gemv_rows_rules_and_cpu_reference():
     assert ops.rows_ok(1, 4096, 1) and ops.rows_ok(4, 14336, 4) and ops.rows_ok(1, 14336, 1)
-    assert not ops.rows_ok(5, 4096, 1)            # M > 4: tiled kernels
+    assert ops.rows_ok(5, 4096, 1) and ops.rows_ok(16, 4096, 2)   # 8 / 16 staged rows
+    assert not ops.rows_ok(16, 4096, 1)           # 16 x 4096 x 2 B: over the 64 KB LDS budget
+    assert not ops.rows_ok(17, 4096, 4)           # M > 16: tiled kernels
     assert not ops.rows_ok(4, 14336, 1)           # X slice over the 64 KB LDS budget
     assert not ops.rows_ok(1, 4096, 3)            # K % (512 * split)
     x = torch.randn(2, 1024, dtype=torch.bfloat16)

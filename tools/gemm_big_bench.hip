@@ -67,6 +67,12 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int warm = getenv("GB_WARM") ? atoi(getenv("GB_WARM")) : 0;
+  // GB_TAIL=0: no split tail (the whole-tile schedule of rounds 1-3)
+  const int tail = getenv("GB_TAIL") ? atoi(getenv("GB_TAIL")) : 1;
+  const size_t ws_tail_bytes = ka_gemm_big_ws_bytes();
+  void* ws_tail = nullptr;
+  CK(hipMalloc(&ws_tail, ws_tail_bytes));
+  CK(hipMemset(ws_tail, 0, ws_tail_bytes));
   const int rounds = getenv("GB_ROUNDS") ? atoi(getenv("GB_ROUNDS")) : 3;
   int bad = 0;
 
@@ -120,7 +126,7 @@ int main(int argc, char** argv) {
       const bf16_t* w = W + (size_t)(r % nrot) * N * K;
       if (epi == 5) return ka_gemm_big_argmax(didx, dval, X, w, M, N, K, K, dmask, dmidx, words, 0, ws, st);
       if (part) return ka_gemm_big_splitk(P, X, w, M, N, K, K, split, epi == 2, 8, st);
-      return ka_gemm_big(Y, R, X, w, M, N, K, K, ldy, epi, gm, st);
+      return ka_gemm_big(Y, R, X, w, M, N, K, K, ldy, epi, gm, tail ? ws_tail : nullptr, tail ? ws_tail_bytes : 0, st);
     };
     auto blas = [&](int r) {
       const bf16_t* w = W + (size_t)(r % nrot) * N * K;
@@ -228,6 +234,15 @@ int main(int argc, char** argv) {
     std::sort(tm.begin(), tm.end());
     std::sort(tb.begin(), tb.end());
     const double fl = 2.0 * M * N * K;
+    int pf = 0, pt = 0;
+    const int ps = (epi == 0 || epi == 3 || epi == 4) && tail ? ka_gemm_big_plan(M, N, epi, K, ws_tail_bytes, &pf, &pt) : 1;
+    int terr = 0;
+    CK(hipMemcpy(&terr, ws_tail, 4, hipMemcpyDeviceToHost));
+    if (terr) {
+      printf("%s: split-tail error word set\n", argv[ci]);
+      bad = 1;
+    }
+    printf("tail s=%d (%d whole + %d split tiles) ", ps, pf, pt);
     printf("M=%5d N=%6d K=%5d epi=%d gm=%d : gemm_big %8.2f us %7.1f TF/s | rocBLAS %8.2f us %7.1f TF/s | "
            "ratio %.3f | maxerr %.3g (ref max %.3g)%s\n",
            M, N, K, epi, gm, tm[0], fl / (tm[0] * 1e-6) / 1e12, tb[0], fl / (tb[0] * 1e-6) / 1e12, tb[0] / tm[0], err,
