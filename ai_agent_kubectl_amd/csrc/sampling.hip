@@ -122,6 +122,35 @@ extern "C" int ka_argmax_finish(int* out_idx, float* out_val, const float* part_
   KA_CHECK_LAUNCH();
 }
 
+// Vocab-parallel greedy combine under TP (A3): vals / idxs [ranks][rows] all-gathered from every
+// rank's (max, global token id); out_idx[row] = the id of the largest value, the lowest id on ties
+// (= the lowest rank: each rank owns a contiguous vocab slice).  One lane per row.
+__global__ __launch_bounds__(256) void argmax_combine_kernel(int* __restrict__ out_idx, const float* __restrict__ vals,
+                                                             const int* __restrict__ idxs, int rows, int ranks) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= rows) return;
+  float best = vals[row];
+  int bidx = idxs[row];
+  for (int r = 1; r < ranks; ++r) {
+    const float v = vals[(size_t)r * rows + row];
+    const int ix = idxs[(size_t)r * rows + row];
+    if (v > best || (v == best && ix < bidx)) {
+      best = v;
+      bidx = ix;
+    }
+  }
+  out_idx[row] = bidx;
+}
+
+extern "C" int ka_argmax_combine(int* out_idx, const float* vals, const int* idxs, int rows, int ranks,
+                                 hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (ranks < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(argmax_combine_kernel, dim3((rows + 255) / 256), dim3(256), 0, stream, out_idx, vals, idxs, rows,
+                     ranks);
+  KA_CHECK_LAUNCH();
+}
+
 // slices > 1 needs a workspace of rows * slices floats + rows * slices ints (ka_argmax_slices).
 extern "C" int ka_argmax_slices(int rows, int vocab) {
   if (rows >= 128) return 1;

@@ -255,11 +255,17 @@ class ModelRunner:
                 best = (int(cfg), t_fu)
             else:
                 t_un = _time(lambda w: ops.silu_mul(ops.linear(x, w, defer_reduce=True)), ws)
-                best = (0, t_un)
+                fused = (0, float("inf"))
                 for cfg in ops.DECODE_SWIGLU_CFGS:
                     t = _time(lambda w: ops.linear_gm_swiglu(x, w, cfg), ws)
-                    if t < best[1]:
-                        best = (cfg, t)
+                    if t < fused[1]:
+                        fused = (cfg, t)
+                # the unfused path's gate_up is a hipBLASLt plan: the hand-written fused kernel is
+                # taken within the plan's margin too (ops/autotune.py BLAS_MARGIN)
+                from ..ops.autotune import BLAS_MARGIN
+                plan = ops.GEMM_PLAN.get((M, ws[0].shape[0], ws[0].shape[1]), ("blas",))
+                margin = BLAS_MARGIN if plan[0] == "blas" else 0.0
+                best = fused if fused[1] < t_un * (1.0 + margin) else (0, t_un)
             if best[0]:
                 ops.DECODE_SWIGLU_CFG[M] = best[0]
             report[M] = {"cfg": best[0], "fused_us": round(best[1], 1), "unfused_us": round(t_un, 1)}

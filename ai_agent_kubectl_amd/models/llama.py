@@ -76,6 +76,14 @@ class LlamaModel:
         # eager steps only: record `mark_event` when layer `mark_layer` starts (-1: never)
         self.mark_layer = -1
         self.mark_event = None
+        # small-batch decode: while attention, O-proj and the second norm run (HBM mostly idle), a
+        # side stream reads the first KA_DECODE_PREFETCH_MB of this layer's gate_up weights into the
+        # Infinity Cache so the gate_up GEMV starts on cache hits (fork / join inside the captured
+        # graph).  0 (default): off.
+        self.prefetch_bytes = int(float(os.environ.get("KA_DECODE_PREFETCH_MB", "0")) * (1 << 20))
+        self.prefetch_max_b = int(os.environ.get("KA_DECODE_PREFETCH_MAX_B", "4"))
+        self.prefetch_blocks = int(os.environ.get("KA_DECODE_PREFETCH_BLOCKS", "64"))
+        self._side = None
 
     def _layer(self, i):
         p = f"layers.{i}."
@@ -109,6 +117,7 @@ class LlamaModel:
             # the fused decode attention reduces bf16 QKV partials too (KA_BF16_QKV_PARTIALS);
             # rope_kv_write needs fp32 ones
             qkv = ops.linear(x, L["wqkv"], defer_reduce=True, bf16_partials=fused and self.bf16_qkv_partials)
+            side = self._fork_prefetch(L, T) if meta.is_decode else None
             if fused:
                 # RoPE + KV append + attention in one kernel (the rotated q never goes to HBM)
                 a = ops.decode_attention_rope(qkv, meta.positions, self.cos_sin, meta.slot_mapping, k_cache[li],
@@ -136,6 +145,8 @@ class LlamaModel:
             h = ops.linear(a.reshape(a.shape[0], self.hq * self.D), L["wo"], defer_reduce=fuse,
                            bf16_partials=self.bf16_partials)
             x = self._reduce_norm(h, L["ln2"], eps, residual, True)
+            if side is not None:   # join: the gate_up GEMV reads what the side stream prefetched
+                torch.cuda.current_stream(self.device).wait_stream(side)
             combined = False
             if cfg.is_moe:
                 h, combined = moe_forward(x, L, cfg, self.ep_rank, self.ep_size, meta.is_decode, self.comm)
@@ -164,6 +175,19 @@ class LlamaModel:
         # prefill: only the sequences' last rows are sampled, so only they are normed
         idx = meta.logits_indices
         return ops.rmsnorm(h.index_select(0, idx), self.W["norm"], eps, residual=residual.index_select(0, idx))
+
+    def _fork_prefetch(self, L, T: int):
+        """Start the side-stream prefetch of this layer's gate_up weights (see __init__); returns the
+        stream to join before gate_up, or None."""
+        if not self.prefetch_bytes or T > self.prefetch_max_b or not self.device.type == "cuda" or "w13" not in L:
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        side = self._side
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            ops.prefetch(L["w13"], self.prefetch_bytes, self.prefetch_blocks)
+        return side
 
     def _reduce_norm(self, h, w, eps, residual, pending: bool):
         """residual += all_reduce(h) (when `pending`); return rmsnorm(residual) * w.  TP = 1: h may be
@@ -206,5 +230,4 @@ class LlamaModel:
             return idx
         vals = self.comm.all_gather(val)                       # [t, S]
         idxs = self.comm.all_gather(idx)                       # [t, S]
-        best = torch.argmax(vals, dim=0)                       # first max = lowest rank = lowest id on ties
-        return idxs.gather(0, best.unsqueeze(0)).squeeze(0)
+        return ops.argmax_combine(vals, idxs)                  # lowest id (= lowest rank) on ties

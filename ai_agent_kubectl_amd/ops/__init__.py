@@ -256,6 +256,19 @@ def masked_argmax(logits: torch.Tensor, mask_bits: Optional[torch.Tensor], mask_
     return out_idx, out_val
 
 
+def argmax_combine(vals: torch.Tensor, idxs: torch.Tensor) -> torch.Tensor:
+    """TP vocab-parallel greedy combine: vals / idxs [ranks, S] (every rank's best value and global token
+    id) -> [S] int32 id of the largest value, the lowest id on ties (csrc/sampling.hip)."""
+    if _ref(vals):
+        return ref.argmax_combine(vals, idxs)
+    lib = require()
+    t, S = vals.shape
+    out = torch.empty(S, dtype=torch.int32, device=vals.device)
+    vals, idxs = vals.float().contiguous(), idxs.to(torch.int32).contiguous()
+    check(lib.ka_argmax_combine(_p(out), _p(vals), _p(idxs), S, t, _stream()), "argmax_combine")
+    return out
+
+
 GB_BN = 256   # csrc/gemm_big.hip output tile (weight rows)
 
 
@@ -492,7 +505,7 @@ DECODE_SWIGLU_CFGS = (2, 3, 4, 5, 12)
 def decode_swiglu_ok(x: torch.Tensor, w13: torch.Tensor) -> bool:
     M, K = x.shape
     return (x.is_contiguous() and w13.is_contiguous() and w13.shape[1] == K and K % 64 == 0
-            and w13.shape[0] % 32 == 0 and 32 <= M <= TILE_MAX_M)
+            and w13.shape[0] % 32 == 0 and 8 <= M <= TILE_MAX_M)
 
 
 def decode_swiglu_cfg(x: torch.Tensor, w13: torch.Tensor) -> int:

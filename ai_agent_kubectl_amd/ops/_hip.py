@@ -57,6 +57,7 @@ _SIGS = {
     "ka_gemm_big_err": [P, P],
     "ka_gemm_big_argmax": [P, P, P, P, I, I, I, I, P, P, I, I, P, P],
     "ka_argmax_finish": [P, P, P, P, I, I, I, P],
+    "ka_argmax_combine": [P, P, P, I, I, P],
     "ka_gm_bn": [I],
     "ka_gm_bm": [I],
     "ka_moe_align": [P, P, P, I, I, I, P],

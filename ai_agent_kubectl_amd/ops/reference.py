@@ -135,3 +135,12 @@ def moe_topk(router_logits: torch.Tensor, k: int):
     w, ids = torch.topk(p, k, dim=-1)
     w = w / w.sum(-1, keepdim=True)
     return w, ids.to(torch.int32)
+
+
+def argmax_combine(vals: torch.Tensor, idxs: torch.Tensor) -> torch.Tensor:
+    """[ranks, S] (value, global id) pairs -> [S] int32: the largest value, the lowest id on ties."""
+    v = vals.float()
+    best = v.max(dim=0, keepdim=True).values
+    big = torch.iinfo(torch.int32).max
+    cand = torch.where(v == best, idxs.to(torch.int64), torch.full_like(idxs, big, dtype=torch.int64))
+    return cand.min(dim=0).values.to(torch.int32)

@@ -1,0 +1,75 @@
+"""Decode-step device time per batch bucket, by replaying the captured decode hipGraph of the real
+Llama-3-8B engine (random weights, every row at a ~120-token context), with optional A/B settings
+that need a re-capture (e.g. the small-batch gate_up prefetch, KA_DECODE_PREFETCH_MB).
+
+    python scripts/bench_decode_graph.py [--buckets 1,4,256] [--prefetch "0:64,32:64,64:256"]
+
+--prefetch: comma list of MB:blocks settings, each re-captured and timed (0 = off).
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ai_agent_kubectl_amd.engine.builder import EngineOptions, build_engine  # noqa: E402
+from ai_agent_kubectl_amd.engine.sequence import SamplingParams, Sequence  # noqa: E402
+from ai_agent_kubectl_amd.llm.engine_backend import EngineLLM  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--buckets", default="1,4,256")
+    ap.add_argument("--prefetch", default="0:64")
+    ap.add_argument("--reps", type=int, default=100)
+    args = ap.parse_args()
+    buckets = tuple(int(b) for b in args.buckets.split(","))
+    eng = build_engine(EngineOptions(model=args.model, device="cuda", max_batch=max(buckets), graph_buckets=buckets,
+                                     kv_cache_tokens=65536, max_model_len=512))
+    r = eng.runner
+    be = EngineLLM(eng, max_new_tokens=64, ignore_eos=True)
+    sch = eng.scheduler
+    sch.gather_max_s = 0.0
+    params = SamplingParams(max_new_tokens=64, ignore_eos=True)
+    with torch.inference_mode():
+        for i in range(max(buckets)):
+            sch.add(Sequence(prompt_ids=be.prompt_ids(f"list pods in namespace team-{i}"), params=params))
+        while sch.waiting:   # prefill everyone (eager), so the decode rows have real contexts
+            b = sch.schedule()
+            eng._apply(b, r.execute(b))
+            sch.on_step_done(b)
+        batch = sch.schedule()
+        assert batch.is_decode
+    m = r.model
+    first = True
+    for setting in args.prefetch.split(","):
+        mb, blocks = (float(x) for x in setting.split(":"))
+        m.prefetch_bytes, m.prefetch_blocks = int(mb * (1 << 20)), int(blocks)
+        r.graphs.clear()
+        r.graph_pool = None
+        r.capture_graphs(autotune=first)   # the persisted GEMM plan / LM head / SwiGLU decisions, once
+        first = False
+        out = []
+        for B in buckets:
+            sub = type(batch)(batch.seqs[:B], [1] * B, is_decode=True)
+            r._pack_decode(sub, B)
+            n = r._off["bt"] + B * r.max_blocks
+            r.d_stage[:n].copy_(r.h_stage[:n])
+            g = r.graphs[B]
+            for _ in range(5):
+                g.replay()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            out.append(f"B={B}: {e0.elapsed_time(e1) / args.reps:.3f} ms")
+        print(f"prefetch {mb:g} MB x {int(blocks)} blocks: " + ", ".join(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -27,7 +27,7 @@ def test_linear_gm_swiglu_cpu_is_reference():
         ops.DECODE_SWIGLU_CFG.clear()
         ops.DECODE_SWIGLU_CFG.update(saved)
     assert ops.decode_swiglu_ok(x, w13)
-    assert not ops.decode_swiglu_ok(x[:16], w13)                       # M < 32: GEMV / skinny paths
+    assert ops.decode_swiglu_ok(x[:16], w13) and not ops.decode_swiglu_ok(x[:4], w13)   # M < 8: GEMV paths
     assert not ops.decode_swiglu_ok(x, torch.zeros(2 * 56, 256, dtype=torch.bfloat16))   # I % 16
 
 
@@ -48,3 +48,10 @@ def test_swiglu_gemm_shape_rules():
     assert ops.swiglu_gemm_ok(x, torch.zeros(2 * 14336, 4096, dtype=torch.bfloat16))
     assert not ops.swiglu_gemm_ok(x, torch.zeros(2 * 14336 + 128, 4096, dtype=torch.bfloat16))
     assert not ops.swiglu_gemm_ok(x[:, :4000], torch.zeros(256, 4000, dtype=torch.bfloat16))
+
+
+def test_argmax_combine_reference_ties_lowest_id():
+    """TP vocab-parallel combine (A3): the largest gathered value wins, the lowest global id on ties."""
+    vals = torch.tensor([[1.0, 5.0, 2.0], [3.0, 5.0, 2.0], [3.0, 1.0, 7.0]])
+    idxs = torch.tensor([[10, 11, 12], [1000, 1001, 1002], [2000, 2001, 2002]], dtype=torch.int32)
+    assert ops.argmax_combine(vals, idxs).tolist() == [1000, 11, 2002]
