@@ -84,6 +84,11 @@ class LlamaModel:
         self.prefetch_max_b = int(os.environ.get("KA_DECODE_PREFETCH_MAX_B", "4"))
         self.prefetch_blocks = int(os.environ.get("KA_DECODE_PREFETCH_BLOCKS", "64"))
         self._side = None
+        # batch-1 decode: every layer in ONE persistent launch (csrc/decode_persistent.hip) instead of
+        # ~7 kernels per layer.  KA_PERSISTENT_DECODE=1 enables it where the geometry allows.
+        self.persistent = os.environ.get("KA_PERSISTENT_DECODE", "0") == "1"
+        self._pd = None   # (layer pointer table, workspace)
+        self.persistent_stamps = None   # diagnostics: int64 [2, L, 16] phase timestamps (scripts/)
 
     def _layer(self, i):
         p = f"layers.{i}."
@@ -96,6 +101,8 @@ class LlamaModel:
         cfg = self.cfg
         eps = cfg.norm_eps
         h = ops.embedding(input_ids, self.W["embed"])
+        if meta.is_decode and input_ids.shape[0] == 1 and self.persistent_ok():
+            return self._forward_persistent(h, meta, k_cache, v_cache)
         residual = None
         pending = False   # h holds this rank's partial of a row-parallel output (TP all-reduce due)
         T = input_ids.shape[0]
@@ -175,6 +182,38 @@ class LlamaModel:
         # prefill: only the sequences' last rows are sampled, so only they are normed
         idx = meta.logits_indices
         return ops.rmsnorm(h.index_select(0, idx), self.W["norm"], eps, residual=residual.index_select(0, idx))
+
+    def persistent_ok(self) -> bool:
+        cfg = self.cfg
+        return (self.persistent and self.device.type == "cuda" and self._local_comm and not cfg.is_moe
+                and self.D == 128 and self.hq % self.hkv == 0 and self.hq // self.hkv <= 4
+                and cfg.hidden % 512 == 0 and cfg.intermediate % 512 == 0 and (self.hq * self.D) % 512 == 0
+                and cfg.hidden <= 16384 and cfg.intermediate <= 16384)
+
+    def _forward_persistent(self, h0, meta: AttnMeta, k_cache, v_cache) -> torch.Tensor:
+        """Batch-1 decode through the persistent all-layers kernel; returns the final-normed hidden
+        state [1, H] like `forward`."""
+        if self._pd is None:
+            ptrs = [[L[k].data_ptr() for k in ("wqkv", "wo", "w13", "w2", "ln1", "ln2")] for L in self.layers]
+            table = torch.tensor(ptrs, dtype=torch.int64, device=self.device)
+            lib = ops._hip.require()
+            ws = torch.zeros(int(lib.ka_decode_persistent_ws(self.cfg.hidden, self.hq, self.hkv,
+                                                               self.cfg.intermediate)),
+                             dtype=torch.uint8, device=self.device)
+            self._pd = (table, ws)
+        table, ws = self._pd
+        assert k_cache.shape[3] == 16, "persistent decode needs KV block 16"   # [L, NB, hkv, 16, 128]
+        hout = ops.decode_persistent(h0, table, len(self.layers), self.hq, self.hkv, self.cfg.intermediate,
+                                     self.cfg.norm_eps, self.scale, k_cache, v_cache, meta.positions,
+                                     meta.slot_mapping, meta.block_tables[0], meta.ctx_lens, self.cos_sin, ws,
+                                     self.persistent_stamps)
+        return ops.rmsnorm(hout, self.W["norm"], self.cfg.norm_eps)
+
+    def persistent_err(self) -> int:
+        """Error word of the last persistent launch (a grid wait that ran out; 0 in a correct run)."""
+        if self._pd is None:
+            return 0
+        return int(ops._hip.require().ka_decode_persistent_err(self._pd[1].data_ptr(), ops._stream()))
 
     def _fork_prefetch(self, L, T: int):
         """Start the side-stream prefetch of this layer's gate_up weights (see __init__); returns the

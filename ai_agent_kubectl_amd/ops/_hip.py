@@ -27,7 +27,7 @@ P = ctypes.c_void_p
 I = ctypes.c_int
 F = ctypes.c_float
 
-_RESTYPES = {"ka_gemm_big_ws_bytes": ctypes.c_size_t}
+_RESTYPES = {"ka_gemm_big_ws_bytes": ctypes.c_size_t, "ka_decode_persistent_ws": ctypes.c_size_t}
 
 _SIGS = {
     "ka_rmsnorm": [P, P, P, P, I, I, F, P],
@@ -58,6 +58,9 @@ _SIGS = {
     "ka_gemm_big_argmax": [P, P, P, P, I, I, I, I, P, P, I, I, P, P],
     "ka_argmax_finish": [P, P, P, P, I, I, I, P],
     "ka_argmax_combine": [P, P, P, I, I, P],
+    "ka_decode_persistent": [P, P, P, I, I, I, I, I, F, F, P, P, ctypes.c_long, P, P, P, P, P, P, P, P],
+    "ka_decode_persistent_ws": [I, I, I, I],
+    "ka_decode_persistent_err": [P, P],
     "ka_gm_bn": [I],
     "ka_gm_bm": [I],
     "ka_moe_align": [P, P, P, I, I, I, P],

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--buckets", default="1,4,256")
     ap.add_argument("--prefetch", default="0:64")
     ap.add_argument("--reps", type=int, default=100)
+    ap.add_argument("--persistent", default="0", help="comma list of 0/1: the batch-1 persistent decode kernel")
     args = ap.parse_args()
     buckets = tuple(int(b) for b in args.buckets.split(","))
     eng = build_engine(EngineOptions(model=args.model, device="cuda", max_batch=max(buckets), graph_buckets=buckets,
@@ -44,9 +45,11 @@ def main():
         assert batch.is_decode
     m = r.model
     first = True
-    for setting in args.prefetch.split(","):
+    settings = [(p, pe) for p in args.prefetch.split(",") for pe in args.persistent.split(",")]
+    for setting, pers in settings:
         mb, blocks = (float(x) for x in setting.split(":"))
         m.prefetch_bytes, m.prefetch_blocks = int(mb * (1 << 20)), int(blocks)
+        m.persistent = pers == "1"
         r.graphs.clear()
         r.graph_pool = None
         r.capture_graphs(autotune=first)   # the persisted GEMM plan / LM head / SwiGLU decisions, once
@@ -68,7 +71,33 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             out.append(f"B={B}: {e0.elapsed_time(e1) / args.reps:.3f} ms")
-        print(f"prefetch {mb:g} MB x {int(blocks)} blocks: " + ", ".join(out), flush=True)
+        print(f"prefetch {mb:g} MB x {int(blocks)} blocks, persistent {pers}: " + ", ".join(out), flush=True)
+        if m.persistent:
+            print("  persistent error word:", m.persistent_err(), flush=True)
+            # phase breakdown of one replay (workgroup 0 = a group's attention leader, 1 = not)
+            m.persistent_stamps = torch.zeros((2, len(m.layers), 16), dtype=torch.int64, device="cuda")
+            sub = type(batch)(batch.seqs[:1], [1], is_decode=True)
+            r._pack_decode(sub, 1)
+            r.d_stage[:r._off["bt"] + r.max_blocks].copy_(r.h_stage[:r._off["bt"] + r.max_blocks])
+            h0 = m.W["embed"][:1].clone()
+            from ai_agent_kubectl_amd.models.llama import AttnMeta
+            meta = AttnMeta(positions=r._view("pos", 1), slot_mapping=r._view("slots", 1),
+                            block_tables=r._view("bt", 1), ctx_lens=r._view("ctx", 1),
+                            logits_indices=r.d_logits_idx[:1], is_decode=True)
+            for _ in range(3):
+                m._forward_persistent(h0, meta, r.k_cache, r.v_cache)
+            torch.cuda.synchronize()
+            stv = m.persistent_stamps.cpu().double() / 100.0   # 100 MHz -> us
+            names = ["norm1", "qkv", "grp-wait", "attn", "barB", "O", "barC", "norm2", "gate_up", "barD", "down",
+                     "barE"]
+            for w in range(2):
+                d = stv[w, 1:-1, 1:13] - stv[w, 1:-1, 0:12]   # layers 1 .. L-2, consecutive stamp gaps
+                ok = (stv[w, 1:-1, 1:13] > 0)
+                parts = ", ".join(f"{n} {float(d[:, k][ok[:, k]].mean()) if ok[:, k].any() else float('nan'):.1f}"
+                                  for k, n in enumerate(names))
+                per_layer = float((stv[w, 1:-1, 12] - stv[w, 1:-1, 0]).mean())
+                print(f"  wg{w} per layer {per_layer:.1f} us: {parts}", flush=True)
+            m.persistent_stamps = None
 
 
 if __name__ == "__main__":

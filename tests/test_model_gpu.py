@@ -451,3 +451,77 @@ def test_mixtral_forward_hip_vs_reference():
     params = SamplingParams(max_new_tokens=6, ignore_eos=True)
     seqs = eng.generate_blocking([be.prompt_ids(q) for q in QUERIES[:3]], params, forced_prefix=be._forced)
     assert all(len(s.output_ids) == len(be._forced) + 6 for s in seqs)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_persistent_decode_matches_kernel_chain_and_fp32(graphs):
+    """csrc/decode_persistent.hip (every layer of a batch-1 decode step in one launch, grid-wide
+    arrival counters) against the per-kernel decode chain and the fp32 references, over 6 decode
+    steps of one sequence (the real Llama-3-8B layer geometry, 2 layers): hidden states within bf16
+    tolerance, the same KV appended, the tokens equal to the chain's, the error word clear — eagerly
+    and as the captured B = 1 hipGraph."""
+    from ai_agent_kubectl_amd.engine.sequence import Sequence
+    from ai_agent_kubectl_amd.models.llama import AttnMeta
+    eng = _engine("llama3-8b-2l", graphs=graphs, buckets=(1,), max_batch=1, kv_cache_tokens=8192)
+    be = EngineLLM(eng, max_new_tokens=16, ignore_eos=True)
+    sch, r = eng.scheduler, eng.runner
+    sch.gather_max_s = 0.0
+    m = r.model
+    with torch.inference_mode():
+        sch.add(Sequence(prompt_ids=be.prompt_ids("list all pods in kube-system"),
+                         params=SamplingParams(max_new_tokens=16, ignore_eos=True)))
+        b = sch.schedule()
+        eng._apply(b, r.execute(b))
+        sch.on_step_done(b)
+        for step in range(6):
+            batch = sch.schedule()
+            assert batch.is_decode and len(batch.seqs) == 1
+            r._pack_decode(batch, 1)
+            n = r._off["bt"] + r.max_blocks
+            r.d_stage[:n].copy_(r.h_stage[:n])
+            meta = AttnMeta(positions=r._view("pos", 1), slot_mapping=r._view("slots", 1),
+                            block_tables=r._view("bt", 1), ctx_lens=r._view("ctx", 1),
+                            logits_indices=r.d_logits_idx[:1], is_decode=True)
+            ids = r._view("ids", 1)
+            kc, vc = r.k_cache.clone(), r.v_cache.clone()
+            kr, vr = r.k_cache.clone(), r.v_cache.clone()
+            m.persistent = False
+            h_chain = m.forward(ids, meta, kc, vc)
+            with ops.force_reference():
+                h_ref = m.forward(ids, meta, kr, vr)
+            m.persistent = True
+            assert m.persistent_ok()
+            kp, vp = r.k_cache.clone(), r.v_cache.clone()
+            h_p = m.forward(ids, meta, kp, vp)
+            torch.cuda.synchronize()
+            assert m.persistent_err() == 0
+            torch.testing.assert_close(h_p.float(), h_ref.float(), atol=0.1, rtol=0.05)
+            torch.testing.assert_close(h_p.float(), h_chain.float(), atol=0.1, rtol=0.05)
+            slot = int(r._view("slots", 1)[0])
+            blk, off = slot // 16, slot % 16
+            # layer 0's appended K / V come from the same embedding: bf16-exact up to the norm's
+            # rounding; later layers see the fp32 residual stream (the chain's is bf16)
+            for kk, ref_c, tol in ((kp, kc, 2e-2), (vp, vc, 2e-2)):
+                got = kk[0, blk, :, off] if kk is kp else kk[0, blk, :, :, off]
+                want = ref_c[0, blk, :, off] if kk is kp else ref_c[0, blk, :, :, off]
+                torch.testing.assert_close(got.float(), want.float(), atol=tol, rtol=tol)
+            torch.testing.assert_close(kp[:, blk, :, off].float(), kc[:, blk, :, off].float(), atol=0.1, rtol=0.05)
+            torch.testing.assert_close(vp[:, blk, :, :, off].float(), vc[:, blk, :, :, off].float(), atol=0.1, rtol=0.05)
+            mask = r._view("mask", 1) if r.mask_bits is not None else None
+            tok = m.sample(h_p, r.mask_bits, mask)[:1].tolist()
+            if graphs:   # the captured B = 1 graph runs the same kernel: the same token
+                r.graphs.clear()
+                r.graph_pool = None
+                r.capture_graphs(autotune=False)
+                r._pack_decode(batch, 1)          # capture_graphs reset the staging image
+                r.d_stage[:n].copy_(r.h_stage[:n])
+                r.graphs[1].replay()
+                torch.cuda.synchronize()
+                assert r.d_out[:1].tolist() == tok, (step, r.d_out[:1].tolist(), tok)
+                assert m.persistent_err() == 0
+            else:   # the persistent step's cache writes are the real ones from here on
+                r.k_cache.copy_(kp)
+                r.v_cache.copy_(vp)
+            m.persistent = False
+            eng._apply(batch, tok)
+            sch.on_step_done(batch)
