@@ -30,7 +30,7 @@
 
 namespace pd {
 
-constexpr int NT = 512, NW = NT / 64, RING = 8, HD = 128, KBS = 16;
+constexpr int NT = 512, NW = NT / 64, RING = 16, HD = 128, KBS = 16;
 
 struct Layer {
   const bf16_t* wqkv;   // [(hq + 2 hkv) 128, H]
@@ -60,7 +60,7 @@ struct Args {
   bf16_t* attn;         // [hq 128]
   bf16_t* act;          // [I]
   int* sync;            // [0] grid arrivals, [1 .. hkv] group arrivals, [63] error word (zeroed per launch)
-  unsigned long long* stamps;   // diagnostics (nullptr: off): [2 workgroups][L][16] s_memrealtime (100 MHz)
+  unsigned long long* stamps;   // diagnostics (nullptr: off): [G workgroups][L][16] s_memrealtime (100 MHz)
 };
 
 KA_DEV float ld_sc1(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -114,54 +114,79 @@ KA_DEV float dot8(uint4 w, uint4 x, float acc) {
 }
 
 // One wave's weight stream over `n` rows of length K (row(i) -> global row index): 1 KB per load
-// instruction (64 lanes x 16 B along K), a RING-deep register ring.  start() issues the first RING
-// loads (before the wait for the activations); run() consumes them against x in LDS and calls
-// done(i, value) with the row's dot product (every lane holds it).
+// instruction (64 lanes x 16 B along K) by LDS-DMA (`buffer_load_dwordx4 ... lds`) into the wave's own
+// RING-slot LDS ring, so the bytes in flight cost no VGPRs (a register ring of the same depth spilled).
+// start() issues the first RING pieces (before the wait for the activations); run() waits for the
+// oldest piece (a static vmcnt: exactly RING pieces are always outstanding, the tail re-reads the last
+// chunk), reads it back (each lane its own 16 B), dots it with x in LDS and refills the slot.  Row
+// results stay in registers (lane i holds row i: no store may sit between the counted loads) and
+// are returned by run(); the caller writes them after drain().
 template <class RowFn>
 struct Stream {
   const bf16_t* W;
   int K, KC, total, lane;
   RowFn row;
-  uint4 w[RING];
+  uint32_t nbytes;
+  uint32_t ring;   // LDS byte address of this wave's ring (wave-uniform)
   int issued;
-  KA_DEV const bf16_t* addr(int j) const {
-    const int jj = min(j, total - 1);   // past the end: re-read the last chunk (static ring counts)
+  // wave-uniform part of piece j's byte offset (row start + chunk) -> soffset; the lane's 16 B -> voffset
+  KA_DEV uint32_t soff(int j) const {
+    const int jj = min(j, total - 1);
     const int i = jj / KC, c = jj - i * KC;
-    return W + (size_t)row(i) * K + c * 512 + lane * 8;
+    return __builtin_amdgcn_readfirstlane(((uint32_t)row(i) * (uint32_t)K + (uint32_t)(c * 512)) * 2u);
+  }
+  KA_DEV void issue(int j) {
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)(j % RING) * 1024u), so = soff(j);
+    const uint32_t off = (uint32_t)lane * 16u;
+    // rebuild the descriptor from wave-uniform (readfirstlane) halves so it lives in SGPRs
+    const uint64_t wp = (uint64_t)(uintptr_t)W;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)wp),
+                   hi = __builtin_amdgcn_readfirstlane((uint32_t)(wp >> 32)),
+                   nb = __builtin_amdgcn_readfirstlane(nbytes);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>((uintptr_t)(((uint64_t)hi << 32) | lo)), (short)0, (int)nb, 0x00020000);
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "s"(dst), "v"(off), "s"(rs), "s"(so)
+                 : "memory");
   }
   KA_DEV void start() {
     issued = 0;
     if (total <= 0) return;
 #pragma unroll
-    for (int r = 0; r < RING; ++r) w[r] = ld_w(addr(issued++));
+    for (int r = 0; r < RING; ++r) issue(issued++);
   }
-  template <class Done>
-  KA_DEV void run(const uint4* xs, Done done) {
-    if (total <= 0) return;
+  KA_DEV float run(const uint4* xs) {
+    float mine = 0.f;
+    if (total <= 0) return mine;
     float acc = 0.f;
     int cc = 0, ri = 0;
-    for (int base = 0; base < total; base += RING) {
+    for (int j = 0; j < total; ++j) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING - 1) : "memory");   // piece j has landed
+      uint4 w;
+      const uint32_t src = ring + (uint32_t)(j % RING) * 1024u + (uint32_t)lane * 16u;
+      asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(w) : "v"(src) : "memory");
+      issue(issued++);   // the slot is free again: refill it RING pieces ahead
+      acc = dot8(w, xs[cc * 64 + lane], acc);
+      if (++cc == KC) {
+        cc = 0;
+        float v = acc;
 #pragma unroll
-      for (int r = 0; r < RING; ++r) {
-        if (base + r < total) {
-          acc = dot8(w[r], xs[cc * 64 + lane], acc);
-          if (++cc == KC) {
-            cc = 0;
-            float v = acc;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            done(ri++, v);
-            acc = 0.f;
-          }
-          w[r] = ld_w(addr(issued++));
-        }
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == ri) mine = v;
+        ++ri;
+        acc = 0.f;
       }
     }
+    return mine;
   }
+  KA_DEV void drain() const { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 };
 template <class RowFn>
-KA_DEV Stream<RowFn> make_stream(const bf16_t* W, int K, int n, int lane, RowFn row) {
-  Stream<RowFn> s{W, K, K / 512, n * (K / 512), lane, row};
+KA_DEV Stream<RowFn> make_stream(const bf16_t* W, int N, int K, int n, int lane, uint32_t ring, RowFn row) {
+  Stream<RowFn> s{W, K, K / 512, n * (K / 512), lane, row, (uint32_t)N * (uint32_t)K * 2u, ring, 0};
   return s;
 }
 
@@ -184,9 +209,11 @@ KA_DEV void rmsnorm_to_lds(const Args& a, const bf16_t* g, bf16_t* xs, float* re
   __syncthreads();
 }
 
-// LDS layout (bytes): x / act staging [0, 32 KB); attention scratch from 32 KB; norm reduction at the end
-constexpr int LDS_X = 0, LDS_ATT = 32768, LDS_RED = 96 * 1024 - 64;
-constexpr int LDS_BYTES = 96 * 1024;   // > 80 KB: one workgroup per CU
+// LDS layout (bytes): x / act staging [0, 28 KB) (the attention leader's scratch reuses it: x is dead
+// between the QKV rows and the O rows); the waves' weight rings [28 KB, 28 KB + 8 x RING KB); the norm
+// reduction at the end.  > 80 KB: one workgroup per CU.
+constexpr int LDS_X = 0, LDS_ATT = 0, LDS_RING = 28 * 1024, LDS_RED = LDS_RING + NW * RING * 1024;
+constexpr int LDS_BYTES = LDS_RED + 64;
 
 __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint4 lds_u4[];
@@ -194,6 +221,9 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
   bf16_t* const xs = reinterpret_cast<bf16_t*>(lds + LDS_X);
   const uint4* const xs4 = reinterpret_cast<const uint4*>(lds + LDS_X);
   float* const red = reinterpret_cast<float*>(lds + LDS_RED);
+  // this wave's LDS-DMA weight ring (LDS byte address; dynamic LDS is the kernel's only LDS object)
+  const uint32_t ring = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)lds_u4 + LDS_RING + (threadIdx.x >> 6) * RING * 1024);
   const int G = gridDim.x, wg = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int gw = wg * NW + wave, nwaves = G * NW;
@@ -210,7 +240,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
   // residual := the embedding (each wave initialises the elements it owns)
   const int own0 = gw * h_per_wave, own1 = min(H, own0 + h_per_wave);
   for (int r = own0 + lane; r < own1; r += 64) st_sc1(a.res + r, bf2f(a.h0[r]));
-  arrive_wait(gcnt, ++nbar * G, err);
+  arrive(gcnt);
 
   const int qv0 = (in_grp * NW + wave) * qkv_per_wave;
   const int nq = max(0, min(qkv_rows, qv0 + qkv_per_wave) - qv0);
@@ -224,30 +254,35 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
   const int g0 = gw * i_per_wave, ng = max(0, min(I, g0 + i_per_wave) - g0);
   auto gu_row = [=](int i) { return (i & 1) ? I + g0 + (i >> 1) : g0 + (i >> 1); };   // gate, up, gate, ...
 
-  // phase stamps of workgroup 0 (its group's attention leader) and workgroup 1 (not a leader)
-  unsigned long long* const st = (a.stamps != nullptr && wg < 2 && tid == 0) ? a.stamps + (size_t)wg * a.L * 16 : nullptr;
+  // phase stamps of every workgroup (diagnostics)
+  unsigned long long* const st = (a.stamps != nullptr && tid == 0) ? a.stamps + (size_t)wg * a.L * 16 : nullptr;
 #define PD_STAMP(k) \
   do {              \
     if (st) st[l * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
   for (int l = 0; l < a.L; ++l) {
     const Layer Lw = a.layers[l];
-    PD_STAMP(0);
     // ---- P1: norm + QKV rows of the group ----
-    auto sq = make_stream(Lw.wqkv, H, nq, lane, qkv_row);
+    // The weight pieces of each phase are issued between the arrival and the wait of the barrier before
+    // it: after the arrival (its vmcnt(0) would otherwise hold the arrival back until they landed),
+    // in flight while the workgroup waits for the others.
+    auto sq = make_stream(Lw.wqkv, (hq + 2 * hkv) * HD, H, nq, lane, ring, qkv_row);
     sq.start();
+    wait_for(gcnt, ++nbar * G, err);
+    PD_STAMP(0);
+    if (st && l > 0) st[(l - 1) * 16 + 12] = st[l * 16];   // the previous layer's barrier E ends here
     rmsnorm_to_lds(a, Lw.ln1, xs, red);
     PD_STAMP(1);
-    sq.run(xs4, [&](int i, float v) {
-      if (lane == 0) {
-        const int r = qkv_row(i);   // pairs of rows share a 4-B word: write bf16 halves with a 2-B sc1 store
-        __hip_atomic_store(reinterpret_cast<unsigned short*>(a.qkv + r), __builtin_bit_cast(unsigned short, f2bf(v)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    });
+    {
+      const float v = sq.run(xs4);
+      sq.drain();
+      if (lane < nq)   // pairs of rows share a 4-B word: bf16 halves by 2-B sc1 stores
+        __hip_atomic_store(reinterpret_cast<unsigned short*>(a.qkv + qkv_row(lane)),
+                           __builtin_bit_cast(unsigned short, f2bf(v)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // the O rows' weights are issued now: they stream while the group waits and attention runs
     PD_STAMP(2);
-    auto so = make_stream(Lw.wo, hq * HD, no, lane, own_row);
+    auto so = make_stream(Lw.wo, H, hq * HD, no, lane, ring, own_row);
     arrive(a.sync + 1 + grp);   // this workgroup's QKV rows are published
     so.start();
     if (in_grp == 0) {
@@ -397,35 +432,35 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       reinterpret_cast<uint4*>(lds + LDS_X)[i] = v;
     }
     __syncthreads();
-    so.run(xs4, [&](int i, float v) {
-      if (lane == 0) {
-        const int r = own0 + i;
-        st_sc1(a.res + r, ld_sc1(a.res + r) + bf2f(f2bf(v)));
-      }
-    });
+    {
+      const float v = so.run(xs4);
+      so.drain();
+      if (lane < no) st_sc1(a.res + own0 + lane, ld_sc1(a.res + own0 + lane) + bf2f(f2bf(v)));
+    }
     PD_STAMP(6);
-    auto sg = make_stream(Lw.w13, H, 2 * ng, lane, gu_row);
+    auto sg = make_stream(Lw.w13, 2 * I, H, 2 * ng, lane, ring, gu_row);
+    arrive(gcnt);
     sg.start();
-    arrive_wait(gcnt, ++nbar * G, err);
+    wait_for(gcnt, ++nbar * G, err);
     PD_STAMP(7);
     // ---- P4: norm + gate / up -> act ----
     rmsnorm_to_lds(a, Lw.ln2, xs, red);
     PD_STAMP(8);
-    float gate = 0.f;
-    sg.run(xs4, [&](int i, float v) {
-      if (!(i & 1)) {
-        gate = bf2f(f2bf(v));
-      } else if (lane == 0) {
-        const float u = bf2f(f2bf(v));
-        const float s = gate / (1.f + __expf(-gate)) * u;
-        __hip_atomic_store(reinterpret_cast<unsigned short*>(a.act + g0 + (i >> 1)),
-                           __builtin_bit_cast(unsigned short, f2bf(s)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    });
+    {
+      const float v = sg.run(xs4);   // lane 2 k: gate row k, lane 2 k + 1: its up row
+      sg.drain();
+      const float u = bf2f(f2bf(__shfl_down(v, 1, 64)));
+      const float gt = bf2f(f2bf(v));
+      if (!(lane & 1) && (lane >> 1) < ng)
+        __hip_atomic_store(reinterpret_cast<unsigned short*>(a.act + g0 + (lane >> 1)),
+                           __builtin_bit_cast(unsigned short, f2bf(gt / (1.f + __expf(-gt)) * u)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
     PD_STAMP(9);
-    auto sd = make_stream(Lw.w2, I, no, lane, own_row);
+    auto sd = make_stream(Lw.w2, H, I, no, lane, ring, own_row);
+    arrive(gcnt);
     sd.start();
-    arrive_wait(gcnt, ++nbar * G, err);
+    wait_for(gcnt, ++nbar * G, err);
     PD_STAMP(10);
     // ---- P5: down rows -> residual ----
     for (int i = tid; i < I / 8; i += NT) {
@@ -438,17 +473,16 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       reinterpret_cast<uint4*>(lds + LDS_X)[i] = v;
     }
     __syncthreads();
-    sd.run(xs4, [&](int i, float v) {
-      if (lane == 0) {
-        const int r = own0 + i;
-        st_sc1(a.res + r, ld_sc1(a.res + r) + bf2f(f2bf(v)));
-      }
-    });
+    {
+      const float v = sd.run(xs4);
+      sd.drain();
+      if (lane < no) st_sc1(a.res + own0 + lane, ld_sc1(a.res + own0 + lane) + bf2f(f2bf(v)));
+    }
     PD_STAMP(11);
-    arrive_wait(gcnt, ++nbar * G, err);
-    PD_STAMP(12);
+    arrive(gcnt);   // the next layer's QKV pieces are issued before the wait (top of the loop)
   }
 #undef PD_STAMP
+  wait_for(gcnt, ++nbar * G, err);
   for (int r = own0 + lane; r < own1; r += 64) a.h_out[r] = f2bf(ld_sc1(a.res + r));
 }
 
@@ -471,7 +505,7 @@ extern "C" size_t ka_decode_persistent_ws(int H, int hq, int hkv, int I) {
 
 // Every layer of a batch-1 decode step (see the header).  layers: device array of L x 6 pointers
 // (wqkv, wo, w13, w2, ln1, ln2); pos / slot / ctx: device int [1]; bt: the sequence's block table;
-// stamps: nullptr, or [2][L][16] uint64 phase timestamps (diagnostics).
+// stamps: nullptr, or [G][L][16] uint64 phase timestamps (diagnostics; G <= the CU count).
 // Requirements: head_dim 128, block 16, hq % hkv == 0, hq / hkv <= 4, H % 512 == 0, I % 512 == 0,
 // hq * 128 % 512 == 0, the grid (the CU count, rounded down to a multiple of hkv) all resident.
 extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* layers, int L, int H, int hq, int hkv,

@@ -88,7 +88,7 @@ class LlamaModel:
         # ~7 kernels per layer.  KA_PERSISTENT_DECODE=1 enables it where the geometry allows.
         self.persistent = os.environ.get("KA_PERSISTENT_DECODE", "0") == "1"
         self._pd = None   # (layer pointer table, workspace)
-        self.persistent_stamps = None   # diagnostics: int64 [2, L, 16] phase timestamps (scripts/)
+        self.persistent_stamps = None   # diagnostics: int64 [CUs, L, 16] phase timestamps (scripts/)
 
     def _layer(self, i):
         p = f"layers.{i}."

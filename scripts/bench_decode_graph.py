@@ -74,8 +74,9 @@ def main():
         print(f"prefetch {mb:g} MB x {int(blocks)} blocks, persistent {pers}: " + ", ".join(out), flush=True)
         if m.persistent:
             print("  persistent error word:", m.persistent_err(), flush=True)
-            # phase breakdown of one replay (workgroup 0 = a group's attention leader, 1 = not)
-            m.persistent_stamps = torch.zeros((2, len(m.layers), 16), dtype=torch.int64, device="cuda")
+            # phase breakdown of one launch, every workgroup (stamp k = the end of phase k - 1)
+            ncu = torch.cuda.get_device_properties(0).multi_processor_count
+            m.persistent_stamps = torch.zeros((ncu, len(m.layers), 16), dtype=torch.int64, device="cuda")
             sub = type(batch)(batch.seqs[:1], [1], is_decode=True)
             r._pack_decode(sub, 1)
             r.d_stage[:r._off["bt"] + r.max_blocks].copy_(r.h_stage[:r._off["bt"] + r.max_blocks])
@@ -88,15 +89,30 @@ def main():
                 m._forward_persistent(h0, meta, r.k_cache, r.v_cache)
             torch.cuda.synchronize()
             stv = m.persistent_stamps.cpu().double() / 100.0   # 100 MHz -> us
+            G = int((stv[:, 1, 0] > 0).sum())
+            stv = stv[:G, 1:-1]                                 # layers 1 .. L-2
             names = ["norm1", "qkv", "grp-wait", "attn", "barB", "O", "barC", "norm2", "gate_up", "barD", "down",
                      "barE"]
-            for w in range(2):
-                d = stv[w, 1:-1, 1:13] - stv[w, 1:-1, 0:12]   # layers 1 .. L-2, consecutive stamp gaps
-                ok = (stv[w, 1:-1, 1:13] > 0)
-                parts = ", ".join(f"{n} {float(d[:, k][ok[:, k]].mean()) if ok[:, k].any() else float('nan'):.1f}"
-                                  for k, n in enumerate(names))
-                per_layer = float((stv[w, 1:-1, 12] - stv[w, 1:-1, 0]).mean())
-                print(f"  wg{w} per layer {per_layer:.1f} us: {parts}", flush=True)
+            per_layer = float((stv[:, :, 12] - stv[:, :, 0]).mean())
+            print(f"  {G} workgroups, per layer {per_layer:.1f} us", flush=True)
+            for k, n in enumerate(names):
+                ok = (stv[:, :, k + 1] > 0) & (stv[:, :, k] > 0)
+                if not ok.any():
+                    continue
+                d = (stv[:, :, k + 1] - stv[:, :, k])[ok]
+                # end-time spread across the grid at this stamp (relative to the layer's first stamp)
+                endt = (stv[:, :, k + 1] - stv[:, :, 0].min(dim=0).values)
+                print(f"  {n:9s} mean {float(d.mean()):6.1f}  p10 {float(d.quantile(0.1)):6.1f}  "
+                      f"p90 {float(d.quantile(0.9)):6.1f}  max {float(d.max()):6.1f}   end: "
+                      f"min {float(endt.min(dim=0).values.mean()):6.1f} max {float(endt.max(dim=0).values.mean()):6.1f}",
+                      flush=True)
+            # per-XCD (wg % 8) mean gate_up / down durations: is the skew a fabric effect?
+            for k, n in ((8, "gate_up"), (10, "down")):
+                d = stv[:, :, k + 1] - stv[:, :, k]
+                xs = [float(d[x::8].mean()) for x in range(8)]
+                print(f"  {n} by XCD: " + " ".join(f"{v:.1f}" for v in xs), flush=True)
+            slow = (stv[:, :, 9] - stv[:, :, 8]).mean(dim=1)
+            print("  slowest gate_up workgroups:", [int(i) for i in slow.argsort(descending=True)[:12]], flush=True)
             m.persistent_stamps = None
 
 
