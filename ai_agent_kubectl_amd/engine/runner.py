@@ -252,7 +252,8 @@ class ModelRunner:
                 continue
             if key(M) in saved:
                 cfg, t_fu, t_un = saved[key(M)]
-                best = (int(cfg), t_fu)
+                best = (int(cfg), t_fu if int(cfg) else t_un)
+                fused = (int(cfg), t_fu)
             else:
                 t_un = _time(lambda w: ops.silu_mul(ops.linear(x, w, defer_reduce=True)), ws)
                 fused = (0, float("inf"))
@@ -268,7 +269,8 @@ class ModelRunner:
                 best = fused if fused[1] < t_un * (1.0 + margin) else (0, t_un)
             if best[0]:
                 ops.DECODE_SWIGLU_CFG[M] = best[0]
-            report[M] = {"cfg": best[0], "fused_us": round(best[1], 1), "unfused_us": round(t_un, 1)}
+            # fused_us: the fastest SwiGLU-epilogue configuration's time, whether or not it was taken
+            report[M] = {"cfg": best[0], "fused_us": round(fused[1], 1), "unfused_us": round(t_un, 1)}
         if mode == "write":
             save_section(path, "decode_swiglu", {key(M): [r["cfg"], r["fused_us"], r["unfused_us"]]
                                                 for M, r in report.items()})
