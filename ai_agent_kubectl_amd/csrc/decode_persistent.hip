@@ -30,7 +30,7 @@
 
 namespace pd {
 
-constexpr int NT = 512, NW = NT / 64, RING = 16, HD = 128, KBS = 16;
+constexpr int NT = 512, NW = NT / 64, RING = 16, HD = 128, KBS = 16, NT_ = NT;
 
 struct Layer {
   const bf16_t* wqkv;   // [(hq + 2 hkv) 128, H]
@@ -59,7 +59,7 @@ struct Args {
   bf16_t* qkv;          // [(hq + 2 hkv) 128]
   bf16_t* attn;         // [hq 128]
   bf16_t* act;          // [I]
-  int* sync;            // [0] grid arrivals, [1 .. hkv] group arrivals, [63] error word (zeroed per launch)
+  int* sync;            // SYNC_BYTES: grid arrival shards, group arrivals, the error word (zeroed per launch)
   unsigned long long* stamps;   // diagnostics (nullptr: off): [G workgroups][L][16] s_memrealtime (100 MHz)
 };
 
@@ -71,11 +71,46 @@ KA_DEV uint32_t ld_sc1u(const bf16_t* p) {
 KA_DEV void st_sc1u(bf16_t* p, uint32_t v) {
   __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+KA_DEV const bf16_t* uniform_ptr(const bf16_t* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const bf16_t*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+}
+
+// Four 16-B sc1 loads in flight, one wait (hand-off table row 1 admits 16-B sc1 loads of bytes stored
+// sc1 in 4-B words); the addresses must all be valid (callers clamp).  The wait also covers the
+// caller's weight pieces in flight — staging runs right after a barrier, when they have landed.
+KA_DEV void ld4_sc1(const uint4* p0, const uint4* p1, const uint4* p2, const uint4* p3, uint4 (&o)[4]) {
+  asm volatile(
+      "global_load_dwordx4 %0, %4, off sc1\n\tglobal_load_dwordx4 %1, %5, off sc1\n\t"
+      "global_load_dwordx4 %2, %6, off sc1\n\tglobal_load_dwordx4 %3, %7, off sc1\n\ts_waitcnt vmcnt(0)"
+      : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3])
+      : "v"(p0), "v"(p1), "v"(p2), "v"(p3)
+      : "memory");
+}
+// n16 16-B words of a handed-off activation (sc1) -> LDS, 4 loads per lane in flight
+KA_DEV void stage_sc1(uint4* dst, const void* src, int n16) {
+  const uint4* sp = static_cast<const uint4*>(src);
+  for (int b0 = 0; b0 < n16; b0 += 4 * NT_) {
+    const int i0 = b0 + (int)threadIdx.x;
+    uint4 o[4];
+    ld4_sc1(sp + min(i0, n16 - 1), sp + min(i0 + NT_, n16 - 1), sp + min(i0 + 2 * NT_, n16 - 1),
+            sp + min(i0 + 3 * NT_, n16 - 1), o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i0 + k * NT_ < n16) dst[i0 + k * NT_] = o[k];
+  }
+}
 
 // Arrival: every wave's stores drained, a workgroup barrier, then one lane adds (MI355X_MICROARCH.md
 // hand-off table, row 1: the add comes after the wait of every wave it signals for).
+// vmcnt(0) expcnt(7) lgkmcnt(15) as a builtin: hipcc sees the scoreboard empty after it.  Placed where
+// the wave's vector memory has drained anyway (arrivals, after handed-off loads), so that no stale
+// "pending" state reaches a streaming loop, where hipcc would put an s_waitcnt vmcnt(0) — a ring
+// drain — into every iteration.
+KA_DEV void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 KA_DEV void arrive(int* cnt) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  vm_drain();
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -95,9 +130,32 @@ KA_DEV void wait_for(const int* cnt, int target, int* err) {
   }
   __syncthreads();
 }
-KA_DEV void arrive_wait(int* cnt, int target, int* err) {
-  arrive(cnt);
-  wait_for(cnt, target, err);
+// Sync words, each counter on a 128-B line of its own: the grid arrival counter in SH shards (workgroup
+// wg adds to shard wg % SH: the workgroups of one XCD under round-robin placement; one unsharded
+// counter serialises 256 adds at ~12 ns each, MI355X_MICROARCH.md price list, fanin / barrier-xcd),
+// the KV groups' arrival counters, the error word.
+constexpr int SH = 8, SYNC_BYTES = 4096, SYNC_GROUP = 256, SYNC_ERR = 1008;
+KA_DEV int* grid_shard(int* sync, int wg) { return sync + 32 * (wg % SH); }
+// Grid wait: lanes 0 .. SH-1 of wave 0 poll one shard each (sc1 loads: hand-off table row 1, every
+// shard of a sharded counter), until every shard holds nbar x its workgroup count.
+KA_DEV void wait_grid(const int* sync, int nbar, int G, int* err) {
+  if (threadIdx.x < 64) {
+    const int s = threadIdx.x;
+    const bool mine = s < SH && s < G;
+    const int target = mine ? nbar * ((G - s + SH - 1) / SH) : 0;
+    int spins = 0;
+    while (true) {
+      const bool ok = !mine || __hip_atomic_load(sync + 32 * s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(2);
+      if ((++spins & 255) == 0 &&
+          (spins > (1 << 20) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        if (s == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
 }
 
 KA_DEV uint4 ld_w(const bf16_t* p) {
@@ -113,14 +171,26 @@ KA_DEV float dot8(uint4 w, uint4 x, float acc) {
   return acc;
 }
 
+// Sum over the 64 lanes as a wave-uniform value: the 16-lane rows by DPP, the four row sums by
+// v_readlane (no LDS round trip, unlike __shfl_xor's ds_bpermute)
+KA_DEV float wave_total(float v) {
+  v = row16_sum(v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0)) +
+         __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16)) +
+         __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32)) +
+         __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+}
+
 // One wave's weight stream over `n` rows of length K (row(i) -> global row index): 1 KB per load
 // instruction (64 lanes x 16 B along K) by LDS-DMA (`buffer_load_dwordx4 ... lds`) into the wave's own
 // RING-slot LDS ring, so the bytes in flight cost no VGPRs (a register ring of the same depth spilled).
-// start() issues the first RING pieces (before the wait for the activations); run() waits for the
-// oldest piece (a static vmcnt: exactly RING pieces are always outstanding, the tail re-reads the last
-// chunk), reads it back (each lane its own 16 B), dots it with x in LDS and refills the slot.  Row
-// results stay in registers (lane i holds row i: no store may sit between the counted loads) and
-// are returned by run(); the caller writes them after drain().
+// start() issues the first RING pieces (before the wait for the activations); run() takes the pieces
+// two at a time: waits for them (a static vmcnt: exactly RING pieces are always outstanding, the tail
+// re-reads the last chunk), reads both and their x chunks back from LDS under one lgkmcnt wait,
+// refills the two slots and dots.  Row results stay in registers (lane i holds row i: no store may sit
+// between the counted loads) and are returned by run(); the caller writes them after drain().
+// Every instruction between the counted loads is asm or VALU / SALU: a compiler-visible vector-memory
+// access there would get an s_waitcnt vmcnt(0) from hipcc — a drain of the whole ring.
 template <class RowFn>
 struct Stream {
   const bf16_t* W;
@@ -128,57 +198,77 @@ struct Stream {
   RowFn row;
   uint32_t nbytes;
   uint32_t ring;   // LDS byte address of this wave's ring (wave-uniform)
-  int issued;
-  // wave-uniform part of piece j's byte offset (row start + chunk) -> soffset; the lane's 16 B -> voffset
-  KA_DEV uint32_t soff(int j) const {
-    const int jj = min(j, total - 1);
-    const int i = jj / KC, c = jj - i * KC;
-    return __builtin_amdgcn_readfirstlane(((uint32_t)row(i) * (uint32_t)K + (uint32_t)(c * 512)) * 2u);
-  }
-  KA_DEV void issue(int j) {
-    const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)(j % RING) * 1024u), so = soff(j);
+  int issued, ni, nc;   // pieces issued; row / chunk of the next piece to issue
+  KA_DEV void issue() {
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)(issued & (RING - 1)) * 1024u);
+    // wave-uniform part of the byte offset (row start + chunk) -> soffset; the lane's 16 B -> voffset
+    const uint32_t so = __builtin_amdgcn_readfirstlane(((uint32_t)row(ni) * (uint32_t)K + (uint32_t)(nc * 512)) * 2u);
     const uint32_t off = (uint32_t)lane * 16u;
-    // rebuild the descriptor from wave-uniform (readfirstlane) halves so it lives in SGPRs
-    const uint64_t wp = (uint64_t)(uintptr_t)W;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)wp),
-                   hi = __builtin_amdgcn_readfirstlane((uint32_t)(wp >> 32)),
-                   nb = __builtin_amdgcn_readfirstlane(nbytes);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>((uintptr_t)(((uint64_t)hi << 32) | lo)), (short)0, (int)nb, 0x00020000);
+    // W is wave-uniform (uniform_ptr at the layer's top): the descriptor lives in SGPRs
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(W), (short)0,
+                                                                        (int)nbytes, 0x00020000);
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
                  "s_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "s"(dst), "v"(off), "s"(rs), "s"(so)
                  : "memory");
+    if (++issued < total && ++nc == KC) {   // past the end: the last piece again (keeps the count static)
+      nc = 0;
+      ++ni;
+    }
   }
   KA_DEV void start() {
-    issued = 0;
+    issued = ni = nc = 0;
     if (total <= 0) return;
 #pragma unroll
-    for (int r = 0; r < RING; ++r) issue(issued++);
+    for (int r = 0; r < RING; ++r) issue();
   }
-  KA_DEV float run(const uint4* xs) {
+  // xaddr: LDS byte address of x (K bf16)
+  KA_DEV float run(uint32_t xaddr) {
     float mine = 0.f;
     if (total <= 0) return mine;
     float acc = 0.f;
     int cc = 0, ri = 0;
-    for (int j = 0; j < total; ++j) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING - 1) : "memory");   // piece j has landed
-      uint4 w;
-      const uint32_t src = ring + (uint32_t)(j % RING) * 1024u + (uint32_t)lane * 16u;
-      asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(w) : "v"(src) : "memory");
-      issue(issued++);   // the slot is free again: refill it RING pieces ahead
-      acc = dot8(w, xs[cc * 64 + lane], acc);
+    const uint32_t lo16 = (uint32_t)lane * 16u;
+    auto finish = [&]() {
       if (++cc == KC) {
         cc = 0;
-        float v = acc;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        const float v = wave_total(acc);
         if (lane == ri) mine = v;
         ++ri;
         acc = 0.f;
       }
+    };
+    int j = 0;
+    for (; j + 1 < total; j += 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING - 2) : "memory");   // pieces j, j + 1 have landed
+      const int cc1 = cc + 1 == KC ? 0 : cc + 1;
+      uint4 w0, w1, x0, x1;
+      asm volatile(
+          "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(w0), "=&v"(w1), "=&v"(x0), "=&v"(x1)
+          : "v"(ring + (uint32_t)(j & (RING - 1)) * 1024u + lo16), "v"(ring + (uint32_t)((j + 1) & (RING - 1)) * 1024u + lo16),
+            "v"(xaddr + (uint32_t)cc * 1024u + lo16), "v"(xaddr + (uint32_t)cc1 * 1024u + lo16)
+          : "memory");
+      issue();   // both slots are free again: refill them RING pieces ahead
+      issue();
+      acc = dot8(w0, x0, acc);
+      finish();
+      acc = dot8(w1, x1, acc);
+      finish();
+    }
+    if (j < total) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING - 1) : "memory");
+      uint4 w0, x0;
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(w0), "=&v"(x0)
+                   : "v"(ring + (uint32_t)(j & (RING - 1)) * 1024u + lo16), "v"(xaddr + (uint32_t)cc * 1024u + lo16)
+                   : "memory");
+      issue();
+      acc = dot8(w0, x0, acc);
+      finish();
     }
     return mine;
   }
@@ -186,17 +276,30 @@ struct Stream {
 };
 template <class RowFn>
 KA_DEV Stream<RowFn> make_stream(const bf16_t* W, int N, int K, int n, int lane, uint32_t ring, RowFn row) {
-  Stream<RowFn> s{W, K, K / 512, n * (K / 512), lane, row, (uint32_t)N * (uint32_t)K * 2u, ring, 0};
+  Stream<RowFn> s{W, K, K / 512, n * (K / 512), lane, row, (uint32_t)N * (uint32_t)K * 2u, ring, 0, 0, 0};
   return s;
 }
 
-// x[i] = bf16(res[i] * rstd * g[i]) into LDS (every workgroup; res read with sc1 loads)
+// x[i] = bf16(res[i] * rstd * g[i]) into LDS (every workgroup): the fp32 residual read once by 16-B
+// sc1 loads (H / 4 words, <= 8 per lane at H <= 16384) and held in registers for the scaling pass
 KA_DEV void rmsnorm_to_lds(const Args& a, const bf16_t* g, bf16_t* xs, float* red) {
-  const int H = a.H;
+  const int H = a.H, n16 = H / 4;
+  const uint4* rp = reinterpret_cast<const uint4*>(a.res);
+  uint4 rv[8];
+  ld4_sc1(rp + min((int)threadIdx.x, n16 - 1), rp + min((int)threadIdx.x + NT, n16 - 1),
+          rp + min((int)threadIdx.x + 2 * NT, n16 - 1), rp + min((int)threadIdx.x + 3 * NT, n16 - 1),
+          *reinterpret_cast<uint4(*)[4]>(&rv[0]));
+  if (n16 > 4 * NT)
+    ld4_sc1(rp + min((int)threadIdx.x + 4 * NT, n16 - 1), rp + min((int)threadIdx.x + 5 * NT, n16 - 1),
+            rp + min((int)threadIdx.x + 6 * NT, n16 - 1), rp + min((int)threadIdx.x + 7 * NT, n16 - 1),
+            *reinterpret_cast<uint4(*)[4]>(&rv[4]));
   float ss = 0.f;
-  for (int i = threadIdx.x; i < H; i += NT) {
-    const float v = ld_sc1(a.res + i);
-    ss += v * v;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if ((int)threadIdx.x + k * NT < n16) {
+      const float4 f = __builtin_bit_cast(float4, rv[k]);
+      ss += f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+    }
   }
   ss = wave_sum(ss);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
@@ -205,7 +308,18 @@ KA_DEV void rmsnorm_to_lds(const Args& a, const bf16_t* g, bf16_t* xs, float* re
 #pragma unroll
   for (int w = 0; w < NW; ++w) tot += red[w];
   const float rstd = rsqrtf(tot / (float)H + a.eps);
-  for (int i = threadIdx.x; i < H; i += NT) xs[i] = f2bf(ld_sc1(a.res + i) * rstd * bf2f(g[i]));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int i = (int)threadIdx.x + k * NT;
+    if (i < n16) {
+      const float4 f = __builtin_bit_cast(float4, rv[k]);
+      const uint2 gw = *reinterpret_cast<const uint2*>(g + 4 * i);
+      uint2 o;
+      o.x = pack2(f.x * rstd * lo_f(gw.x), f.y * rstd * hi_f(gw.x));
+      o.y = pack2(f.z * rstd * lo_f(gw.y), f.w * rstd * hi_f(gw.y));
+      *reinterpret_cast<uint2*>(xs + 4 * i) = o;
+    }
+  }
   __syncthreads();
 }
 
@@ -213,15 +327,17 @@ KA_DEV void rmsnorm_to_lds(const Args& a, const bf16_t* g, bf16_t* xs, float* re
 // between the QKV rows and the O rows); the waves' weight rings [28 KB, 28 KB + 8 x RING KB); the norm
 // reduction at the end.  > 80 KB: one workgroup per CU.
 constexpr int LDS_X = 0, LDS_ATT = 0, LDS_RING = 28 * 1024, LDS_RED = LDS_RING + NW * RING * 1024;
-constexpr int LDS_BYTES = LDS_RED + 64;
+constexpr int LDS_OUT = LDS_RED + 64, LDS_BYTES = LDS_OUT + 1024;   // LDS_OUT: a phase's bf16 row results
 
 __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint4 lds_u4[];
   char* const lds = reinterpret_cast<char*>(lds_u4);
   bf16_t* const xs = reinterpret_cast<bf16_t*>(lds + LDS_X);
-  const uint4* const xs4 = reinterpret_cast<const uint4*>(lds + LDS_X);
   float* const red = reinterpret_cast<float*>(lds + LDS_RED);
+  bf16_t* const ob = reinterpret_cast<bf16_t*>(lds + LDS_OUT);
   // this wave's LDS-DMA weight ring (LDS byte address; dynamic LDS is the kernel's only LDS object)
+  const uint32_t xaddr = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)lds_u4 + LDS_X);
   const uint32_t ring = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)lds_u4 + LDS_RING + (threadIdx.x >> 6) * RING * 1024);
   const int G = gridDim.x, wg = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -233,24 +349,38 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
   const int qkv_per_wave = (qkv_rows + per_group * NW - 1) / (per_group * NW);
   const int h_per_wave = (H + nwaves - 1) / nwaves;         // O / down rows = owned residual elements
   const int i_per_wave = (I + nwaves - 1) / nwaves;         // gate (and up) rows
-  int* const gcnt = a.sync;
-  int* const err = a.sync + 63;
+  int* const gcnt = grid_shard(a.sync, wg);
+  int* const err = a.sync + SYNC_ERR;
   int nbar = 0;   // grid barriers passed
 
   // residual := the embedding (each wave initialises the elements it owns)
   const int own0 = gw * h_per_wave, own1 = min(H, own0 + h_per_wave);
+  // the token's position / slot / context (fixed for the launch) and the attention loop's trip count
+  const int p = a.pos[0], slot = a.slot[0], ctx = a.ctx[0];
+  const int ncached = ctx - 1, nblk = (ncached + KBS - 1) / KBS;
   for (int r = own0 + lane; r < own1; r += 64) st_sc1(a.res + r, bf2f(a.h0[r]));
   arrive(gcnt);
 
   const int qv0 = (in_grp * NW + wave) * qkv_per_wave;
   const int nq = max(0, min(qkv_rows, qv0 + qkv_per_wave) - qv0);
-  auto qkv_row = [=](int i) {   // group-local row -> row of wqkv (q heads of the group, its k, its v)
-    const int r = qv0 + i;
+  auto qkv_grow = [=](int r) {   // group-local row -> row of wqkv (q heads of the group, its k, its v)
     return r < Gq * HD ? grp * Gq * HD + r : r < (Gq + 1) * HD ? hq * HD + grp * HD + (r - Gq * HD)
                                                             : (hq + hkv) * HD + grp * HD + (r - (Gq + 1) * HD);
   };
+  auto qkv_row = [=](int i) { return qkv_grow(qv0 + i); };
+  // the workgroup's group-local QKV rows and act elements: even starts and counts, so their bf16 results
+  // leave in 4-B sc1 stores of row pairs (every segment boundary of qkv_grow is even too)
+  const int wq0 = in_grp * NW * qkv_per_wave, wqn = max(0, min(qkv_rows, wq0 + NW * qkv_per_wave) - wq0);
+  const int wa0 = wg * NW * i_per_wave, wan = max(0, min(I, wa0 + NW * i_per_wave) - wa0);
   const int no = max(0, own1 - own0);
   auto own_row = [=](int i) { return own0 + i; };
+  // O rows go to the workgroups that run no attention only: a leader's context loads would otherwise
+  // queue behind its own O weight pieces (issued before the attention).  O's residual element != its
+  // down owner is fine: each phase has one writer per element and a barrier after it.
+  const int o_per_wave = (H + (G - hkv) * NW - 1) / ((G - hkv) * NW);
+  const int ow0 = in_grp == 0 ? 0 : ((grp * (per_group - 1) + in_grp - 1) * NW + wave) * o_per_wave;
+  const int n_o = in_grp == 0 ? 0 : max(0, min(H, ow0 + o_per_wave) - ow0);
+  auto o_row = [=](int i) { return ow0 + i; };
   const int g0 = gw * i_per_wave, ng = max(0, min(I, g0 + i_per_wave) - g0);
   auto gu_row = [=](int i) { return (i & 1) ? I + g0 + (i >> 1) : g0 + (i >> 1); };   // gate, up, gate, ...
 
@@ -261,33 +391,42 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     if (st) st[l * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
   for (int l = 0; l < a.L; ++l) {
-    const Layer Lw = a.layers[l];
+    // the layer's pointers made wave-uniform (SGPRs) here, once: left in the VGPRs of their vector
+    // load, hipcc's wait insertion put an s_waitcnt vmcnt(0) — a drain of the whole weight ring — into
+    // every streaming-loop iteration that used them
+    Layer Lw = a.layers[l];
+    Lw.wqkv = uniform_ptr(Lw.wqkv);
+    Lw.wo = uniform_ptr(Lw.wo);
+    Lw.w13 = uniform_ptr(Lw.w13);
+    Lw.w2 = uniform_ptr(Lw.w2);
+    Lw.ln1 = uniform_ptr(Lw.ln1);
+    Lw.ln2 = uniform_ptr(Lw.ln2);
     // ---- P1: norm + QKV rows of the group ----
     // The weight pieces of each phase are issued between the arrival and the wait of the barrier before
     // it: after the arrival (its vmcnt(0) would otherwise hold the arrival back until they landed),
     // in flight while the workgroup waits for the others.
     auto sq = make_stream(Lw.wqkv, (hq + 2 * hkv) * HD, H, nq, lane, ring, qkv_row);
     sq.start();
-    wait_for(gcnt, ++nbar * G, err);
+    wait_grid(a.sync, ++nbar, G, err);
     PD_STAMP(0);
     if (st && l > 0) st[(l - 1) * 16 + 12] = st[l * 16];   // the previous layer's barrier E ends here
     rmsnorm_to_lds(a, Lw.ln1, xs, red);
     PD_STAMP(1);
     {
-      const float v = sq.run(xs4);
+      const float v = sq.run(xaddr);
       sq.drain();
-      if (lane < nq)   // pairs of rows share a 4-B word: bf16 halves by 2-B sc1 stores
-        __hip_atomic_store(reinterpret_cast<unsigned short*>(a.qkv + qkv_row(lane)),
-                           __builtin_bit_cast(unsigned short, f2bf(v)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane < nq) ob[wave * qkv_per_wave + lane] = f2bf(v);
+      __syncthreads();
+      if (2 * tid < wqn) st_sc1u(a.qkv + qkv_grow(wq0 + 2 * tid), reinterpret_cast<const uint32_t*>(ob)[tid]);
     }
     // the O rows' weights are issued now: they stream while the group waits and attention runs
     PD_STAMP(2);
-    auto so = make_stream(Lw.wo, H, hq * HD, no, lane, ring, own_row);
-    arrive(a.sync + 1 + grp);   // this workgroup's QKV rows are published
+    auto so = make_stream(Lw.wo, H, hq * HD, n_o, lane, ring, o_row);
+    arrive(a.sync + SYNC_GROUP + 32 * grp);   // this workgroup's QKV rows are published
     so.start();
     if (in_grp == 0) {
       // ---- P2: the group's attention (its first workgroup) ----
-      wait_for(a.sync + 1 + grp, (l + 1) * per_group, err);
+      wait_for(a.sync + SYNC_GROUP + 32 * grp, (l + 1) * per_group, err);
       PD_STAMP(3);
       float* const qf = reinterpret_cast<float*>(lds + LDS_ATT);            // [Gq][128] rotated q
       float* const kn = qf + Gq * HD;                                        // [128] rotated new k
@@ -296,7 +435,6 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       float* const mo = pw + NW * Gq * 16;                                   // [NW][Gq] (m, l) + [NW][Gq][128] o
       float* const lo = mo + NW * Gq;
       float* const oo = lo + NW * Gq;
-      const int p = a.pos[0], slot = a.slot[0], ctx = a.ctx[0];
       const float* cs = a.cos_sin + (size_t)p * HD;
       // RoPE (neox halves) on the group's q heads and k; v as is
       for (int it = tid; it < (Gq + 2) * (HD / 2); it += NT) {
@@ -316,6 +454,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
         }
       }
       __syncthreads();
+      PD_STAMP(13);
       bf16_t* const kc = a.k_cache + (size_t)l * a.cache_layer;
       bf16_t* const vc = a.v_cache + (size_t)l * a.cache_layer;
       const size_t hs = (size_t)KBS * HD;   // elements per (block, head)
@@ -325,12 +464,17 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
         vc[((size_t)blk * hkv + grp) * hs + tid * KBS + off] = f2bf(vn[tid]);
       }
       // cached tokens [0, ctx - 1): wave w takes blocks w, w + NW, ...; lane (hh = lane >> 4, t = lane & 15)
-      const int ncached = ctx - 1, nblk = (ncached + KBS - 1) / KBS;
       float m_w = -INFINITY, l_w = 0.f;   // this lane's row hh (lanes of one 16-lane row agree)
       float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // o[hh][2 lane + e], hh < 4
       const int hh = lane >> 4, t = lane & 15;
+      int blk_next = wave < nblk ? a.bt[wave] : 0;   // the block table one block ahead
       for (int bi = wave; bi < nblk; bi += NW) {
-        const int blk = a.bt[bi];
+        const int blk = blk_next;
+        blk_next = bi + NW < nblk ? a.bt[bi + NW] : 0;
+        // the block's V (P V below) in flight together with its K
+        const bf16_t* vp = vc + ((size_t)blk * hkv + grp) * hs + (2 * lane) * KBS;
+        const uint4 va0 = *reinterpret_cast<const uint4*>(vp), va1 = *reinterpret_cast<const uint4*>(vp + 8);
+        const uint4 vb0 = *reinterpret_cast<const uint4*>(vp + KBS), vb1 = *reinterpret_cast<const uint4*>(vp + KBS + 8);
         const int tok = bi * KBS + t;
         float s = -INFINITY;
         if (hh < Gq && tok < ncached) {
@@ -361,9 +505,6 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         // P V: lane owns dims 2 lane, 2 lane + 1 of every row; V block is [dim][16 tokens]
         const int nvalid = min(KBS, ncached - bi * KBS);
-        const bf16_t* vp = vc + ((size_t)blk * hkv + grp) * hs + (2 * lane) * KBS;
-        const uint4 va0 = *reinterpret_cast<const uint4*>(vp), va1 = *reinterpret_cast<const uint4*>(vp + 8);
-        const uint4 vb0 = *reinterpret_cast<const uint4*>(vp + KBS), vb1 = *reinterpret_cast<const uint4*>(vp + KBS + 8);
         const uint32_t v0[8] = {va0.x, va0.y, va0.z, va0.w, va1.x, va1.y, va1.z, va1.w};
         const uint32_t v1[8] = {vb0.x, vb0.y, vb0.z, vb0.w, vb1.x, vb1.y, vb1.z, vb1.w};
 #pragma unroll
@@ -396,6 +537,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
         oo[(wave * Gq + r) * HD + 2 * lane + 1] = acc[1][r];
       }
       __syncthreads();
+      PD_STAMP(14);
       // merge the waves and the new token: thread -> (row, dim)
       for (int it = tid; it < Gq * HD; it += NT) {
         const int r = it / HD, d = it - r * HD;
@@ -420,61 +562,47 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     }
     PD_STAMP(4);
     // ---- P3: O rows -> residual ----
-    arrive_wait(gcnt, ++nbar * G, err);
+    arrive(gcnt);
+    wait_grid(a.sync, ++nbar, G, err);
     PD_STAMP(5);
-    for (int i = tid; i < hq * HD / 8; i += NT) {   // attn (sc1) -> LDS
-      const bf16_t* src = a.attn + i * 8;
-      uint4 v;
-      v.x = ld_sc1u(src);
-      v.y = ld_sc1u(src + 2);
-      v.z = ld_sc1u(src + 4);
-      v.w = ld_sc1u(src + 6);
-      reinterpret_cast<uint4*>(lds + LDS_X)[i] = v;
-    }
+    stage_sc1(reinterpret_cast<uint4*>(lds + LDS_X), a.attn, hq * HD / 8);   // attn (sc1) -> LDS
+    vm_drain();
     __syncthreads();
     {
-      const float v = so.run(xs4);
+      const float v = so.run(xaddr);
       so.drain();
-      if (lane < no) st_sc1(a.res + own0 + lane, ld_sc1(a.res + own0 + lane) + bf2f(f2bf(v)));
+      if (lane < n_o) st_sc1(a.res + ow0 + lane, ld_sc1(a.res + ow0 + lane) + bf2f(f2bf(v)));
     }
     PD_STAMP(6);
     auto sg = make_stream(Lw.w13, 2 * I, H, 2 * ng, lane, ring, gu_row);
     arrive(gcnt);
     sg.start();
-    wait_for(gcnt, ++nbar * G, err);
+    wait_grid(a.sync, ++nbar, G, err);
     PD_STAMP(7);
     // ---- P4: norm + gate / up -> act ----
     rmsnorm_to_lds(a, Lw.ln2, xs, red);
     PD_STAMP(8);
     {
-      const float v = sg.run(xs4);   // lane 2 k: gate row k, lane 2 k + 1: its up row
+      const float v = sg.run(xaddr);   // lane 2 k: gate row k, lane 2 k + 1: its up row
       sg.drain();
       const float u = bf2f(f2bf(__shfl_down(v, 1, 64)));
       const float gt = bf2f(f2bf(v));
-      if (!(lane & 1) && (lane >> 1) < ng)
-        __hip_atomic_store(reinterpret_cast<unsigned short*>(a.act + g0 + (lane >> 1)),
-                           __builtin_bit_cast(unsigned short, f2bf(gt / (1.f + __expf(-gt)) * u)), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      if (!(lane & 1) && (lane >> 1) < ng) ob[wave * i_per_wave + (lane >> 1)] = f2bf(gt / (1.f + __expf(-gt)) * u);
+      __syncthreads();
+      if (2 * tid < wan) st_sc1u(a.act + wa0 + 2 * tid, reinterpret_cast<const uint32_t*>(ob)[tid]);
     }
     PD_STAMP(9);
     auto sd = make_stream(Lw.w2, H, I, no, lane, ring, own_row);
     arrive(gcnt);
     sd.start();
-    wait_for(gcnt, ++nbar * G, err);
+    wait_grid(a.sync, ++nbar, G, err);
     PD_STAMP(10);
     // ---- P5: down rows -> residual ----
-    for (int i = tid; i < I / 8; i += NT) {
-      const bf16_t* src = a.act + i * 8;
-      uint4 v;
-      v.x = ld_sc1u(src);
-      v.y = ld_sc1u(src + 2);
-      v.z = ld_sc1u(src + 4);
-      v.w = ld_sc1u(src + 6);
-      reinterpret_cast<uint4*>(lds + LDS_X)[i] = v;
-    }
+    stage_sc1(reinterpret_cast<uint4*>(lds + LDS_X), a.act, I / 8);   // act (sc1) -> LDS
+    vm_drain();
     __syncthreads();
     {
-      const float v = sd.run(xs4);
+      const float v = sd.run(xaddr);
       sd.drain();
       if (lane < no) st_sc1(a.res + own0 + lane, ld_sc1(a.res + own0 + lane) + bf2f(f2bf(v)));
     }
@@ -482,8 +610,12 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     arrive(gcnt);   // the next layer's QKV pieces are issued before the wait (top of the loop)
   }
 #undef PD_STAMP
-  wait_for(gcnt, ++nbar * G, err);
+  wait_grid(a.sync, ++nbar, G, err);
   for (int r = own0 + lane; r < own1; r += 64) a.h_out[r] = f2bf(ld_sc1(a.res + r));
+}
+
+__global__ __launch_bounds__(256) void zero_sync_kernel(int* __restrict__ sync) {
+  for (int i = threadIdx.x; i < SYNC_BYTES / 4; i += 256) sync[i] = 0;
 }
 
 static int num_cus() {
@@ -500,7 +632,7 @@ static int num_cus() {
 
 // Workspace bytes: residual (fp32 H) + qkv + attn + act (bf16) + the sync words.
 extern "C" size_t ka_decode_persistent_ws(int H, int hq, int hkv, int I) {
-  return 256 + (size_t)H * 4 + (size_t)(hq + 2 * hkv) * 128 * 2 + (size_t)hq * 128 * 2 + (size_t)I * 2 + 1024;
+  return pd::SYNC_BYTES + (size_t)H * 4 + (size_t)(hq + 2 * hkv) * 128 * 2 + (size_t)hq * 128 * 2 + (size_t)I * 2 + 1024;
 }
 
 // Every layer of a batch-1 decode step (see the header).  layers: device array of L x 6 pointers
@@ -513,11 +645,18 @@ extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* lay
                                     const int* pos, const int* slot, const int* bt, const int* ctx,
                                     const float* cos_sin, void* ws, void* stamps, hipStream_t stream) {
   if (L <= 0) return 0;
-  if (hq % hkv || hq / hkv > 4 || H % 512 || I % 512 || (hq * 128) % 512 || H > 16384 || I > 16384 ||
+  if (hq % hkv || hq / hkv > 4 || hkv > 16 || H % 512 || I % 512 || (hq * 128) % 512 || H > 16384 || I > 16384 ||
       ws == nullptr)
     return (int)hipErrorInvalidValue;
   const int G = (pd::num_cus() / hkv) * hkv;
   if (G < hkv) return (int)hipErrorInvalidValue;
+  {   // every wave's rows fit its 64 lanes (lane i = row i) and the LDS result buffer
+    const int per_group = G / hkv, nw = G * pd::NW;
+    const int q = ((hq / hkv + 2) * 128 + per_group * pd::NW - 1) / (per_group * pd::NW);
+    const int hpw = (H + nw - 1) / nw, ipw = (I + nw - 1) / nw;
+    const int opw = G > hkv ? (H + (G - hkv) * pd::NW - 1) / ((G - hkv) * pd::NW) : 65;
+    if (q > 64 || hpw > 64 || 2 * ipw > 64 || opw > 64) return (int)hipErrorInvalidValue;
+  }
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pd::decode_layers_kernel),
@@ -546,22 +685,26 @@ extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* lay
   a.cos_sin = cos_sin;
   a.sync = reinterpret_cast<int*>(w);
   a.stamps = static_cast<unsigned long long*>(stamps);
-  a.res = reinterpret_cast<float*>(w + 256);
-  a.qkv = reinterpret_cast<bf16_t*>(w + 256 + (size_t)H * 4);
+  a.res = reinterpret_cast<float*>(w + pd::SYNC_BYTES);
+  a.qkv = reinterpret_cast<bf16_t*>(w + pd::SYNC_BYTES + (size_t)H * 4);
   a.attn = a.qkv + (size_t)(hq + 2 * hkv) * 128;
   a.act = a.attn + (size_t)hq * 128;
-  // the arrival counters and the error word start at zero in every launch (a memset node in the graph)
-  hipError_t e = hipMemsetAsync(w, 0, 256, stream);
-  if (e != hipSuccess) return (int)e;
+  // the arrival counters and the error word start at zero in every launch.  A kernel, not
+  // hipMemsetAsync: captured into a hipGraph, the memset node left the words at 0xF3C00000 on
+  // ROCm 7.2 (every grid wait then ran out; scripts/debug_pd_graph.py)
+  hipLaunchKernelGGL(pd::zero_sync_kernel, dim3(1), dim3(256), 0, stream, reinterpret_cast<int*>(w));
   hipLaunchKernelGGL(pd::decode_layers_kernel, dim3(G), dim3(pd::NT), pd::LDS_BYTES, stream, a);
   KA_CHECK_LAUNCH();
 }
+
+// Byte offset of the error word in the workspace (the runner reads it back with every B = 1 step).
+extern "C" int ka_decode_persistent_err_offset() { return pd::SYNC_ERR * 4; }
 
 // The error word of the last launch (a barrier wait that ran out: some workgroup never ran), cleared.
 extern "C" int ka_decode_persistent_err(void* ws, hipStream_t stream) {
   int v = 0;
   if (ws == nullptr) return 0;
-  (void)hipMemcpyAsync(&v, static_cast<char*>(ws) + 63 * 4, 4, hipMemcpyDeviceToHost, stream);
+  (void)hipMemcpyAsync(&v, static_cast<char*>(ws) + pd::SYNC_ERR * 4, 4, hipMemcpyDeviceToHost, stream);
   (void)hipStreamSynchronize(stream);
   return v;
 }

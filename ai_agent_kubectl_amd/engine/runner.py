@@ -43,6 +43,12 @@ class CollectiveTimeout(RuntimeError):
     requests with 503 and marks the engine unhealthy / exits for the supervisor to restart it."""
 
 
+class PersistentStall(RuntimeError):
+    """The batch-1 persistent decode kernel (csrc/decode_persistent.hip) gave up a grid-wide wait:
+    some workgroup never ran (the GPU shared with another kernel), so the step's hidden state is
+    stale.  Recoverable: the engine fails the in-flight requests and recovers; the runner has
+    already switched batch-1 decode back to the per-kernel chain."""
+
 
 class StepHandle(NamedTuple):
     """A step queued on the device and not yet read back (`collect`)."""
@@ -117,7 +123,7 @@ class ModelRunner:
         # the one-shot TP collectives' error word rides back with every step's tokens (a pinned
         # 4-byte copy behind them on the same stream: no extra synchronisation), one slot per launch
         # parity like the token outputs
-        self._h_errs = [torch.zeros(1, dtype=torch.int32, pin_memory=pin) for _ in range(4)]
+        self._h_errs = [torch.zeros(2, dtype=torch.int32, pin_memory=pin) for _ in range(4)]
         self._eflip = 0
         # TP decode overlap: rank 0 queues step t+1 (header + staging broadcast + graph) before
         # reading step t back.  Needs collectives that are stream-ordered on the device (RCCL):
@@ -405,7 +411,7 @@ class ModelRunner:
                                                self.d_out.index_select(0, self.d_fix[nf:2 * nf].long()))
         self._launch_decode(Bp, n_copy)
         ho[:B].copy_(self.d_out[:B], non_blocking=True)
-        eh = self._copy_err()
+        eh = self._copy_err(persistent=Bp == 1 and self.model.persistent_ok())
         ev = None
         if self.device.type == "cuda":
             ev = torch.cuda.Event()
@@ -478,22 +484,34 @@ class ModelRunner:
         car = getattr(self.comm, "custom_ar", None)
         return car.state[2:3] if car is not None else None
 
-    def _copy_err(self) -> Optional[torch.Tensor]:
-        """Queue the error word's readback behind the step just launched (None without one-shot
-        collectives)."""
+    def _copy_err(self, persistent: bool = False) -> Optional[torch.Tensor]:
+        """Queue the error word's readback behind the step just launched: [one-shot collectives,
+        persistent decode kernel] (None when the step has neither)."""
         src = self._err_word()
-        if src is None:
+        psrc = self.model.persistent_err_word() if persistent else None
+        if src is None and psrc is None:
             return None
         h = self._h_errs[self._eflip]
         self._eflip = (self._eflip + 1) % len(self._h_errs)
-        h.copy_(src, non_blocking=True)
+        h.zero_()
+        if src is not None:
+            h[0:1].copy_(src, non_blocking=True)
+        if psrc is not None:
+            h[1:2].copy_(psrc, non_blocking=True)
         return h
 
-    @staticmethod
-    def _check_err(h: Optional[torch.Tensor]) -> None:
-        if h is not None and int(h[0]):
+    def _check_err(self, h: Optional[torch.Tensor]) -> None:
+        if h is None:
+            return
+        if int(h[0]):
             raise CollectiveTimeout("one-shot TP collective: a peer never arrived (spin timeout); "
                                     "the step's results are stale")
+        if int(h[1]):
+            self.model.persistent = False   # the chain from now on: co-residency cannot be relied on
+            logger.error("persistent decode kernel: a grid wait ran out; batch-1 decode falls back to "
+                         "the kernel chain")
+            raise PersistentStall("persistent decode: a workgroup never ran (grid wait timeout); "
+                                  "the step's results are stale")
 
     def collect(self, handle: "StepHandle") -> List[int]:
         ev, ho, B, t0 = handle.event, handle.host_out, handle.rows, handle.t0

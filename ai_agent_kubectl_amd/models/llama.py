@@ -85,8 +85,9 @@ class LlamaModel:
         self.prefetch_blocks = int(os.environ.get("KA_DECODE_PREFETCH_BLOCKS", "64"))
         self._side = None
         # batch-1 decode: every layer in ONE persistent launch (csrc/decode_persistent.hip) instead of
-        # ~7 kernels per layer.  KA_PERSISTENT_DECODE=1 enables it where the geometry allows.
-        self.persistent = os.environ.get("KA_PERSISTENT_DECODE", "0") == "1"
+        # ~7 kernels per layer (3.13 vs 3.44 ms/step for Llama-3-8B, profiles/r4/persistent_decode/),
+        # wherever the geometry allows; KA_PERSISTENT_DECODE=0 keeps the kernel chain.
+        self.persistent = os.environ.get("KA_PERSISTENT_DECODE", "1") == "1"
         self._pd = None   # (layer pointer table, workspace)
         self.persistent_stamps = None   # diagnostics: int64 [CUs, L, 16] phase timestamps (scripts/)
 
@@ -208,6 +209,14 @@ class LlamaModel:
                                      meta.slot_mapping, meta.block_tables[0], meta.ctx_lens, self.cos_sin, ws,
                                      self.persistent_stamps)
         return ops.rmsnorm(hout, self.W["norm"], self.cfg.norm_eps)
+
+    def persistent_err_word(self) -> Optional[torch.Tensor]:
+        """The persistent kernel's error word in its workspace (int32 [1], cleared by every launch),
+        for the runner's per-step readback; None before the first launch."""
+        if self._pd is None:
+            return None
+        off = int(ops._hip.require().ka_decode_persistent_err_offset())
+        return self._pd[1][off:off + 4].view(torch.int32)
 
     def persistent_err(self) -> int:
         """Error word of the last persistent launch (a grid wait that ran out; 0 in a correct run)."""

@@ -61,6 +61,7 @@ _SIGS = {
     "ka_decode_persistent": [P, P, P, I, I, I, I, I, F, F, P, P, ctypes.c_long, P, P, P, P, P, P, P, P],
     "ka_decode_persistent_ws": [I, I, I, I],
     "ka_decode_persistent_err": [P, P],
+    "ka_decode_persistent_err_offset": [],
     "ka_gm_bn": [I],
     "ka_gm_bm": [I],
     "ka_moe_align": [P, P, P, I, I, I, P],

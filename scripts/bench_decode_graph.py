@@ -71,6 +71,8 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             out.append(f"B={B}: {e0.elapsed_time(e1) / args.reps:.3f} ms")
+            if B == 1 and m.persistent:   # the replays' own error word (a wait that ran out = invalid timing)
+                out.append(f"graph err {m.persistent_err()}")
         print(f"prefetch {mb:g} MB x {int(blocks)} blocks, persistent {pers}: " + ", ".join(out), flush=True)
         if m.persistent:
             print("  persistent error word:", m.persistent_err(), flush=True)
@@ -106,6 +108,11 @@ def main():
                       f"p90 {float(d.quantile(0.9)):6.1f}  max {float(d.max()):6.1f}   end: "
                       f"min {float(endt.min(dim=0).values.mean()):6.1f} max {float(endt.max(dim=0).values.mean()):6.1f}",
                       flush=True)
+            lead = stv[:, :, 13] > 0   # attention leaders: RoPE / context blocks / merge
+            if lead.any():
+                sub = [("rope", 3, 13), ("blocks", 13, 14), ("merge", 14, 4)]
+                print("  attention: " + ", ".join(f"{n} {float((stv[:, :, b] - stv[:, :, a])[lead].mean()):.1f}"
+                                                  for n, a, b in sub), flush=True)
             # per-XCD (wg % 8) mean gate_up / down durations: is the skew a fabric effect?
             for k, n in ((8, "gate_up"), (10, "down")):
                 d = stv[:, :, k + 1] - stv[:, :, k]
