@@ -30,7 +30,17 @@
 
 namespace pd {
 
-constexpr int NT = 512, NW = NT / 64, RING = 16, HD = 128, KBS = 16, NT_ = NT;
+#ifndef KA_PD_RING
+#define KA_PD_RING 16
+#endif
+#ifndef KA_PD_ROT
+#define KA_PD_ROT 0   // measured: no effect (profiles/r4/persistent_decode)
+#endif
+#ifndef KA_PD_NT
+#define KA_PD_NT 1
+#endif
+constexpr int NT = 512, NW = NT / 64, RING = KA_PD_RING, HD = 128, KBS = 16, NT_ = NT;
+static_assert((RING & (RING - 1)) == 0 && RING >= 2 && RING <= 16, "ring: a power of two <= 16");
 
 struct Layer {
   const bf16_t* wqkv;   // [(hq + 2 hkv) 128, H]
@@ -75,6 +85,24 @@ KA_DEV const bf16_t* uniform_ptr(const bf16_t* p) {
   const uint64_t v = (uint64_t)(uintptr_t)p;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   return reinterpret_cast<const bf16_t*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+}
+
+// An SGPR holding 0 (a literal 0 is not accepted as the soffset of the LDS-DMA form)
+KA_DEV uint32_t sgpr_zero() {
+  uint32_t z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return z;
+}
+// One 1-KB LDS-DMA piece: 16 B per lane from base + voff (base wave-uniform) to LDS lds_dst + 16 lane
+KA_DEV void dma_1k(const bf16_t* base, uint32_t voff, uint32_t lds_dst) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(uniform_ptr(base)), (short)0,
+                                                                      1 << 30, 0x00020000);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "s"(__builtin_amdgcn_readfirstlane(lds_dst)), "v"(voff), "s"(rs), "s"(sgpr_zero())
+               : "memory");
 }
 
 // Four 16-B sc1 loads in flight, one wait (hand-off table row 1 admits 16-B sc1 loads of bytes stored
@@ -199,16 +227,24 @@ struct Stream {
   uint32_t nbytes;
   uint32_t ring;   // LDS byte address of this wave's ring (wave-uniform)
   int issued, ni, nc;   // pieces issued; row / chunk of the next piece to issue
+  int rot;              // every row is read from chunk `rot` on, wrapping (see make_stream)
   KA_DEV void issue() {
     const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)(issued & (RING - 1)) * 1024u);
     // wave-uniform part of the byte offset (row start + chunk) -> soffset; the lane's 16 B -> voffset
-    const uint32_t so = __builtin_amdgcn_readfirstlane(((uint32_t)row(ni) * (uint32_t)K + (uint32_t)(nc * 512)) * 2u);
+    const int c = nc + rot >= KC ? nc + rot - KC : nc + rot;
+    const uint32_t so = __builtin_amdgcn_readfirstlane(((uint32_t)row(ni) * (uint32_t)K + (uint32_t)(c * 512)) * 2u);
     const uint32_t off = (uint32_t)lane * 16u;
     // W is wave-uniform (uniform_ptr at the layer's top): the descriptor lives in SGPRs
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(W), (short)0,
                                                                         (int)nbytes, 0x00020000);
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+    // nt: weights are read once per token (MI355X_MICROARCH.md nt-weights: issued -> landed -18 %)
+#if KA_PD_NT
+#define KA_PD_LDS_LOAD "buffer_load_dwordx4 %2, %3, %4 offen nt lds"
+#else
+#define KA_PD_LDS_LOAD "buffer_load_dwordx4 %2, %3, %4 offen lds"
+#endif
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t" KA_PD_LDS_LOAD "\n\t"
                  "s_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "s"(dst), "v"(off), "s"(rs), "s"(so)
@@ -243,14 +279,15 @@ struct Stream {
     int j = 0;
     for (; j + 1 < total; j += 2) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING - 2) : "memory");   // pieces j, j + 1 have landed
-      const int cc1 = cc + 1 == KC ? 0 : cc + 1;
+      const int xc = cc + rot >= KC ? cc + rot - KC : cc + rot;   // x chunks of pieces j, j + 1
+      const int xc1 = xc + 1 == KC ? 0 : xc + 1;
       uint4 w0, w1, x0, x1;
       asm volatile(
           "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
           "s_waitcnt lgkmcnt(0)"
           : "=&v"(w0), "=&v"(w1), "=&v"(x0), "=&v"(x1)
           : "v"(ring + (uint32_t)(j & (RING - 1)) * 1024u + lo16), "v"(ring + (uint32_t)((j + 1) & (RING - 1)) * 1024u + lo16),
-            "v"(xaddr + (uint32_t)cc * 1024u + lo16), "v"(xaddr + (uint32_t)cc1 * 1024u + lo16)
+            "v"(xaddr + (uint32_t)xc * 1024u + lo16), "v"(xaddr + (uint32_t)xc1 * 1024u + lo16)
           : "memory");
       issue();   // both slots are free again: refill them RING pieces ahead
       issue();
@@ -264,7 +301,8 @@ struct Stream {
       uint4 w0, x0;
       asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
                    : "=&v"(w0), "=&v"(x0)
-                   : "v"(ring + (uint32_t)(j & (RING - 1)) * 1024u + lo16), "v"(xaddr + (uint32_t)cc * 1024u + lo16)
+                   : "v"(ring + (uint32_t)(j & (RING - 1)) * 1024u + lo16),
+                     "v"(xaddr + (uint32_t)(cc + rot >= KC ? cc + rot - KC : cc + rot) * 1024u + lo16)
                    : "memory");
       issue();
       acc = dot8(w0, x0, acc);
@@ -275,8 +313,12 @@ struct Stream {
   KA_DEV void drain() const { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 };
 template <class RowFn>
-KA_DEV Stream<RowFn> make_stream(const bf16_t* W, int N, int K, int n, int lane, uint32_t ring, RowFn row) {
-  Stream<RowFn> s{W, K, K / 512, n * (K / 512), lane, row, (uint32_t)N * (uint32_t)K * 2u, ring, 0, 0, 0};
+// gw: the wave's grid-wide index.  Each wave starts its rows at chunk gw mod K/512: waves that leave
+// a grid barrier together would otherwise all read the same 1-KB column of their rows at once —
+// addresses equal modulo the row pitch, the same few HBM channels.
+KA_DEV Stream<RowFn> make_stream(const bf16_t* W, int N, int K, int n, int lane, uint32_t ring, RowFn row, int gw) {
+  Stream<RowFn> s{W, K, K / 512, n * (K / 512), lane, row, (uint32_t)N * (uint32_t)K * 2u, ring, 0, 0, 0,
+                  KA_PD_ROT ? gw % (K / 512) : 0};
   return s;
 }
 
@@ -358,6 +400,9 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
   // the token's position / slot / context (fixed for the launch) and the attention loop's trip count
   const int p = a.pos[0], slot = a.slot[0], ctx = a.ctx[0];
   const int ncached = ctx - 1, nblk = (ncached + KBS - 1) / KBS;
+  // a leader wave's first two context blocks (fixed for the launch; prefetched every layer)
+  const int blk_w0 = __builtin_amdgcn_readfirstlane(wave < nblk ? a.bt[wave] : 0);
+  const int blk_w1 = __builtin_amdgcn_readfirstlane(wave + NW < nblk ? a.bt[wave + NW] : 0);
   for (int r = own0 + lane; r < own1; r += 64) st_sc1(a.res + r, bf2f(a.h0[r]));
   arrive(gcnt);
 
@@ -405,7 +450,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     // The weight pieces of each phase are issued between the arrival and the wait of the barrier before
     // it: after the arrival (its vmcnt(0) would otherwise hold the arrival back until they landed),
     // in flight while the workgroup waits for the others.
-    auto sq = make_stream(Lw.wqkv, (hq + 2 * hkv) * HD, H, nq, lane, ring, qkv_row);
+    auto sq = make_stream(Lw.wqkv, (hq + 2 * hkv) * HD, H, nq, lane, ring, qkv_row, gw);
     sq.start();
     wait_grid(a.sync, ++nbar, G, err);
     PD_STAMP(0);
@@ -421,9 +466,25 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     }
     // the O rows' weights are issued now: they stream while the group waits and attention runs
     PD_STAMP(2);
-    auto so = make_stream(Lw.wo, H, hq * HD, n_o, lane, ring, o_row);
+    auto so = make_stream(Lw.wo, H, hq * HD, n_o, lane, ring, o_row, gw);
     arrive(a.sync + SYNC_GROUP + 32 * grp);   // this workgroup's QKV rows are published
     so.start();
+    if (in_grp == 0) {
+      // the leader (no O rows: its ring is idle now): this layer's cached K / V blocks (each wave's
+      // first two) into the ring by LDS-DMA, in flight while the group's QKV rows finish
+      const size_t hs = (size_t)KBS * HD;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (wave + k * NW < nblk) {
+          const size_t boff = ((size_t)(k ? blk_w1 : blk_w0) * hkv + grp) * hs + (size_t)l * a.cache_layer;
+#pragma unroll
+          for (int pc = 0; pc < 4; ++pc) {
+            dma_1k(a.k_cache + boff, (uint32_t)pc * 1024u + (uint32_t)lane * 16u, ring + (uint32_t)(k * 8 + pc) * 1024u);
+            dma_1k(a.v_cache + boff, (uint32_t)pc * 1024u + (uint32_t)lane * 16u, ring + (uint32_t)(k * 8 + 4 + pc) * 1024u);
+          }
+        }
+      }
+    }
     if (in_grp == 0) {
       // ---- P2: the group's attention (its first workgroup) ----
       wait_for(a.sync + SYNC_GROUP + 32 * grp, (l + 1) * per_group, err);
@@ -458,6 +519,8 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       bf16_t* const kc = a.k_cache + (size_t)l * a.cache_layer;
       bf16_t* const vc = a.v_cache + (size_t)l * a.cache_layer;
       const size_t hs = (size_t)KBS * HD;   // elements per (block, head)
+      // the ring's K / V have landed (waited before the appends below: stores count in vmcnt too)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (slot >= 0 && tid < HD) {          // append the new token (read by the NEXT launches only)
         const int blk = slot / KBS, off = slot % KBS;
         kc[((size_t)blk * hkv + grp) * hs + off * HD + tid] = f2bf(kn[tid]);
@@ -467,29 +530,58 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       float m_w = -INFINITY, l_w = 0.f;   // this lane's row hh (lanes of one 16-lane row agree)
       float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // o[hh][2 lane + e], hh < 4
       const int hh = lane >> 4, t = lane & 15;
-      int blk_next = wave < nblk ? a.bt[wave] : 0;   // the block table one block ahead
-      for (int bi = wave; bi < nblk; bi += NW) {
-        const int blk = blk_next;
-        blk_next = bi + NW < nblk ? a.bt[bi + NW] : 0;
-        // the block's V (P V below) in flight together with its K
-        const bf16_t* vp = vc + ((size_t)blk * hkv + grp) * hs + (2 * lane) * KBS;
-        const uint4 va0 = *reinterpret_cast<const uint4*>(vp), va1 = *reinterpret_cast<const uint4*>(vp + 8);
-        const uint4 vb0 = *reinterpret_cast<const uint4*>(vp + KBS), vb1 = *reinterpret_cast<const uint4*>(vp + KBS + 8);
+      // the wave's first two blocks are in its ring (LDS-DMA at the layer's top: K [16 tok][128] at
+      // slot 8 k, V [128][16 tok] at slot 8 k + 4); later blocks come from global memory
+      const char* const rbase = lds + LDS_RING + wave * RING * 1024;
+      int kk = 0;
+      for (int bi = wave; bi < nblk; bi += NW, ++kk) {
+        const bool in_ring = kk < 2;
+        const int blk = in_ring ? 0 : a.bt[bi];
         const int tok = bi * KBS + t;
+        uint4 va0, va1, vb0, vb1;   // V of this lane's dims 2 lane, 2 lane + 1 (16 tokens each)
         float s = -INFINITY;
-        if (hh < Gq && tok < ncached) {
-          const bf16_t* kp = kc + ((size_t)blk * hkv + grp) * hs + t * HD;
-          const float* qp = qf + hh * HD;
-          float d = 0.f;
+        const float* qp = qf + hh * HD;
+        if (in_ring) {
+          const uint4* vr = reinterpret_cast<const uint4*>(rbase + kk * 8192 + 4096 + lane * 64);
+          va0 = vr[0];
+          va1 = vr[1];
+          vb0 = vr[2];
+          vb1 = vr[3];
+          if (hh < Gq && tok < ncached) {
+            // chunk order rotated by the token: the 16 tokens' rows (256 B apart) hit distinct banks
+            const char* kr = rbase + kk * 8192 + t * 256;
+            float d = 0.f;
 #pragma unroll
-          for (int c = 0; c < HD / 8; ++c) {
-            const uint4 k8 = *reinterpret_cast<const uint4*>(kp + c * 8);
-            const uint32_t kw[4] = {k8.x, k8.y, k8.z, k8.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) d += qp[c * 8 + 2 * e] * lo_f(kw[e]) + qp[c * 8 + 2 * e + 1] * hi_f(kw[e]);
+            for (int c = 0; c < HD / 8; ++c) {
+              const int ch = (c + t) & (HD / 8 - 1);
+              const uint4 k8 = *reinterpret_cast<const uint4*>(kr + ch * 16);
+              const float4 q0 = *reinterpret_cast<const float4*>(qp + ch * 8);
+              const float4 q1 = *reinterpret_cast<const float4*>(qp + ch * 8 + 4);
+              d += q0.x * lo_f(k8.x) + q0.y * hi_f(k8.x) + q0.z * lo_f(k8.y) + q0.w * hi_f(k8.y);
+              d += q1.x * lo_f(k8.z) + q1.y * hi_f(k8.z) + q1.z * lo_f(k8.w) + q1.w * hi_f(k8.w);
+            }
+            s = d * a.scale_log2;
           }
-          s = d * a.scale_log2;
+        } else {
+          const bf16_t* vp = vc + ((size_t)blk * hkv + grp) * hs + (2 * lane) * KBS;
+          va0 = *reinterpret_cast<const uint4*>(vp);
+          va1 = *reinterpret_cast<const uint4*>(vp + 8);
+          vb0 = *reinterpret_cast<const uint4*>(vp + KBS);
+          vb1 = *reinterpret_cast<const uint4*>(vp + KBS + 8);
+          if (hh < Gq && tok < ncached) {
+            const bf16_t* kp = kc + ((size_t)blk * hkv + grp) * hs + t * HD;
+            float d = 0.f;
+#pragma unroll
+            for (int c = 0; c < HD / 8; ++c) {
+              const uint4 k8 = *reinterpret_cast<const uint4*>(kp + c * 8);
+              const uint32_t kw[4] = {k8.x, k8.y, k8.z, k8.w};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) d += qp[c * 8 + 2 * e] * lo_f(kw[e]) + qp[c * 8 + 2 * e + 1] * hi_f(kw[e]);
+            }
+            s = d * a.scale_log2;
+          }
         }
+        if (bi == wave) PD_STAMP(15);   // the first block's scores (K landed + q.k)
         const float mx = row16_max(s);
         const float mn = fmaxf(m_w, mx);
         const float alpha = mn == -INFINITY ? 1.f : exp2f(m_w - mn);
@@ -536,14 +628,17 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
         oo[(wave * Gq + r) * HD + 2 * lane] = acc[0][r];
         oo[(wave * Gq + r) * HD + 2 * lane + 1] = acc[1][r];
       }
+      float* const snr = oo + NW * Gq * HD;   // [Gq] the new token's scores, one wave per q head
+      if (wave < Gq) {
+        const float v = wave_total(qf[wave * HD + 2 * lane] * kn[2 * lane] + qf[wave * HD + 2 * lane + 1] * kn[2 * lane + 1]);
+        if (lane == 0) snr[wave] = v * a.scale_log2;
+      }
       __syncthreads();
       PD_STAMP(14);
       // merge the waves and the new token: thread -> (row, dim)
       for (int it = tid; it < Gq * HD; it += NT) {
         const int r = it / HD, d = it - r * HD;
-        float sn = 0.f;
-        for (int k = 0; k < HD; ++k) sn += qf[r * HD + k] * kn[k];
-        sn *= a.scale_log2;
+        const float sn = snr[r];
         float M = sn;
         for (int w = 0; w < NW; ++w) M = fmaxf(M, mo[w * Gq + r]);
         float den = exp2f(sn - M), num = den * vn[d];
@@ -574,7 +669,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       if (lane < n_o) st_sc1(a.res + ow0 + lane, ld_sc1(a.res + ow0 + lane) + bf2f(f2bf(v)));
     }
     PD_STAMP(6);
-    auto sg = make_stream(Lw.w13, 2 * I, H, 2 * ng, lane, ring, gu_row);
+    auto sg = make_stream(Lw.w13, 2 * I, H, 2 * ng, lane, ring, gu_row, gw);
     arrive(gcnt);
     sg.start();
     wait_grid(a.sync, ++nbar, G, err);
@@ -592,7 +687,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       if (2 * tid < wan) st_sc1u(a.act + wa0 + 2 * tid, reinterpret_cast<const uint32_t*>(ob)[tid]);
     }
     PD_STAMP(9);
-    auto sd = make_stream(Lw.w2, H, I, no, lane, ring, own_row);
+    auto sd = make_stream(Lw.w2, H, I, no, lane, ring, own_row, gw);
     arrive(gcnt);
     sd.start();
     wait_grid(a.sync, ++nbar, G, err);
@@ -652,6 +747,7 @@ extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* lay
   if (G < hkv) return (int)hipErrorInvalidValue;
   {   // every wave's rows fit its 64 lanes (lane i = row i) and the LDS result buffer
     const int per_group = G / hkv, nw = G * pd::NW;
+    if (per_group < 2) return (int)hipErrorInvalidValue;
     const int q = ((hq / hkv + 2) * 128 + per_group * pd::NW - 1) / (per_group * pd::NW);
     const int hpw = (H + nw - 1) / nw, ipw = (I + nw - 1) / nw;
     const int opw = G > hkv ? (H + (G - hkv) * pd::NW - 1) / ((G - hkv) * pd::NW) : 65;
