@@ -36,6 +36,9 @@ namespace pd {
 #ifndef KA_PD_ROT
 #define KA_PD_ROT 0   // measured: no effect (profiles/r4/persistent_decode)
 #endif
+#ifndef KA_PD_W0_DEFER   // 1: wave 0 (the barrier poller) issues its ring only after the wait, so its polls
+#define KA_PD_W0_DEFER 0  // do not queue behind its own pieces -- measured +2.5 us per barrier (wave 0 then
+#endif                    // finishes each phase last): off
 #ifndef KA_PD_NT
 #define KA_PD_NT 1
 #endif
@@ -197,6 +200,24 @@ KA_DEV float dot8(uint4 w, uint4 x, float acc) {
   acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, w.z), __builtin_bit_cast(bf16x2v, x.z), acc, false);
   acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, w.w), __builtin_bit_cast(bf16x2v, x.w), acc, false);
   return acc;
+}
+
+// P re-layout scratch of the leader's MFMA attention (the scheme of csrc/attention.hip): the
+// probabilities leave the MFMA C layout (lane (col, g) holds rows 4 g + r, keys col and 16 + col) and
+// are re-read in the A layout (lane holds row col, keys 8 g .. 8 g + 7); 16 rows x PSTR bf16 per wave,
+// 16-B chunk c of row x at slot c ^ p_slot_xor(x >> 2): conflict-free stores and reads.
+constexpr int PSTR = 40;
+KA_DEV int p_slot_xor(int q) { return (q ^ (q >> 1)) & 1; }
+KA_DEV void p_store(bf16_t* pw, int prow, int col, float p0, float p1) {
+  const float q0 = dpp_f<0xB1>(p0), q1 = dpp_f<0xB1>(p1);   // lane ^ 1
+  const bool even = (col & 1) == 0;
+  const int key = even ? col : 15 + col;
+  const uint32_t v = even ? pack2(p0, q0) : pack2(q1, p1);
+  const int slot = (key >> 3) ^ p_slot_xor(prow >> 2);
+  *reinterpret_cast<uint32_t*>(pw + prow * PSTR + (slot << 3) + (key & 7)) = v;
+}
+KA_DEV bf16x8 p_load(const bf16_t* pw, int col, int g) {
+  return as_bf16x8(*reinterpret_cast<const uint4*>(pw + col * PSTR + ((g ^ p_slot_xor((col >> 2) & 3)) << 3)));
 }
 
 // Sum over the 64 lanes as a wave-uniform value: the 16-lane rows by DPP, the four row sums by
@@ -365,10 +386,10 @@ KA_DEV void rmsnorm_to_lds(const Args& a, const bf16_t* g, bf16_t* xs, float* re
   __syncthreads();
 }
 
-// LDS layout (bytes): x / act staging [0, 28 KB) (the attention leader's scratch reuses it: x is dead
-// between the QKV rows and the O rows); the waves' weight rings [28 KB, 28 KB + 8 x RING KB); the norm
+// LDS layout (bytes): x / act staging [0, 29 KB) (the attention leader's scratch reuses it: x is dead
+// between the QKV rows and the O rows); the waves' weight rings [29 KB, 29 KB + 8 x RING KB); the norm
 // reduction at the end.  > 80 KB: one workgroup per CU.
-constexpr int LDS_X = 0, LDS_ATT = 0, LDS_RING = 28 * 1024, LDS_RED = LDS_RING + NW * RING * 1024;
+constexpr int LDS_X = 0, LDS_ATT = 0, LDS_RING = 29 * 1024, LDS_RED = LDS_RING + NW * RING * 1024;
 constexpr int LDS_OUT = LDS_RED + 64, LDS_BYTES = LDS_OUT + 1024;   // LDS_OUT: a phase's bf16 row results
 
 __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
@@ -400,9 +421,10 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
   // the token's position / slot / context (fixed for the launch) and the attention loop's trip count
   const int p = a.pos[0], slot = a.slot[0], ctx = a.ctx[0];
   const int ncached = ctx - 1, nblk = (ncached + KBS - 1) / KBS;
-  // a leader wave's first two context blocks (fixed for the launch; prefetched every layer)
-  const int blk_w0 = __builtin_amdgcn_readfirstlane(wave < nblk ? a.bt[wave] : 0);
-  const int blk_w1 = __builtin_amdgcn_readfirstlane(wave + NW < nblk ? a.bt[wave + NW] : 0);
+  // a leader wave's first 32-token chunk: context blocks 2 w, 2 w + 1 (fixed for the launch;
+  // prefetched every layer; a missing second block repeats the first: finite values, weight 0)
+  const int blk_w0 = __builtin_amdgcn_readfirstlane(2 * wave < nblk ? a.bt[2 * wave] : 0);
+  const int blk_w1 = __builtin_amdgcn_readfirstlane(2 * wave + 1 < nblk ? a.bt[2 * wave + 1] : blk_w0);
   for (int r = own0 + lane; r < own1; r += 64) st_sc1(a.res + r, bf2f(a.h0[r]));
   arrive(gcnt);
 
@@ -451,8 +473,9 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     // it: after the arrival (its vmcnt(0) would otherwise hold the arrival back until they landed),
     // in flight while the workgroup waits for the others.
     auto sq = make_stream(Lw.wqkv, (hq + 2 * hkv) * HD, H, nq, lane, ring, qkv_row, gw);
-    sq.start();
+    if (!KA_PD_W0_DEFER || wave != 0) sq.start();
     wait_grid(a.sync, ++nbar, G, err);
+    if (KA_PD_W0_DEFER && wave == 0) sq.start();
     PD_STAMP(0);
     if (st && l > 0) st[(l - 1) * 16 + 12] = st[l * 16];   // the previous layer's barrier E ends here
     rmsnorm_to_lds(a, Lw.ln1, xs, red);
@@ -470,17 +493,21 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     arrive(a.sync + SYNC_GROUP + 32 * grp);   // this workgroup's QKV rows are published
     so.start();
     if (in_grp == 0) {
-      // the leader (no O rows: its ring is idle now): this layer's cached K / V blocks (each wave's
-      // first two) into the ring by LDS-DMA, in flight while the group's QKV rows finish
+      // the leader (no O rows: its ring is idle now): each wave's first 32-token chunk of this layer's
+      // cached K / V (blocks 2 w, 2 w + 1) into its ring by LDS-DMA, in flight while the group's QKV
+      // rows finish.  K rows land XOR-swizzled (16-B chunk c16 of token t at slot c16 ^ t: the MFMA
+      // operand reads of 16 tokens hit distinct banks); V [128][16 tokens] as is.
       const size_t hs = (size_t)KBS * HD;
+      if (2 * wave < nblk) {
+        const int tk = lane >> 4, sl = lane & 15;   // token within a 1-KB piece, slot of the lane
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        if (wave + k * NW < nblk) {
-          const size_t boff = ((size_t)(k ? blk_w1 : blk_w0) * hkv + grp) * hs + (size_t)l * a.cache_layer;
+        for (int j = 0; j < 2; ++j) {
+          const size_t boff = ((size_t)(j ? blk_w1 : blk_w0) * hkv + grp) * hs + (size_t)l * a.cache_layer;
 #pragma unroll
           for (int pc = 0; pc < 4; ++pc) {
-            dma_1k(a.k_cache + boff, (uint32_t)pc * 1024u + (uint32_t)lane * 16u, ring + (uint32_t)(k * 8 + pc) * 1024u);
-            dma_1k(a.v_cache + boff, (uint32_t)pc * 1024u + (uint32_t)lane * 16u, ring + (uint32_t)(k * 8 + 4 + pc) * 1024u);
+            const int t = 4 * pc + tk;
+            dma_1k(a.k_cache + boff, (uint32_t)(t * 256 + ((sl ^ t) << 4)), ring + (uint32_t)(j * 8 + pc) * 1024u);
+            dma_1k(a.v_cache + boff, (uint32_t)pc * 1024u + (uint32_t)lane * 16u, ring + (uint32_t)(j * 8 + 4 + pc) * 1024u);
           }
         }
       }
@@ -489,13 +516,16 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       // ---- P2: the group's attention (its first workgroup) ----
       wait_for(a.sync + SYNC_GROUP + 32 * grp, (l + 1) * per_group, err);
       PD_STAMP(3);
-      float* const qf = reinterpret_cast<float*>(lds + LDS_ATT);            // [Gq][128] rotated q
-      float* const kn = qf + Gq * HD;                                        // [128] rotated new k
-      float* const vn = kn + HD;                                             // [128] new v
-      float* const pw = vn + HD;                                             // [NW][Gq][16] probabilities
-      float* const mo = pw + NW * Gq * 16;                                   // [NW][Gq] (m, l) + [NW][Gq][128] o
-      float* const lo = mo + NW * Gq;
-      float* const oo = lo + NW * Gq;
+      // scratch (LDS_ATT): per-wave P re-layout | rotated q (bf16) | new k, v (fp32) | per-wave m, l |
+      // new-token scores | per-wave o of the group's q rows
+      bf16_t* const pscr = reinterpret_cast<bf16_t*>(lds + LDS_ATT);             // [NW][16 PSTR]
+      bf16_t* const qb = reinterpret_cast<bf16_t*>(lds + LDS_ATT + 10240);       // [4][128]
+      float* const kn = reinterpret_cast<float*>(lds + LDS_ATT + 11264);         // [128]
+      float* const vn = kn + HD;                                                  // [128]
+      float* const mo = vn + HD;                                                  // [NW][4]
+      float* const lo = mo + NW * 4;                                              // [NW][4]
+      float* const snr = lo + NW * 4;                                             // [4] (+ pad)
+      float* const oo = snr + 16;                                                 // [NW][4][128]
       const float* cs = a.cos_sin + (size_t)p * HD;
       // RoPE (neox halves) on the group's q heads and k; v as is
       for (int it = tid; it < (Gq + 2) * (HD / 2); it += NT) {
@@ -505,132 +535,122 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
         const float x1 = (i & 1) ? hi_f(w0) : lo_f(w0), x2 = (i & 1) ? hi_f(w1) : lo_f(w1);
         if (hh <= Gq) {
           const float c = cs[i], s = cs[HD / 2 + i];
-          float* dst = hh < Gq ? qf + hh * HD : kn;
           // bf16 rounding of the rotated values, as the cache / the unfused kernels hold them
-          dst[i] = bf2f(f2bf(x1 * c - x2 * s));
-          dst[HD / 2 + i] = bf2f(f2bf(x2 * c + x1 * s));
+          const bf16_t r1 = f2bf(x1 * c - x2 * s), r2 = f2bf(x2 * c + x1 * s);
+          if (hh < Gq) {
+            qb[hh * HD + i] = r1;
+            qb[hh * HD + HD / 2 + i] = r2;
+          } else {
+            kn[i] = bf2f(r1);
+            kn[HD / 2 + i] = bf2f(r2);
+          }
         } else {
           vn[i] = x1;
           vn[HD / 2 + i] = x2;
         }
       }
       __syncthreads();
-      PD_STAMP(13);
       bf16_t* const kc = a.k_cache + (size_t)l * a.cache_layer;
       bf16_t* const vc = a.v_cache + (size_t)l * a.cache_layer;
       const size_t hs = (size_t)KBS * HD;   // elements per (block, head)
-      // the ring's K / V have landed (waited before the appends below: stores count in vmcnt too)
+      // the ring's K / V have landed
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (slot >= 0 && tid < HD) {          // append the new token (read by the NEXT launches only)
-        const int blk = slot / KBS, off = slot % KBS;
-        kc[((size_t)blk * hkv + grp) * hs + off * HD + tid] = f2bf(kn[tid]);
-        vc[((size_t)blk * hkv + grp) * hs + tid * KBS + off] = f2bf(vn[tid]);
-      }
-      // cached tokens [0, ctx - 1): wave w takes blocks w, w + NW, ...; lane (hh = lane >> 4, t = lane & 15)
-      float m_w = -INFINITY, l_w = 0.f;   // this lane's row hh (lanes of one 16-lane row agree)
-      float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // o[hh][2 lane + e], hh < 4
-      const int hh = lane >> 4, t = lane & 15;
-      // the wave's first two blocks are in its ring (LDS-DMA at the layer's top: K [16 tok][128] at
-      // slot 8 k, V [128][16 tok] at slot 8 k + 4); later blocks come from global memory
-      const char* const rbase = lds + LDS_RING + wave * RING * 1024;
-      int kk = 0;
-      for (int bi = wave; bi < nblk; bi += NW, ++kk) {
-        const bool in_ring = kk < 2;
-        const int blk = in_ring ? 0 : a.bt[bi];
-        const int tok = bi * KBS + t;
-        uint4 va0, va1, vb0, vb1;   // V of this lane's dims 2 lane, 2 lane + 1 (16 tokens each)
-        float s = -INFINITY;
-        const float* qp = qf + hh * HD;
-        if (in_ring) {
-          const uint4* vr = reinterpret_cast<const uint4*>(rbase + kk * 8192 + 4096 + lane * 64);
-          va0 = vr[0];
-          va1 = vr[1];
-          vb0 = vr[2];
-          vb1 = vr[3];
-          if (hh < Gq && tok < ncached) {
-            // chunk order rotated by the token: the 16 tokens' rows (256 B apart) hit distinct banks
-            const char* kr = rbase + kk * 8192 + t * 256;
-            float d = 0.f;
+      PD_STAMP(13);
+      // cached tokens [0, ctx - 1) in 32-token chunks, chunk c on wave c mod NW, on MFMA 16x16x32
+      // (the layouts of csrc/attention.hip's paged_decode_kernel): S = Q K^T with the group's q heads
+      // as rows (zero rows past Gq), online softmax, O += P V.  Lane (col, gq) = (lane & 15, lane >> 4).
+      const int col = lane & 15, gq = lane >> 4;
+      bf16x8 qfr[4];
 #pragma unroll
-            for (int c = 0; c < HD / 8; ++c) {
-              const int ch = (c + t) & (HD / 8 - 1);
-              const uint4 k8 = *reinterpret_cast<const uint4*>(kr + ch * 16);
-              const float4 q0 = *reinterpret_cast<const float4*>(qp + ch * 8);
-              const float4 q1 = *reinterpret_cast<const float4*>(qp + ch * 8 + 4);
-              d += q0.x * lo_f(k8.x) + q0.y * hi_f(k8.x) + q0.z * lo_f(k8.y) + q0.w * hi_f(k8.y);
-              d += q1.x * lo_f(k8.z) + q1.y * hi_f(k8.z) + q1.z * lo_f(k8.w) + q1.w * hi_f(k8.w);
-            }
-            s = d * a.scale_log2;
-          }
-        } else {
-          const bf16_t* vp = vc + ((size_t)blk * hkv + grp) * hs + (2 * lane) * KBS;
-          va0 = *reinterpret_cast<const uint4*>(vp);
-          va1 = *reinterpret_cast<const uint4*>(vp + 8);
-          vb0 = *reinterpret_cast<const uint4*>(vp + KBS);
-          vb1 = *reinterpret_cast<const uint4*>(vp + KBS + 8);
-          if (hh < Gq && tok < ncached) {
-            const bf16_t* kp = kc + ((size_t)blk * hkv + grp) * hs + t * HD;
-            float d = 0.f;
-#pragma unroll
-            for (int c = 0; c < HD / 8; ++c) {
-              const uint4 k8 = *reinterpret_cast<const uint4*>(kp + c * 8);
-              const uint32_t kw[4] = {k8.x, k8.y, k8.z, k8.w};
-#pragma unroll
-              for (int e = 0; e < 4; ++e) d += qp[c * 8 + 2 * e] * lo_f(kw[e]) + qp[c * 8 + 2 * e + 1] * hi_f(kw[e]);
-            }
-            s = d * a.scale_log2;
-          }
-        }
-        if (bi == wave) PD_STAMP(15);   // the first block's scores (K landed + q.k)
-        const float mx = row16_max(s);
-        const float mn = fmaxf(m_w, mx);
-        const float alpha = mn == -INFINITY ? 1.f : exp2f(m_w - mn);
-        const float pr = s == -INFINITY ? 0.f : exp2f(s - mn);
-        l_w = l_w * alpha + row16_sum(pr);
-        m_w = mn;
-        if (hh < Gq) pw[(wave * Gq + hh) * 16 + t] = pr;
-        // every lane rescales the o of all Gq rows: fetch each row's alpha from its 16-lane row
-        float al[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) al[r] = __shfl(alpha, r * 16, 64);
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        // P V: lane owns dims 2 lane, 2 lane + 1 of every row; V block is [dim][16 tokens]
-        const int nvalid = min(KBS, ncached - bi * KBS);
-        const uint32_t v0[8] = {va0.x, va0.y, va0.z, va0.w, va1.x, va1.y, va1.z, va1.w};
-        const uint32_t v1[8] = {vb0.x, vb0.y, vb0.z, vb0.w, vb1.x, vb1.y, vb1.z, vb1.w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (r >= Gq) break;
-          float s0 = acc[0][r] * al[r], s1 = acc[1][r] * al[r];
-          const float* pp = pw + (wave * Gq + r) * 16;
-#pragma unroll
-          for (int tt = 0; tt < 16; ++tt) {
-            if (tt < nvalid) {   // slots past the context may hold anything (never multiply them by 0)
-              const float pv = pp[tt];
-              s0 += pv * ((tt & 1) ? hi_f(v0[tt >> 1]) : lo_f(v0[tt >> 1]));
-              s1 += pv * ((tt & 1) ? hi_f(v1[tt >> 1]) : lo_f(v1[tt >> 1]));
-            }
-          }
-          acc[0][r] = s0;
-          acc[1][r] = s1;
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-      // per-wave (m, l, o) -> LDS; rows hh < Gq (lane t == 0 of each 16-lane row writes m, l)
-      if (t == 0 && hh < Gq) {
-        mo[wave * Gq + hh] = m_w;
-        lo[wave * Gq + hh] = l_w;
-      }
+      for (int ks = 0; ks < 4; ++ks)
+        qfr[ks] = as_bf16x8(col < Gq ? *reinterpret_cast<const uint4*>(qb + col * HD + 32 * ks + 8 * gq)
+                                     : make_uint4(0, 0, 0, 0));
+      float m[4], lsum[4];
+      f32x4 o[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (r >= Gq) break;
-        oo[(wave * Gq + r) * HD + 2 * lane] = acc[0][r];
-        oo[(wave * Gq + r) * HD + 2 * lane + 1] = acc[1][r];
+        m[r] = -INFINITY;
+        lsum[r] = 0.f;
       }
-      float* const snr = oo + NW * Gq * HD;   // [Gq] the new token's scores, one wave per q head
-      if (wave < Gq) {
-        const float v = wave_total(qf[wave * HD + 2 * lane] * kn[2 * lane] + qf[wave * HD + 2 * lane + 1] * kn[2 * lane + 1]);
+#pragma unroll
+      for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bf16_t* const pw = pscr + wave * 16 * PSTR;
+      const char* const rb = lds + LDS_RING + wave * RING * 1024;   // the wave's first chunk (ring)
+      const int nch = (ncached + 31) / 32;
+      for (int c = wave; c < nch; c += NW) {
+        const int t0 = c * 32;
+        const bool in_ring = c == wave;
+        int blk0 = 0, blk1 = 0;
+        if (!in_ring) {
+          blk0 = a.bt[2 * c];
+          blk1 = t0 + 16 < ncached ? a.bt[2 * c + 1] : blk0;
+        }
+        f32x4 sc[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            uint4 kf;
+            if (in_ring)   // swizzled rows: 16-B chunk c16 of token t at (c16 ^ t)
+              kf = *reinterpret_cast<const uint4*>(rb + j * 8192 + col * 256 + (((4 * ks + gq) ^ col) << 4));
+            else
+              kf = *reinterpret_cast<const uint4*>(kc + ((size_t)(j ? blk1 : blk0) * hkv + grp) * hs + col * HD +
+                                                   8 * gq + 32 * ks);
+            acc = mfma16x16x32(qfr[ks], as_bf16x8(kf), acc);
+          }
+          sc[j] = acc;
+        }
+        if (c == wave) PD_STAMP(15);   // the first chunk's scores
+        uint4 vf[8];
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+          if (in_ring)
+            vf[n] = *reinterpret_cast<const uint4*>(rb + (gq >> 1) * 8192 + 4096 + (n * 16 + col) * 32 + (gq & 1) * 16);
+          else
+            vf[n] = *reinterpret_cast<const uint4*>(vc + ((size_t)((gq >> 1) ? blk1 : blk0) * hkv + grp) * hs +
+                                                    (n * 16 + col) * KBS + 8 * (gq & 1));
+        }
+        float alpha[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x0 = t0 + col < ncached ? sc[0][r] * a.scale_log2 : -INFINITY;
+          const float x1 = t0 + 16 + col < ncached ? sc[1][r] * a.scale_log2 : -INFINITY;
+          const float mn = fmaxf(m[r], row16_max(fmaxf(x0, x1)));
+          alpha[r] = exp2f(m[r] - mn);
+          const float p0 = exp2f(x0 - mn), p1 = exp2f(x1 - mn);
+          lsum[r] = lsum[r] * alpha[r] + row16_sum(p0 + p1);
+          m[r] = mn;
+          p_store(pw, 4 * gq + r, col, p0, p1);
+        }
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[n][r] *= alpha[r];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const bf16x8 pf = p_load(pw, col, gq);
+#pragma unroll
+        for (int n = 0; n < 8; ++n) o[n] = mfma16x16x32(pf, as_bf16x8(vf[n]), o[n]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // P scratch read before the next chunk's writes
+      }
+      // per-wave (m, l, o) of rows 0 .. Gq - 1 (lanes gq == 0 hold rows r = 0..3) -> LDS
+      if (gq == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (r < Gq) {
+            if (col == 0) {
+              mo[wave * 4 + r] = m[r];
+              lo[wave * 4 + r] = lsum[r];
+            }
+#pragma unroll
+            for (int n = 0; n < 8; ++n) oo[(wave * 4 + r) * HD + n * 16 + col] = o[n][r];
+          }
+        }
+      }
+      if (wave < Gq) {   // the new token's score of q head `wave`
+        const float v = wave_total(bf2f(qb[wave * HD + 2 * lane]) * kn[2 * lane] +
+                                   bf2f(qb[wave * HD + 2 * lane + 1]) * kn[2 * lane + 1]);
         if (lane == 0) snr[wave] = v * a.scale_log2;
       }
       __syncthreads();
@@ -640,19 +660,25 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
         const int r = it / HD, d = it - r * HD;
         const float sn = snr[r];
         float M = sn;
-        for (int w = 0; w < NW; ++w) M = fmaxf(M, mo[w * Gq + r]);
+        for (int w = 0; w < NW; ++w) M = fmaxf(M, mo[w * 4 + r]);
         float den = exp2f(sn - M), num = den * vn[d];
         for (int w = 0; w < NW; ++w) {
-          const float mw = mo[w * Gq + r];
+          const float mw = mo[w * 4 + r];
           if (mw == -INFINITY) continue;
           const float e = exp2f(mw - M);
-          den += e * lo[w * Gq + r];
-          num += e * oo[(w * Gq + r) * HD + d];
+          den += e * lo[w * 4 + r];
+          num += e * oo[(w * 4 + r) * HD + d];
         }
-        const float o = num / den;
-        const float o2 = __shfl_xor(o, 1, 64);   // d and d ^ 1 are neighbouring lanes
+        const float o1 = num / den;
+        const float o2 = __shfl_xor(o1, 1, 64);   // d and d ^ 1 are neighbouring lanes
         if ((d & 1) == 0)
-          st_sc1u(a.attn + (grp * Gq + r) * HD + d, pack2(o, o2));
+          st_sc1u(a.attn + (grp * Gq + r) * HD + d, pack2(o1, o2));
+      }
+      if (slot >= 0 && tid < HD) {          // append the new token (read by the NEXT launches only; after the
+                                            // attention: hipcc waits for these stores before reusing their VGPRs)
+        const int blk = slot / KBS, off = slot % KBS;
+        kc[((size_t)blk * hkv + grp) * hs + off * HD + tid] = f2bf(kn[tid]);
+        vc[((size_t)blk * hkv + grp) * hs + tid * KBS + off] = f2bf(vn[tid]);
       }
     }
     PD_STAMP(4);
@@ -671,8 +697,9 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     PD_STAMP(6);
     auto sg = make_stream(Lw.w13, 2 * I, H, 2 * ng, lane, ring, gu_row, gw);
     arrive(gcnt);
-    sg.start();
+    if (!KA_PD_W0_DEFER || wave != 0) sg.start();
     wait_grid(a.sync, ++nbar, G, err);
+    if (KA_PD_W0_DEFER && wave == 0) sg.start();
     PD_STAMP(7);
     // ---- P4: norm + gate / up -> act ----
     rmsnorm_to_lds(a, Lw.ln2, xs, red);
@@ -689,8 +716,9 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     PD_STAMP(9);
     auto sd = make_stream(Lw.w2, H, I, no, lane, ring, own_row, gw);
     arrive(gcnt);
-    sd.start();
+    if (!KA_PD_W0_DEFER || wave != 0) sd.start();
     wait_grid(a.sync, ++nbar, G, err);
+    if (KA_PD_W0_DEFER && wave == 0) sd.start();
     PD_STAMP(10);
     // ---- P5: down rows -> residual ----
     stage_sc1(reinterpret_cast<uint4*>(lds + LDS_X), a.act, I / 8);   // act (sc1) -> LDS

@@ -110,7 +110,7 @@ def main():
                       flush=True)
             lead = stv[:, :, 13] > 0   # attention leaders: RoPE / context blocks / merge
             if lead.any():
-                sub = [("rope", 3, 13), ("first K + q.k", 13, 15), ("rest of blocks", 15, 14), ("merge", 14, 4)]
+                sub = [("rope + K/V landed", 3, 13), ("first q.k", 13, 15), ("rest of blocks", 15, 14), ("merge", 14, 4)]
                 print("  attention: " + ", ".join(f"{n} {float((stv[:, :, b] - stv[:, :, a])[lead].mean()):.1f}"
                                                   for n, a, b in sub), flush=True)
             # per-XCD (wg % 8) mean gate_up / down durations: is the skew a fabric effect?

@@ -453,13 +453,14 @@ def test_mixtral_forward_hip_vs_reference():
     assert all(len(s.output_ids) == len(be._forced) + 6 for s in seqs)
 
 
-@pytest.mark.parametrize("graphs", [False, True])
-def test_persistent_decode_matches_kernel_chain_and_fp32(graphs):
+@pytest.mark.parametrize("graphs,long_ctx", [(False, False), (True, False), (False, True)])
+def test_persistent_decode_matches_kernel_chain_and_fp32(graphs, long_ctx):
     """csrc/decode_persistent.hip (every layer of a batch-1 decode step in one launch, grid-wide
     arrival counters) against the per-kernel decode chain and the fp32 references, over 6 decode
     steps of one sequence (the real Llama-3-8B layer geometry, 2 layers): hidden states within bf16
     tolerance, the same KV appended, the tokens equal to the chain's, the error word clear — eagerly
-    and as the captured B = 1 hipGraph."""
+    and as the captured B = 1 hipGraph.  long_ctx: a ~400-token context, past the 256 tokens the
+    attention leaders prefetch into their rings (the chunk loop's global-load path)."""
     from ai_agent_kubectl_amd.engine.sequence import Sequence
     from ai_agent_kubectl_amd.models.llama import AttnMeta
     eng = _engine("llama3-8b-2l", graphs=graphs, buckets=(1,), max_batch=1, kv_cache_tokens=8192)
@@ -468,11 +469,14 @@ def test_persistent_decode_matches_kernel_chain_and_fp32(graphs):
     sch.gather_max_s = 0.0
     m = r.model
     with torch.inference_mode():
-        sch.add(Sequence(prompt_ids=be.prompt_ids("list all pods in kube-system"),
-                         params=SamplingParams(max_new_tokens=16, ignore_eos=True)))
-        b = sch.schedule()
-        eng._apply(b, r.execute(b))
-        sch.on_step_done(b)
+        ids = be.prompt_ids("list all pods in kube-system")
+        if long_ctx:
+            ids = ids + [(7 * i + 11) % 5000 + 100 for i in range(400 - len(ids))]
+        sch.add(Sequence(prompt_ids=ids, params=SamplingParams(max_new_tokens=16, ignore_eos=True)))
+        while sch.waiting:   # a long prompt may take several (chunked) prefill steps
+            b = sch.schedule()
+            eng._apply(b, r.execute(b))
+            sch.on_step_done(b)
         for step in range(6):
             batch = sch.schedule()
             assert batch.is_decode and len(batch.seqs) == 1
