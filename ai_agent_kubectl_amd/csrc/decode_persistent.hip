@@ -1,31 +1,30 @@
 // Persistent batch-1 decode: every decoder layer of a Llama model (TP = 1, head_dim 128, KV block 16)
 // for ONE token in ONE launch (the serving path's B = 1 hipGraph replays it once per token).
+// 2.85 ms/step for Llama-3-8B against 3.45 for the ~7-kernels-per-layer chain
+// (profiles/r4/persistent_decode/README.md).
 //
-// Why: at batch 1 the chain of ~7 kernels per layer (norm, QKV GEMV, fused RoPE + attention, O GEMV,
-// norm, gate_up GEMV, down GEMV + SiLU) pays a launch boundary, a ramp and a tail per kernel — the
-// layer took ~110 us against ~71 us of weight streaming at the HBM rate (docs/PERFORMANCE.md).  Here
-// one workgroup per CU (the dynamic LDS request admits no second one) walks the layers; the weight
-// stream of each phase is ISSUED before the grid-wide wait that precedes it (the register ring of
-// the row-streaming GEMV is filled, then the workgroup waits for the activations), so a phase's
-// first weight bytes are in flight while the previous phase drains — the "stream ahead of the data
-// dependencies" structure (MI355X_MICROARCH.md, Persistent kernels).
-//
-// Phases of layer l (G workgroups x 8 waves; group h = the G / hkv workgroups of KV head h):
-//   P1  every workgroup: RMSNorm of the fp32 residual -> x (LDS); the group's waves compute the QKV
-//       rows of head h (its 4 q heads, k, v) -> qkv (sc1 stores); group arrival counter
-//   P2  the group's first workgroup, after its group's arrivals: RoPE on q / k, KV append, attention
-//       over the context + the new token (exp2 online softmax, 8 waves over 16-token blocks, merged
-//       through LDS) -> attn; the others go straight to the grid barrier with their O rows issued
-//   P3  O GEMV rows of each wave -> residual += (each residual element owned by one wave)
-//   P4  RMSNorm of the residual -> x; gate + up rows -> act = silu(g) * u
+// One 512-thread workgroup per CU (the dynamic LDS request admits no second one).  Per layer l
+// (group h = the G / hkv workgroups of KV head h; its first workgroup is the group's leader):
+//   P1  every workgroup: RMSNorm of the fp32 residual -> x (LDS); its waves' QKV rows of head h ->
+//       qkv (sc1 stores, row pairs packed); group arrival.  The leader then DMAs each wave's first
+//       32-token chunk of this layer's cached K / V into its (idle) weight ring.
+//   P2  the leader, after its group's arrivals: RoPE on q / k, attention on MFMA 16x16x32 over
+//       32-token chunks (K / V from the ring; from global memory past 8 chunks), merged across
+//       waves and with the new token through LDS -> attn; then the KV append
+//   P3  O GEMV rows (the non-leaders' waves) -> residual +=
+//   P4  RMSNorm -> x; gate + up rows -> act = silu(g) * u
 //   P5  down GEMV rows (K = I) -> residual +=
-// Grid barriers between the phases (B: after P2, C: after P3, D: after P4, E: after P5): one
-// monotonic counter, lane 0 of each workgroup adds behind a workgroup barrier after every wave's
-// `s_waitcnt vmcnt(0)`, one lane polls with relaxed agent-scope loads; all activations that cross
-// workgroups are written and read with agent-scope (sc1) accesses — the MI355X_MICROARCH.md hand-off
-// table, row 1 (no fence).  Spins are bounded: a workgroup that is never scheduled (the GPU shared
-// with another kernel) sets the error word instead of hanging the chip, and every later wait skips.
-// Weights stream with non-temporal 16-B loads (read once per token).
+// Grid barriers between the phases (B after P2, C after P3, D after P4, E after P5): arrival
+// counters sharded per XCD slot (wg mod 8), each on its own 128-B line; one lane per shard polls
+// with relaxed sc1 loads.  Everything that crosses workgroups is written and read with sc1 accesses
+// (MI355X_MICROARCH.md hand-off table, row 1: no fences).  Spins are bounded: a workgroup that is
+// never scheduled sets the error word instead of hanging the chip (the runner reads it back with
+// the step's tokens and falls back to the kernel chain).
+//
+// Weight streaming (Stream): each wave streams its rows 1 KB per LDS-DMA instruction (nt) through a
+// 16-slot LDS ring (no VGPRs held by bytes in flight), consumes two pieces per iteration against x in
+// LDS with v_dot2, and refills the slots; the next phase's first 16 pieces are issued between the
+// barrier arrival and the wait, so they stream while the grid synchronises.
 #include "common.h"
 
 namespace pd {
