@@ -67,6 +67,15 @@ struct DecodeFuse {
   const int* slot_mapping;
   bf16_t* k_cache;
   bf16_t* v_cache;
+  // cascade (shared-prefix) mode, nshared != nullptr and *nshared > 0: the first *nshared blocks of
+  // every sequence's table are the same physical blocks (prefix cache).  The chunk loop then skips
+  // them, the rotated q rows go to q_out, and the merged (unnormalised o, max, denominator) go to
+  // part_o / part_ml instead of `out`; cascade_prefix_kernel attends the shared blocks once per
+  // (kv head, 16 query rows) and merges.
+  const int* nshared;
+  bf16_t* q_out;      // [B, hq, 128]
+  float* part_o;      // [B, hq, 128]
+  float* part_ml;     // [B, hq, 2]
 };
 
 __device__ __forceinline__ uint2 dq_ld4(const DecodeFuse& f, size_t off) {
@@ -101,8 +110,12 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
   const int G = hq / hkv;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, grp = lane >> 4;
+  int ns = 0;   // cascade: shared leading blocks, attended by cascade_prefix_kernel
+  if constexpr (FUSED) {
+    if (fz.nshared != nullptr) ns = *fz.nshared;
+  }
   // fused: the chunk loop covers the cached tokens only; the new one is merged from LDS
-  const int ctx = ctx_lens[b] - (FUSED ? 1 : 0);
+  const int ctx = ctx_lens[b] - (FUSED ? 1 : 0) - ns * KBS;
 
   __shared__ __attribute__((aligned(16))) float smem[NW * 16 * 2 + NW * 16 * (HD + 4)];
   // per-wave P scratch; fused: first the staging of the G rotated q rows + k ((G + 1) x 128 bf16,
@@ -118,7 +131,7 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
   // depend only on the block table, so their HBM latency overlaps the fused prologue's (split-K
   // partial loads, RoPE, cache append) instead of following it.  At the serving shape (context
   // <= 128 tokens, one chunk per wave) that is the whole chunk loop's memory traffic.
-  const int* bt = block_tables + (size_t)b * max_blocks;
+  const int* bt = block_tables + (size_t)b * max_blocks + ns;
   const int nchunks = (ctx + 31) >> 5;
   const size_t head_stride = (size_t)KBS * HD;  // elements per (block, head)
   uint4 kr[2][4], vr[8];
@@ -196,6 +209,13 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
       }
     }
     __syncthreads();
+    if (ns > 0) {   // cascade: the rotated q rows for cascade_prefix_kernel
+      for (int i = threadIdx.x; i < G * 16; i += 64 * NW) {
+        const int row = i >> 4, c8 = (i & 15) * 8;
+        *reinterpret_cast<uint4*>(fz.q_out + ((size_t)b * hq + h * G + row) * HD + c8) =
+            *reinterpret_cast<const uint4*>(&p_lds[0][0] + row * HD + c8);
+      }
+    }
   }
 
   if constexpr (FUSED) {
@@ -330,6 +350,14 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
         }
       }
     }
+    if (FUSED && ns > 0) {   // cascade: the unnormalised partial, merged by cascade_prefix_kernel
+      const size_t idx = (size_t)b * hq + h * G + row;
+      float* po = fz.part_o + idx * HD + d0;
+      *reinterpret_cast<float4*>(po) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      *reinterpret_cast<float4*>(po + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+      if (d0 == 0) *reinterpret_cast<float2*>(fz.part_ml + idx * 2) = make_float2(M, den);
+      continue;
+    }
     const float inv = den > 0.f ? 1.f / den : 0.f;
     uint4 res = make_uint4(pack2(acc[0] * inv, acc[1] * inv), pack2(acc[2] * inv, acc[3] * inv),
                            pack2(acc[4] * inv, acc[5] * inv), pack2(acc[6] * inv, acc[7] * inv));
@@ -384,7 +412,8 @@ extern "C" int ka_paged_decode_rope(void* out, const void* qkv, const float* P, 
   if (head_dim != HD || block_size != KBS || hq % hkv != 0 || hq / hkv > 15) return (int)hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
   DecodeFuse fz{static_cast<const bf16_t*>(qkv), P, split, p_bf16, (size_t)batch * (hq + 2 * hkv) * HD, positions,
-                cos_sin, slot_mapping, static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache)};
+                cos_sin, slot_mapping, static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache),
+                nullptr, nullptr, nullptr, nullptr};
   auto args = [&](auto kern, int nw) {
     hipLaunchKernelGGL(kern, dim3(hkv, batch), dim3(64 * nw), 0, stream, static_cast<bf16_t*>(out), nullptr,
                        static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), block_tables,
@@ -392,6 +421,161 @@ extern "C" int ka_paged_decode_rope(void* out, const void* qkv, const float* P, 
   };
   if (decode_two_waves(batch, hq, hkv)) args(paged_decode_kernel<true, 2>, 2);
   else args(paged_decode_kernel<true, 4>, 4);
+  KA_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Cascade decode attention, part 2 (after paged_decode_kernel<true> in cascade mode): the nshared
+// leading blocks that every sequence of the batch shares (the prefix cache hands all of them the
+// same physical blocks) are attended ONCE per (kv head, 16 query rows) instead of once per
+// sequence: at B = 256 with an 80-token shared prefix the chain kernel read those blocks 256 times
+// (≈ 80 MB of L2 traffic per layer).  Wave w of workgroup (h, y) takes sequences
+// (4 y + w) 16 / G ..: 16 query rows (16 / G sequences x G heads) on MFMA 16x16x32 over 32-token
+// chunks (the layouts of paged_decode_kernel), then merges with the per-sequence partial.
+template <int G>
+__global__ __launch_bounds__(256) void cascade_prefix_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ qrot,
+                                                             const float* __restrict__ part_o,
+                                                             const float* __restrict__ part_ml,
+                                                             const bf16_t* __restrict__ k_cache,
+                                                             const bf16_t* __restrict__ v_cache,
+                                                             const int* __restrict__ block_tables,
+                                                             const int* __restrict__ nshared, int batch, int hq, int hkv,
+                                                             float scale_log2) {
+  const int ns = *nshared;
+  if (ns <= 0) return;   // no shared prefix this step: paged_decode_kernel wrote the outputs
+  constexpr int SPW = 16 / G;   // sequences per wave
+  const int h = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int s0 = (blockIdx.y * 4 + wave) * SPW;
+  __shared__ __attribute__((aligned(16))) bf16_t p_lds[4][16 * PSTR];
+  if (s0 >= batch) return;   // (no workgroup barrier below)
+  const int ntok = ns * KBS, nchunks = (ntok + 31) >> 5;
+  const size_t head_stride = (size_t)KBS * HD;
+  const int qs = s0 + col / G;   // query row col: sequence qs, head h G + col % G
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+    qf[ks] = as_bf16x8(qs < batch ? *reinterpret_cast<const uint4*>(qrot + ((size_t)qs * hq + h * G + col % G) * HD +
+                                                                  8 * grp + 32 * ks)
+                                  : make_uint4(0, 0, 0, 0));
+  float m[4], l[4];
+  f32x4 o[8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m[r] = -INFINITY;
+    l[r] = 0.f;
+  }
+#pragma unroll
+  for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16_t* pw = p_lds[wave];
+  for (int c = 0; c < nchunks; ++c) {
+    const int t0 = c * 32;
+    const int blk0 = block_tables[2 * c], blk1 = 2 * c + 1 < ns ? block_tables[2 * c + 1] : blk0;
+    uint4 kr[2][4], vr[8];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bf16_t* kp = k_cache + ((size_t)(j ? blk1 : blk0) * hkv + h) * head_stride + col * HD + 8 * grp;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) kr[j][ks] = *reinterpret_cast<const uint4*>(kp + 32 * ks);
+    }
+    const bf16_t* vp = v_cache + ((size_t)((grp >> 1) ? blk1 : blk0) * hkv + h) * head_stride + col * KBS + 8 * (grp & 1);
+#pragma unroll
+    for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(vp + (size_t)n * 16 * KBS);
+    f32x4 sc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) acc = mfma16x16x32(qf[ks], as_bf16x8(kr[j][ks]), acc);
+      sc[j] = acc;
+    }
+    float alpha[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float x0 = t0 + col < ntok ? sc[0][r] * scale_log2 : -INFINITY;
+      const float x1 = t0 + 16 + col < ntok ? sc[1][r] * scale_log2 : -INFINITY;
+      const float mn = fmaxf(m[r], row16_max(fmaxf(x0, x1)));
+      alpha[r] = exp2f(m[r] - mn);
+      const float p0 = exp2f(x0 - mn), p1 = exp2f(x1 - mn);
+      l[r] = l[r] * alpha[r] + row16_sum(p0 + p1);
+      m[r] = mn;
+      p_store(pw, 4 * grp + r, col, p0, p1);
+    }
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[n][r] *= alpha[r];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bf16x8 pf = p_load(pw, col, grp);
+#pragma unroll
+    for (int n = 0; n < 8; ++n) o[n] = mfma16x16x32(pf, as_bf16x8(vr[n]), o[n]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  // merge: lane (col, grp) holds rows 4 grp + r, dims 16 n + col
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 4 * grp + r, seq = s0 + row / G;
+    if (seq >= batch) continue;
+    const size_t idx = (size_t)seq * hq + h * G + row % G;
+    const float2 ml = *reinterpret_cast<const float2*>(part_ml + idx * 2);
+    const float M = fmaxf(m[r], ml.x);
+    const float ea = exp2f(m[r] - M), eb = ml.x == -INFINITY ? 0.f : exp2f(ml.x - M);
+    const float inv = 1.f / (ea * l[r] + eb * ml.y);
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int d = n * 16 + col;
+      out[idx * HD + d] = f2bf((ea * o[n][r] + eb * part_o[idx * HD + d]) * inv);
+    }
+  }
+}
+
+// Workspace bytes of the cascade mode: partial o (fp32) + (max, denominator) + rotated q (bf16).
+extern "C" size_t ka_decode_cascade_ws(int batch, int hq) {
+  return (size_t)batch * hq * (HD * 4 + 8 + HD * 2);
+}
+
+// ka_paged_decode_rope with the shared-prefix cascade: nshared (device int [1]) leading blocks of
+// every block table are shared by the whole batch (0: the plain kernel's result, the second kernel
+// returns at once).  Needs hq / hkv in {1, 2, 4, 8, 16}.
+extern "C" int ka_paged_decode_rope_cascade(void* out, const void* qkv, const float* P, int split, int p_bf16,
+                                            void* k_cache, void* v_cache, const int* positions, const float* cos_sin,
+                                            const int* slot_mapping, const int* block_tables, int max_blocks,
+                                            const int* ctx_lens, int batch, int hq, int hkv, int head_dim,
+                                            int block_size, float scale, const int* nshared, void* ws,
+                                            hipStream_t stream) {
+  if (batch <= 0) return 0;
+  const int G = hq / hkv;
+  if (head_dim != HD || block_size != KBS || hq % hkv != 0 || G > 15 || 16 % G != 0 || ws == nullptr ||
+      nshared == nullptr)
+    return (int)hipErrorInvalidValue;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  float* part_o = static_cast<float*>(ws);
+  float* part_ml = part_o + (size_t)batch * hq * HD;
+  bf16_t* q_out = reinterpret_cast<bf16_t*>(part_ml + (size_t)batch * hq * 2);
+  DecodeFuse fz{static_cast<const bf16_t*>(qkv), P, split, p_bf16, (size_t)batch * (hq + 2 * hkv) * HD, positions,
+                cos_sin, slot_mapping, static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache),
+                nshared, q_out, part_o, part_ml};
+  auto args = [&](auto kern, int nw) {
+    hipLaunchKernelGGL(kern, dim3(hkv, batch), dim3(64 * nw), 0, stream, static_cast<bf16_t*>(out), nullptr,
+                       static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), block_tables,
+                       max_blocks, ctx_lens, hq, hkv, scale_log2, fz);
+  };
+  if (decode_two_waves(batch, hq, hkv)) args(paged_decode_kernel<true, 2>, 2);
+  else args(paged_decode_kernel<true, 4>, 4);
+  const int spw = 16 / G;
+  const dim3 grid(hkv, (batch + 4 * spw - 1) / (4 * spw));
+#define KA_CASCADE(GV)                                                                                                    \
+  hipLaunchKernelGGL(cascade_prefix_kernel<GV>, grid, dim3(256), 0, stream, static_cast<bf16_t*>(out), q_out, part_o, \
+                     part_ml, static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), block_tables,   \
+                     nshared, batch, hq, hkv, scale_log2)
+  switch (G) {
+    case 1: KA_CASCADE(1); break;
+    case 2: KA_CASCADE(2); break;
+    case 4: KA_CASCADE(4); break;
+    default: KA_CASCADE(8); break;
+  }
+#undef KA_CASCADE
   KA_CHECK_LAUNCH();
 }
 

@@ -40,6 +40,7 @@ class AttnMeta:
     max_q_len: int = 1
     num_decode: int = 0                # mixed step: the first num_decode sequences are 1-token decode rows
     num_tokens: int = 0                # real tokens when the step is padded (rows beyond are padding)
+    shared_blocks: Optional[torch.Tensor] = None   # decode: [1] leading blocks shared by every row (cascade)
 
 
 class LlamaModel:
@@ -130,7 +131,7 @@ class LlamaModel:
                 # RoPE + KV append + attention in one kernel (the rotated q never goes to HBM)
                 a = ops.decode_attention_rope(qkv, meta.positions, self.cos_sin, meta.slot_mapping, k_cache[li],
                                               v_cache[li], meta.block_tables, meta.ctx_lens, self.hq, self.hkv,
-                                              self.D, self.scale)
+                                              self.D, self.scale, shared_blocks=meta.shared_blocks)
             else:
                 q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, k_cache[li],
                                       v_cache[li], self.hq, self.hkv, self.D)

@@ -170,12 +170,24 @@ def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float,
     return out
 
 
+_CASCADE_WS = {}
+
+
+def cascade_ok(B: int, hq: int, hkv: int) -> bool:
+    g = hq // hkv
+    return hq % hkv == 0 and g in (1, 2, 4, 8)
+
+
 def decode_attention_rope(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, block_tables, ctx_lens,
-                          hq: int, hkv: int, d: int, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                          hq: int, hkv: int, d: int, scale: float, out: Optional[torch.Tensor] = None,
+                          shared_blocks: Optional[torch.Tensor] = None) -> torch.Tensor:
     """One decode token per sequence: RoPE + paged-KV append + paged attention in ONE kernel
     (attention.hip, paged_decode_kernel<true>): the rotated queries never leave the chip and the new
     token is merged from LDS.  `qkv` may be a `SplitK` (the QKV projection's fp32 or bf16 partials).
-    Equivalent to `attention_decode(rope_kv_write(qkv, ...), ...)` (the CPU path)."""
+    shared_blocks (device int32 [1]): the number of leading block-table entries the whole batch
+    shares (prefix cache); > 0 runs the cascade (the shared blocks attended once per kv head and 16
+    query rows by cascade_prefix_kernel, merged with each sequence's own part).  Equivalent to
+    `attention_decode(rope_kv_write(qkv, ...), ...)` (the CPU path)."""
     lead = qkv.P if isinstance(qkv, SplitK) else qkv
     if _ref(lead) or d != 128 or k_cache.shape[2] != 16 or hq % hkv or hq // hkv > 15:
         if isinstance(qkv, SplitK) and qkv.is_bf16:
@@ -189,6 +201,17 @@ def decode_attention_rope(qkv, positions, cos_sin, slot_mapping, k_cache, v_cach
         src, P, split, pb = None, _p(qkv.P), qkv.split, int(qkv.is_bf16)
     else:
         src, P, split, pb = _p(qkv), None, 1, 0
+    if shared_blocks is not None and cascade_ok(B, hq, hkv):
+        key = (k_cache.device, B, hq)
+        ws = _CASCADE_WS.get(key)
+        if ws is None:   # allocated by the eager warm-up before graph capture
+            ws = torch.empty(int(lib.ka_decode_cascade_ws(B, hq)), dtype=torch.uint8, device=k_cache.device)
+            _CASCADE_WS[key] = ws
+        check(lib.ka_paged_decode_rope_cascade(_p(out), src, P, split, pb, _p(k_cache), _p(v_cache), _p(positions),
+                                               _p(cos_sin), _p(slot_mapping), _p(block_tables), block_tables.shape[1],
+                                               _p(ctx_lens), B, hq, hkv, d, k_cache.shape[2], float(scale),
+                                               _p(shared_blocks), _p(ws), _stream()), "paged_decode_rope_cascade")
+        return out
     check(lib.ka_paged_decode_rope(_p(out), src, P, split, pb, _p(k_cache), _p(v_cache), _p(positions), _p(cos_sin),
                                    _p(slot_mapping), _p(block_tables), block_tables.shape[1], _p(ctx_lens), B, hq,
                                    hkv, d, k_cache.shape[2], float(scale), _stream()), "paged_decode_rope")

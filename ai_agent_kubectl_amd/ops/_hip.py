@@ -27,7 +27,8 @@ P = ctypes.c_void_p
 I = ctypes.c_int
 F = ctypes.c_float
 
-_RESTYPES = {"ka_gemm_big_ws_bytes": ctypes.c_size_t, "ka_decode_persistent_ws": ctypes.c_size_t}
+_RESTYPES = {"ka_gemm_big_ws_bytes": ctypes.c_size_t, "ka_decode_persistent_ws": ctypes.c_size_t,
+             "ka_decode_cascade_ws": ctypes.c_size_t}
 
 _SIGS = {
     "ka_rmsnorm": [P, P, P, P, I, I, F, P],
@@ -39,6 +40,8 @@ _SIGS = {
     "ka_moe_topk": [P, P, P, I, I, I, P],
     "ka_paged_decode": [P, P, P, P, P, I, P, I, I, I, I, I, F, P],
     "ka_paged_decode_rope": [P, P, P, I, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, P],
+    "ka_paged_decode_rope_cascade": [P, P, P, I, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, P, P, P],
+    "ka_decode_cascade_ws": [I, I],
     "ka_paged_prefill": [P, P, P, P, P, I, P, P, I, I, I, I, I, I, F, P],
     "ka_gemm_skinny": [P, P, P, P, I, I, I, I, P],
     "ka_gemv_swiglu": [P, P, P, P, I, I, I, I, P],

@@ -167,6 +167,53 @@ def test_decode_attention_rope_fused(hq, hkv, reps, split):
     assert got[-1].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("hq,hkv,ns", [(32, 8, 5), (32, 8, 1), (32, 8, 0), (64, 8, 6), (8, 8, 4), (16, 8, 3)])
+@pytest.mark.parametrize("S", [33, 256])
+def test_decode_attention_rope_cascade(hq, hkv, ns, S):
+    """Cascade decode attention (the first ns blocks of every row's table are the same physical
+    blocks, attended once by cascade_prefix_kernel and merged) == the plain fused kernel == the fp32
+    reference, including rows whose own part is only the new token, a padding row, and ns = 0 (the
+    second kernel returns at once)."""
+    import random
+    rng = random.Random(ns * 7 + S)
+    d, nb = 128, 5000
+    k1, v1 = _cache(nb, hkv)
+    k2, v2 = k1.clone(), v1.clone()
+    shared = list(range(1, ns + 1))                       # physical blocks 1 .. ns
+    ctx_lens, rows = [], []
+    free = ns + 1
+    for s in range(S - 1):
+        own_tok = rng.choice([1, 1, 2, 16, 17, 40, 100])     # incl. the new token
+        c = ns * 16 + own_tok
+        n_own = (c + 15) // 16 - ns
+        rows.append(shared + list(range(free, free + n_own)))
+        free += n_own
+        ctx_lens.append(c)
+    rows.append([0])                                      # padding row
+    ctx_lens.append(0)
+    mb = max(len(r) for r in rows)
+    bt = torch.zeros(S, mb, dtype=torch.int32)
+    for i, r in enumerate(rows):
+        bt[i, :len(r)] = torch.tensor(r, dtype=torch.int32)
+    bt = bt.to(DEV)
+    ctx = torch.tensor(ctx_lens, dtype=torch.int32, device=DEV)
+    btc = bt.cpu()
+    slots = torch.tensor([int(btc[s, (c - 1) // 16]) * 16 + (c - 1) % 16 if c > 0 else -1
+                          for s, c in enumerate(ctx_lens)], dtype=torch.int32, device=DEV)
+    pos = (ctx - 1).clamp(min=0)
+    cs = ref.rope_cos_sin(4096, d, 5e5, device=DEV)
+    qkv = torch.randn(S, (hq + 2 * hkv) * d, device=DEV, dtype=BF)
+    nsh = torch.tensor([ns], dtype=torch.int32, device=DEV)
+    scale = d ** -0.5
+    got = ops.decode_attention_rope(qkv, pos, cs, slots, k1, v1, bt, ctx, hq, hkv, d, scale, shared_blocks=nsh)
+    plain = ops.decode_attention_rope(qkv, pos, cs, slots, k2, v2, bt, ctx, hq, hkv, d, scale)
+    assert torch.equal(k1, k2) and torch.equal(v1, v2)
+    q = ops.rope_kv_write(qkv, pos, cs, slots, k2.clone(), v2.clone(), hq, hkv, d)
+    want = ref.attention_decode(q, k2, v2, bt, ctx, scale)
+    close(got[:-1], want[:-1], atol=2e-2)
+    close(got[:-1], plain[:-1], atol=2e-2)
+
+
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 8)])
 @pytest.mark.parametrize("qlens,ctxs", [([90], [90]), ([7, 1, 33, 20], [71, 130, 33, 84]), ([130, 1], [130, 5])])
 def test_paged_prefill(hq, hkv, qlens, ctxs):

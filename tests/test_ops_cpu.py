@@ -55,3 +55,16 @@ def test_argmax_combine_reference_ties_lowest_id():
     vals = torch.tensor([[1.0, 5.0, 2.0], [3.0, 5.0, 2.0], [3.0, 1.0, 7.0]])
     idxs = torch.tensor([[10, 11, 12], [1000, 1001, 1002], [2000, 2001, 2002]], dtype=torch.int32)
     assert ops.argmax_combine(vals, idxs).tolist() == [1000, 11, 2002]
+
+
+def test_shared_prefix_len():
+    """engine/runner.py shared_prefix_len: the leading block-table columns every row shares, capped."""
+    import numpy as np
+    from ai_agent_kubectl_amd.engine.runner import shared_prefix_len
+    bt = np.array([[1, 2, 3, 9, 0], [1, 2, 3, 7, 8], [1, 2, 4, 5, 6]], dtype=np.int32)
+    assert shared_prefix_len(bt, 5) == 2
+    assert shared_prefix_len(bt[:2], 5) == 3
+    assert shared_prefix_len(bt[:2], 2) == 2
+    assert shared_prefix_len(bt[:1], 4) == 4
+    assert shared_prefix_len(bt, 0) == 0
+    assert shared_prefix_len(np.array([[5, 1], [6, 1]], dtype=np.int32), 2) == 0
