@@ -292,6 +292,18 @@ def _client_proc(cid, nproc, args, rank, port, C, shared, out_q):
 
 
 # ---------------------------------------------------------------------------------------------
+def _barrier(dist):
+    """A barrier that leaves the GPU alone on gloo: dist.barrier() resolves the accelerator
+    (torch._C._get_accelerator) and so opens the device in every rank, though the ranks issue no
+    GPU work (scripts/kfd_probe.py); on a box with a per-GPU process limit, N ranks + N replicas +
+    torchrun then exceed it at N = 8.  A CPU all-reduce synchronises the same way."""
+    if dist.get_backend() == "gloo":
+        import torch
+        dist.all_reduce(torch.zeros(1))
+    else:
+        dist.barrier()
+
+
 def bench_devices(world):
     """Engine devices of the N replicas: cuda:0..N-1, or BENCH_DEVICE (one device for every replica,
     e.g. `cpu` for the CPU test of this path, or a comma list)."""
@@ -450,7 +462,7 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
             if bad:
                 raise RuntimeError(f"priming failed: {bad[:2]}")
         if world > 1:
-            dist.barrier()
+            _barrier(dist)
         t_build = time.perf_counter() - t_build
 
         ctx = mp.get_context("spawn")
@@ -465,7 +477,7 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
         while done.value < warm_target:
             time.sleep(0.005)
         if world > 1:
-            dist.barrier()
+            _barrier(dist)
         m0 = asyncio.run(scrape_engine_metrics(port)) if rank == 0 else {}
         roles = ([("server", srv.pid)] if srv is not None else []) + [("client", p.pid) for p in procs]
         c0 = cpu_snapshot(roles)
@@ -481,7 +493,7 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
         phase.value = 2
         m1 = asyncio.run(scrape_engine_metrics(port)) if rank == 0 else {}
         if world > 1:
-            dist.barrier()
+            _barrier(dist)
         lat = {}
         errors = []
         for _ in procs:
@@ -492,7 +504,7 @@ def run_tcp(args, rank, local, world, C, buckets, dist):
         for p in procs:
             p.join(timeout=30)
         if world > 1:
-            dist.barrier()   # every rank's clients are done before rank 0 stops the server
+            _barrier(dist)   # every rank's clients are done before rank 0 stops the server
         if errors:
             raise RuntimeError("bad replies: %s" % errors[:3])
         d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1}
@@ -602,7 +614,7 @@ def run_asgi(args, rank, local, world, C, buckets, dist, prefix_caching=True):
                       partial_tokens=getattr(eng.bm, "partial_tokens", 0), chained_steps=eng.chained_steps,
                       engine_idle_s=eng.idle_s)
         if world > 1:
-            await loop.run_in_executor(None, dist.barrier)
+            await loop.run_in_executor(None, _barrier, dist)
         return st
 
     async def run():
@@ -752,7 +764,7 @@ def main():
             detail["tcp_vs_asgi"] = round(results["tcp"]["out"]["value"] / results["asgi"]["out"]["value"], 3)
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.barrier()
+        _barrier(dist)
         dist.destroy_process_group()
 
 
