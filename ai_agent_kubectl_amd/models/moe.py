@@ -8,7 +8,8 @@ attention all-reduce already produced them).  Two ways to combine the experts (S
   right after (`LlamaModel.forward`).  Decode messages are a few KB-MB and latency-bound, and the
   collective is shape-static, so it sits inside the decode hipGraphs;
 * all-to-all dispatch / combine (`moe_alltoall`, eager prefill when EP > 1 and
-  MOE_DISPATCH=a2a, the default): each rank routes only its 1/ep token shard, sends every
+  MOE_DISPATCH=a2a, the default; `moe_alltoall_static` with fixed per-pair capacities and no host
+  read, graph-capturable, everywhere when MOE_DISPATCH=a2a-static): each rank routes only its 1/ep token shard, sends every
   (token, slot) row to the rank owning its expert (A5 dispatch, `all_to_all_single` with exact
   split sizes), runs its local experts on what it received, sends the rows back (A5 combine),
   applies the router weights at the source and all-gathers the shards.  Per rank that moves
@@ -135,18 +136,21 @@ def _local_experts(xr, er, L, e0):
         ones = torch.ones((R, 1), dtype=torch.float32, device=xr.device)
         fn = ops.moe_experts if R <= MOE_HIP_MAX_ROWS else ops.moe_experts_grouped
         return fn(xr, w13, w2, ones, er.view(R, 1).to(torch.int32), e0)
-    out = torch.empty_like(xr)
+    out = torch.zeros_like(xr)
     el = er.long() - e0
+    # rows of other ranks' experts / padding (id -1, moe_alltoall_static) sort last and stay zero
+    el = torch.where((el >= 0) & (el < w13.shape[0]), el, torch.full_like(el, w13.shape[0]))
     order = torch.argsort(el, stable=True)
-    counts = torch.bincount(el, minlength=w13.shape[0]).tolist()   # one host sync (hipBLASLt shapes)
-    xs = xr.index_select(0, order)
+    counts = torch.bincount(el, minlength=w13.shape[0] + 1)[:w13.shape[0]].tolist()   # one host sync (hipBLASLt shapes)
+    n = sum(counts)
+    xs = xr.index_select(0, order[:n])
     ys = torch.empty_like(xs)
     off = 0
     for e, c in enumerate(counts):
         if c:
             ys[off:off + c] = F.linear(ops.silu_mul(F.linear(xs[off:off + c], w13[e])), w2[e])
             off += c
-    out.index_copy_(0, order, ys)
+    out.index_copy_(0, order[:n], ys)
     return out
 
 
@@ -185,6 +189,48 @@ def moe_alltoall(x, L, cfg, comm):
     return full.reshape(p * ts, H)[:T]
 
 
+def moe_alltoall_static(x, L, cfg, comm):
+    """A5 with shape-static split sizes, so it can be captured in a hipGraph (no host read): every
+    rank sends every rank exactly cap = ts * k rows (the most one destination can get from a shard of
+    ts tokens), the rows placed by a device-side running count per destination and the unused slots
+    carrying expert id -1 (computed as zero by the receiver).  Same result as `moe_alltoall`; moves
+    p * cap rows each way instead of the exact counts -- the price of static shapes, small at decode
+    batch sizes where the messages are latency-bound."""
+    p, r = comm.world_size, comm.rank
+    T, H = x.shape
+    k, E = cfg.top_k, cfg.num_experts
+    el = E // p
+    ts = -(-T // p)
+    cap = ts * k
+    lo, hi = min(T, r * ts), min(T, (r + 1) * ts)
+    xs = x[lo:hi]
+    t_loc = hi - lo
+    dev = x.device
+    if t_loc:
+        w, ids = ops.moe_topk(ops.linear(xs, L["router"]), k)
+    else:
+        w, ids = (torch.zeros((0, k), dtype=torch.float32, device=dev), torch.zeros((0, k), dtype=torch.int32, device=dev))
+    flat_ids = ids.reshape(-1).long()                                 # [n = t_loc * k]
+    dest = torch.div(flat_ids, el, rounding_mode="floor")
+    onehot = (dest.unsqueeze(1) == torch.arange(p, device=dev).unsqueeze(0)).to(torch.int64)   # [n, p]
+    pos = (onehot.cumsum(0) - 1).gather(1, dest.unsqueeze(1)).squeeze(1)   # row's index within its destination
+    slot = dest * cap + pos                                           # unique in [0, p * cap)
+    tok = torch.div(torch.arange(flat_ids.shape[0], device=dev), k, rounding_mode="floor")
+    send_x = x.new_zeros((p * cap, H))
+    send_x.index_copy_(0, slot, xs.index_select(0, tok))
+    send_e = torch.full((p * cap,), -1, dtype=torch.int32, device=dev)
+    send_e.index_copy_(0, slot, flat_ids.to(torch.int32))
+    recv_x = comm.all_to_all_single(send_x)                           # A5 dispatch, equal splits
+    recv_e = comm.all_to_all_single(send_e)
+    y = _local_experts(recv_x, recv_e, L, r * el)
+    back = comm.all_to_all_single(y)                                  # A5 combine: rows return to `slot`
+    contrib = back.index_select(0, slot).float() * w.reshape(-1).unsqueeze(1)
+    out = torch.zeros((ts, H), dtype=torch.float32, device=dev)
+    out.index_add_(0, tok, contrib)
+    full = comm.all_gather(out.to(x.dtype))                          # [p, ts, H]
+    return full.reshape(p * ts, H)[:T]
+
+
 def moe_dispatch_mode() -> str:
     return os.environ.get("MOE_DISPATCH", "a2a")
 
@@ -192,9 +238,15 @@ def moe_dispatch_mode() -> str:
 def moe_forward(x, L, cfg, ep_rank, ep_size, is_decode: bool, comm=None):
     """Returns (out, combined): `combined` is True when the output is already summed over the EP
     group (all-to-all path) and the caller's all-reduce must be skipped."""
-    if (comm is not None and ep_size > 1 and not is_decode and moe_dispatch_mode() == "a2a"
-            and not (x.is_cuda and torch.cuda.is_current_stream_capturing())):
-        return moe_alltoall(x, L, cfg, comm), True
+    mode = moe_dispatch_mode()
+    if comm is not None and ep_size > 1:
+        capturing = x.is_cuda and torch.cuda.is_current_stream_capturing()
+        # MOE_DISPATCH=a2a (default): exact-count all-to-all for prefill, the all-reduce combine in
+        # the decode graphs; a2a-static: the shape-static all-to-all everywhere (graph-capturable)
+        if mode == "a2a-static":
+            return moe_alltoall_static(x, L, cfg, comm), True
+        if mode == "a2a" and not is_decode and not capturing:
+            return moe_alltoall(x, L, cfg, comm), True
     if x.is_cuda and not ops._FORCE_REF:
         if x.shape[0] * cfg.top_k <= MOE_HIP_MAX_ROWS:
             return moe_hip(x, L, cfg, ep_rank, ep_size), False

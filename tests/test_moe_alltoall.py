@@ -1,4 +1,5 @@
-"""Expert-parallel all-to-all dispatch / combine (models/moe.py `moe_alltoall`)
+"""Expert-parallel all-to-all dispatch / combine (models/moe.py `moe_alltoall` and
+the shape-static, graph-capturable `moe_alltoall_static`)
 over real torch.distributed process groups (gloo, world_size 2 and 4): the token-sharded
 all-to-all path must equal the single-process MoE over all experts, including shards that are
 short or empty (T not divisible by, or smaller than, the world size)."""
@@ -35,7 +36,7 @@ def _worker(rank, world, port, T_list, queue):
     torch.set_num_threads(1)
     import torch.distributed as dist
     from ai_agent_kubectl_amd.models.config import get_config
-    from ai_agent_kubectl_amd.models.moe import moe_alltoall, moe_forward
+    from ai_agent_kubectl_amd.models.moe import moe_alltoall, moe_alltoall_static, moe_forward
     from ai_agent_kubectl_amd.parallel.comm import make_comm
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = make_comm(None)
@@ -54,7 +55,12 @@ def _worker(rank, world, port, T_list, queue):
         part, combined = moe_forward(x, L, cfg, rank, world, True, comm)
         assert not combined
         comm.all_reduce(part)
-        outs.append(tuple(t.numpy() for t in (y, y2, part)))
+        y3 = moe_alltoall_static(x, L, cfg, comm)   # shape-static splits (graph-capturable form)
+        os.environ["MOE_DISPATCH"] = "a2a-static"
+        y4, combined = moe_forward(x, L, cfg, rank, world, True, comm)   # decode goes through it too
+        assert combined
+        del os.environ["MOE_DISPATCH"]
+        outs.append(tuple(t.numpy() for t in (y, y2, part, y3, y4)))
     queue.put((rank, outs))
     dist.barrier()
     dist.destroy_process_group()
@@ -91,7 +97,9 @@ def test_moe_alltoall_matches_single_process(world):
         x = torch.randn(T, cfg.hidden, generator=torch.Generator().manual_seed(T))
         ref = moe_grouped(x, W, cfg, 0, 1)
         for r in range(world):
-            y, y2, part = (torch.from_numpy(a) for a in res[r][i])
+            y, y2, part, y3, y4 = (torch.from_numpy(a) for a in res[r][i])
+            torch.testing.assert_close(y3, ref, rtol=1e-4, atol=1e-4)
+            torch.testing.assert_close(y4, ref, rtol=1e-4, atol=1e-4)
             torch.testing.assert_close(y, ref, rtol=1e-4, atol=1e-4)
             torch.testing.assert_close(y2, ref, rtol=1e-4, atol=1e-4)
             torch.testing.assert_close(part, ref, rtol=1e-4, atol=1e-4)
