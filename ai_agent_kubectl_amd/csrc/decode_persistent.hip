@@ -35,9 +35,9 @@ namespace pd {
 #ifndef KA_PD_ROT
 #define KA_PD_ROT 0   // measured: no effect (profiles/r4/persistent_decode)
 #endif
-#ifndef KA_PD_W0_DEFER   // 1: wave 0 (the barrier poller) issues its ring only after the wait, so its polls
-#define KA_PD_W0_DEFER 0  // do not queue behind its own pieces -- measured +2.5 us per barrier (wave 0 then
-#endif                    // finishes each phase last): off
+#ifndef KA_PD_PREISSUE    // pieces of the next phase issued before a grid barrier's wait (the rest after it);
+#define KA_PD_PREISSUE 16 // (deferring all of the polling wave's pieces measured +2.5 us per barrier)
+#endif
 #ifndef KA_PD_NT
 #define KA_PD_NT 1
 #endif
@@ -274,11 +274,20 @@ struct Stream {
       ++ni;
     }
   }
+  // the first N pieces (N < RING: the rest by top_up<N>() after the barrier wait, so the wait's polls
+  // queue behind fewer of the CU's own pieces)
+  template <int N = RING>
   KA_DEV void start() {
     issued = ni = nc = 0;
     if (total <= 0) return;
 #pragma unroll
-    for (int r = 0; r < RING; ++r) issue();
+    for (int r = 0; r < N; ++r) issue();
+  }
+  template <int N>
+  KA_DEV void top_up() {
+    if (total <= 0) return;
+#pragma unroll
+    for (int r = N; r < RING; ++r) issue();
   }
   // xaddr: LDS byte address of x (K bf16)
   KA_DEV float run(uint32_t xaddr) {
@@ -472,9 +481,9 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     // it: after the arrival (its vmcnt(0) would otherwise hold the arrival back until they landed),
     // in flight while the workgroup waits for the others.
     auto sq = make_stream(Lw.wqkv, (hq + 2 * hkv) * HD, H, nq, lane, ring, qkv_row, gw);
-    if (!KA_PD_W0_DEFER || wave != 0) sq.start();
+    sq.template start<KA_PD_PREISSUE>();
     wait_grid(a.sync, ++nbar, G, err);
-    if (KA_PD_W0_DEFER && wave == 0) sq.start();
+    sq.template top_up<KA_PD_PREISSUE>();
     PD_STAMP(0);
     if (st && l > 0) st[(l - 1) * 16 + 12] = st[l * 16];   // the previous layer's barrier E ends here
     rmsnorm_to_lds(a, Lw.ln1, xs, red);
@@ -696,9 +705,9 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     PD_STAMP(6);
     auto sg = make_stream(Lw.w13, 2 * I, H, 2 * ng, lane, ring, gu_row, gw);
     arrive(gcnt);
-    if (!KA_PD_W0_DEFER || wave != 0) sg.start();
+    sg.template start<KA_PD_PREISSUE>();
     wait_grid(a.sync, ++nbar, G, err);
-    if (KA_PD_W0_DEFER && wave == 0) sg.start();
+    sg.template top_up<KA_PD_PREISSUE>();
     PD_STAMP(7);
     // ---- P4: norm + gate / up -> act ----
     rmsnorm_to_lds(a, Lw.ln2, xs, red);
@@ -715,9 +724,9 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     PD_STAMP(9);
     auto sd = make_stream(Lw.w2, H, I, no, lane, ring, own_row, gw);
     arrive(gcnt);
-    if (!KA_PD_W0_DEFER || wave != 0) sd.start();
+    sd.template start<KA_PD_PREISSUE>();
     wait_grid(a.sync, ++nbar, G, err);
-    if (KA_PD_W0_DEFER && wave == 0) sd.start();
+    sd.template top_up<KA_PD_PREISSUE>();
     PD_STAMP(10);
     // ---- P5: down rows -> residual ----
     stage_sc1(reinterpret_cast<uint4*>(lds + LDS_X), a.act, I / 8);   // act (sc1) -> LDS
