@@ -438,7 +438,7 @@ class ModelRunner:
                                                self.d_out.index_select(0, self.d_fix[nf:2 * nf].long()))
         self._launch_decode(Bp, n_copy)
         ho[:B].copy_(self.d_out[:B], non_blocking=True)
-        eh = self._copy_err(persistent=Bp == 1 and self.model.persistent_ok())
+        eh = self._copy_err(persistent=self._persistent_step(Bp))
         ev = None
         if self.device.type == "cuda":
             ev = torch.cuda.Event()
@@ -510,6 +510,10 @@ class ModelRunner:
     def _err_word(self) -> Optional[torch.Tensor]:
         car = getattr(self.comm, "custom_ar", None)
         return car.state[2:3] if car is not None else None
+
+    def _persistent_step(self, Bp: int) -> bool:
+        """The decode step of bucket Bp runs the persistent kernel (its error word is read back)."""
+        return Bp == 1 and self.model.persistent_ok()
 
     def _copy_err(self, persistent: bool = False) -> Optional[torch.Tensor]:
         """Queue the error word's readback behind the step just launched: [one-shot collectives,

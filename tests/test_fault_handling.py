@@ -92,6 +92,34 @@ def test_collective_timeout_is_503_never_200_and_fatal(tiny):
         eng.healthy, eng.last_error = True, None
 
 
+def test_persistent_stall_is_503_then_chain_serves(tiny):
+    """The persistent batch-1 kernel's error word set (a grid wait ran out) turns the step into a
+    recoverable PersistentStall at readback: the request gets 503 (never the stale tokens), the
+    engine recovers with the persistent path switched off, and the next request is served."""
+    from ai_agent_kubectl_amd.engine.runner import PersistentStall
+    eng, be = tiny
+    app = _app(be)
+    r, m = eng.runner, eng.runner.model
+    word = torch.tensor([1], dtype=torch.int32)
+    saved = (r._persistent_step, m.persistent_err_word, m.persistent)
+    r._persistent_step = lambda Bp: Bp == 1
+    m.persistent_err_word = lambda: word
+    m.persistent = True
+    r0 = eng.recoveries
+    try:
+        rs = asyncio.run(_post_all(app, be, ["list pods in kube-system"]))
+        assert rs[0].status_code == 503, rs[0].text
+        assert "grid wait timeout" in rs[0].json()["detail"]
+        assert isinstance(eng.last_error, PersistentStall) and not eng.is_fatal(eng.last_error)
+        assert eng.healthy and eng.recoveries == r0 + 1 and m.persistent is False
+        word.zero_()
+        rs = asyncio.run(_post_all(app, be, ["get nodes please"]))
+        assert rs[0].status_code == 200
+    finally:
+        r._persistent_step, m.persistent_err_word, m.persistent = saved
+        eng.healthy, eng.last_error = True, None
+
+
 def test_error_word_clear_is_transparent(tiny):
     """A zero error word changes nothing (the readback rides behind every step's tokens)."""
     eng, be = tiny
