@@ -241,7 +241,11 @@ class ModelRunner:
                 midx = (torch.zeros(M, dtype=torch.int32, device=self.device) if self.mask_bits is not None else None)
                 t_un = _time(lambda w: ops.masked_argmax(ops.linear(x, w), self.mask_bits, midx, m.vocab_offset), [lm])
                 t_fu = _time(lambda w: ops.lm_head_argmax(x, w, self.mask_bits, midx, m.vocab_offset), [lm])
-                fused = t_fu < t_un
+                # within the plan's margin the hand-written fused kernel is taken over a hipBLASLt plan
+                # (ops/autotune.py BLAS_MARGIN), as for the GEMM plan and the decode SwiGLU
+                from ..ops.autotune import BLAS_MARGIN
+                plan = ops.GEMM_PLAN.get((M, lm.shape[0], K), ("blas",))
+                fused = t_fu < t_un * (1.0 + (BLAS_MARGIN if plan[0] == "blas" else 0.0))
             ops.LM_HEAD_FUSED[M] = bool(fused)
             report[M] = {"fused_us": round(t_fu, 1), "unfused_us": round(t_un, 1), "fused": bool(fused)}
         if mode == "write":
@@ -282,7 +286,10 @@ class ModelRunner:
             else:
                 t_un = _time(lambda w: ops.silu_mul(ops.linear(x, w, defer_reduce=True)), ws)
                 fused = (0, float("inf"))
-                for cfg in ops.DECODE_SWIGLU_CFGS:
+                cands = list(ops.DECODE_SWIGLU_CFGS)
+                if M >= ops.BIG_PLAN_MIN_M and ops.swiglu_gemm_ok(x, ws[0]):
+                    cands.append(ops.DECODE_SWIGLU_BIG)   # csrc/gemm_big.hip's SwiGLU epilogue
+                for cfg in cands:
                     t = _time(lambda w: ops.linear_gm_swiglu(x, w, cfg), ws)
                     if t < fused[1]:
                         fused = (cfg, t)

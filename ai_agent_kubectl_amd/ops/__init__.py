@@ -8,6 +8,7 @@ hand-written kernel wins (decode GEMV, MoE grouped GEMM).
 """
 from __future__ import annotations
 
+import bisect
 import os
 from typing import NamedTuple, Optional, Tuple
 
@@ -383,9 +384,41 @@ def skinny_split(M: int, N: int, K: int, target_wgs: int = 0) -> int:
 # (M, N, K) -> ("skinny", split) | ("gm", split, cfg) | ("rows", split, rows per wave) | ("blas", 0);
 # filled by ops.autotune at engine start for the decode batch buckets.  PLAN_CHOICES is the set
 # `linear` dispatches on (tests and the autotuner check plans against it).
-PLAN_CHOICES = ("skinny", "gm", "rows", "blas")
+PLAN_CHOICES = ("skinny", "gm", "rows", "big", "blas")
+BIG_PLAN_MIN_M = 128   # smallest M the autotuner times csrc/gemm_big.hip at (256 x 256 tiles)
 GEMM_PLAN: dict = {}
 TILE_MAX_M = 512      # largest M the autotuner plans for (decode buckets and small mixed steps)
+_PLAN_MS: dict = {}   # (N, K) -> sorted planned M, rebuilt when GEMM_PLAN changes size
+_PLAN_MS_SIZE = [-1]
+
+
+def plan_for(M: int, N: int, K: int):
+    """GEMM_PLAN entry for (M, N, K); a row count no bucket was timed at (a mixed step of, say, 300
+    rows) takes the plan of the smallest planned M above it, so it stays on the hand-written kernel
+    that bucket measured fastest (every plan's kernels take any M up to their bucket)."""
+    plan = GEMM_PLAN.get((M, N, K))
+    if plan is not None:
+        return plan
+    if _PLAN_MS_SIZE[0] != len(GEMM_PLAN):
+        _PLAN_MS.clear()
+        for (m, n, k) in GEMM_PLAN:
+            _PLAN_MS.setdefault((n, k), []).append(m)
+        for v in _PLAN_MS.values():
+            v.sort()
+        _PLAN_MS_SIZE[0] = len(GEMM_PLAN)
+    ms = _PLAN_MS.get((N, K))
+    if not ms:
+        return None
+    i = bisect.bisect_left(ms, M)
+    if i == len(ms):
+        return None
+    plan = GEMM_PLAN.get((ms[i], N, K))
+    if plan is None:   # an entry replaced by another of the same count: rebuild on the next call
+        _PLAN_MS_SIZE[0] = -1
+        return None
+    if plan is not None and plan[0] == "rows" and not rows_ok(M, K, plan[1]):
+        return None
+    return plan
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool = False,
@@ -410,7 +443,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
     if M > TILE_MAX_M or K % 64 != 0 or N % 4 != 0 or not x.is_contiguous():
         return torch.nn.functional.linear(x, w)
     if not split:
-        plan = GEMM_PLAN.get((M, N, K))
+        plan = plan_for(M, N, K)
         if plan is None:
             if M > SKINNY_MAX_M:
                 return torch.nn.functional.linear(x, w)
@@ -420,6 +453,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
             return linear_gm(x, w, plan[2], plan[1], defer_reduce, bf16_partials)
         elif plan[0] == "rows":
             return linear_rows(x, w, plan[1], plan[2], defer_reduce)
+        elif plan[0] == "big":
+            return linear_big(x, w)
         else:
             split = plan[1]
     if M > SKINNY_MAX_M:
@@ -540,6 +575,10 @@ def big_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 DECODE_SWIGLU = os.environ.get("KA_DECODE_SWIGLU", "auto")
 DECODE_SWIGLU_CFG: dict = {}
 DECODE_SWIGLU_CFGS = (2, 3, 4, 5, 12)
+# DECODE_SWIGLU_CFG value for "csrc/gemm_big.hip's SwiGLU epilogue" (ops.linear_swiglu): its 256 x 256
+# tiles with one wave per SIMD read a quarter of the ring kernel's LDS bytes per MFMA, which pays from
+# M ~ 256 up (the fused LM head's measurement)
+DECODE_SWIGLU_BIG = 100
 
 
 def decode_swiglu_ok(x: torch.Tensor, w13: torch.Tensor) -> bool:
@@ -553,6 +592,8 @@ def decode_swiglu_cfg(x: torch.Tensor, w13: torch.Tensor) -> int:
     if DECODE_SWIGLU == "0" or _ref(x):
         return 0
     cfg = DECODE_SWIGLU_CFG.get(x.shape[0], 0)
+    if cfg == DECODE_SWIGLU_BIG and not swiglu_gemm_ok(x, w13):
+        return 0
     return cfg if cfg and decode_swiglu_ok(x, w13) else 0
 
 
@@ -684,11 +725,14 @@ def linear_gm(x: torch.Tensor, w: torch.Tensor, cfg: int, split: int = 1, defer_
 
 def linear_gm_swiglu(x: torch.Tensor, w13: torch.Tensor, cfg: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """silu(x @ gate.T) * (x @ up.T) for w13 = [gate; up] through csrc/gemm_mfma.hip configuration
-    `cfg` with the SwiGLU epilogue (the DMA sources gather gate / up in 16-row chunks): [M, I] bf16."""
+    `cfg` with the SwiGLU epilogue (the DMA sources gather gate / up in 16-row chunks): [M, I] bf16.
+    cfg DECODE_SWIGLU_BIG: csrc/gemm_big.hip's SwiGLU epilogue instead (ops.linear_swiglu)."""
     M, K = x.shape
     I = w13.shape[0] // 2
     if _ref(x):
         return ref.silu_mul(ref.linear(x, w13))
+    if cfg == DECODE_SWIGLU_BIG:
+        return linear_swiglu(x, w13, out)
     lib = require()
     out = torch.empty((M, I), dtype=x.dtype, device=x.device) if out is None else out
     check(lib.ka_gemm_mfma_swiglu(_p(out), _p(x), _p(w13), M, I, K, x.stride(0), out.stride(0), int(cfg), _stream()),

@@ -13,8 +13,8 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from . import (GEMM_PLAN, SKINNY_MAX_M, TILE_MAX_M, gm_shape, linear, linear_gm, linear_rows, rmsnorm, rows_ok,
-               skinny_split)
+from . import (BIG_PLAN_MIN_M, GEMM_PLAN, SKINNY_MAX_M, TILE_MAX_M, big_gemm_ok, gm_shape, linear, linear_big,
+               linear_gm, linear_rows, rmsnorm, rows_ok, skinny_split)
 
 logger = logging.getLogger("app.engine")
 
@@ -255,6 +255,10 @@ def _tune(groups, Ms, norm_fed=frozenset(), bf16_partials: bool = True, consumer
                 t = _time(lambda w: norm(linear_gm(x, w, cfg, sp, defer_reduce=fed, bf16_partials=bf16)), ws)
                 if t < best[3]:
                     best = ("gm", sp, cfg, t)
+            if M >= BIG_PLAN_MIN_M and big_gemm_ok(x, ws[0]):   # 256 x 256 tiles, one wave per SIMD
+                t = _time(lambda w: norm(linear_big(x, w)), ws)
+                if t < best[3]:
+                    best = ("big", 0, 0, t)
             if best[3] > t_blas * (1.0 + BLAS_MARGIN):
                 best = ("blas", 0, 0, t_blas)
             GEMM_PLAN[(M, N, K)] = (best[0], best[1], best[2])

@@ -416,6 +416,47 @@ def test_decode_swiglu_gemm_vs_fp32(M, I, cfg):
     close(y, torch.nn.functional.silu(g) * u, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("M", [160, 256, 320, 512])
+def test_decode_swiglu_big_vs_fp32(M):
+    """Decode buckets whose SwiGLU plan is csrc/gemm_big.hip (DECODE_SWIGLU_BIG): the model calls
+    linear_gm_swiglu with that marker; compared with fp32 silu(x gate^T) * (x up^T)."""
+    K, I = 4096, 1792
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w13 = (torch.randn(2 * I, K, device=DEV) / math.sqrt(K)).to(BF)
+    y = ops.linear_gm_swiglu(x, w13, ops.DECODE_SWIGLU_BIG)
+    assert y.shape == (M, I)
+    g = x.float() @ w13[:I].float().t()
+    u = x.float() @ w13[I:].float().t()
+    close(y, torch.nn.functional.silu(g) * u, atol=2e-2, rtol=2e-2)
+    saved = dict(ops.DECODE_SWIGLU_CFG)
+    try:
+        ops.DECODE_SWIGLU_CFG[M] = ops.DECODE_SWIGLU_BIG
+        assert ops.decode_swiglu_cfg(x, w13) == (0 if ops.DECODE_SWIGLU == "0" else ops.DECODE_SWIGLU_BIG)
+        # a weight gemm_big's SwiGLU cannot take (2I % 256 != 0) falls back to the unfused path
+        assert ops.decode_swiglu_cfg(x, w13[:2 * 1776]) == 0
+    finally:
+        ops.DECODE_SWIGLU_CFG.clear()
+        ops.DECODE_SWIGLU_CFG.update(saved)
+
+
+@pytest.mark.parametrize("M", [128, 256, 320, 512])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336)])
+def test_gemm_plan_big_dispatch(M, N, K):
+    """A decode-bucket plan entry "big" sends ops.linear to csrc/gemm_big.hip (with or without
+    defer_reduce: it returns the bf16 product, which the fused norm / attention consumers take)."""
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(BF)
+    want = x.float() @ w.float().t()
+    ops.GEMM_PLAN[(M, N, K)] = ("big", 0, 0)
+    try:
+        close(ops.linear(x, w), want, atol=3e-2, rtol=2e-2)
+        y = ops.linear(x, w, defer_reduce=True, bf16_partials=True)
+        assert not isinstance(y, ops.SplitK)
+        close(y, want, atol=3e-2, rtol=2e-2)
+    finally:
+        ops.GEMM_PLAN.pop((M, N, K), None)
+
+
 def test_decode_swiglu_plan_dispatch():
     """ops.decode_swiglu_cfg follows the per-bucket plan and the shape rules."""
     x = torch.randn(256, 4096, device=DEV, dtype=BF)
@@ -545,7 +586,7 @@ def test_gemm_autotune_plan_dispatch():
     rep = tune_linear({(6144, 4096): ws}, [1, 64, 256, 320])
     assert set(k[0] for k in rep) == {1, 64, 256, 320}
     assert all(v["choice"] in ops.PLAN_CHOICES for v in rep.values())
-    for M in (1, 64, 256, 320):
+    for M in (1, 64, 200, 256, 300, 320):   # 200 / 300: no bucket, the next bucket's plan (ops.plan_for)
         x = torch.randn(M, 4096, device=DEV, dtype=BF)
         close(ops.linear(x, ws[0]), x.float() @ ws[0].float().t(), atol=3e-2, rtol=2e-2)
     for key in list(ops.GEMM_PLAN):

@@ -68,3 +68,28 @@ def test_shared_prefix_len():
     assert shared_prefix_len(bt[:1], 4) == 4
     assert shared_prefix_len(bt, 0) == 0
     assert shared_prefix_len(np.array([[5, 1], [6, 1]], dtype=np.int32), 2) == 0
+
+
+def test_plan_for_takes_the_next_bucket_up():
+    """ops.plan_for: exact (M, N, K) entries first; an un-timed row count (a mixed step of 300 rows)
+    takes the smallest planned bucket above it; none past the largest bucket; a batch-1..4 GEMV
+    plan ("rows") only where its row rule holds."""
+    saved = dict(ops.GEMM_PLAN)
+    try:
+        ops.GEMM_PLAN.clear()
+        ops.GEMM_PLAN[(256, 64, 128)] = ("gm", 4, 12)
+        ops.GEMM_PLAN[(320, 64, 128)] = ("blas", 0, 0)
+        ops.GEMM_PLAN[(512, 64, 128)] = ("gm", 2, 3)
+        ops.GEMM_PLAN[(4, 64, 4096)] = ("rows", 2, 4)
+        assert ops.plan_for(256, 64, 128) == ("gm", 4, 12)
+        assert ops.plan_for(200, 64, 128) == ("gm", 4, 12)
+        assert ops.plan_for(300, 64, 128) == ("blas", 0, 0)
+        assert ops.plan_for(321, 64, 128) == ("gm", 2, 3)
+        assert ops.plan_for(513, 64, 128) is None
+        assert ops.plan_for(300, 96, 128) is None
+        assert ops.plan_for(3, 64, 4096) == (("rows", 2, 4) if ops.rows_ok(3, 4096, 2) else None)
+        ops.GEMM_PLAN[(384, 64, 128)] = ("gm", 4, 3)   # the lookup table follows new entries
+        assert ops.plan_for(321, 64, 128) == ("gm", 4, 3)
+    finally:
+        ops.GEMM_PLAN.clear()
+        ops.GEMM_PLAN.update(saved)
