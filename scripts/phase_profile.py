@@ -40,12 +40,14 @@ def main():
     ap.add_argument("--concurrency", type=int, default=256)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--decode-steps", type=int, default=8)
+    ap.add_argument("--budget", type=int, default=0, help="tokens per step (0: the model's default, as bench.py)")
+    ap.add_argument("--prefill-steps", type=int, default=3, help="mixed steps profiled one by one")
     a = ap.parse_args()
     C = a.concurrency
     buckets = tuple(b for b in (1, 8, 16, 32, 64, 128, 192, 256, 384, 512) if b <= C) + ((C,) if C not in (1, 8, 16, 32, 64, 128, 192, 256, 384, 512) else ())
     eng = build_engine(EngineOptions(model=a.model, device="cuda:0", max_batch=C, graph_buckets=buckets,
                                      kv_cache_tokens=max(65536, C * 528), max_model_len=512, ignore_eos=True,
-                                     max_batched_tokens=16384))
+                                     max_batched_tokens=a.budget))
     eng.runner.capture_graphs()
     be = EngineLLM(eng, max_new_tokens=16, ignore_eos=True)
     params = SamplingParams(max_new_tokens=16, ignore_eos=True)
@@ -53,10 +55,6 @@ def main():
     for w in range(2):   # warm: publish the instruction blocks, exercise the plans
         eng.generate_blocking([be.prompt_ids(bench.make_query(0, w, i)) for i in range(C)], params,
                               forced_prefix=be._forced)
-    seqs = [Sequence(prompt_ids=be.prompt_ids(bench.make_query(0, 9, i)), params=params,
-                     forced_prefix=list(be._forced)) for i in range(C)]
-    for s in seqs:
-        eng.scheduler.add(s)
     acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
 
     def one_step():
@@ -66,16 +64,41 @@ def main():
         eng.scheduler.on_step_done(batch)
         return batch
 
+    def admit(wave):
+        for i in range(C):
+            eng.scheduler.add(Sequence(prompt_ids=be.prompt_ids(bench.make_query(0, wave, i)), params=params,
+                                       forced_prefix=list(be._forced)))
+
+    # wave 9 unprofiled: the wall time of each admission (mixed) step, the profiler's hooks off
+    admit(9)
     torch.cuda.synchronize()
-    with torch.profiler.profile(activities=acts) as prof_p:
+    walls = []
+    while True:
         t0 = time.perf_counter()
         b = one_step()
         torch.cuda.synchronize()
-        tp = time.perf_counter() - t0
-    print(f"PREFILL step: {len(b.seqs)} seqs, {b.num_tokens} tokens, {len(b.copies)} block copies, "
-          f"wall {tp * 1e3:.2f} ms ({b.num_tokens / tp:.0f} tok/s)")
-    print(table(prof_p))
-    one_step()   # (the first decode step after admission)
+        if b.is_decode:
+            break
+        walls.append((b.num_tokens, len(b.seqs), (time.perf_counter() - t0) * 1e3))
+    print("MIXED steps, unprofiled (tokens, seqs, wall ms):", [(n, q, round(w, 2)) for n, q, w in walls])
+    while eng.scheduler.has_work():
+        one_step()
+    # wave 10 profiled step by step: device time per kernel of each admission step
+    admit(10)
+    torch.cuda.synchronize()
+    for _ in range(a.prefill_steps):
+        with torch.profiler.profile(activities=acts) as prof_p:
+            t0 = time.perf_counter()
+            b = one_step()
+            torch.cuda.synchronize()
+            tp = time.perf_counter() - t0
+        print(f"PREFILL step: {len(b.seqs)} seqs, {b.num_tokens} tokens, decode={b.is_decode}, "
+              f"{len(b.copies)} block copies, wall {tp * 1e3:.2f} ms under the profiler")
+        print(table(prof_p))
+        if b.is_decode:
+            break
+    while not b.is_decode:
+        b = one_step()
     torch.cuda.synchronize()
     with torch.profiler.profile(activities=acts) as prof_d:
         t0 = time.perf_counter()
