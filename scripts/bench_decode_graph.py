@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--prefetch", default="0:64")
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--persistent", default="0", help="comma list of 0/1: the batch-1 persistent decode kernel")
+    ap.add_argument("--plan-first", action="store_true",
+                    help="load the GEMM plan / LM head / SwiGLU decisions before the prefill (so its steps of "
+                         "<= 512 rows dispatch on them, as in serving)")
     args = ap.parse_args()
     buckets = tuple(int(b) for b in args.buckets.split(","))
     eng = build_engine(EngineOptions(model=args.model, device="cuda", max_batch=max(buckets), graph_buckets=buckets,
@@ -34,6 +37,8 @@ def main():
     sch = eng.scheduler
     sch.gather_max_s = 0.0
     params = SamplingParams(max_new_tokens=64, ignore_eos=True)
+    if args.plan_first:
+        r.gemm_plan, r.lm_head_plan, r.swiglu_plan = r.autotune(), r.tune_lm_head(), r.tune_swiglu()
     with torch.inference_mode():
         for i in range(max(buckets)):
             sch.add(Sequence(prompt_ids=be.prompt_ids(f"list pods in namespace team-{i}"), params=params))

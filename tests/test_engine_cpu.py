@@ -628,6 +628,7 @@ def test_scheduler_gather_is_short_for_steady_arrivals():
     sch2 = Scheduler(BlockManager(256, 16), max_batch=64, max_batched_tokens=4096, gather_max_s=0.1,
                      gather_quiet_s=0.005)
     sch2._idle_since, sch2._drained = time.perf_counter(), 64     # a 64-request wave just drained
+    sch2.burst_quiet_s = 0.05   # a loaded host (pytest -n) may oversleep the 2-ms gaps past the default
     sch2.add(_seq(10))
     t0 = time.perf_counter()
     while sch2.gathering() and time.perf_counter() - t0 < 0.2:
