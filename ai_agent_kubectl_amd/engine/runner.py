@@ -299,8 +299,7 @@ class ModelRunner:
                 plan = ops.GEMM_PLAN.get((M, ws[0].shape[0], ws[0].shape[1]), ("blas",))
                 margin = BLAS_MARGIN if plan[0] == "blas" else 0.0
                 best = fused if fused[1] < t_un * (1.0 + margin) else (0, t_un)
-            if best[0]:
-                ops.DECODE_SWIGLU_CFG[M] = best[0]
+            ops.DECODE_SWIGLU_CFG[M] = best[0]   # 0 (unfused) is kept too: un-timed M take the next bucket
             # fused_us: the fastest SwiGLU-epilogue configuration's time, whether or not it was taken
             report[M] = {"cfg": best[0], "fused_us": round(fused[1], 1), "unfused_us": round(t_un, 1)}
         if mode == "write":

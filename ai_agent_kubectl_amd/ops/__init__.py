@@ -588,10 +588,17 @@ def decode_swiglu_ok(x: torch.Tensor, w13: torch.Tensor) -> bool:
 
 
 def decode_swiglu_cfg(x: torch.Tensor, w13: torch.Tensor) -> int:
-    """The gemm_mfma configuration for this decode gate_up + SwiGLU, 0 for the unfused path."""
+    """The gemm_mfma configuration for this decode gate_up + SwiGLU, 0 for the unfused path.  A row
+    count no bucket was timed at (a mixed step's pruned last layer, e.g. 282 sequences) takes the
+    decision of the smallest timed bucket above it, as ops.plan_for does for the GEMM plan."""
     if DECODE_SWIGLU == "0" or _ref(x):
         return 0
-    cfg = DECODE_SWIGLU_CFG.get(x.shape[0], 0)
+    M = x.shape[0]
+    cfg = DECODE_SWIGLU_CFG.get(M)
+    if cfg is None:
+        ms = sorted(DECODE_SWIGLU_CFG)
+        i = bisect.bisect_left(ms, M)
+        cfg = DECODE_SWIGLU_CFG[ms[i]] if i < len(ms) else 0
     if cfg == DECODE_SWIGLU_BIG and not swiglu_gemm_ok(x, w13):
         return 0
     return cfg if cfg and decode_swiglu_ok(x, w13) else 0

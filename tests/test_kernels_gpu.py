@@ -466,8 +466,14 @@ def test_decode_swiglu_plan_dispatch():
         ops.DECODE_SWIGLU_CFG.clear()
         assert ops.decode_swiglu_cfg(x, w13) == 0
         ops.DECODE_SWIGLU_CFG[256] = 2
-        assert ops.decode_swiglu_cfg(x, w13) == (0 if ops.DECODE_SWIGLU == "0" else 2)
+        ops.DECODE_SWIGLU_CFG[128] = 0   # timed, unfused won
+        on = ops.DECODE_SWIGLU != "0"
+        assert ops.decode_swiglu_cfg(x, w13) == (2 if on else 0)
         assert ops.decode_swiglu_cfg(x[:128], w13) == 0
+        assert ops.decode_swiglu_cfg(x[:200], w13) == (2 if on else 0)   # un-timed: the next bucket up
+        assert ops.decode_swiglu_cfg(x[:100], w13) == 0
+        x3 = torch.randn(300, 4096, device=DEV, dtype=BF)
+        assert ops.decode_swiglu_cfg(x3, w13) == 0   # above every timed bucket
     finally:
         ops.DECODE_SWIGLU_CFG.clear()
         ops.DECODE_SWIGLU_CFG.update(saved)
