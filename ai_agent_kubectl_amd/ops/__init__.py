@@ -381,7 +381,8 @@ def skinny_split(M: int, N: int, K: int, target_wgs: int = 0) -> int:
     return split
 
 
-# (M, N, K) -> ("skinny", split) | ("gm", split, cfg) | ("rows", split, rows per wave) | ("blas", 0);
+# (M, N, K) -> ("skinny", split) | ("gm", split, cfg) | ("rows", split, rows per wave) | ("big", 0, 0)
+# (csrc/gemm_big.hip) | ("blas", 0);
 # filled by ops.autotune at engine start for the decode batch buckets.  PLAN_CHOICES is the set
 # `linear` dispatches on (tests and the autotuner check plans against it).
 PLAN_CHOICES = ("skinny", "gm", "rows", "big", "blas")
@@ -416,7 +417,7 @@ def plan_for(M: int, N: int, K: int):
     if plan is None:   # an entry replaced by another of the same count: rebuild on the next call
         _PLAN_MS_SIZE[0] = -1
         return None
-    if plan is not None and plan[0] == "rows" and not rows_ok(M, K, plan[1]):
+    if plan[0] == "rows" and not rows_ok(M, K, plan[1]):
         return None
     return plan
 
