@@ -219,25 +219,39 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   const int rdA = (wn * C::TN * 16 + r16) * C::RB, rdB = (wm * C::TM * 16 + r16) * C::RB;
   const int ch0 = swz<C::KT>(r16, grp) * 16, ch1 = swz<C::KT>(r16, 4 + grp) * 16;
 
-  auto compute = [&](int stage) {
+  // k-loop, one barrier per k-step.  KA_GM_PIPE 1 (default): after the barrier a wave issues all
+  // 2 (TN + TM) fragment reads of its stage at once, then the DMA of stage t + STAGES - 1 (which
+  // refills the slot every wave finished reading before the barrier), then the MFMAs: one LDS round
+  // trip per k-step is exposed, overlapped with the DMA issue, instead of one per k-half with the DMA
+  // issue in front (with one wave per SIMD nothing else hides it).  2-7 % on the decode plan's shapes
+  // (profiles/r4/gm_pipe/).  A branch-free variant (tail DMAs clamped, one constant vmcnt) measured no
+  // better and lost 7 % on 8-step k-loops.  0: the former order.
+#ifndef KA_GM_PIPE
+#define KA_GM_PIPE 1
+#endif
+  bf16x8 fa[C::KT / 32][C::TN], fb[C::KT / 32][C::TM];
+  auto read_frags = [&](int stage) {
     const char* sa = lds_c + stage * C::STAGE_BYTES;
     const char* sb = sa + C::A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < C::KT / 32; ++kk) {
       const int ch = kk ? ch1 : ch0;
-      bf16x8 fa[C::TN], fb[C::TM];
 #pragma unroll
       for (int i = 0; i < C::TN; ++i)
-        fa[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(sa + rdA + i * 16 * C::RB + ch));
+        fa[kk][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(sa + rdA + i * 16 * C::RB + ch));
 #pragma unroll
       for (int j = 0; j < C::TM; ++j)
-        fb[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(sb + rdB + j * 16 * C::RB + ch));
+        fb[kk][j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(sb + rdB + j * 16 * C::RB + ch));
+    }
+  };
+  auto mma = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < C::KT / 32; ++kk)
 #pragma unroll
       for (int i = 0; i < C::TN; ++i)
 #pragma unroll
         for (int j = 0; j < C::TM; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
   };
 
   // prologue: STAGES - 1 stages in flight
@@ -268,8 +282,17 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
     block_sync();
     if (t == 0) BSTAMP(1);
     const int tn = t + C::STAGES - 1;
+#if KA_GM_PIPE
+    read_frags(t % C::STAGES);
+    __builtin_amdgcn_sched_barrier(0);
     if (tn < nk) issue(tn % C::STAGES, tn);
-    compute(t % C::STAGES);
+    __builtin_amdgcn_sched_barrier(0);
+    mma();
+#else
+    if (tn < nk) issue(tn % C::STAGES, tn);
+    read_frags(t % C::STAGES);
+    mma();
+#endif
   }
   BSTAMP(2);
 
