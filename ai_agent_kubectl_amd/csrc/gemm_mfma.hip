@@ -28,6 +28,8 @@
 // (accumulators in VGPRs with in-place MFMAs; the tables in profiles/r2/ were measured with it)
 #include "common.h"
 
+#include <utility>
+
 namespace gm {
 
 constexpr int BK = 64;
@@ -74,6 +76,23 @@ KA_DEV void block_sync() {
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 }
+
+// fragment read in asm with an immediate offset: the compiler neither sees it nor counts it, so the
+// k-loop's counted lgkmcnt waits (wait_frags) are the whole synchronisation of the fragment registers
+template <int OFF>
+KA_DEV void lds_rd(bf16x8& d, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF) : "memory");
+}
+// fragments f[I..N) of one k-half: lds_rd at BASE + I * STRIDE (compile-time immediates)
+template <int I, int N, int STRIDE, int BASE>
+struct RdFrags {
+  static KA_DEV void run(bf16x8* f, uint32_t a) {
+    if constexpr (I < N) {
+      lds_rd<BASE + I * STRIDE>(f[I], a);
+      RdFrags<I + 1, N, STRIDE, BASE>::run(f, a);
+    }
+  }
+};
 
 struct Args {
   const bf16_t* X;   // [M, ldx]
@@ -219,17 +238,47 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   const int rdA = (wn * C::TN * 16 + r16) * C::RB, rdB = (wm * C::TM * 16 + r16) * C::RB;
   const int ch0 = swz<C::KT>(r16, grp) * 16, ch1 = swz<C::KT>(r16, 4 + grp) * 16;
 
-  // k-loop, one barrier per k-step.  KA_GM_PIPE 1 (default): after the barrier a wave issues all
-  // 2 (TN + TM) fragment reads of its stage at once, then the DMA of stage t + STAGES - 1 (which
-  // refills the slot every wave finished reading before the barrier), then the MFMAs: one LDS round
-  // trip per k-step is exposed, overlapped with the DMA issue, instead of one per k-half with the DMA
-  // issue in front (with one wave per SIMD nothing else hides it).  2-7 % on the decode plan's shapes
-  // (profiles/r4/gm_pipe/).  A branch-free variant (tail DMAs clamped, one constant vmcnt) measured no
-  // better and lost 7 % on 8-step k-loops.  0: the former order.
+  // k-loop, one barrier per k-step.  After the barrier a wave issues all 2 (TN + TM) fragment reads
+  // of its stage at once, then the DMA of stage t + STAGES - 1 (which refills the slot every wave
+  // finished reading before the barrier), then the MFMAs: one LDS round trip per k-step is exposed,
+  // overlapped with the DMA issue, instead of one per k-half with the DMA issue in front (with one
+  // wave per SIMD nothing else hides it): 2-7 % on the decode plan's shapes (profiles/r4/gm_pipe/).
+  // KA_GM_PIPE 2 (default): the reads are asm and each k-half's MFMAs wait with a counted lgkmcnt
+  // for their own fragments only (hipcc's own bookkeeping emits lgkmcnt(0) before the first MFMA):
+  // 0-10 % more.  1: the same order with compiler-issued reads and waits.  A branch-free variant (tail
+  // DMAs clamped, one constant vmcnt) measured no better and lost 7 % on 8-step k-loops.
 #ifndef KA_GM_PIPE
-#define KA_GM_PIPE 1
+#define KA_GM_PIPE 2
 #endif
   bf16x8 fa[C::KT / 32][C::TN], fb[C::KT / 32][C::TM];
+#if KA_GM_PIPE == 2
+  // asm fragment reads, in the order fa[0][..], fb[0][..], fa[1][..], ...: k-half kk's MFMAs wait with
+  // lgkmcnt((KT / 32 - 1 - kk) (TN + TM)) for their own fragments only (LDS-DMA counts on vmcnt alone)
+  static_assert(C::TN + C::TM <= 15, "lgkmcnt immediate");
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)lds;
+  auto read_frags_asm = [&](int stage) {
+    const uint32_t base = lds0 + (uint32_t)(stage * C::STAGE_BYTES);
+#pragma unroll
+    for (int kk = 0; kk < C::KT / 32; ++kk) {
+      const uint32_t aA = base + (uint32_t)(rdA + (kk ? ch1 : ch0));
+      const uint32_t aB = base + (uint32_t)(rdB + (kk ? ch1 : ch0));
+      RdFrags<0, C::TN, 16 * C::RB, 0>::run(fa[kk], aA);
+      RdFrags<0, C::TM, 16 * C::RB, C::A_BYTES>::run(fb[kk], aB);
+    }
+  };
+  // the fragment registers of k-half kk are operands of the wait, so no MFMA reading them is
+  // scheduled above it
+  auto wait_frags = [&](int kk) {   // kk is a constant at both call sites (the branch folds)
+    if (kk == 0 && C::KT == 64)
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(C::TN + C::TM) : "memory");
+    else
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < C::TN; ++i) asm volatile("" : "+v"(fa[kk][i]));
+#pragma unroll
+    for (int j = 0; j < C::TM; ++j) asm volatile("" : "+v"(fb[kk][j]));
+  };
+#endif
   auto read_frags = [&](int stage) {
     const char* sa = lds_c + stage * C::STAGE_BYTES;
     const char* sb = sa + C::A_BYTES;
@@ -244,14 +293,16 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
         fb[kk][j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(sb + rdB + j * 16 * C::RB + ch));
     }
   };
+  auto mma_half = [&](int kk) {
+#pragma unroll
+    for (int i = 0; i < C::TN; ++i)
+#pragma unroll
+      for (int j = 0; j < C::TM; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+  };
   auto mma = [&]() {
 #pragma unroll
-    for (int kk = 0; kk < C::KT / 32; ++kk)
-#pragma unroll
-      for (int i = 0; i < C::TN; ++i)
-#pragma unroll
-        for (int j = 0; j < C::TM; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+    for (int kk = 0; kk < C::KT / 32; ++kk) mma_half(kk);
   };
 
   // prologue: STAGES - 1 stages in flight
@@ -259,6 +310,9 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   for (int s = 0; s < C::STAGES - 1; ++s)
     if (s < nk) issue(s, s);
   constexpr int PER = C::GA + C::GB;
+#if KA_GM_PIPE == 2
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // no scalar load left in flight: lgkm counts in order
+#endif
   for (int t = 0; t < nk; ++t) {
     // stage t landed (this wave's part): later stages may stay in flight
     // outstanding after this point: stages t+1 .. min(nk-1, t+STAGES-2) of this wave
@@ -282,15 +336,21 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
     block_sync();
     if (t == 0) BSTAMP(1);
     const int tn = t + C::STAGES - 1;
-#if KA_GM_PIPE
-    read_frags(t % C::STAGES);
-    __builtin_amdgcn_sched_barrier(0);
+#if KA_GM_PIPE == 2
+    read_frags_asm(t % C::STAGES);
     if (tn < nk) issue(tn % C::STAGES, tn);
-    __builtin_amdgcn_sched_barrier(0);
-    mma();
+    wait_frags(0);
+    mma_half(0);
+    if constexpr (C::KT == 64) {
+      __builtin_amdgcn_sched_barrier(0);   // the first k-half's MFMAs stay above the second wait
+      wait_frags(1);
+      mma_half(1);
+    }
 #else
-    if (tn < nk) issue(tn % C::STAGES, tn);
     read_frags(t % C::STAGES);
+    __builtin_amdgcn_sched_barrier(0);
+    if (tn < nk) issue(tn % C::STAGES, tn);
+    __builtin_amdgcn_sched_barrier(0);
     mma();
 #endif
   }
