@@ -13,5 +13,5 @@ timeout -k 10 400 python scripts/phase_profile.py --concurrency 256 > $OUT/phase
 timeout -k 10 400 python scripts/phase_profile.py --concurrency 1 > $OUT/phase_c1.log 2>&1
 rc=$?
 echo "exit=$rc"
-tail -3 $OUT/*.log
+tail -n 3 $OUT/*.log
 exit $rc
