@@ -73,10 +73,72 @@ def build_hip(force: bool = False, verbose: bool = False, extra_flags=()) -> str
         objs = list(ex.map(compile_one, srcs))
     tmp = HIP_LIB + ".tmp"
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp])
+    check_lgkm_windows(verbose)
     os.replace(tmp, HIP_LIB)
     if verbose:
         print("built", HIP_LIB)
     return HIP_LIB
+
+
+# Kernels whose k-loops read LDS fragments with inline-asm ds_reads and wait for them with a COUNTED
+# `s_waitcnt lgkmcnt(N)` (gemm_mfma.hip KA_GM_PIPE 2, gemm_big.hip): the count is only right if the
+# compiler puts no LGKM operation of its own (scalar/kernarg load, LDS access, flat access, message)
+# between those reads and the wait.  hipcc cannot see the asm, so a different compiler version or
+# scheduling choice could silently break it; check_lgkm_windows() re-verifies every build.
+LGKM_CHECKED = {"gemm_mfma.hip": r"gemm_kernel", "gemm_big.hip": r"gemm256_kernel"}
+
+
+def lgkm_window_violations(asm_text: str, func_pat: str):
+    """(number of asm fragment reads seen, [(function, line, instruction)] of compiler-issued LGKM
+    operations inside an asm-read window: after an asm ds_read, before the next lgkmcnt wait)."""
+    import re
+    bad, fn, in_asm, pending, nreads = [], None, False, False, 0
+    for ln, line in enumerate(asm_text.splitlines(), 1):
+        m = re.match(r"^(_Z\S+):", line)
+        if m:
+            fn = m.group(1) if re.search(func_pat, m.group(1)) else None
+            pending = False
+            continue
+        if fn is None:
+            continue
+        t = line.strip()
+        if t.startswith(";;#ASMSTART"):
+            in_asm = True
+            continue
+        if t.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        if not t or t.startswith(";") or t.startswith("."):
+            continue
+        op = t.split()[0]
+        if in_asm and op.startswith("ds_read"):
+            pending, nreads = True, nreads + 1
+            continue
+        if op == "s_waitcnt" and "lgkmcnt" in t:
+            pending = False
+            continue
+        if pending and (op.startswith(("s_load", "s_buffer_load", "flat_", "s_sendmsg"))
+                        or (op.startswith("ds_") and not in_asm)):
+            bad.append((fn, ln, t))
+    return nreads, bad
+
+
+def check_lgkm_windows(verbose: bool = False) -> None:
+    """Compile the LGKM_CHECKED sources to device assembly and fail the build on any violation."""
+    for name, pat in LGKM_CHECKED.items():
+        src = os.path.join(CSRC, name)
+        out = os.path.join(LIB_DIR, "obj", name + ".s")
+        _run([HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "--cuda-device-only", "-S",
+              *file_flags(src), src, "-o", out])
+        with open(out) as f:
+            nreads, bad = lgkm_window_violations(f.read(), pat)
+        if nreads == 0:
+            raise RuntimeError(f"{name}: no asm fragment reads found in the {pat} kernels (checker out of date?)")
+        if bad:
+            raise RuntimeError(f"{name}: compiler LGKM operations inside counted asm-read windows "
+                               f"(the lgkmcnt counts would be wrong): {bad[:5]}")
+        if verbose:
+            print(f"lgkm windows ok: {name} ({nreads} asm reads)")
 
 
 def build_runtime(force: bool = False, verbose: bool = False) -> str:

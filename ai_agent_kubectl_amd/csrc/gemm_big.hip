@@ -35,10 +35,10 @@
 //     (gb_rp_ab.log, gb_cw_ab.log);
 //   * XCD-aware tile order (T1): the bijective round-robin remap, then GM m-tiles x all n-tiles
 //     super-rows so the panels of the tiles running together on one XCD are L2 hits.
-// Measured at 0.90-0.92x rocBLAS's MT256x256x64 kernel on the plain shapes at M = 4096 and 0.96-0.98x
-// at M ~ 3000; the SwiGLU epilogue (no [M, 2I] write, no SiLU pass) makes gate_up + SiLU a net win,
-// which is what the engine dispatches (ops.linear_swiglu); the other prefill projections stay
-// hipBLASLt (profiles/r3/README.md).
+// Measured (round 4, profiles/r4/gemm_big_tail/README.md, interleaved with rocBLAS in one process):
+// gate_up + SwiGLU 1.05x rocBLAS (+ its separate SiLU pass) at M = 2944, QKV 0.79-0.84x at M = 2944-4096
+// (1.5 rounds of 256 x 256 tiles), O / down ~0.9x; the SwiGLU epilogue (no [M, 2I] write, no SiLU pass)
+// makes gate_up + SiLU a net win, which is what the engine dispatches (ops.linear_swiglu).
 // Engine dispatch: EPI_SWIGLU (prefill / mixed-step gate_up, ops.linear_swiglu) and EPI_ARGMAX (the
 // fused LM head, ops.lm_head_argmax, per decode bucket where ModelRunner.tune_lm_head times it
 // faster).  EPI_BF16 is the plain GEMM the harness (tools/gemm_big_bench.hip) and scripts/gb_diag.py
@@ -178,7 +178,9 @@ KA_DEV void tile_of(int L, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
 // VMEM-store-data / VALU-write hazard around asm it cannot see, so the asm stores carry their own
 // wait states (without them a few lanes' data were corrupted: profiles/r4/gemm_big_tail/).
 #ifndef KA_GB_TAIL_MODE
-#define KA_GB_TAIL_MODE 2   // measured fastest, and exact in every test (profiles/r4/gemm_big_tail/)
+#define KA_GB_TAIL_MODE 1   // sc1 stores + agent-scope release / acquire fences: correct by the memory model
+                            // (mode 2, fence-free, measured ~1 % faster on tail shapes but rests on
+                            // observed hardware behaviour: opt-in)
 #endif
 template <int N>
 KA_DEV void st_slab8(float* p, const f32x4 (&v)[8], const int (&q)[8]) {

@@ -211,11 +211,18 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   const char* Wb = reinterpret_cast<const char*>(Wg);
   const char* Xb = reinterpret_cast<const char*>(a.X);
 
+  // every kernel argument the k-loop needs is read into registers here, before the loop: under
+  // KA_GM_PIPE 2 the asm fragment reads are waited for with a counted lgkmcnt, which a scalar
+  // (s_load) kernarg read issued between the reads and that wait would break.  The asm makes wnt an
+  // opaque SGPR value, so hipcc cannot rematerialise it from the kernarg segment inside the loop
+  // (build.py check_lgkm_windows verifies the k-loop's read windows in the generated assembly).
+  int wnt = a.wnt;
+  asm volatile("" : "+s"(wnt));
   auto issue = [&](int stage, int t) {
     char* sa = lds_c + stage * C::STAGE_BYTES;
     char* sb = sa + C::A_BYTES;
     const uint32_t kofs = (uint32_t)t * C::RB;
-    if (a.wnt) {
+    if (wnt) {
 #pragma unroll
       for (int j = 0; j < C::GA; ++j) glds16<2>(Wb + offA[j] + kofs, sa + (j * C::NW + wave) * 1024);
     } else {

@@ -148,7 +148,10 @@ class ModelRunner:
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
         self.stats = {"decode_steps": 0, "prefill_steps": 0, "graph_replays": 0, "decode_ms": 0.0,
-                      "prefill_ms": 0.0, "prefill_tokens": 0}
+                      "prefill_ms": 0.0, "prefill_tokens": 0, "persistent_stalls": 0}
+        # bucket -> the captured graph holds the persistent decode kernel (its error word must be read
+        # back on every replay of that graph, whatever model.persistent says now)
+        self.graph_persistent: Dict[int, bool] = {}
 
     # ------------------------------------------------------------------------------------------
     def _view(self, name: str, n: int) -> torch.Tensor:
@@ -359,6 +362,7 @@ class ModelRunner:
             if self.graph_pool is None:
                 self.graph_pool = g.pool()
             self.graphs[B] = g
+            self.graph_persistent[B] = B == 1 and self.model.persistent_ok()
         torch.cuda.synchronize(self.device)
         return time.perf_counter() - t0
 
@@ -518,7 +522,11 @@ class ModelRunner:
         return car.state[2:3] if car is not None else None
 
     def _persistent_step(self, Bp: int) -> bool:
-        """The decode step of bucket Bp runs the persistent kernel (its error word is read back)."""
+        """The decode step of bucket Bp runs the persistent kernel (its error word is read back): the
+        captured graph decides when there is one (a graph captured with the kernel keeps launching it
+        after model.persistent is turned off), the model's current setting otherwise."""
+        if Bp in self.graphs:
+            return self.graph_persistent.get(Bp, False)
         return Bp == 1 and self.model.persistent_ok()
 
     def _copy_err(self, persistent: bool = False) -> Optional[torch.Tensor]:
@@ -545,8 +553,14 @@ class ModelRunner:
                                     "the step's results are stale")
         if int(h[1]):
             self.model.persistent = False   # the chain from now on: co-residency cannot be relied on
+            # a graph captured with the persistent kernel would keep replaying it: drop those graphs,
+            # their buckets run eagerly (the kernel chain) from the next step on
+            for b in [b for b, p in self.graph_persistent.items() if p]:
+                self.graphs.pop(b, None)
+                self.graph_persistent.pop(b, None)
+            self.stats["persistent_stalls"] += 1
             logger.error("persistent decode kernel: a grid wait ran out; batch-1 decode falls back to "
-                         "the kernel chain")
+                         "the kernel chain (stall #%d)", self.stats["persistent_stalls"])
             raise PersistentStall("persistent decode: a workgroup never ran (grid wait timeout); "
                                   "the step's results are stale")
 

@@ -27,6 +27,15 @@ from .config import ModelConfig
 from .moe import moe_forward
 
 
+def persistent_default() -> bool:
+    """KA_PERSISTENT_DECODE: 0 off, 1 on, auto (default) on unless the GPU is shared with another
+    engine (KA_GPU_MEM_SHARE < 1): co-residency of the persistent grid is not guaranteed there."""
+    mode = os.environ.get("KA_PERSISTENT_DECODE", "auto")
+    if mode in ("0", "1"):
+        return mode == "1"
+    return float(os.environ.get("KA_GPU_MEM_SHARE", "1")) >= 1.0
+
+
 @dataclass
 class AttnMeta:
     """Per-step metadata (device int32 tensors unless noted)."""
@@ -86,9 +95,12 @@ class LlamaModel:
         self.prefetch_blocks = int(os.environ.get("KA_DECODE_PREFETCH_BLOCKS", "64"))
         self._side = None
         # batch-1 decode: every layer in ONE persistent launch (csrc/decode_persistent.hip) instead of
-        # ~7 kernels per layer (3.13 vs 3.44 ms/step for Llama-3-8B, profiles/r4/persistent_decode/),
-        # wherever the geometry allows; KA_PERSISTENT_DECODE=0 keeps the kernel chain.
-        self.persistent = os.environ.get("KA_PERSISTENT_DECODE", "1") == "1"
+        # ~7 kernels per layer (2.85 vs 3.44 ms/step for Llama-3-8B, profiles/r4/persistent_decode/,
+        # profiles/r4/zero_cijk_decode/), wherever the geometry allows.  Its grid barriers need every
+        # workgroup resident, which only holds when this engine owns the GPU: KA_PERSISTENT_DECODE=auto
+        # (default) turns it off when several replicas / ranks share the device (KA_GPU_MEM_SHARE < 1,
+        # parallel/dp.py), 1 forces it on, 0 keeps the kernel chain.
+        self.persistent = persistent_default()
         self._pd = None   # (layer pointer table, workspace)
         self.persistent_stamps = None   # diagnostics: int64 [CUs, L, 16] phase timestamps (scripts/)
 

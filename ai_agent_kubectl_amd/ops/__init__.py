@@ -424,11 +424,14 @@ def plan_for(M: int, N: int, K: int):
 
 def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool = False,
            bf16_partials: bool = False):
-    """y = x @ w.T (w is [out, in]).  Decode-sized M goes to the hand-written weight-streaming
-    kernel (M <= 256, csrc/gemm_skinny.hip), the LDS-DMA MFMA kernel (M <= 512, csrc/gemm_mfma.hip)
-    or hipBLASLt, whichever the autotuned plan measured fastest for this (M, N, K); prefill / mixed
-    steps (M > 512) go to csrc/gemm_big.hip (`linear_big`, KA_PREFILL_GEMM) where the shape allows,
-    else hipBLASLt via F.linear.
+    """y = x @ w.T (w is [out, in]).  M <= TILE_MAX_M (decode buckets, small mixed steps): the kernel
+    the per-(M, N, K) plan (GEMM_PLAN, ops/tuned/gemm_plan_mi355x.json or timed at engine start by
+    ops.autotune) measured fastest — row GEMV ("rows", csrc/gemm_skinny.hip), split-K weight
+    streaming ("skinny"), the LDS-DMA ring kernels ("gm", csrc/gemm_mfma.hip), csrc/gemm_big.hip
+    ("big") or hipBLASLt ("blas"); an M no bucket planned takes the next larger bucket's plan, and
+    without any plan M <= SKINNY_MAX_M streams through gemm_skinny.  Prefill / mixed steps
+    (M > TILE_MAX_M) go to csrc/gemm_big.hip (`linear_big`) under KA_PREFILL_GEMM=big where the shape
+    allows, else hipBLASLt via F.linear.
     defer_reduce: when the chosen kernel splits K, return its partials as a `SplitK` for a consumer
     that fuses the reduction instead of running the reduce kernel.
     bf16_partials: with defer_reduce, a gemm_mfma plan stores those partials as bf16

@@ -120,6 +120,56 @@ def test_persistent_stall_is_503_then_chain_serves(tiny):
         eng.healthy, eng.last_error = True, None
 
 
+class _FakeGraph:
+    """Stands in for a captured bucket-1 decode graph: replay runs the step eagerly."""
+    def __init__(self, runner, B):
+        self.runner, self.B, self.replays = runner, B, 0
+
+    def replay(self):
+        self.replays += 1
+        self.runner._decode_forward(self.B)
+
+
+def test_persistent_stall_drops_the_persistent_graph(tiny):
+    """with decode graphs on, the bucket-1 graph captured with the persistent kernel
+    keeps launching it after model.persistent is switched off.  The runner must keep reading that
+    graph's error word while it exists, and a stall must drop the graph (batch 1 then runs the kernel
+    chain eagerly) instead of replaying stale results without an error."""
+    from ai_agent_kubectl_amd.engine.runner import PersistentStall
+    eng, be = tiny
+    app = _app(be)
+    r, m = eng.runner, eng.runner.model
+    word = torch.tensor([0], dtype=torch.int32)
+    saved = (m.persistent_err_word, m.persistent, dict(r.graphs), dict(r.graph_persistent))
+    g = _FakeGraph(r, 1)
+    r.graphs[1] = g
+    r.graph_persistent[1] = True
+    m.persistent_err_word = lambda: word
+    m.persistent = False          # the model's flag alone no longer decides: the graph holds the kernel
+    stalls0 = r.stats["persistent_stalls"]
+    try:
+        assert r._persistent_step(1)
+        rs = asyncio.run(_post_all(app, be, ["list pods in default"]))
+        assert rs[0].status_code == 200 and g.replays > 0
+        word.fill_(1)
+        rs = asyncio.run(_post_all(app, be, ["list pods in kube-public"]))
+        assert rs[0].status_code == 503, rs[0].text
+        assert isinstance(eng.last_error, PersistentStall)
+        assert 1 not in r.graphs and 1 not in r.graph_persistent
+        assert r.stats["persistent_stalls"] == stalls0 + 1
+        assert not r._persistent_step(1)
+        n = g.replays
+        rs = asyncio.run(_post_all(app, be, ["get deployments now"]))   # word still set: not read any more
+        assert rs[0].status_code == 200 and g.replays == n
+    finally:
+        m.persistent_err_word, m.persistent = saved[0], saved[1]
+        r.graphs.clear()
+        r.graphs.update(saved[2])
+        r.graph_persistent.clear()
+        r.graph_persistent.update(saved[3])
+        eng.healthy, eng.last_error = True, None
+
+
 def test_error_word_clear_is_transparent(tiny):
     """A zero error word changes nothing (the readback rides behind every step's tokens)."""
     eng, be = tiny
@@ -174,3 +224,20 @@ def test_watchdog_verdict_with_exit_on_fatal_fails_inflight_and_exits():
     eng.exit_on_fatal, eng._exit = False, eng2_exits.append
     eng.mark_unhealthy("again")              # without exit_on_fatal: only unhealthy
     assert eng2_exits == []
+
+
+def test_persistent_default_off_on_a_shared_gpu(monkeypatch):
+    """the persistent kernel's grid barriers need the whole GPU, so the default
+    (auto) turns it off when several replicas share one device (KA_GPU_MEM_SHARE < 1, set by
+    parallel/dp.py); an explicit KA_PERSISTENT_DECODE=0/1 wins either way."""
+    from ai_agent_kubectl_amd.models.llama import persistent_default
+    monkeypatch.delenv("KA_PERSISTENT_DECODE", raising=False)
+    monkeypatch.delenv("KA_GPU_MEM_SHARE", raising=False)
+    assert persistent_default()
+    monkeypatch.setenv("KA_GPU_MEM_SHARE", "0.5")
+    assert not persistent_default()
+    monkeypatch.setenv("KA_PERSISTENT_DECODE", "1")
+    assert persistent_default()
+    monkeypatch.setenv("KA_GPU_MEM_SHARE", "1.0")
+    monkeypatch.setenv("KA_PERSISTENT_DECODE", "0")
+    assert not persistent_default()

@@ -93,3 +93,26 @@ def test_plan_for_takes_the_next_bucket_up():
     finally:
         ops.GEMM_PLAN.clear()
         ops.GEMM_PLAN.update(saved)
+
+
+def test_lgkm_window_checker_flags_compiler_lgkm_ops():
+    """build.py re-verifies that no compiler-issued LGKM operation sits between the
+    k-loop's asm fragment reads and their counted lgkmcnt wait (gemm_mfma KA_GM_PIPE 2, gemm_big)."""
+    from ai_agent_kubectl_amd.build import lgkm_window_violations
+    ok = """_ZN2gm11gemm_kernelI1EEvNS_4ArgsE:
+\t;;#ASMSTART
+\tds_read_b128 v[0:3], v10 offset:0
+\t;;#ASMEND
+\tv_mfma_f32_16x16x32_bf16 a[0:3], v[4:7], v[8:11], a[0:3]
+\t;;#ASMSTART
+\ts_waitcnt lgkmcnt(4)
+\t;;#ASMEND
+\ts_load_dword s4, s[0:1], 0x10
+\tds_write_b32 v1, v2
+"""
+    n, bad = lgkm_window_violations(ok, "gemm_kernel")
+    assert n == 1 and bad == []
+    broken = ok.replace("\tv_mfma", "\ts_load_dwordx2 s[6:7], s[0:1], 0x8\n\tv_mfma")
+    n, bad = lgkm_window_violations(broken, "gemm_kernel")
+    assert n == 1 and len(bad) == 1 and "s_load_dwordx2" in bad[0][2]
+    assert lgkm_window_violations(broken, "other_kernel") == (0, [])
