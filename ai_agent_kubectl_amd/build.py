@@ -123,6 +123,42 @@ def lgkm_window_violations(asm_text: str, func_pat: str):
     return nreads, bad
 
 
+def mfma_span_valu(asm_text: str, func_pat: str):
+    """[(function, line, instruction)] of compiler-issued VALU instructions between the first and the
+    last inline-asm MFMA of each matching function.  gemm_big's k-loop is all asm (MFMAs with pinned
+    AGPR accumulators, fragment reads, LDS-DMA): hipcc cannot see those MFMAs read their A / B VGPRs
+    for several cycles after issue, so a VALU write it schedules there may overwrite an operand still
+    being read (seen: a mask register reusing a dead A fragment's VGPR -> sparse wrong outputs)."""
+    import re
+    bad, fn, lines = [], None, []
+
+    def flush():
+        if fn is None:
+            return
+        idx = [i for i, (_, t, a) in enumerate(lines) if a and t.startswith("v_mfma")]
+        if idx:
+            for ln, t, a in lines[idx[0]:idx[-1]]:
+                if not a and t.startswith("v_") and not t.startswith("v_mfma"):
+                    bad.append((fn, ln, t))
+
+    in_asm = False
+    for ln, line in enumerate(asm_text.splitlines(), 1):
+        m = re.match(r"^(_Z\S+):", line)
+        if m:
+            flush()
+            fn, lines = (m.group(1) if re.search(func_pat, m.group(1)) else None), []
+            continue
+        t = line.strip()
+        if t.startswith(";;#ASMSTART"):
+            in_asm = True
+        elif t.startswith(";;#ASMEND"):
+            in_asm = False
+        elif fn is not None and t and not t.startswith((";", ".")):
+            lines.append((ln, t, in_asm))
+    flush()
+    return bad
+
+
 def check_lgkm_windows(verbose: bool = False) -> None:
     """Compile the LGKM_CHECKED sources to device assembly and fail the build on any violation."""
     for name, pat in LGKM_CHECKED.items():
@@ -137,6 +173,12 @@ def check_lgkm_windows(verbose: bool = False) -> None:
         if bad:
             raise RuntimeError(f"{name}: compiler LGKM operations inside counted asm-read windows "
                                f"(the lgkmcnt counts would be wrong): {bad[:5]}")
+        if name == "gemm_big.hip":
+            with open(out) as f:
+                valu = mfma_span_valu(f.read(), pat)
+            if valu:
+                raise RuntimeError(f"{name}: compiler VALU inside the asm-MFMA k-loop (operand WAR hazard "
+                                   f"against in-flight MFMAs): {valu[:5]}")
         if verbose:
             print(f"lgkm windows ok: {name} ({nreads} asm reads)")
 

@@ -49,15 +49,28 @@
 // gate_up output never exists); residual add (Y = X W^T + R, R may alias Y).
 #include "common.h"
 
+#include <algorithm>
+#include <cstdlib>
 #include <utility>
 
 
 namespace gb {
 
-constexpr int BN = 256, BM = 256, BK = 64, NT = 256;
-constexpr int TILE_A = BN * BK * 2, TILE_B = BM * BK * 2;   // 32 KB each
-constexpr int STAGE = TILE_A + TILE_B;                        // 64 KB
-constexpr int LDS = 2 * STAGE;   // two 64-deep buffers (a 5-slot ring of 32-deep stages measured slower)
+// Tile geometry per TN = 16-row W (MFMA A) fragments per wave: TN 8 is the 256 x 256 tile, TN 6 a
+// 192 (W rows) x 256 (X rows) tile for shapes whose 256-wide tiles leave a fractional last round
+// (QKV, N = 6144: 384 tiles = 1.5 rounds of 256 CUs at M = 4096; 512 x 192-row tiles = 2 full rounds).
+constexpr int BM = 256, BK = 64, NT = 256;
+template <int TN>
+struct Geo {
+  static constexpr int BN = 32 * TN;                        // W rows of a tile (two waves of 16 TN)
+  static constexpr int TILE_A = BN * BK * 2;                // 32 / 24 KB
+  static constexpr int TILE_B = BM * BK * 2;                // 32 KB
+  static constexpr int STAGE = TILE_A + TILE_B;
+  static constexpr int LDS = 2 * STAGE;   // two 64-deep buffers (a 5-slot ring of 32-deep stages measured slower)
+  static constexpr int LDS_TOTAL = LDS + 4 * 8192;         // + the epilogue scratch (8 KB per wave)
+  static constexpr int PIECES = TN + 8;                     // 1-KB LDS-DMA pieces per wave per k-tile
+};
+constexpr int BN = Geo<8>::BN;   // the 256-wide tile (SwiGLU / argmax / split-K epilogues)
 
 enum Epi : int { EPI_BF16 = 0, EPI_P32 = 1, EPI_P16 = 2, EPI_SWIGLU = 3, EPI_ADD = 4, EPI_ARGMAX = 5 };
 
@@ -123,17 +136,19 @@ KA_DEV void ds_read16(bf16x8& dst, uint32_t addr) {
 // the same piece under a shared M0: piece P (< 4) of a 4-KB LDS group writes M0 + 1024 P (the immediate
 // offset applies to both the LDS destination and the global address, so the lane's global offset is
 // pre-biased by -1024 P); P == 0 saves M0 and points it at the group, P == 3 restores it
-template <int P>
+// LAST: the group's final piece (P == 3 of a 4-piece group; P == 1 of the 2-piece W group of TN 6)
+template <int P, bool LAST>
 KA_DEV void dma16g(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t lds_addr, uint32_t& keep) {
+  static_assert(P > 0 || !LAST, "a group has at least two pieces");
   if constexpr (P == 0)
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds"
                  : "=&s"(keep)
                  : "v"(voff), "s"(r), "s"(lds_addr), "s"(soff)
                  : "memory");
-  else if constexpr (P == 3)
-    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:3072 lds\n\ts_mov_b32 m0, %3"
+  else if constexpr (LAST)
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:%3 lds\n\ts_mov_b32 m0, %4"
                  :
-                 : "v"(voff), "s"(r), "s"(soff), "s"(keep)
+                 : "v"(voff), "s"(r), "s"(soff), "i"(P * 1024), "s"(keep)
                  : "memory");
   else
     asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:%3 lds"
@@ -183,40 +198,41 @@ KA_DEV void tile_of(int L, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
                             // observed hardware behaviour: opt-in)
 #endif
 template <int N>
-KA_DEV void st_slab8(float* p, const f32x4 (&v)[8], const int (&q)[8]) {
+KA_DEV void st_slab(float* p, const f32x4 (&v)[N], const int (&q)[N]) {
 #if KA_GB_TAIL_MODE == 0
 #pragma unroll
-  for (int e = 0; e < 8; ++e) *reinterpret_cast<f32x4*>(p + q[e] * 256) = v[e];
+  for (int e = 0; e < N; ++e) *reinterpret_cast<f32x4*>(p + q[e] * 256) = v[e];
 #else
-  asm volatile(
-      "global_store_dwordx4 %0, %8, off sc1\n\tglobal_store_dwordx4 %1, %9, off sc1\n\t"
-      "global_store_dwordx4 %2, %10, off sc1\n\tglobal_store_dwordx4 %3, %11, off sc1\n\t"
-      "global_store_dwordx4 %4, %12, off sc1\n\tglobal_store_dwordx4 %5, %13, off sc1\n\t"
-      "global_store_dwordx4 %6, %14, off sc1\n\tglobal_store_dwordx4 %7, %15, off sc1\n\ts_nop 4" ::"v"(p + q[0] * 256),
-      "v"(p + q[1] * 256), "v"(p + q[2] * 256), "v"(p + q[3] * 256), "v"(p + q[4] * 256), "v"(p + q[5] * 256),
-      "v"(p + q[6] * 256), "v"(p + q[7] * 256), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]),
-      "v"(v[6]), "v"(v[7])
-      : "memory");
+  // each store carries its own wait states (VMEM store data vs a following VALU write of its VGPRs)
+#pragma unroll
+  for (int e = 0; e < N; ++e)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p + q[e] * 256), "v"(v[e]) : "memory");
+  asm volatile("s_nop 4" ::: "memory");
 #endif
 }
-KA_DEV void ld_slab8(f32x4 (&t)[8], const float* p, const int (&q)[8]) {
+template <int N>
+KA_DEV void ld_slab(f32x4 (&t)[N], const float* p, const int (&q)[N]) {
 #if KA_GB_TAIL_MODE == 2
 #pragma unroll
-  for (int e = 0; e < 8; ++e)
+  for (int e = 0; e < N; ++e)
     asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(t[e]) : "v"(p + q[e] * 256) : "memory");
-  // the loads' registers are operands of the wait, so no use is scheduled above it
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
-               "+v"(t[7])::"memory");
+  // the loads' registers are operands of the wait, so no use (or copy) is scheduled above it
+  static_assert(N == 6 || N == 8, "slab width");
+  if constexpr (N == 8)
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]),
+                 "+v"(t[6]), "+v"(t[7])::"memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5])::"memory");
 #else
 #pragma unroll
-  for (int e = 0; e < 8; ++e) t[e] = *reinterpret_cast<const f32x4*>(p + q[e] * 256);
+  for (int e = 0; e < N; ++e) t[e] = *reinterpret_cast<const f32x4*>(p + q[e] * 256);
 #endif
 }
 
 // Tail slice hand-off of one wave's 128 x 128 quadrant (Args.full .. comment): every slice publishes
-// its fp32 quadrant to slot k of the tile's slab (the epilogue's mode 1, tail_store8), waits for its
+// its fp32 quadrant to slot k of the tile's slab (the epilogue's mode 1, tail_store), waits for its
 // own stores, then takes an arrival ticket; the slice whose ticket is the last one (all others have
-// published before arriving) runs the epilogue on the sum of the slots (mode 2, tail_fetch8) and
+// published before arriving) runs the epilogue on the sum of the slots (mode 2, tail_fetch) and
 // resets the counter for the next launch.  The accumulators are read at ONE place of the epilogue
 // (a second read, or summing into them, made hipcc move the whole tile into VGPRs and spill).
 KA_DEV bool tail_ticket(const Args& a, int tt, int w, int lane) {
@@ -242,31 +258,38 @@ KA_DEV bool tail_ticket(const Args& a, int tt, int w, int lane) {
   return true;
 }
 
+// slab slot of (tail tile tt, slice k, wave w): [TN 8 accumulator rows of 64 lanes] f32x4 per wave
+template <int TN>
 KA_DEV float* tail_slot(const Args& a, int tt, int k, int w, int lane) {
-  return a.slab + ((((size_t)tt * a.tail_s + k) * 4 + w) * 64) * 256 + lane * 4;
+  return a.slab + ((((size_t)tt * a.tail_s + k) * 4 + w) * (TN * 8)) * 256 + lane * 4;
 }
 
 // this slice's accumulators q[e] -> its slot
-KA_DEV void tail_store8(const Args& a, int tt, int k, int w, int lane, const int (&q)[8], const f32x4 (&v)[8]) {
-  st_slab8<8>(tail_slot(a, tt, k, w, lane), v, q);
+template <int TN, int N>
+KA_DEV void tail_store(const Args& a, int tt, int k, int w, int lane, const int (&q)[N], const f32x4 (&v)[N]) {
+  st_slab<N>(tail_slot<TN>(a, tt, k, w, lane), v, q);
 }
 
 // v[e] = sum over the tile's ts slots of accumulator q[e] of this lane (after tail_ticket's acquire)
-KA_DEV void tail_fetch8(const Args& a, int tt, int w, int lane, const int (&q)[8], f32x4 (&v)[8]) {
+template <int TN, int N>
+KA_DEV void tail_fetch(const Args& a, int tt, int w, int lane, const int (&q)[N], f32x4 (&v)[N]) {
   const int ts = a.tail_s;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int e = 0; e < N; ++e) v[e] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int k = 0; k < ts; ++k) {
-    const float* const p = tail_slot(a, tt, k, w, lane);
-    f32x4 t[8];
-    ld_slab8(t, p, q);
+    const float* const p = tail_slot<TN>(a, tt, k, w, lane);
+    f32x4 t[N];
+    ld_slab<N>(t, p, q);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += t[e];
+    for (int e = 0; e < N; ++e) v[e] += t[e];
   }
 }
 
-template <int EPI>
+template <int EPI, int TN>
 __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
+  using GE = Geo<TN>;
+  constexpr int BNT = GE::BN, TILE_A = GE::TILE_A, STAGE = GE::STAGE, PIECES = GE::PIECES;
+  static_assert(TN == 8 || ((EPI == EPI_BF16 || EPI == EPI_ADD) && TN == 6), "TN 6: plain / residual epilogues");
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
   char* const L = reinterpret_cast<char*>(lds);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -332,16 +355,17 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   // LDS byte address of the staging array (dynamic LDS: the only LDS object of this kernel)
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)lds;
   const int r16 = lane & 15, grp = lane >> 4;
-  // DMA sources: wave-instruction j (< 8) of this wave fills staged rows 64 w + 8 j .. + 8 (1 KB) of
-  // the W and of the X tile, so a wave's pieces are contiguous 1-KB blocks (4 per M0 value)
+  // DMA sources: wave-instruction j of this wave fills staged W rows 8 TN w + 8 j .. + 8 (j < TN) and
+  // X rows 64 w + 8 j .. + 8 (j < 8), 1 KB each, so a wave's pieces are contiguous 1-KB blocks (up to
+  // 4 per M0 value)
   const int r8 = lane >> 3, slot = lane & 7;
-  uint32_t offA[8], offB[8];
+  uint32_t offA[TN], offB[8];
   auto set_offsets = [&](int tm_, int tn_, int kt0_) {
     const int m0_ = tm_ * BM;
     const uint32_t kb = (uint32_t)kt0_ * (uint32_t)(BK * 2);   // byte offset of the unit's k range
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int row = 64 * w + 8 * j + r8;
+    for (int j = 0; j < TN; ++j) {
+      const int row = 8 * TN * w + 8 * j + r8;
       const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
       int wrow;
       if constexpr (EPI == EPI_SWIGLU) {
@@ -349,39 +373,72 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
         // is gate (c even) or up (c odd) of output columns 128 tn + 16 (c >> 1) + 0..15
         wrow = 128 * tn_ + 16 * (row >> 5) + (row & 15) + ((row >> 4) & 1) * a.I;
       } else {
-        wrow = min(tn_ * BN + row, a.N - 1);
+        wrow = min(tn_ * BNT + row, a.N - 1);
       }
       offA[j] = ((uint32_t)wrow * (uint32_t)a.K + ch) * 2u + kb + BIAS - (uint32_t)(j & 3) * 1024u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = 64 * w + 8 * j + r8;
+      const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
       offB[j] = ((uint32_t)min(m0_ + row, a.M - 1) * (uint32_t)a.ldx + ch) * 2u + kb + BIAS -
                 (uint32_t)(j & 3) * 1024u;
     }
   };
   set_offsets(tm, tn, kt0);
-  // DMA piece s (< 16) of a k-tile: W (s < 8) or X (s >= 8) rows 64 w + 8 (s & 7) .. + 8; M0 is set
-  // once per 4 pieces (s & 3 == 0) and restored after the fourth
-  const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)w * 8192u);
+  // DMA piece s (< PIECES) of a k-tile: W (s < TN) or X (s >= TN); M0 is set once per group of up to 4
+  // pieces and restored after the group's last
+  const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)w * (uint32_t)(TN * 1024));
+  const uint32_t ldsx = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)TILE_A + (uint32_t)w * 8192u);
   uint32_t m0keep = 0;
-#define GB_DMA(S, BUF, T)                                                                                     \
-  dma16g<(S) & 3>(((S) >> 3) ? rX : rW, ((S) >> 3) ? offB[(S) & 7] : offA[(S) & 7], (uint32_t)(T) * (BK * 2), \
-                  ldsw + (BUF) * STAGE + ((S) >> 3) * TILE_A + (((S) >> 2) & 1) * 4096, m0keep)
+  auto dma = [&](auto sc, auto bufc, int T) {
+    constexpr int S = decltype(sc)::value, BUF = decltype(bufc)::value;
+    const uint32_t soff = (uint32_t)T * (BK * 2);
+    if constexpr (S < TN) {
+      constexpr int P = S & 3;
+      constexpr bool LAST = P == 3 || S == TN - 1;
+      dma16g<P, LAST>(rW, offA[S], soff, ldsw + BUF * STAGE + (S >> 2) * 4096, m0keep);
+    } else {
+      constexpr int J = S - TN, P = J & 3;
+      dma16g<P, P == 3>(rX, offB[J], soff, ldsx + BUF * STAGE + (J >> 2) * 4096, m0keep);
+    }
+  };
 
   // fragment read bases (bytes, LDS address): [buffer][k half] of the A (W) and B (X) quadrants
   const int sw = (r16 >> 1) & 7;
   const uint32_t c0 = ((0 + grp) ^ sw) * 16, c1 = ((4 + grp) ^ sw) * 16;
-  const uint32_t rA = lds0 + (wn * 128 + r16) * 128, rB = lds0 + TILE_A + (wm * 128 + r16) * 128;
+  const uint32_t rA = lds0 + (wn * TN * 16 + r16) * 128, rB = lds0 + TILE_A + (wm * 128 + r16) * 128;
   const uint32_t bA00 = rA + c0, bA01 = rA + c1, bA10 = rA + STAGE + c0, bA11 = rA + STAGE + c1;
   const uint32_t bB00 = rB + c0, bB01 = rB + c1, bB10 = rB + STAGE + c0, bB11 = rB + STAGE + c1;
 
-  f32x4 acc[8][8];
-  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  f32x4 acc[TN][8];
+  bf16x8 fa0[TN], fb0[8], fa1[TN], fb1[8];
 
-  // read S of a fragment set: A fragment S >> 1 (S even) or B fragment S >> 1 (S odd)
-  auto rd = [&](auto sc, bf16x8* FA, bf16x8* FB, uint32_t ba, uint32_t bb) {
+  // the k-loop schedule per k-tile (two fragment sets F0 = k 0..31 and F1 = k 32..63, NQ MFMAs each,
+  // issued as groups of 4)
+  constexpr int NRD = TN + 8;        // fragment reads per set
+  constexpr int NQ = TN * 8;         // MFMAs per set
+  constexpr int GPS = NQ / 4;        // groups per set
+  constexpr int NG = 2 * GPS;        // groups per k-tile (32 at TN 8)
+  constexpr int RW = NG - 4;         // F0(t + 1) read window: the k-tile's last 4 groups
+  static_assert(NRD <= 16, "a read window holds 16 reads");
+  // read S of a fragment set in window order 1 (A0 B0 A1 B1 ..., the B's past A(TN-1) last):
+  auto rd1 = [&](auto sc, bf16x8* FA, bf16x8* FB, uint32_t ba, uint32_t bb) {
     constexpr int S = decltype(sc)::value;
-    if constexpr (S & 1) ds_read16<(S >> 1) * 2048>(FB[S >> 1], bb);
-    else ds_read16<(S >> 1) * 2048>(FA[S >> 1], ba);
+    if constexpr (S < 2 * TN) {
+      if constexpr (S & 1) ds_read16<(S >> 1) * 2048>(FB[S >> 1], bb);
+      else ds_read16<(S >> 1) * 2048>(FA[S >> 1], ba);
+    } else {
+      ds_read16<(S - TN) * 2048>(FB[S - TN], bb);
+    }
   };
-  // MFMAs 4S .. 4S+3 of the 8 x 8 set
+  // ... and in window order 2 (B0 .. B7, then A0 .. A(TN-1)): row 0 of the next call needs A0 and every B
+  auto rd2 = [&](auto sc, bf16x8* FA, bf16x8* FB, uint32_t ba, uint32_t bb) {
+    constexpr int S = decltype(sc)::value;
+    if constexpr (S < 8) ds_read16<S * 2048>(FB[S], bb);
+    else ds_read16<(S - 8) * 2048>(FA[S - 8], ba);
+  };
+  // MFMAs 4S .. 4S+3 of the TN x 8 set
   auto mma4 = [&](auto sc, const bf16x8* FA, const bf16x8* FB) {
     constexpr int S = decltype(sc)::value;
     static_for<4>([&](auto qc) {
@@ -389,39 +446,43 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
       mfma_acc(acc[q >> 3][q & 7], FA[q >> 3], FB[q & 7]);
     });
   };
-  // one 64-deep k-tile per call as 32 groups of 4 MFMAs (groups 0-15 on F0, 16-31 on
-  // F1), the fragment reads and the LDS-DMA pieces in separate windows of the MFMA stream (the
-  // order hipBLASLt's MT256x256x64 DirectToLds kernel uses on gfx950; it measured faster than a
-  // window carrying both):
-  //   groups 0-3:   F1(t) <- buffer BUF, 4 reads before each group
+  // one 64-deep k-tile per call as NG groups of 4 MFMAs (groups 0 .. GPS-1 on F0, the rest on F1),
+  // the fragment reads and the LDS-DMA pieces in separate windows of the MFMA stream (the order
+  // hipBLASLt's MT256x256x64 DirectToLds kernel uses; it measured faster than a window carrying both):
+  //   groups 0-3:   F1(t) <- buffer BUF, one read before each MFMA
   //   lgkmcnt(0) + barrier #1: every wave's reads of buffer BUF are done (F0(t) was read at the end
   //                 of the previous call)
-  //   groups 4-27:  the 16 pieces of k-tile T into buffer BUF, 2 of every 3 groups (1 per 6 MFMAs)
-  //   vmcnt(16) + barrier #2: the k-tile staged one call earlier has landed in buffer BUF ^ 1
-  //   groups 28-31: F0(t + 1) <- buffer BUF ^ 1, 4 reads before each (F0(t) retired at group 15)
+  //   groups 4 .. RW-1: the PIECES pieces of k-tile T into buffer BUF, spread evenly (2 of every 3
+  //                 groups at TN 8)
+  //   vmcnt(PIECES) + barrier #2: the k-tile staged one call earlier has landed in buffer BUF ^ 1
+  //   groups RW .. NG-1: F0(t + 1) <- buffer BUF ^ 1, one read before each MFMA (F0(t) retired at
+  //                 group GPS - 1)
+  // (Every DMA is issued unconditionally: skipping the last unit's re-stage behind a runtime flag put
+  // VALU work (the flag's mask) into the MFMA stream, where hipcc's register reuse wrote an A-fragment
+  // VGPR still being read by an in-flight asm MFMA it cannot see (sparse wrong outputs in the SwiGLU
+  // and argmax epilogues), and it bought nothing measurable on the single-round shapes.)
   auto iter = [&](auto bufc, int T) {
     constexpr int BUF = decltype(bufc)::value;
-    static_for<32>([&](auto gc) {
+    static_for<NG>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
-      constexpr int RW = 28;               // F0(t+1) read window: groups 28-31 (starting it one
-                                           // group earlier measured the same, gb_sc_ab.log rw27)
-      if constexpr (g < 4 || (g >= RW && g < RW + 4)) {   // read windows: one fragment read before each MFMA
+      if constexpr (g < 4 || g >= RW) {   // read windows: one fragment read before each MFMA
         static_for<4>([&](auto qc) {
           constexpr int qq = decltype(qc)::value;
-          if constexpr (g < 4)
-            rd(std::integral_constant<int, 4 * g + qq>{}, fa1, fb1, BUF ? bA11 : bA01, BUF ? bB11 : bB01);
-          else   // B0..B7 first, then A0..A7: row 0 of the next call needs A0 and every B
-            rd(std::integral_constant<int, (4 * (g - RW) + qq) < 8 ? 2 * (4 * (g - RW) + qq) + 1
-                                                                   : 2 * (4 * (g - RW) + qq - 8)>{},
-               fa0, fb0, BUF ? bA00 : bA10, BUF ? bB00 : bB10);
-          constexpr int q = 4 * (g & 15) + qq;
-          // the previous call's F0 reads are waited for here, per A fragment: row 0 (A0, all B)
-          // before MFMA 0 (A1..A7 and this call's first read may still be in flight), row 1 (A1)
+          constexpr int S = 4 * (g < 4 ? g : g - RW) + qq;
+          if constexpr (S < NRD) {
+            if constexpr (g < 4)
+              rd1(std::integral_constant<int, S>{}, fa1, fb1, BUF ? bA11 : bA01, BUF ? bB11 : bB01);
+            else
+              rd2(std::integral_constant<int, S>{}, fa0, fb0, BUF ? bA00 : bA10, BUF ? bB00 : bB10);
+          }
+          constexpr int q = 4 * (g % GPS) + qq;
+          // the previous call's F0 reads (order 2) are waited for here, per A fragment: row 0 (A0,
+          // all B) before MFMA 0 (A1.. and this call's first read may still be in flight), row 1 (A1)
           // before MFMA 8; rows 2.. are covered by barrier #1's lgkmcnt(0).  No copy of a fragment
           // register sits between (checked in the disassembly: the loop has no v_mov)
-          if constexpr (q == 0) wait_lgkm<8>();
-          if constexpr (q == 8) wait_lgkm<15>();
-          if constexpr (g < 16) mfma_acc(acc[q >> 3][q & 7], fa0[q >> 3], fb0[q & 7]);
+          if constexpr (g < 4 && q == 0) wait_lgkm<TN>();
+          if constexpr (g < 4 && q == 8) wait_lgkm<TN + 7>();
+          if constexpr (g < GPS) mfma_acc(acc[q >> 3][q & 7], fa0[q >> 3], fb0[q & 7]);
           else mfma_acc(acc[q >> 3][q & 7], fa1[q >> 3], fb1[q & 7]);
         });
       }
@@ -429,14 +490,19 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
         wait_lgkm0();
         block_sync();
       }
-      if constexpr (g >= 4 && g < RW && (g - 4) % 3 != 2) GB_DMA(((g - 4) / 3) * 2 + (g - 4) % 3, BUF, T);
+      if constexpr (g >= 4 && g < RW) {   // the DMA pieces whose slot falls in this group
+        static_for<PIECES>([&](auto pc) {
+          constexpr int pp = decltype(pc)::value;
+          if constexpr (4 + (pp * (RW - 4)) / PIECES == g) dma(pc, bufc, T);
+        });
+      }
       if constexpr (g == RW) {
-        wait_vm<16>();
+        wait_vm<PIECES>();
         block_sync();
       }
-      if constexpr (g >= 4 && !(g >= RW && g < RW + 4)) {
-        if constexpr (g < 16) mma4(std::integral_constant<int, g>{}, fa0, fb0);
-        else mma4(std::integral_constant<int, g - 16>{}, fa1, fb1);
+      if constexpr (g >= 4 && g < RW) {
+        if constexpr (g < GPS) mma4(std::integral_constant<int, g>{}, fa0, fb0);
+        else mma4(std::integral_constant<int, g - GPS>{}, fa1, fb1);
       }
     });
     // (no lgkmcnt wait here: the next call waits per fragment; the tile's last call waits below)
@@ -445,8 +511,8 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   using I1 = std::integral_constant<int, 1>;
 
   // prologue of the first tile: k-tiles 0 and 1 in flight
-  static_for<16>([&](auto sc) { GB_DMA(decltype(sc)::value, 0, 0); });
-  static_for<16>([&](auto sc) { GB_DMA(decltype(sc)::value, 1, 1); });
+  static_for<PIECES>([&](auto sc) { dma(sc, I0{}, 0); });
+  static_for<PIECES>([&](auto sc) { dma(sc, I1{}, 1); });
   // epilogue scratch: 8 KB per wave past the two staging buffers (never a DMA target)
   char* const Q = L + 2 * STAGE + w * 8192;
 
@@ -461,15 +527,15 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     }
     const int nk = nku;
     const int m0 = tm * BM;
-    // k-tile 0 landed: the 16 youngest vector-memory operations are k-tile 1's DMA or the previous
+    // k-tile 0 landed: the PIECES youngest vector-memory operations are k-tile 1's DMA or the previous
     // tile's epilogue stores, everything older (k-tile 0) is done.  (The previous tile's last call
     // already read these fragments; reading them again here keeps F0 dead across the epilogue,
     // which would otherwise spill.)
-    wait_vm<16>();
+    wait_vm<PIECES>();
     block_sync();
-    static_for<16>([&](auto sc) { rd(sc, fa0, fb0, bA00, bB00); });
+    static_for<NRD>([&](auto sc) { rd2(sc, fa0, fb0, bA00, bB00); });
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < TN; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     wait_lgkm0();
@@ -491,11 +557,11 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
         wait_lgkm0();   // the last call's F0 reads land before the epilogue may reuse those registers
       }
     }
-    // epilogue.  acc[i][j][r] = C[n = 128 wn + 16 i + 4 grp + r][m = 128 wm + 16 j + r16] of the
+    // epilogue.  acc[i][j][r] = C[n = 16 TN wn + 16 i + 4 grp + r][m = 128 wm + 16 j + r16] of the
     // tile.  bf16 / SwiGLU: the wave's quadrant is transposed through its 8 KB of LDS in row passes
     // into [m][n] rows and stored as whole 16-B lanes instead of 8-B pieces scattered over 16 rows.
 #pragma unroll
-    for (int i = 0; i < 8; ++i)   // the asm MFMAs' results are read only after mfma_drain's wait states
+    for (int i = 0; i < TN; ++i)   // the asm MFMAs' results are read only after mfma_drain's wait states
 #pragma unroll
       for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
     // the epilogue of a whole tile / split-K slice / the last-arriving tail slice (a lambda called from
@@ -595,7 +661,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
             const int q[8] = {16 * pp + 4 * p, 16 * pp + 8 + 4 * p, 16 * pp + 4 * p + 1, 16 * pp + 8 + 4 * p + 1,
                               16 * pp + 4 * p + 2, 16 * pp + 8 + 4 * p + 2, 16 * pp + 4 * p + 3, 16 * pp + 8 + 4 * p + 3};
             if (mode == 2) {
-              tail_fetch8(a, tt, w, lane, q, v);
+              tail_fetch<TN>(a, tt, w, lane, q, v);
             } else {
               static_for<4>([&](auto jc) {
                 constexpr int jj = decltype(jc)::value;
@@ -603,7 +669,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
                 v[2 * jj + 1] = acc[2 * pp + 1][4 * p + jj];
               });
               if (mode == 1) {
-                tail_store8(a, tt, tslice, w, lane, q, v);
+                tail_store<TN>(a, tt, tslice, w, lane, q, v);
                 return;
               }
             }
@@ -628,28 +694,29 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
           }
         });
       } else {
-        // quadrant: 128 rows (m) x 128 columns (n) = 256 B per row, in 4 passes of 32 rows; 16-B chunk
-        // index ^ (row & 15)
+        // quadrant: 128 rows (m) x 16 TN columns (n), 256-B LDS rows (2 TN of their 16 chunks used), in
+        // 4 passes of 32 rows; 16-B chunk index ^ (row & 15)
         const int rl = lane >> 4, cl = lane & 15;
-        const int n = tn * BN + wn * 128 + 8 * cl;
+        const int n = tn * BNT + wn * 16 * TN + 8 * cl;
         static_for<4>([&](auto pc) {
           constexpr int p = decltype(pc)::value;
-          static_for<2>([&](auto jc) {   // groups of 8: accumulator column 2 p + jj, all i
+          static_for<2>([&](auto jc) {   // groups of TN: accumulator column 2 p + jj, all i
             constexpr int jj = decltype(jc)::value;
-            f32x4 v8[8];
-            const int q[8] = {2 * p + jj, 8 + 2 * p + jj, 16 + 2 * p + jj, 24 + 2 * p + jj,
-                              32 + 2 * p + jj, 40 + 2 * p + jj, 48 + 2 * p + jj, 56 + 2 * p + jj};
+            f32x4 v8[TN];
+            int q[TN];
+  #pragma unroll
+            for (int i = 0; i < TN; ++i) q[i] = 8 * i + 2 * p + jj;
             if (mode == 2) {
-              tail_fetch8(a, tt, w, lane, q, v8);
+              tail_fetch<TN>(a, tt, w, lane, q, v8);
             } else {
-              static_for<8>([&](auto ic) { v8[decltype(ic)::value] = acc[decltype(ic)::value][2 * p + jj]; });
+              static_for<TN>([&](auto ic) { v8[decltype(ic)::value] = acc[decltype(ic)::value][2 * p + jj]; });
               if (mode == 1) {
-                tail_store8(a, tt, tslice, w, lane, q, v8);
+                tail_store<TN>(a, tt, tslice, w, lane, q, v8);
                 return;
               }
             }
   #pragma unroll
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < TN; ++i) {
               const f32x4 v = v8[i];
               const int row = 16 * jj + r16, col = 16 * i + 4 * grp;
               const int ch = (col >> 3) ^ (row & 15);
@@ -657,7 +724,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
                   make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
             }
           });
-          if (mode != 1 && n < a.N) {
+          if (mode != 1 && cl < 2 * TN && n < a.N) {
   #pragma unroll
             for (int it = 0; it < 8; ++it) {
               const int row = 4 * it + rl, m = m0 + 128 * wm + 32 * p + row;
@@ -691,10 +758,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     tslice = ntk;
   }
   wait_vm<0>();   // the trailing re-stage DMA: nothing may land in LDS after the workgroup ends
-#undef GB_DMA
 }
-
-constexpr int LDS_TOTAL = LDS + 4 * 8192;   // staging buffers + the epilogue scratch (160 KB)
 
 static int num_cus() {
   static int n = 0;
@@ -709,13 +773,14 @@ static int num_cus() {
 // Workspace of the split tail: [err + pad 256 B][counters: TAIL_MAX_TILES x 4 waves x 2][slabs]
 constexpr int TAIL_MAX_TILES = 1024;
 constexpr size_t TAIL_HDR = 256 + (size_t)TAIL_MAX_TILES * 8 * 4;
-constexpr size_t TAIL_SLAB = (size_t)BM * BN * 4;   // one tile's fp32 accumulators (4 quadrants)
+constexpr size_t tail_slab(int tn) { return (size_t)BM * 32 * tn * 4; }   // one tile's fp32 accumulators
+constexpr size_t TAIL_SLAB = tail_slab(8);
 
 // The tail split for T tiles on G persistent workgroups, in k-tile times: the tail's last round
 // takes ceil(span / G) slices of ~nkt / s k-tiles; each slice publishes its fp32 tile and the last
 // arriving one reads all s back (XCD-local L2) before its epilogue.
 // Returns s (1: no split) and sets full / tail tiles.
-static int choose_tail(int T, int G, int nkt, size_t ws_bytes, int& full, int& tail) {
+static int choose_tail(int T, int G, int nkt, size_t ws_bytes, int& full, int& tail, size_t slab = TAIL_SLAB) {
   full = T;
   tail = 0;
   const int rem = T % G;
@@ -724,7 +789,7 @@ static int choose_tail(int T, int G, int nkt, size_t ws_bytes, int& full, int& t
   double best = (double)nkt;   // s = 1: one more round of whole tiles
   int bs = 1;
   for (int s = 2; s <= 8 && s <= trips; ++s) {
-    if (TAIL_HDR + (size_t)rem * s * TAIL_SLAB > ws_bytes || rem > TAIL_MAX_TILES) break;
+    if (TAIL_HDR + (size_t)rem * s * slab > ws_bytes || rem > TAIL_MAX_TILES) break;
     const int span = (rem + 7) / 8 * 8 * s;
     // + publishing the quadrant (~1.5 k-tile times) + the last slice reading s slabs (~1.8 each)
     const double t = (double)((span + G - 1) / G) * (double)((trips + s - 1) / s) * 2.0 + 1.5 + 1.8 * s;
@@ -740,18 +805,43 @@ static int choose_tail(int T, int G, int nkt, size_t ws_bytes, int& full, int& t
   return bs;
 }
 
-template <int EPI>
+// Tile width for the plain / residual epilogues: the 192-row W tile (TN 6) when the 256-wide tiles
+// leave a fractional last round that the 192-wide ones fill (QKV, N = 6144, at M = 4096: 384 tiles =
+// 1.5 rounds vs 512 = 2 rounds of 3/4 the work).  Cost in rounds of a 256 x 256 tile: whole rounds,
+// plus a last partial round at ~0.5 + 0.65 x its fill (the split tail: measured 0.62 of a round at a
+// 1/8 fill, 0.82 at 1/2), the 192 tile's round at 0.78 (3/4 of the MFMAs, a little less staging
+// reuse): QKV at M = 4096 runs 167 us on 192-wide tiles vs 204 on 256-wide, at M = 2944 152 vs 169
+// (profiles/r5/gemm_big_tn/).  KA_GB_TN=6|8 forces a width where it applies.
+static int choose_tn(int M, int N, int epi, int G) {
+  if ((epi != EPI_BF16 && epi != EPI_ADD) || N % 192 != 0) return 8;
+  static int force = -1;
+  if (force < 0) {
+    const char* e = getenv("KA_GB_TN");
+    force = e ? atoi(e) : 0;
+  }
+  if (force == 6 || force == 8) return force;
+  const int tm = (M + BM - 1) / BM;
+  auto cost = [&](int tiles, double unit) {
+    const int whole = tiles / G, rem = tiles % G;
+    const double part = rem ? std::min(1.0, 0.5 + 0.65 * rem / (double)G) : 0.0;
+    return (whole + part) * unit;
+  };
+  return cost(tm * (N / 192), 0.78) < cost(tm * ((N + 255) / 256), 1.0) ? 6 : 8;
+}
+
+template <int EPI, int TN>
 static int launch(const Args& a0, hipStream_t st, void* ws = nullptr, size_t ws_bytes = 0) {
+  using GE = Geo<TN>;
   static bool attr = false;
-  auto kern = &gemm256_kernel<EPI>;
+  auto kern = &gemm256_kernel<EPI, TN>;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_TOTAL);
+                              GE::LDS_TOTAL);
     attr = true;
   }
   Args a = a0;
   a.tiles_m = (a.M + BM - 1) / BM;
-  a.tiles_n = EPI == EPI_SWIGLU ? a.I / 128 : (a.N + BN - 1) / BN;
+  a.tiles_n = EPI == EPI_SWIGLU ? a.I / 128 : (a.N + GE::BN - 1) / GE::BN;
   const int split = (EPI == EPI_P32 || EPI == EPI_P16) ? a.split : 1;
   const int tiles = a.tiles_m * a.tiles_n;
   // one workgroup per CU (the LDS allows no more); a persistent grid is a multiple of 8 (XCDs)
@@ -762,7 +852,7 @@ static int launch(const Args& a0, hipStream_t st, void* ws = nullptr, size_t ws_
   a.tail_tiles = 0;
   a.span = 0;
   if (EPI == EPI_BF16 || EPI == EPI_SWIGLU || EPI == EPI_ADD) {
-    a.tail_s = choose_tail(tiles, cus, a.K / BK, ws ? ws_bytes : 0, a.full, a.tail_tiles);
+    a.tail_s = choose_tail(tiles, cus, a.K / BK, ws ? ws_bytes : 0, a.full, a.tail_tiles, tail_slab(TN));
     if (a.tail_s > 1) {
       char* base = static_cast<char*>(ws);
       a.err = reinterpret_cast<int*>(base);
@@ -773,8 +863,16 @@ static int launch(const Args& a0, hipStream_t st, void* ws = nullptr, size_t ws_
     }
   }
   const int grid = total <= cus ? total : cus;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS_TOTAL, st, a);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), GE::LDS_TOTAL, st, a);
   return (int)hipGetLastError();
+}
+
+template <int EPI>
+static int launch_tn(const Args& a, hipStream_t st, void* ws, size_t ws_bytes) {
+  if constexpr (EPI == EPI_BF16 || EPI == EPI_ADD) {
+    if (choose_tn(a.M, a.N, EPI, num_cus() & ~7) == 6) return launch<EPI, 6>(a, st, ws, ws_bytes);
+  }
+  return launch<EPI, 8>(a, st, ws, ws_bytes);
 }
 
 }  // namespace gb
@@ -791,13 +889,13 @@ extern "C" int ka_gemm_big(void* Y, const void* R, const void* X, const void* W,
   gb::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), static_cast<bf16_t*>(Y),
              static_cast<const bf16_t*>(R), M, N, K, ldx, ldy, 0, 0, gm > 0 ? gm : 8, N / 2};
   switch (epi) {
-    case gb::EPI_BF16: return gb::launch<gb::EPI_BF16>(a, stream, ws, ws_bytes);
+    case gb::EPI_BF16: return gb::launch_tn<gb::EPI_BF16>(a, stream, ws, ws_bytes);
     case gb::EPI_SWIGLU:
       if (N % 256 != 0) return (int)hipErrorInvalidValue;
-      return gb::launch<gb::EPI_SWIGLU>(a, stream, ws, ws_bytes);
+      return gb::launch<gb::EPI_SWIGLU, 8>(a, stream, ws, ws_bytes);
     case gb::EPI_ADD:
       if (R == nullptr) return (int)hipErrorInvalidValue;
-      return gb::launch<gb::EPI_ADD>(a, stream, ws, ws_bytes);
+      return gb::launch_tn<gb::EPI_ADD>(a, stream, ws, ws_bytes);
   }
   return (int)hipErrorInvalidValue;
 }
@@ -808,9 +906,14 @@ extern "C" size_t ka_gemm_big_ws_bytes() { return gb::TAIL_HDR + (size_t)512 * g
 
 // The split that ka_gemm_big would use (tests / diagnostics): tail_s, and the whole / tail tile counts.
 extern "C" int ka_gemm_big_plan(int M, int N, int epi, int K, size_t ws_bytes, int* full, int* tail) {
-  const int tm = (M + gb::BM - 1) / gb::BM, tn = epi == gb::EPI_SWIGLU ? N / 256 : (N + gb::BN - 1) / gb::BN;
-  return gb::choose_tail(tm * tn, gb::num_cus() & ~7, K / gb::BK, ws_bytes, *full, *tail);
+  const int G = gb::num_cus() & ~7;
+  const int TN = gb::choose_tn(M, N, epi, G);
+  const int tm = (M + gb::BM - 1) / gb::BM, tn = epi == gb::EPI_SWIGLU ? N / 256 : (N + 32 * TN - 1) / (32 * TN);
+  return gb::choose_tail(tm * tn, G, K / gb::BK, ws_bytes, *full, *tail, gb::tail_slab(TN));
 }
+
+// The tile width ka_gemm_big runs (M, N, epi) with: 8 (256 W rows) or 6 (192 W rows).
+extern "C" int ka_gemm_big_tn(int M, int N, int epi) { return gb::choose_tn(M, N, epi, gb::num_cus() & ~7); }
 
 // Error word of the split tail (a slice that waited ~0.1 s for the others); cleared by the read.
 extern "C" int ka_gemm_big_err(void* ws, hipStream_t stream) {
@@ -835,7 +938,7 @@ extern "C" int ka_gemm_big_splitk(void* P, const void* X, const void* W, int M, 
   a.split = split;
   a.kp = K / split;
   a.P = P;
-  return bf16_out ? gb::launch<gb::EPI_P16>(a, stream) : gb::launch<gb::EPI_P32>(a, stream);
+  return bf16_out ? gb::launch<gb::EPI_P16, 8>(a, stream) : gb::launch<gb::EPI_P32, 8>(a, stream);
 }
 
 extern "C" int ka_argmax_finish(int* out_idx, float* out_val, const float* part_val, const int* part_idx, int rows,
@@ -859,7 +962,7 @@ extern "C" int ka_gemm_big_argmax(int* out_idx, float* out_val, const void* X, c
   int* pi = reinterpret_cast<int*>(pv + (size_t)M * tiles_n);
   gb::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), nullptr, nullptr, M, N, K, ldx, 8, 0, 0,
              8, N / 2, mask_bits, mask_idx, mask_words, vocab_offset, pv, pi};
-  int rc = gb::launch<gb::EPI_ARGMAX>(a, stream);
+  int rc = gb::launch<gb::EPI_ARGMAX, 8>(a, stream);
   if (rc != 0) return rc;
   return ka_argmax_finish(out_idx, out_val, pv, pi, M, tiles_n, vocab_offset, stream);
 }

@@ -57,6 +57,7 @@ _SIGS = {
     "ka_gemm_big": [P, P, P, P, I, I, I, I, I, I, I, P, ctypes.c_size_t, P],
     "ka_gemm_big_ws_bytes": [],
     "ka_gemm_big_plan": [I, I, I, I, ctypes.c_size_t, P, P],
+    "ka_gemm_big_tn": [I, I, I],
     "ka_gemm_big_err": [P, P],
     "ka_gemm_big_argmax": [P, P, P, P, I, I, I, I, P, P, I, I, P, P],
     "ka_argmax_finish": [P, P, P, P, I, I, I, P],

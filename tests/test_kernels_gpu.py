@@ -799,7 +799,7 @@ def _gb_plan(M, N, K, epi):
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 6144, 4096), (2944, 6144, 4096), (777, 6144, 4096), (4096, 4096, 4096),
-                                   (2900, 4096, 14336), (513, 1024, 512)])
+                                   (2900, 4096, 14336), (513, 1024, 512), (4096, 1152, 4096), (1000, 1152, 2048)])
 def test_gemm_big_linear_split_tail_vs_fp32(M, N, K):
     """ops.linear_big (EPI_BF16) over shapes whose last round of tiles is split over K and over shapes
     that need no split; full matrices against the fp32 reference, the counters left at zero (the
@@ -816,12 +816,22 @@ def test_gemm_big_linear_split_tail_vs_fp32(M, N, K):
 
 
 def test_gemm_big_split_tail_plans():
-    """The shapes the bench's mixed steps produce get a split tail where the last round is short."""
-    s, full, tail = _gb_plan(4096, 6144, 4096, 0)      # QKV: 384 tiles = 256 + 128
-    assert s > 1 and full == 256 and tail == 128
+    """The shapes the bench's mixed steps produce get the tile width and split tail that fill the
+    last round: QKV at M = 4096 runs 192-wide tiles (512 = 2 whole rounds) instead of 384 256-wide
+    ones (1.5 rounds); at M = 2944 the 256-wide tiles with a split tail (288 = 256 + 32)."""
+    lib = _hip.require()
+    assert lib.ka_gemm_big_tn(4096, 6144, 0) == 6 and lib.ka_gemm_big_tn(4096, 6144, 4) == 6
+    assert _gb_plan(4096, 6144, 4096, 0)[0] == 1
+    assert lib.ka_gemm_big_tn(2944, 6144, 0) == 8
+    s, full, tail = _gb_plan(2944, 6144, 4096, 0)      # 12 x 24 = 288 = 256 + 32
+    assert s > 1 and full == 256 and tail == 32
+    assert lib.ka_gemm_big_tn(4096, 1152, 0) == 6      # 96 tiles of 192: the tail split on the 192 tile
+    assert _gb_plan(4096, 1152, 4096, 0)[0] > 1
     s, full, tail = _gb_plan(2944, 28672, 4096, 3)     # gate_up + SwiGLU: 12 x 112 = 1344 = 5 x 256 + 64
     assert s > 1 and full == 1280 and tail == 64
+    assert lib.ka_gemm_big_tn(2944, 28672, 3) == 8
     assert _gb_plan(4096, 4096, 4096, 0)[0] == 1       # O: exactly one round
+    assert lib.ka_gemm_big_tn(4096, 4096, 0) == 8      # (4096 is no multiple of 192)
 
 
 @pytest.mark.parametrize("M", [2944, 1100, 4096])

@@ -116,3 +116,36 @@ def test_lgkm_window_checker_flags_compiler_lgkm_ops():
     n, bad = lgkm_window_violations(broken, "gemm_kernel")
     assert n == 1 and len(bad) == 1 and "s_load_dwordx2" in bad[0][2]
     assert lgkm_window_violations(broken, "other_kernel") == (0, [])
+
+
+def test_plan_ladder_anomalies_flags_slower_smaller_bucket():
+    """a bucket whose planned GEMM time exceeds the next larger bucket's (whose
+    plan also runs the smaller M) is a tuning miss; ladder_anomalies finds it per (N, K, consumer)."""
+    from ai_agent_kubectl_amd.ops.autotune import ladder_anomalies
+    plans = {"4,28672,4096,plain": ["skinny", 1, 0, 47.8, 49.2], "8,28672,4096,plain": ["gm", 1, 5, 42.2, 50.0],
+             "16,28672,4096,plain": ["gm", 1, 5, 42.4, 49.6], "8,4096,4096,norm": ["gm", 8, 5, 13.8, 31.9],
+             "16,4096,4096,norm": ["gm", 8, 5, 13.5, 27.5]}
+    bad = ladder_anomalies(plans)
+    assert [b[0] for b in bad] == ["4,28672,4096,plain"]
+    assert ladder_anomalies(plans, tol=0.2) == []
+
+
+def test_mfma_span_valu_checker():
+    """build.py refuses a gemm_big build whose all-asm k-loop got a compiler VALU instruction between
+    asm MFMAs (a WAR hazard on operands hipcc cannot see being read)."""
+    from ai_agent_kubectl_amd.build import mfma_span_valu
+    ok = """_ZN2gb14gemm256_kernelILi3ELi8EEEvNS_4ArgsE:
+\tv_mov_b32 v1, 0
+\t;;#ASMSTART
+\tv_mfma_f32_16x16x32_bf16 a[0:3], v[56:59], v[4:7], a[0:3]
+\t;;#ASMEND
+\ts_and_b64 vcc, exec, s[4:5]
+\t;;#ASMSTART
+\tv_mfma_f32_16x16x32_bf16 a[4:7], v[56:59], v[8:11], a[4:7]
+\t;;#ASMEND
+\tv_add_u32 v2, v1, v3
+"""
+    assert mfma_span_valu(ok, "gemm256_kernel") == []
+    bad = ok.replace("\ts_and_b64", "\tv_cndmask_b32_e64 v56, 0, 1, s[58:59]\n\ts_and_b64")
+    got = mfma_span_valu(bad, "gemm256_kernel")
+    assert len(got) == 1 and "v_cndmask" in got[0][2]

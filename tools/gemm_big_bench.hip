@@ -3,10 +3,12 @@
 // in the same process, interleaved per round (cdna_hip_programming.md §5.4 rule 24).  No torch.
 //
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/gemm_big_bench.hip -lrocblas -o tools/gemm_big_bench
-//   tools/gemm_big_bench M,N,K,epi[,gm] ...     epi: 0 bf16, 3 SwiGLU (N = 2I), 4 residual add,
+//   tools/gemm_big_bench M,N,K,epi[,gm[,tn]] ... epi: 0 bf16, 3 SwiGLU (N = 2I), 4 residual add,
 //                                               5 fused LM head + masked argmax (rocBLAS: GEMM only),
 //                                               1 / 2 split-K fp32 / bf16 partials (the 5th field is the
-//                                               split; the consumer's reduction is not timed)
+//                                               split; the consumer's reduction is not timed);
+//                                               tn 6 / 8 (epi 0 / 4): also time that tile width
+//                                               (`alt`) beside the automatic choice
 //
 // Weights rotate over copies that exceed the 256 MB Infinity Cache unless GB_WARM=1.
 #include "../ai_agent_kubectl_amd/csrc/gemm_big.hip"
@@ -77,8 +79,8 @@ int main(int argc, char** argv) {
   int bad = 0;
 
   for (int ci = 1; ci < argc; ++ci) {
-    int M, N, K, epi, gm = 8;
-    if (sscanf(argv[ci], "%d,%d,%d,%d,%d", &M, &N, &K, &epi, &gm) < 4) {
+    int M, N, K, epi, gm = 8, tn_alt = 0;
+    if (sscanf(argv[ci], "%d,%d,%d,%d,%d,%d", &M, &N, &K, &epi, &gm, &tn_alt) < 4) {
       fprintf(stderr, "bad case %s\n", argv[ci]);
       return 2;
     }
@@ -128,6 +130,16 @@ int main(int argc, char** argv) {
       if (part) return ka_gemm_big_splitk(P, X, w, M, N, K, K, split, epi == 2, 8, st);
       return ka_gemm_big(Y, R, X, w, M, N, K, K, ldy, epi, gm, tail ? ws_tail : nullptr, tail ? ws_tail_bytes : 0, st);
     };
+    // the other tile width, launched directly (same split-tail workspace)
+    auto alt = [&](int r) {
+      const bf16_t* w = W + (size_t)(r % nrot) * N * K;
+      gb::Args a{X, w, Y, R, M, N, K, K, ldy, 0, 0, gm, N / 2};
+      void* wsp = tail ? ws_tail : nullptr;
+      const size_t wsb = tail ? ws_tail_bytes : 0;
+      if (epi == 4) return tn_alt == 6 ? gb::launch<gb::EPI_ADD, 6>(a, st, wsp, wsb) : gb::launch<gb::EPI_ADD, 8>(a, st, wsp, wsb);
+      return tn_alt == 6 ? gb::launch<gb::EPI_BF16, 6>(a, st, wsp, wsb) : gb::launch<gb::EPI_BF16, 8>(a, st, wsp, wsb);
+    };
+    const bool has_alt = (epi == 0 || epi == 4) && (tn_alt == 6 || tn_alt == 8) && N % (32 * tn_alt) == 0;
     auto blas = [&](int r) {
       const bf16_t* w = W + (size_t)(r % nrot) * N * K;
       const float alpha = 1.f, beta = 0.f;
@@ -226,13 +238,35 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       return ms * 1e3 / iters;
     };
-    std::vector<double> tm, tb;
+    // the alternative width's correctness on the same sampled rows (Y is overwritten by it)
+    double alt_err = 0;
+    if (has_alt) {
+      if (alt(0)) {
+        printf("%s: alt launch error\n", argv[ci]);
+        bad = 1;
+      }
+      CK(hipStreamSynchronize(st));
+      std::vector<uint16_t> g2((size_t)ldy), r2((size_t)N);
+      for (int s = 0; s < S; ++s) {
+        CK(hipMemcpy(g2.data(), Y + (size_t)rows[s] * ldy, ldy * 2, hipMemcpyDeviceToHost));
+        if (R) CK(hipMemcpy(r2.data(), R + (size_t)rows[s] * N, N * 2, hipMemcpyDeviceToHost));
+        for (int c = 0; c < ldy; ++c)
+          alt_err = std::max(alt_err, std::fabs(bf(g2[c]) - (ref[(size_t)s * N + c] + (R ? bf(r2[c]) : 0.0))));
+      }
+      if (!(alt_err <= 0.02 * std::max(1.0, mr))) {
+        printf("%s: alt tn=%d MISMATCH %g\n", argv[ci], tn_alt, alt_err);
+        bad = 1;
+      }
+    }
+    std::vector<double> tm, tb, ta;
     for (int r = 0; r < rounds; ++r) {
       tm.push_back(time(mine));
+      if (has_alt) ta.push_back(time(alt));
       tb.push_back(time(blas));
     }
     std::sort(tm.begin(), tm.end());
     std::sort(tb.begin(), tb.end());
+    std::sort(ta.begin(), ta.end());
     const double fl = 2.0 * M * N * K;
     int pf = 0, pt = 0;
     const int ps = (epi == 0 || epi == 3 || epi == 4) && tail ? ka_gemm_big_plan(M, N, epi, K, ws_tail_bytes, &pf, &pt) : 1;
@@ -242,7 +276,8 @@ int main(int argc, char** argv) {
       printf("%s: split-tail error word set\n", argv[ci]);
       bad = 1;
     }
-    printf("tail s=%d (%d whole + %d split tiles) ", ps, pf, pt);
+    printf("tn=%d tail s=%d (%d whole + %d split tiles) ", ka_gemm_big_tn(M, N, epi), ps, pf, pt);
+    if (has_alt) printf("[alt tn=%d %8.2f us %7.1f TF/s ratio %.3f] ", tn_alt, ta[0], 2.0 * M * N * K / (ta[0] * 1e-6) / 1e12, tb[0] / ta[0]);
     printf("M=%5d N=%6d K=%5d epi=%d gm=%d : gemm_big %8.2f us %7.1f TF/s | rocBLAS %8.2f us %7.1f TF/s | "
            "ratio %.3f | maxerr %.3g (ref max %.3g)%s\n",
            M, N, K, epi, gm, tm[0], fl / (tm[0] * 1e-6) / 1e12, tb[0], fl / (tb[0] * 1e-6) / 1e12, tb[0] / tm[0], err,
