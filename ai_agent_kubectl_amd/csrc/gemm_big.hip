@@ -203,11 +203,28 @@ KA_DEV void st_slab(float* p, const f32x4 (&v)[N], const int (&q)[N]) {
 #pragma unroll
   for (int e = 0; e < N; ++e) *reinterpret_cast<f32x4*>(p + q[e] * 256) = v[e];
 #else
-  // each store carries its own wait states (VMEM store data vs a following VALU write of its VGPRs)
-#pragma unroll
-  for (int e = 0; e < N; ++e)
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p + q[e] * 256), "v"(v[e]) : "memory");
-  asm volatile("s_nop 4" ::: "memory");
+  // all stores in ONE asm statement followed by the wait states of the VMEM-store-data / VALU-write
+  // hazard (hipcc cannot see the stores: with per-store statements and 2 wait states each, the
+  // register allocator's next VALU write corrupted store data in a few lanes)
+  static_assert(N == 6 || N == 8, "slab width");
+  if constexpr (N == 8)
+    asm volatile(
+        "global_store_dwordx4 %0, %8, off sc1\n\tglobal_store_dwordx4 %1, %9, off sc1\n\t"
+        "global_store_dwordx4 %2, %10, off sc1\n\tglobal_store_dwordx4 %3, %11, off sc1\n\t"
+        "global_store_dwordx4 %4, %12, off sc1\n\tglobal_store_dwordx4 %5, %13, off sc1\n\t"
+        "global_store_dwordx4 %6, %14, off sc1\n\tglobal_store_dwordx4 %7, %15, off sc1\n\ts_nop 4" ::"v"(p + q[0] * 256),
+        "v"(p + q[1] * 256), "v"(p + q[2] * 256), "v"(p + q[3] * 256), "v"(p + q[4] * 256), "v"(p + q[5] * 256),
+        "v"(p + q[6] * 256), "v"(p + q[7] * 256), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]),
+        "v"(v[6]), "v"(v[7])
+        : "memory");
+  else
+    asm volatile(
+        "global_store_dwordx4 %0, %6, off sc1\n\tglobal_store_dwordx4 %1, %7, off sc1\n\t"
+        "global_store_dwordx4 %2, %8, off sc1\n\tglobal_store_dwordx4 %3, %9, off sc1\n\t"
+        "global_store_dwordx4 %4, %10, off sc1\n\tglobal_store_dwordx4 %5, %11, off sc1\n\ts_nop 4" ::"v"(p + q[0] * 256),
+        "v"(p + q[1] * 256), "v"(p + q[2] * 256), "v"(p + q[3] * 256), "v"(p + q[4] * 256), "v"(p + q[5] * 256),
+        "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5])
+        : "memory");
 #endif
 }
 template <int N>
@@ -421,6 +438,12 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   constexpr int GPS = NQ / 4;        // groups per set
   constexpr int NG = 2 * GPS;        // groups per k-tile (32 at TN 8)
   constexpr int RW = NG - 4;         // F0(t + 1) read window: the k-tile's last 4 groups
+#ifndef KA_GB_B1
+#define KA_GB_B1 4
+#endif
+  constexpr int B1 = KA_GB_B1;       // barrier #1's group: 4 = right after the F1 read window; 5 / 6
+                                     // give the window's last reads 4 / 8 more MFMAs before lgkmcnt(0)
+  static_assert(B1 >= 4 && B1 <= 6, "barrier #1 group");
   static_assert(NRD <= 16, "a read window holds 16 reads");
   // read S of a fragment set in window order 1 (A0 B0 A1 B1 ..., the B's past A(TN-1) last):
   auto rd1 = [&](auto sc, bf16x8* FA, bf16x8* FB, uint32_t ba, uint32_t bb) {
@@ -486,14 +509,15 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
           else mfma_acc(acc[q >> 3][q & 7], fa1[q >> 3], fb1[q & 7]);
         });
       }
-      if constexpr (g == 4) {
+      if constexpr (g == 4 && B1 > 4) wait_lgkm<15>();   // row 2 (A2) of F0: all but 15 reads done
+      if constexpr (g == B1) {
         wait_lgkm0();
         block_sync();
       }
-      if constexpr (g >= 4 && g < RW) {   // the DMA pieces whose slot falls in this group
+      if constexpr (g >= B1 && g < RW) {   // the DMA pieces whose slot falls in this group
         static_for<PIECES>([&](auto pc) {
           constexpr int pp = decltype(pc)::value;
-          if constexpr (4 + (pp * (RW - 4)) / PIECES == g) dma(pc, bufc, T);
+          if constexpr (B1 + (pp * (RW - B1)) / PIECES == g) dma(pc, bufc, T);
         });
       }
       if constexpr (g == RW) {

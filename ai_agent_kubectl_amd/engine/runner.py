@@ -262,6 +262,49 @@ class ModelRunner:
         return report
 
     @torch.inference_mode()
+    def tune_prefill(self) -> dict:
+        """Prefill / mixed-step projections (ops.PREFILL_GEMM auto): csrc/gemm_big.hip against hipBLASLt
+        per (N, K) of the model's QKV / O / down at the row-count buckets of ops.PREFILL_BUCKETS, on
+        the model's own weights rotated over layers (the persisted decision in the plan file, section
+        prefill, unless KA_GEMM_PLAN=tune / write).  Fills ops.PREFILL_PLAN: gemm_big where it is within
+        KA_PREFILL_MARGIN (default 0.02) of hipBLASLt."""
+        m = self.model
+        ops.PREFILL_PLAN.clear()
+        if self.device.type != "cuda" or ops.PREFILL_GEMM != "auto":
+            return {}
+        from ..ops.autotune import _time, load_section, plan_mode, save_section
+        margin = float(os.environ.get("KA_PREFILL_MARGIN", "0.02"))
+        groups = {}
+        for L in m.layers:
+            for k in ("wqkv", "wo", "w2"):
+                w = L.get(k)
+                if w is not None and w.dim() == 2:
+                    groups.setdefault(tuple(w.shape), []).append(w)
+        mode, path = plan_mode()
+        saved = load_section(path, "prefill") if mode == "file" else {}
+        report = {}
+        for (N, K), ws in groups.items():
+            ws = ws[:4]
+            for M in ops.PREFILL_BUCKETS:
+                key = f"{M},{N},{K}"
+                if key in saved:
+                    big, t_big, t_blas = saved[key]
+                else:
+                    x = torch.randn(M, K, device=self.device, dtype=ws[0].dtype)
+                    if not ops.big_gemm_ok(x, ws[0]):
+                        break
+                    t_blas = _time(lambda w: torch.nn.functional.linear(x, w), ws, reps=6)
+                    t_big = _time(lambda w: ops.linear_big(x, w), ws, reps=6)
+                    big = t_big <= t_blas * (1.0 + margin)
+                    del x
+                ops.PREFILL_PLAN[(M, N, K)] = bool(big)
+                report[key] = [bool(big), round(float(t_big), 1), round(float(t_blas), 1)]
+        if mode == "write":
+            save_section(path, "prefill", report)
+        logger.info("prefill gemm plan: %s", report)
+        return report
+
+    @torch.inference_mode()
     def tune_swiglu(self) -> dict:
         """Per decode bucket: gate_up with the ring kernel's SwiGLU epilogue (ops.linear_gm_swiglu,
         each configuration) against the GEMM plan's gate_up + SiLU·mul, on the model's own w13
@@ -273,6 +316,7 @@ class ModelRunner:
         ws = [L["w13"] for L in m.layers if L.get("w13") is not None and L["w13"].dim() == 2][:8]
         if not ws:
             return {}
+        w2s = [L["w2"] for L in m.layers if L.get("w2") is not None and L["w2"].dim() == 2][:8]
         from ..ops.autotune import _time, load_section, plan_mode, save_section
         report = {}
         mode, path = plan_mode()   # persisted like the GEMM plan (section decode_swiglu)
@@ -287,13 +331,23 @@ class ModelRunner:
                 best = (int(cfg), t_fu if int(cfg) else t_un)
                 fused = (int(cfg), t_fu)
             else:
-                t_un = _time(lambda w: ops.silu_mul(ops.linear(x, w, defer_reduce=True)), ws)
+                small = M <= ops.GEMV_SWIGLU_MAX_M and len(w2s) == len(ws)
+                if small:
+                    # the unfused path at these rows computes SiLU·mul inside the down GEMV's staging
+                    # (ops.swiglu_linear): compare gate_up + down, both ways (indices pair w13 / w2)
+                    pair = {id(a): b for a, b in zip(ws, w2s)}
+                    t_un = _time(lambda w: ops.swiglu_linear(ops.linear(x, w, defer_reduce=True), pair[id(w)]), ws)
+                else:
+                    t_un = _time(lambda w: ops.silu_mul(ops.linear(x, w, defer_reduce=True)), ws)
                 fused = (0, float("inf"))
                 cands = list(ops.DECODE_SWIGLU_CFGS)
                 if M >= ops.BIG_PLAN_MIN_M and ops.swiglu_gemm_ok(x, ws[0]):
                     cands.append(ops.DECODE_SWIGLU_BIG)   # csrc/gemm_big.hip's SwiGLU epilogue
                 for cfg in cands:
-                    t = _time(lambda w: ops.linear_gm_swiglu(x, w, cfg), ws)
+                    if small:
+                        t = _time(lambda w: ops.linear(ops.linear_gm_swiglu(x, w, cfg), pair[id(w)]), ws)
+                    else:
+                        t = _time(lambda w: ops.linear_gm_swiglu(x, w, cfg), ws)
                     if t < fused[1]:
                         fused = (cfg, t)
                 # the unfused path's gate_up is a hipBLASLt plan: the hand-written fused kernel is
@@ -342,6 +396,7 @@ class ModelRunner:
             self.gemm_plan = self.autotune()
             self.lm_head_plan = self.tune_lm_head()
             self.swiglu_plan = self.tune_swiglu()
+            self.prefill_plan = self.tune_prefill()
         self.h_np[:] = 0
         o = self._off
         for name in ("slots",):

@@ -483,14 +483,27 @@ def linear(x: torch.Tensor, w: torch.Tensor, split: int = 0, defer_reduce: bool 
 # M).  KA_PREFILL_SWIGLU=0 restores hipBLASLt + silu_mul.
 PREFILL_SWIGLU = os.environ.get("KA_PREFILL_SWIGLU", "1") == "1"
 PREFILL_SWIGLU_MIN_M = int(os.environ.get("KA_PREFILL_SWIGLU_MIN_M", "513"))
-# Prefill / mixed-step QKV, O and down projections (M > TILE_MAX_M): KA_PREFILL_GEMM=big runs them on
-# csrc/gemm_big.hip with the split tail; the default stays hipBLASLt (F.linear), which measured
-# faster on these plain shapes (gemm_big 0.79-0.92x rocBLAS at M = 2944-4096: profiles/r4/gemm_big_tail/).
-PREFILL_GEMM = os.environ.get("KA_PREFILL_GEMM", "blas")
+# Prefill / mixed-step QKV, O and down projections (M > TILE_MAX_M): KA_PREFILL_GEMM=big runs them all
+# on csrc/gemm_big.hip (split tail, 192-wide tiles where they fill the rounds), blas all on hipBLASLt
+# (F.linear), auto (default) per shape and row-count bucket from PREFILL_PLAN: ModelRunner.tune_prefill
+# times both on the model's own weights at engine start (persisted in the plan file, section prefill)
+# and keeps gemm_big where it is within PREFILL_MARGIN of hipBLASLt.
+PREFILL_GEMM = os.environ.get("KA_PREFILL_GEMM", "auto")
+PREFILL_PLAN: dict = {}          # (M bucket, N, K) -> True: gemm_big
+PREFILL_BUCKETS = (1024, 2048, 3072, 4096, 6144, 8192)
+
+
+def prefill_bucket(M: int) -> int:
+    i = bisect.bisect_left(PREFILL_BUCKETS, M)
+    return PREFILL_BUCKETS[min(i, len(PREFILL_BUCKETS) - 1)]
 
 
 def use_big_gemm(x: torch.Tensor, w: torch.Tensor) -> bool:
-    return PREFILL_GEMM == "big" and not _ref(x) and x.shape[0] > TILE_MAX_M and big_gemm_ok(x, w)
+    if PREFILL_GEMM == "blas" or _ref(x) or x.shape[0] <= TILE_MAX_M or not big_gemm_ok(x, w):
+        return False
+    if PREFILL_GEMM == "big":
+        return True
+    return PREFILL_PLAN.get((prefill_bucket(x.shape[0]), w.shape[0], w.shape[1]), False)
 GB_EPI_SWIGLU = 3
 
 
@@ -586,9 +599,12 @@ DECODE_SWIGLU_BIG = 100
 
 
 def decode_swiglu_ok(x: torch.Tensor, w13: torch.Tensor) -> bool:
+    """Rows the ring kernel's SwiGLU epilogue takes: any M up to TILE_MAX_M (rows past M re-read row
+    M - 1); below 8 rows ModelRunner.tune_swiglu weighs it against the GEMV path with the activation in
+    the down projection's staging (ops.swiglu_linear), down projection included."""
     M, K = x.shape
     return (x.is_contiguous() and w13.is_contiguous() and w13.shape[1] == K and K % 64 == 0
-            and w13.shape[0] % 32 == 0 and 8 <= M <= TILE_MAX_M)
+            and w13.shape[0] % 32 == 0 and 1 <= M <= TILE_MAX_M)
 
 
 def decode_swiglu_cfg(x: torch.Tensor, w13: torch.Tensor) -> int:

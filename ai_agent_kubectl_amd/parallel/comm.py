@@ -158,6 +158,50 @@ class TorchComm:
         self.dist.barrier(group=self.group)
 
 
+class VirtualRankComm:
+    """One rank of a `world`-way TP / EP group run ALONE on one GPU, the collectives left out: every
+    collective returns its input (all_gather replicates it `world` times, all_to_all returns what this
+    rank would keep).  For timing one rank's share of a TP = 8 step (scripts/bench_virtual_rank.py)
+    and for tuning the per-rank shard shapes' kernel plans on a single GPU — never for numerics (the
+    partial sums are not reduced).  `allreduce_calls` / `allreduce_bytes` count what a real group
+    would have exchanged."""
+
+    device_ordered = True
+    custom_ar = None
+
+    def __init__(self, world: int, rank: int = 0):
+        self.world_size, self.rank = world, rank
+        self.allreduce_calls = 0
+        self.allreduce_bytes = 0
+        self.timer = None
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        self.allreduce_calls += 1
+        self.allreduce_bytes += t.numel() * t.element_size()
+        return t
+
+    def all_reduce_rmsnorm(self, t: torch.Tensor, w: torch.Tensor, eps: float, residual=None) -> torch.Tensor:
+        from .. import ops
+        self.all_reduce(t)
+        return ops.rmsnorm(t, w, eps, residual=residual)
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        return t.unsqueeze(0).expand((self.world_size,) + tuple(t.shape)).contiguous()
+
+    def all_to_all_single(self, t: torch.Tensor, out_splits=None, in_splits=None) -> torch.Tensor:
+        rows = sum(out_splits) if out_splits is not None else t.shape[0]
+        out = torch.zeros((rows,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        n = min(rows, t.shape[0])
+        out[:n].copy_(t[:n])
+        return out
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        return t
+
+    def barrier(self) -> None:
+        return None
+
+
 def make_comm(group=None):
     import torch.distributed as dist
 

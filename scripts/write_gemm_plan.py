@@ -42,6 +42,7 @@ for model in sys.argv[1:] or ["llama3-8b"]:
     # the engine-start decisions persisted next to the plan (sections lm_head / decode_swiglu)
     print("lm_head:", eng.runner.tune_lm_head(), flush=True)
     print("decode_swiglu:", eng.runner.tune_swiglu(), flush=True)
+    print("prefill:", eng.runner.tune_prefill(), flush=True)
     if COPY_TO:
         os.makedirs(COPY_TO, exist_ok=True)
         shutil.copy(DEFAULT_PLAN_FILE, COPY_TO)

@@ -402,7 +402,8 @@ def test_gemv_rows_swiglu_down_vs_fp32(M):
 
 
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5, 12])
-@pytest.mark.parametrize("M,I", [(32, 14336), (100, 1792), (256, 14336), (300, 1792), (512, 1792)])
+@pytest.mark.parametrize("M,I", [(1, 1792), (4, 14336), (32, 14336), (100, 1792), (256, 14336), (300, 1792),
+                                 (512, 1792)])
 def test_decode_swiglu_gemm_vs_fp32(M, I, cfg):
     """Decode gate_up with the gemm_mfma SwiGLU epilogue over the model's [gate; up] weight (the
     weight DMAs gather 16-row gate / up chunks) against fp32 silu(x gate^T) * (x up^T)."""
@@ -818,13 +819,14 @@ def test_gemm_big_linear_split_tail_vs_fp32(M, N, K):
 def test_gemm_big_split_tail_plans():
     """The shapes the bench's mixed steps produce get the tile width and split tail that fill the
     last round: QKV at M = 4096 runs 192-wide tiles (512 = 2 whole rounds) instead of 384 256-wide
-    ones (1.5 rounds); at M = 2944 the 256-wide tiles with a split tail (288 = 256 + 32)."""
+    ones (1.5 rounds); at M = 2944 192-wide tiles with a split tail (384 = 256 + 128; measured 152 us
+    against 169 for 288 256-wide tiles with theirs, profiles/r5/gemm_big_tn/)."""
     lib = _hip.require()
     assert lib.ka_gemm_big_tn(4096, 6144, 0) == 6 and lib.ka_gemm_big_tn(4096, 6144, 4) == 6
     assert _gb_plan(4096, 6144, 4096, 0)[0] == 1
-    assert lib.ka_gemm_big_tn(2944, 6144, 0) == 8
-    s, full, tail = _gb_plan(2944, 6144, 4096, 0)      # 12 x 24 = 288 = 256 + 32
-    assert s > 1 and full == 256 and tail == 32
+    assert lib.ka_gemm_big_tn(2944, 6144, 0) == 6
+    s, full, tail = _gb_plan(2944, 6144, 4096, 0)      # 12 x 32 = 384 = 256 + 128
+    assert s > 1 and full == 256 and tail == 128
     assert lib.ka_gemm_big_tn(4096, 1152, 0) == 6      # 96 tiles of 192: the tail split on the 192 tile
     assert _gb_plan(4096, 1152, 4096, 0)[0] > 1
     s, full, tail = _gb_plan(2944, 28672, 4096, 3)     # gate_up + SwiGLU: 12 x 112 = 1344 = 5 x 256 + 64

@@ -27,7 +27,7 @@ def test_linear_gm_swiglu_cpu_is_reference():
         ops.DECODE_SWIGLU_CFG.clear()
         ops.DECODE_SWIGLU_CFG.update(saved)
     assert ops.decode_swiglu_ok(x, w13)
-    assert ops.decode_swiglu_ok(x[:16], w13) and not ops.decode_swiglu_ok(x[:4], w13)   # M < 8: GEMV paths
+    assert ops.decode_swiglu_ok(x[:16], w13) and ops.decode_swiglu_ok(x[:4], w13)   # M < 8: tune_swiglu decides
     assert not ops.decode_swiglu_ok(x, torch.zeros(2 * 56, 256, dtype=torch.bfloat16))   # I % 16
 
 
@@ -149,3 +149,19 @@ def test_mfma_span_valu_checker():
     bad = ok.replace("\ts_and_b64", "\tv_cndmask_b32_e64 v56, 0, 1, s[58:59]\n\ts_and_b64")
     got = mfma_span_valu(bad, "gemm256_kernel")
     assert len(got) == 1 and "v_cndmask" in got[0][2]
+
+
+def test_prefill_gemm_plan_buckets():
+    """ops.PREFILL_GEMM auto: a prefill row count takes the decision of the smallest timed bucket at or
+    above it (the largest one beyond); CPU tensors always run the fp32 reference."""
+    import torch
+    from ai_agent_kubectl_amd import ops
+    assert ops.prefill_bucket(600) == 1024 and ops.prefill_bucket(4080) == 4096
+    assert ops.prefill_bucket(4097) == 6144 and ops.prefill_bucket(20000) == 8192
+    x = torch.zeros(4096, 256, dtype=torch.bfloat16)
+    w = torch.zeros(512, 256, dtype=torch.bfloat16)
+    ops.PREFILL_PLAN[(4096, 512, 256)] = True
+    try:
+        assert not ops.use_big_gemm(x, w)   # CPU: reference path
+    finally:
+        ops.PREFILL_PLAN.pop((4096, 512, 256))
