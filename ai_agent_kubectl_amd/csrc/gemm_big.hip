@@ -171,6 +171,25 @@ KA_DEV void block_sync() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// KA_GB_SCHED 2 helpers: the operation (0 .. nops-1) issued at offset k of a span-slot segment when
+// nops operations are spread evenly over it (-1: none); and the o-th operation of a sequence that
+// interleaves na operations of kind A (returned as 0 .. na-1) with nb of kind B (100 + 0 .. nb-1),
+// one B after every (period - 1) A's, either kind alone once the other has run out.
+constexpr int spread_op(int k, int span, int nops) {
+  for (int o = 0; o < nops; ++o)
+    if ((o * span) / nops == k) return o;
+  return -1;
+}
+constexpr int pick_op(int o, int na, int nb, int period) {
+  int ia = 0, ib = 0;
+  for (int i = 0;; ++i) {
+    const bool b = ib < nb && (i % period == period - 1 || ia >= na);
+    if (i == o) return b ? 100 + ib : ia;
+    if (b) ++ib;
+    else ++ia;
+  }
+}
+
 // dispatch index -> logical index, XCD-contiguous (bijective over the grid: consecutive logical
 // indices run on one XCD and share its L2)
 KA_DEV int xcd_logical(int bid, int nwg) {
@@ -229,7 +248,7 @@ KA_DEV void st_slab(float* p, const f32x4 (&v)[N], const int (&q)[N]) {
 }
 template <int N>
 KA_DEV void ld_slab(f32x4 (&t)[N], const float* p, const int (&q)[N]) {
-#if KA_GB_TAIL_MODE == 2
+#if KA_GB_TAIL_MODE >= 2   // 2: sc1 loads without fences; 3: sc1 loads after the fences of mode 1
 #pragma unroll
   for (int e = 0; e < N; ++e)
     asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(t[e]) : "v"(p + q[e] * 256) : "memory");
@@ -531,6 +550,64 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     });
     // (no lgkmcnt wait here: the next call waits per fragment; the tile's last call waits below)
   };
+  // KA_GB_SCHED 2: one k-tile as five MFMA segments split by four barriers, the fragment reads and the
+  // LDS-DMA pieces handed off per OPERAND (the order of hipBLASLt's gfx950 MT256x256x64 DirectToLds
+  // kernel, read from its disassembly): the W (A) half of the staging buffer is refilled as soon as
+  // every wave has read its F1 A fragments, the X (B) half after their B fragments, and each vmcnt
+  // wait retires only the operand half the next reads need:
+  //   S1  F1(t) A reads (one per 2 MFMAs)           | lgkmcnt(0), 1 MFMA, barrier (A of BUF free)
+  //   S2  F1(t) B reads + the TN A pieces of T      | lgkmcnt(0), 1 MFMA, barrier (B of BUF free)
+  //   S3  B pieces 0-3 of T                          | vmcnt(8 + TN + 4): the A pieces of t + 1 landed,
+  //                                                     1 MFMA, barrier
+  //   S4  F0(t + 1) A reads + B pieces 4-7 of T      | vmcnt(PIECES): the B pieces of t + 1 landed,
+  //                                                     1 MFMA, barrier
+  //   S5  F0(t + 1) B reads
+  // and the next call's first MFMA waits for everything but its own first read (lgkmcnt(1)).
+  constexpr int NS = 2 * NQ;                       // MFMA slots per k-tile
+  constexpr int E1 = NS * 20 / 128, E2 = NS * 51 / 128, E3 = NS * 68 / 128, E4 = NS * 105 / 128;
+  auto iter2 = [&](auto bufc, int T) {
+    constexpr int BUF = decltype(bufc)::value;
+    const uint32_t bA1 = BUF ? bA11 : bA01, bB1 = BUF ? bB11 : bB01;   // F1(t) <- buffer BUF
+    const uint32_t bA0 = BUF ? bA00 : bA10, bB0 = BUF ? bB00 : bB10;   // F0(t + 1) <- buffer BUF ^ 1
+    static_for<NS>([&](auto sc) {
+      constexpr int sl = decltype(sc)::value;
+      // ---- the slot's read / DMA, before its MFMA (each segment's operations spread evenly) ----
+      if constexpr (sl < E1) {
+        constexpr int o = spread_op(sl, E1, TN);
+        if constexpr (o >= 0) ds_read16<o * 2048>(fa1[o], bA1);
+      } else if constexpr (sl > E1 && sl < E2) {   // B reads / A pieces, alternating
+        constexpr int o = spread_op(sl - E1 - 1, E2 - E1 - 1, 8 + TN);
+        if constexpr (o >= 0) {
+          constexpr int c = pick_op(o, 8, TN, 2);
+          if constexpr (c < 100) ds_read16<c * 2048>(fb1[c], bB1);
+          else dma(std::integral_constant<int, c - 100>{}, bufc, T);
+        }
+      } else if constexpr (sl > E2 && sl < E3) {   // B pieces 0-3
+        constexpr int o = spread_op(sl - E2 - 1, E3 - E2 - 1, 4);
+        if constexpr (o >= 0) dma(std::integral_constant<int, TN + o>{}, bufc, T);
+      } else if constexpr (sl > E3 && sl < E4) {   // A reads of F0(t + 1) / B pieces 4-7, R R D ...
+        constexpr int o = spread_op(sl - E3 - 1, E4 - E3 - 1, TN + 4);
+        if constexpr (o >= 0) {
+          constexpr int c = pick_op(o, TN, 4, 3);
+          if constexpr (c < 100) ds_read16<c * 2048>(fa0[c], bA0);
+          else dma(std::integral_constant<int, TN + 4 + (c - 100)>{}, bufc, T);
+        }
+      } else if constexpr (sl > E4) {              // B reads of F0(t + 1)
+        constexpr int o = spread_op(sl - E4 - 1, NS - E4 - 1, 8);
+        if constexpr (o >= 0) ds_read16<o * 2048>(fb0[o], bB0);
+      }
+      // ---- waits before the slot's MFMA ----
+      if constexpr (sl == 0) wait_lgkm<1>();                      // F0(t): all but this call's first read
+      if constexpr (sl == E1 || sl == E2) wait_lgkm0();
+      if constexpr (sl == E3) wait_vm<8 + TN + 4>();
+      if constexpr (sl == E4) wait_vm<PIECES>();
+      // ---- the MFMA ----
+      if constexpr (sl < NQ) mfma_acc(acc[sl >> 3][sl & 7], fa0[sl >> 3], fb0[sl & 7]);
+      else mfma_acc(acc[(sl - NQ) >> 3][(sl - NQ) & 7], fa1[(sl - NQ) >> 3], fb1[(sl - NQ) & 7]);
+      // ---- a barrier after each segment's extra MFMA ----
+      if constexpr (sl == E1 || sl == E2 || sl == E3 || sl == E4) block_sync();
+    });
+  };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
 
@@ -570,8 +647,16 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     for (int t = 0; t < nk; t += 2) {
       const bool last = t + 2 >= nk;
       if (last) set_offsets(ntm, ntn, nkt0);
+#ifndef KA_GB_SCHED
+#define KA_GB_SCHED 1
+#endif
+#if KA_GB_SCHED == 2
+      iter2(I0{}, last ? 0 : t + 2);
+      iter2(I1{}, last ? 1 : t + 3);
+#else
       iter(I0{}, last ? 0 : t + 2);
       iter(I1{}, last ? 1 : t + 3);
+#endif
       // the MFMA wait states inside the loop, before its exit: hipcc does not know the asm MFMAs'
       // latency and may copy accumulators (v_accvgpr_mov) on the exit edge, which would read
       // results still in flight (seen: the argmax epilogue's accumulators shuffled before a drain

@@ -156,7 +156,10 @@ int main(int argc, char** argv) {
       continue;
     }
     CK(hipStreamSynchronize(st));
-    const int S = std::min(M, 32);
+    // GB_FULL=1: every row checked (and the correctness run repeated GB_FULL_REPS times): the split
+    // tail's hand-off is validated on the whole matrix, not on 32 sampled rows
+    const int full_check = getenv("GB_FULL") ? atoi(getenv("GB_FULL")) : 0;
+    const int S = full_check ? M : std::min(M, 32);
     std::vector<int> rows(S);
     for (int s = 0; s < S; ++s) rows[s] = (int)((long)s * (M - 1) / std::max(1, S - 1));
     int* drows;
@@ -206,6 +209,13 @@ int main(int argc, char** argv) {
         }
       }
     }
+    const int creps = full_check ? (getenv("GB_FULL_REPS") ? atoi(getenv("GB_FULL_REPS")) : 4) : 1;
+    for (int cr = 0; cr < creps; ++cr) {
+    if (cr > 0) {
+      if (mine(0)) bad = 1;
+      CK(hipStreamSynchronize(st));
+    }
+    double rep_err = 0;
     for (int s = 0; s < S && epi != 5 && !part; ++s) {
       CK(hipMemcpy(got.data(), Y + (size_t)rows[s] * ldy, ldy * 2, hipMemcpyDeviceToHost));
       if (R) CK(hipMemcpy(rr.data(), R + (size_t)rows[s] * N, N * 2, hipMemcpyDeviceToHost));
@@ -218,8 +228,11 @@ int main(int argc, char** argv) {
           r = ref[(size_t)s * N + c] + (R ? bf(rr[c]) : 0.0);
         }
         err = std::max(err, std::fabs(bf(got[c]) - r));
+        rep_err = std::max(rep_err, std::fabs(bf(got[c]) - r));
         mr = std::max(mr, std::fabs(r));
       }
+    }
+    if (full_check) printf("  full check rep %d: max err %.4g\n", cr, rep_err);
     }
     CK(hipFree(drows));
     CK(hipFree(dref));
