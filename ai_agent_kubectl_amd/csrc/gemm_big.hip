@@ -208,13 +208,17 @@ KA_DEV void tile_of(int L, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
 
 // 16-B store / load of the tail hand-off.  KA_GB_TAIL_MODE 0: plain accesses ordered by agent-scope
 // release / acquire fences; 1: sc1 (write-through) asm stores + the same fences; 2: sc1 asm stores and
-// loads, no fence (MI355X_MICROARCH.md hand-off table, row 1).  hipcc does not pad the
+// loads, no fence (MI355X_MICROARCH.md hand-off table, row 1: one signalling lane per storing wave,
+// per-wave counter, the consumer told by the value its own add returned, all stores and loads sc1
+// 16 B, hipMalloc memory); 3: the sc1 loads of 2 after the fences of 1.  hipcc does not pad the
 // VMEM-store-data / VALU-write hazard around asm it cannot see, so the asm stores carry their own
 // wait states (without them a few lanes' data were corrupted: profiles/r4/gemm_big_tail/).
+// Round 5 full-matrix repeats (profiles/r5/gemm_big_tail_modes/): modes 0 and 1 (plain loads after
+// the acquire fence) read stale slab data in some launches (max err 0.17-0.23 at 2944 x 6144); modes
+// 2 and 3 were exact in every launch, and the fences of mode 3 add 24 us to the whole GEMM (167 vs
+// 143 us; rocBLAS 141).
 #ifndef KA_GB_TAIL_MODE
-#define KA_GB_TAIL_MODE 1   // sc1 stores + agent-scope release / acquire fences: correct by the memory model
-                            // (mode 2, fence-free, measured ~1 % faster on tail shapes but rests on
-                            // observed hardware behaviour: opt-in)
+#define KA_GB_TAIL_MODE 2
 #endif
 template <int N>
 KA_DEV void st_slab(float* p, const f32x4 (&v)[N], const int (&q)[N]) {

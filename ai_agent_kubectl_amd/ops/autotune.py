@@ -93,6 +93,7 @@ def save_plan(path: str, report: Dict, ctx_of: Dict[Tuple[int, int], str]) -> No
     for (M, N, K), r in report.items():
         plans[plan_key(M, N, K, ctx_of[(N, K)])] = [r["choice"], r["split"], r["cfg"], r["us"], r["blas_us"],
                                                    r.get("hand_us", r["us"])]
+    repair_ladder(plans)
     data["device"] = torch.cuda.get_device_name() if torch.cuda.is_available() else "cpu"
     data["note"] = ("ops/autotune.py: [choice, split, cfg, us, hipBLASLt us, best hand-written us] "
                     "per M,N,K,consumer")
@@ -253,6 +254,28 @@ def ladder_anomalies(plans: Dict[str, list], tol: float = 0.03) -> List[Tuple[st
             if us > us2 * (1.0 + tol):
                 out.append((key, key2, us, us2))
     return out
+
+
+def repair_ladder(plans: Dict[str, list], tol: float = 0.03) -> List[str]:
+    """Apply the ladder rule across runs: an entry tuned in an earlier run (another bucket subset, a
+    PLAN_BUCKETS re-tune) whose time exceeds the next larger bucket's takes that bucket's plan (its
+    kernels run the smaller M, in at most the larger bucket's time, which is recorded as an upper
+    bound).  Largest bucket first, so a repaired plan can repair the next smaller one.  Returns the
+    keys changed."""
+    by_shape: Dict[Tuple[int, int, str], List[Tuple[int, str]]] = {}
+    for key in plans:
+        m, n, k, ctx = key.split(",", 3)
+        by_shape.setdefault((int(n), int(k), ctx), []).append((int(m), key))
+    changed = []
+    for (n, k, ctx), rows in by_shape.items():
+        rows.sort(reverse=True)
+        for (m2, key2), (m, key) in zip(rows, rows[1:]):
+            big, small = plans[key2], plans[key]
+            plan = (big[0], big[1], big[2])
+            if float(small[3]) > float(big[3]) * (1.0 + tol) and big[0] != "blas" and _plan_runs(plan, m, k):
+                plans[key] = [big[0], big[1], big[2], float(big[3])] + list(small[4:])
+                changed.append(key)
+    return changed
 
 
 def _tune(groups, Ms, norm_fed=frozenset(), bf16_partials: bool = True, consumers=None) -> Dict:

@@ -130,6 +130,21 @@ def test_plan_ladder_anomalies_flags_slower_smaller_bucket():
     assert ladder_anomalies(plans, tol=0.2) == []
 
 
+def test_repair_ladder_takes_the_larger_buckets_plan():
+    """Entries left by an earlier run with another bucket subset: a bucket slower than the next larger
+    one takes its plan (chained from the largest down); a hipBLASLt plan is never propagated."""
+    from ai_agent_kubectl_amd.ops.autotune import ladder_anomalies, repair_ladder
+    plans = {"32,32000,4096,plain": ["gm", 2, 4, 45.8, 52.6, 45.8], "48,32000,4096,plain": ["gm", 1, 4, 44.9, 53.0, 44.9],
+             "64,32000,4096,plain": ["gm", 1, 5, 40.0, 55.7, 40.0], "1,4096,4096,norm": ["skinny", 4, 0, 9.0, 20.0, 9.0],
+             "2,4096,4096,norm": ["rows", 1, 2, 7.0, 20.0, 7.0], "16,4096,4096,norm": ["rows", 1, 1, 7.5, 20.0, 7.5],
+             "32,4096,4096,norm": ["blas", 0, 0, 5.0, 5.0, 9.0]}
+    changed = repair_ladder(plans)
+    assert sorted(changed) == ["1,4096,4096,norm", "32,32000,4096,plain", "48,32000,4096,plain"]
+    assert plans["32,32000,4096,plain"][:4] == ["gm", 1, 5, 40.0] and plans["32,32000,4096,plain"][4] == 52.6
+    assert plans["2,4096,4096,norm"][0] == "rows" and plans["1,4096,4096,norm"][:3] == ["rows", 1, 2]
+    assert [a[0] for a in ladder_anomalies(plans)] == ["16,4096,4096,norm"]   # blas above: left alone
+
+
 def test_mfma_span_valu_checker():
     """build.py refuses a gemm_big build whose all-asm k-loop got a compiler VALU instruction between
     asm MFMAs (a WAR hazard on operands hipcc cannot see being read)."""
