@@ -34,6 +34,13 @@ namespace gm {
 
 constexpr int BK = 64;
 
+// diagnostic builds only (tools/gemm_bench, wrong results on purpose): leave out the weight DMA (1),
+// the activation DMA (2), the MFMAs (4) or the fragment reads (8), to find what bounds a shape
+#ifndef KA_GM_ABL
+#define KA_GM_ABL 0
+#endif
+
+
 enum Epi : int { EPI_BF16 = 0, EPI_P32 = 1, EPI_P16 = 2, EPI_SWIGLU = 3 };
 
 template <int BN_, int BM_, int WN_, int WM_, int STAGES_, int BK_ = 64>
@@ -69,6 +76,18 @@ KA_DEV void glds16(const void* g, void* l) {
 template <int N>
 KA_DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most `ahead` stages of PER DMAs each are in flight (ahead <= N, static counts)
+template <int N, int PER>
+KA_DEV void wait_ahead(int ahead) {
+  static_assert(N * PER <= 63, "vmcnt immediate");
+  if constexpr (N == 0) {
+    wait_vm<0>();
+  } else {
+    if (ahead >= N) wait_vm<N * PER>();
+    else wait_ahead<N - 1, PER>(ahead);
+  }
 }
 
 KA_DEV void block_sync() {
@@ -222,15 +241,19 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
     char* sa = lds_c + stage * C::STAGE_BYTES;
     char* sb = sa + C::A_BYTES;
     const uint32_t kofs = (uint32_t)t * C::RB;
-    if (wnt) {
+    if (!(KA_GM_ABL & 1)) {
+      if (wnt) {
 #pragma unroll
-      for (int j = 0; j < C::GA; ++j) glds16<2>(Wb + offA[j] + kofs, sa + (j * C::NW + wave) * 1024);
-    } else {
+        for (int j = 0; j < C::GA; ++j) glds16<2>(Wb + offA[j] + kofs, sa + (j * C::NW + wave) * 1024);
+      } else {
 #pragma unroll
-      for (int j = 0; j < C::GA; ++j) glds16(Wb + offA[j] + kofs, sa + (j * C::NW + wave) * 1024);
+        for (int j = 0; j < C::GA; ++j) glds16(Wb + offA[j] + kofs, sa + (j * C::NW + wave) * 1024);
+      }
     }
+    if (!(KA_GM_ABL & 2)) {
 #pragma unroll
-    for (int j = 0; j < C::GB; ++j) glds16(Xb + offB[j] + kofs, sb + (j * C::NW + wave) * 1024);
+      for (int j = 0; j < C::GB; ++j) glds16(Xb + offB[j] + kofs, sb + (j * C::NW + wave) * 1024);
+    }
   };
 
   f32x4 acc[C::TN][C::TM];
@@ -264,6 +287,7 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   static_assert(C::TN + C::TM <= 15, "lgkmcnt immediate");
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) u32x4*)lds;
   auto read_frags_asm = [&](int stage) {
+    if (KA_GM_ABL & 8) return;
     const uint32_t base = lds0 + (uint32_t)(stage * C::STAGE_BYTES);
 #pragma unroll
     for (int kk = 0; kk < C::KT / 32; ++kk) {
@@ -301,6 +325,7 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
     }
   };
   auto mma_half = [&](int kk) {
+    if (KA_GM_ABL & 4) return;
 #pragma unroll
     for (int i = 0; i < C::TN; ++i)
 #pragma unroll
@@ -324,19 +349,7 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
     // stage t landed (this wave's part): later stages may stay in flight
     // outstanding after this point: stages t+1 .. min(nk-1, t+STAGES-2) of this wave
     if constexpr (C::STAGES >= 3) {
-      const int ahead = min(nk - 1 - t, C::STAGES - 2);
-      if constexpr (C::STAGES >= 5) {
-        if (ahead >= 3) wait_vm<3 * PER>();
-        else if (ahead == 2) wait_vm<2 * PER>();
-        else if (ahead == 1) wait_vm<PER>();
-        else wait_vm<0>();
-      } else if constexpr (C::STAGES == 4) {
-        if (ahead >= 2) wait_vm<2 * PER>();
-        else if (ahead == 1) wait_vm<PER>();
-        else wait_vm<0>();
-      } else {
-        if (ahead >= 1) wait_vm<PER>(); else wait_vm<0>();
-      }
+      wait_ahead<C::STAGES - 2, PER>(min(nk - 1 - t, C::STAGES - 2));
     } else {
       wait_vm<0>();
     }
@@ -684,7 +697,18 @@ static int launch_grouped(const Args& a0, int split, hipStream_t st) {
   X(3, 256, 128, 4, 2, 3, 64)    \
   X(4, 128, 128, 2, 2, 3, 64)    \
   X(5, 128, 64, 2, 1, 3, 64)     \
-  X(12, 128, 128, 2, 2, 4, 64)
+  X(12, 128, 128, 2, 2, 4, 64)    \
+  GM_EXTRA_CFGS(X)
+// measurement-only configurations (tools/gemm_bench -DKA_GM_EXTRA): 32-deep k-steps, deeper rings
+#ifdef KA_GM_EXTRA
+#define GM_EXTRA_CFGS(X)          \
+  X(20, 128, 256, 2, 4, 6, 32)    \
+  X(21, 128, 128, 2, 2, 8, 32)    \
+  X(22, 256, 128, 4, 2, 6, 32)    \
+  X(23, 128, 256, 2, 4, 5, 32)
+#else
+#define GM_EXTRA_CFGS(X)
+#endif
 
 template <class C, int EPI>
 static int launch(const Args& a0, int split, hipStream_t st) {
