@@ -104,6 +104,13 @@ struct Args {
   float* slab;   // [tail tile][tail_s slices][4 waves][64 accumulators][64 lanes] f32x4
   int* cnt;      // [tail tile][4 waves][arrivals, spare]
   int* err;      // reserved error word (0)
+  // grouped (MoE experts, gemm256_kernel<.., GR>): X holds the routed rows sorted by expert
+  // (ka_moe_sort), chunk_tab[tiles_m][4] = (expert, first sorted row, rows, 0) of the 256-row chunks
+  // (rows 0: an unused entry); W is [groups][N][K]; EPI_BF16 stores sorted row r at output row
+  // out_rows[r] (the slot order moe_combine reads), EPI_SWIGLU at sorted row r (the next GEMM's X)
+  const int* chunk_tab;
+  const int* out_rows;
+  int groups;
 };
 
 // Every instruction of the k-loop is an asm statement, so the program order written below IS the
@@ -325,11 +332,12 @@ KA_DEV void tail_fetch(const Args& a, int tt, int w, int lane, const int (&q)[N]
   }
 }
 
-template <int EPI, int TN>
+template <int EPI, int TN, bool GR = false>
 __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   using GE = Geo<TN>;
   constexpr int BNT = GE::BN, TILE_A = GE::TILE_A, STAGE = GE::STAGE, PIECES = GE::PIECES;
   static_assert(TN == 8 || ((EPI == EPI_BF16 || EPI == EPI_ADD) && TN == 6), "TN 6: plain / residual epilogues");
+  static_assert(!GR || (TN == 8 && (EPI == EPI_BF16 || EPI == EPI_SWIGLU)), "grouped: bf16 / SwiGLU, 256 x 256");
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
   char* const L = reinterpret_cast<char*>(lds);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -341,14 +349,20 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   // grid of `total` workgroups would be: an id keeps its XCD (b mod 8), so the tiles running together
   // on one XCD are still neighbours.  The next tile's first two k-tiles are staged during the last
   // two k-steps of the current one, so the epilogue overlaps their landing.
-  constexpr bool TAILOK = EPI == EPI_BF16 || EPI == EPI_SWIGLU || EPI == EPI_ADD;
+  constexpr bool TAILOK = (EPI == EPI_BF16 || EPI == EPI_SWIGLU || EPI == EPI_ADD) && !GR;
   const int total = SPLIT ? a.tiles_m * a.tiles_n * a.split : (TAILOK ? a.full + a.span : a.tiles_m * a.tiles_n);
   const int nkt = a.K / BK;
   // unit v -> tile (tm, tn), k-tiles [kt0, kt0 + nk), tail tile index tt (-1: a whole tile / split-K slice);
   // false for the holes of the last tail group (tail_tiles not a multiple of 8)
-  auto decode = [&](int v, int& tm, int& tn, int& kt0, int& nk, int& tt, int& tk) -> bool {
+  // GR: (ge, gr0, gnr) = the chunk's expert, first sorted row and row count (scalar loads of the
+  // chunk table, here at a tile boundary, outside every counted wait window); false for an unused entry
+  auto decode = [&](int v, int& tm, int& tn, int& kt0, int& nk, int& tt, int& tk, int& ge, int& gr0,
+                    int& gnr) -> bool {
     tt = -1;
     tk = 0;
+    ge = 0;
+    gr0 = 0;
+    gnr = 0;
     if constexpr (SPLIT) {   // the split slices of a tile on one XCD
       int lg = xcd_logical(v, total);
       const int ks = lg % a.split;
@@ -362,6 +376,13 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
       tile_of(xcd_logical(v, TAILOK ? a.full : total), a.tiles_m, a.tiles_n, a.gm, tm, tn);
       kt0 = 0;
       nk = nkt;
+      if constexpr (GR) {
+        const int* c = a.chunk_tab + 4 * tm;
+        ge = c[0];
+        gr0 = c[1];
+        gnr = c[2];
+        return gnr > 0;
+      }
       return true;
     }
     // tail: groups of 8 tiles x tail_s slices; slice k of tile 8 g + l is unit 8 (g tail_s + k) + l, so
@@ -379,8 +400,8 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     return true;
   };
   const int G = (int)gridDim.x;
-  int vb = blockIdx.x, tm = 0, tn = 0, kt0 = 0, nku = nkt, tt = -1, tslice = 0;
-  while (vb < total && !decode(vb, tm, tn, kt0, nku, tt, tslice)) vb += G;
+  int vb = blockIdx.x, tm = 0, tn = 0, kt0 = 0, nku = nkt, tt = -1, tslice = 0, ge = 0, gr0 = 0, gnr = 0;
+  while (vb < total && !decode(vb, tm, tn, kt0, nku, tt, tslice, ge, gr0, gnr)) vb += G;
   if (vb >= total) return;   // only holes for this workgroup: nothing staged, nothing to wait for
 
   // the descriptors start BIAS bytes before the operands, so the per-lane offsets (pre-biased by
@@ -388,7 +409,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   constexpr uint32_t BIAS = 3072;
   const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<char*>(reinterpret_cast<const char*>(a.W)) - BIAS, (short)0,
-      (int)((uint32_t)a.N * (uint32_t)a.K * 2u + BIAS), 0x00020000);
+      (int)((uint32_t)(GR ? a.groups : 1) * (uint32_t)a.N * (uint32_t)a.K * 2u + BIAS), 0x00020000);
   const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<char*>(reinterpret_cast<const char*>(a.X)) - BIAS, (short)0,
       (int)((uint32_t)a.M * (uint32_t)a.ldx * 2u + BIAS), 0x00020000);
@@ -400,7 +421,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   // 4 per M0 value)
   const int r8 = lane >> 3, slot = lane & 7;
   uint32_t offA[TN], offB[8];
-  auto set_offsets = [&](int tm_, int tn_, int kt0_) {
+  auto set_offsets = [&](int tm_, int tn_, int kt0_, int ge_, int gr0_, int gnr_) {
     const int m0_ = tm_ * BM;
     const uint32_t kb = (uint32_t)kt0_ * (uint32_t)(BK * 2);   // byte offset of the unit's k range
 #pragma unroll
@@ -415,17 +436,19 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
       } else {
         wrow = min(tn_ * BNT + row, a.N - 1);
       }
+      if constexpr (GR) wrow += ge_ * a.N;   // expert ge_'s weights
       offA[j] = ((uint32_t)wrow * (uint32_t)a.K + ch) * 2u + kb + BIAS - (uint32_t)(j & 3) * 1024u;
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int row = 64 * w + 8 * j + r8;
       const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
-      offB[j] = ((uint32_t)min(m0_ + row, a.M - 1) * (uint32_t)a.ldx + ch) * 2u + kb + BIAS -
-                (uint32_t)(j & 3) * 1024u;
+      // GR: the chunk's rows, rows past its count re-read its last row (their results are not stored)
+      const int xr = GR ? gr0_ + min(row, gnr_ - 1) : min(m0_ + row, a.M - 1);
+      offB[j] = ((uint32_t)xr * (uint32_t)a.ldx + ch) * 2u + kb + BIAS - (uint32_t)(j & 3) * 1024u;
     }
   };
-  set_offsets(tm, tn, kt0);
+  set_offsets(tm, tn, kt0, ge, gr0, gnr);
   // DMA piece s (< PIECES) of a k-tile: W (s < TN) or X (s >= TN); M0 is set once per group of up to 4
   // pieces and restored after the group's last
   const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)w * (uint32_t)(TN * 1024));
@@ -622,16 +645,21 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   char* const Q = L + 2 * STAGE + w * 8192;
 
   for (;;) {
-    int nvb = vb + G, ntm = tm, ntn = tn, nkt0 = kt0, nnk = nku, ntt = tt, ntk = tslice;
-    while (nvb < total && !decode(nvb, ntm, ntn, nkt0, nnk, ntt, ntk)) nvb += G;
+    int nvb = vb + G, ntm = tm, ntn = tn, nkt0 = kt0, nnk = nku, ntt = tt, ntk = tslice, nge = ge, ngr0 = gr0,
+        ngnr = gnr;
+    while (nvb < total && !decode(nvb, ntm, ntn, nkt0, nnk, ntt, ntk, nge, ngr0, ngnr)) nvb += G;
     const bool more = nvb < total;
     if (!more) {   // without a next unit: re-stage this one (never consumed)
       ntm = tm;
       ntn = tn;
       nkt0 = kt0;
+      nge = ge;
+      ngr0 = gr0;
+      ngnr = gnr;
     }
     const int nk = nku;
-    const int m0 = tm * BM;
+    const int m0 = GR ? gr0 : tm * BM;
+    const int mend = GR ? gr0 + gnr : a.M;   // rows past it are not stored
     // k-tile 0 landed: the PIECES youngest vector-memory operations are k-tile 1's DMA or the previous
     // tile's epilogue stores, everything older (k-tile 0) is done.  (The previous tile's last call
     // already read these fragments; reading them again here keeps F0 dead across the epilogue,
@@ -650,7 +678,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     // tile's, whose last DMA was the previous trip's).
     for (int t = 0; t < nk; t += 2) {
       const bool last = t + 2 >= nk;
-      if (last) set_offsets(ntm, ntn, nkt0);
+      if (last) set_offsets(ntm, ntn, nkt0, nge, ngr0, ngnr);
 #ifndef KA_GB_SCHED
 #define KA_GB_SCHED 1
 #endif
@@ -803,7 +831,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
           for (int it = 0; it < 8; ++it) {
             const int row = 8 * it + rl, m = m0 + 128 * wm + 64 * p + row;
             const u32x4 v = *reinterpret_cast<const u32x4*>(Q + row * 128 + ((cl ^ (row & 7)) * 16));
-            if (m < a.M) *reinterpret_cast<u32x4*>(a.Y + (size_t)m * a.ldy + ocol) = v;
+            if (m < mend) *reinterpret_cast<u32x4*>(a.Y + (size_t)m * a.ldy + ocol) = v;
           }
         });
       } else {
@@ -842,8 +870,8 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
             for (int it = 0; it < 8; ++it) {
               const int row = 4 * it + rl, m = m0 + 128 * wm + 32 * p + row;
               u32x4 v = *reinterpret_cast<const u32x4*>(Q + row * 256 + ((cl ^ (row & 15)) * 16));
-              if (m >= a.M) continue;
-              bf16_t* y = a.Y + (size_t)m * a.ldy + n;
+              if (m >= mend) continue;
+              bf16_t* y = a.Y + (size_t)(GR ? a.out_rows[m] : m) * a.ldy + n;
               if constexpr (EPI == EPI_ADD) {
                 const u32x4 rr = *reinterpret_cast<const u32x4*>(a.R + (size_t)m * a.ldy + n);
   #pragma unroll
@@ -869,6 +897,9 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     nku = nnk;
     tt = ntt;
     tslice = ntk;
+    ge = nge;
+    gr0 = ngr0;
+    gnr = ngnr;
   }
   wait_vm<0>();   // the trailing re-stage DMA: nothing may land in LDS after the workgroup ends
 }
@@ -980,6 +1011,29 @@ static int launch(const Args& a0, hipStream_t st, void* ws = nullptr, size_t ws_
   return (int)hipGetLastError();
 }
 
+// grouped: tiles_m = the chunk table's entries (an upper bound of the chunks the routing produces:
+// unused entries are skipped), no split tail
+template <int EPI>
+static int launch_grouped(const Args& a0, hipStream_t st) {
+  static bool attr = false;
+  auto kern = &gemm256_kernel<EPI, 8, true>;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Geo<8>::LDS_TOTAL);
+    attr = true;
+  }
+  Args a = a0;
+  a.tiles_n = EPI == EPI_SWIGLU ? a.I / 128 : a.N / BN;
+  a.full = a.tiles_m * a.tiles_n;
+  a.tail_s = 1;
+  a.tail_tiles = 0;
+  a.span = 0;
+  const int cus = num_cus() & ~7;
+  const int total = a.full;
+  hipLaunchKernelGGL(kern, dim3(total <= cus ? total : cus), dim3(NT), Geo<8>::LDS_TOTAL, st, a);
+  return (int)hipGetLastError();
+}
+
 template <int EPI>
 static int launch_tn(const Args& a, hipStream_t st, void* ws, size_t ws_bytes) {
   if constexpr (EPI == EPI_BF16 || EPI == EPI_ADD) {
@@ -1009,6 +1063,30 @@ extern "C" int ka_gemm_big(void* Y, const void* R, const void* X, const void* W,
     case gb::EPI_ADD:
       if (R == nullptr) return (int)hipErrorInvalidValue;
       return gb::launch_tn<gb::EPI_ADD>(a, stream, ws, ws_bytes);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+// Grouped (MoE) GEMM over expert-sorted rows (ka_moe_sort): for every chunk c < chunks of the table
+// (expert e, first row r0, n rows), Y rows of X[r0 .. r0 + n) W[e]^T.  W [groups][N][K] (SwiGLU:
+// [groups][2I][K], gate rows then up rows per expert).  epi 0: Y [*, ldy] row out_rows[r] for sorted
+// row r; epi 3: Y [M, ldy] sorted row r = silu(x gate^T) * (x up^T).  X [M, ldx] (M = the sorted rows'
+// capacity).  Requirements: K % 128 == 0, N % 256 == 0, groups * N * K * 2 < 2^31 - 4 KB.
+extern "C" int ka_gemm_big_grouped(void* Y, const void* X, const void* W, const int* chunk_tab, int chunks,
+                                   const int* out_rows, int M, int N, int K, int ldx, int ldy, int groups, int epi,
+                                   hipStream_t stream) {
+  if (M <= 0 || N <= 0 || chunks <= 0) return 0;
+  if (K % 128 != 0 || N % 256 != 0 || ldx % 8 != 0 || ldy % 8 != 0 || groups < 1 || chunk_tab == nullptr ||
+      (double)groups * N * K * 2.0 >= 2147483648.0 - 4096.0 || (epi == gb::EPI_BF16 && out_rows == nullptr))
+    return (int)hipErrorInvalidValue;
+  gb::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), static_cast<bf16_t*>(Y), nullptr, M, N, K,
+             ldx, ldy, chunks, 0, 8, N / 2};
+  a.chunk_tab = chunk_tab;
+  a.out_rows = out_rows;
+  a.groups = groups;
+  switch (epi) {
+    case gb::EPI_BF16: return gb::launch_grouped<gb::EPI_BF16>(a, stream);
+    case gb::EPI_SWIGLU: return gb::launch_grouped<gb::EPI_SWIGLU>(a, stream);
   }
   return (int)hipErrorInvalidValue;
 }

@@ -183,6 +183,52 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(bf16_t* __restrict__ o
   }
 }
 
+// Routed rows sorted by local expert for the grouped prefill GEMM (csrc/gemm_big.hip, grouped mode).
+// Block (e, y): expert e's rows [64 y, 64 y + 64) of its list go to sorted rows start_e + i (start_e =
+// the row counts of the experts before e): xs[start_e + i] = x[lists[e][i] / src_div], slot[start_e + i]
+// = lists[e][i].  Block (e, 0) also writes e's chunk-table entries (e, first sorted row, rows, 0), one
+// per 256 rows, after the chunks of the experts before it; the last expert's block zeroes the entries
+// past the last chunk up to max_chunks.
+__global__ __launch_bounds__(256) void moe_sort_kernel(bf16_t* __restrict__ xs, int* __restrict__ slot,
+                                                       int* __restrict__ tab, const bf16_t* __restrict__ x,
+                                                       const int* __restrict__ counts, const int* __restrict__ lists,
+                                                       int lstride, int src_div, int H, int el, int max_chunks) {
+  const int e = blockIdx.x, y = blockIdx.y;
+  int start = 0, cbase = 0;
+  for (int i = 0; i < e; ++i) {   // el <= 64: every block sums the counts before its expert itself
+    const int c = counts[i];
+    start += c;
+    cbase += (c + 255) >> 8;
+  }
+  const int cnt = counts[e];
+  if (y == 0) {
+    const int nch = (cnt + 255) >> 8;
+    for (int c = threadIdx.x; c < nch; c += blockDim.x) {
+      int* t = tab + 4 * (cbase + c);
+      t[0] = e;
+      t[1] = start + 256 * c;
+      t[2] = min(256, cnt - 256 * c);
+      t[3] = 0;
+    }
+    if (e == el - 1)
+      for (int c = cbase + nch + threadIdx.x; c < max_chunks; c += blockDim.x) {
+        int* t = tab + 4 * c;
+        t[0] = t[1] = t[2] = t[3] = 0;
+      }
+  }
+  const int r0 = 64 * y;
+  if (r0 >= cnt) return;
+  const int nr = min(64, cnt - r0);
+  const int* li = lists + (size_t)e * lstride + r0;
+  const int vec = H >> 3;   // 16-B pieces per row
+  for (int p = threadIdx.x; p < nr * vec; p += blockDim.x) {
+    const int i = p / vec, c = p - i * vec;
+    reinterpret_cast<uint4*>(xs + (size_t)(start + r0 + i) * H)[c] =
+        reinterpret_cast<const uint4*>(x + (size_t)(li[i] / src_div) * H)[c];
+  }
+  for (int i = threadIdx.x; i < nr; i += blockDim.x) slot[start + r0 + i] = li[i];
+}
+
 template <int MT>
 static void launch_gemm(bf16_t* Y, float* P, const bf16_t* A, const bf16_t* W, const int* counts, const int* lists,
                         int stride, int el, int N, int K, int src_div, int max_rows, int split, int kps,
@@ -231,5 +277,17 @@ extern "C" int ka_moe_combine(void* out, const void* Y, const float* P, int spli
   if (H % 8 != 0 || split < 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, s, static_cast<bf16_t*>(out),
                      static_cast<const bf16_t*>(Y), P, split, topk_w, topk_ids, k, H, e0, el);
+  KA_CHECK_LAUNCH();
+}
+
+// Expert-sorted rows and the chunk table of the grouped gemm_big prefill path (moe_sort_kernel):
+// xs [rows, H], slot [rows], tab [max_chunks][4]; rows = T * k (the lists' stride and capacity),
+// max_chunks >= ceil(rows / 256) + el.
+extern "C" int ka_moe_sort(void* xs, int* slot, int* tab, const void* x, const int* counts, const int* lists, int rows,
+                           int src_div, int H, int el, int max_chunks, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (el > 64 || H % 8 != 0 || max_chunks < (rows + 255) / 256 + el) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(moe_sort_kernel, dim3(el, (rows + 63) / 64), dim3(256), 0, s, static_cast<bf16_t*>(xs), slot, tab,
+                     static_cast<const bf16_t*>(x), counts, lists, rows, src_div, H, el, max_chunks);
   KA_CHECK_LAUNCH();
 }

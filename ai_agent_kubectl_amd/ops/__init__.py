@@ -842,11 +842,25 @@ def moe_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: to
     return out
 
 
+# MoE prefill expert GEMMs (KA_MOE_PREFILL): "big" = expert-sorted rows through csrc/gemm_big.hip's
+# grouped mode (256 x 256 tiles, SwiGLU epilogue), "gm" = the grouped gemm_mfma ring kernel over
+# gathered rows (MOE_GROUPED_CFG)
+MOE_PREFILL = os.environ.get("KA_MOE_PREFILL", "big")
+
+
+def moe_big_ok(H: int, I: int, El: int) -> bool:
+    """Shapes the grouped gemm_big path takes (ka_gemm_big_grouped / ka_moe_sort requirements)."""
+    return (H % 256 == 0 and I % 128 == 0 and El <= 64
+            and El * 2 * I * H * 2 < 2 ** 31 - 4096 and El * H * I * 2 < 2 ** 31 - 4096)
+
+
 def moe_experts_grouped(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
                         topk_ids: torch.Tensor, e0: int) -> torch.Tensor:
     """Prefill-sized MoE block, device-resident end to end (no host sync): routing lists
-    (moe_align) -> grouped MFMA gate_up GEMM over the gathered token rows -> SiLU·mul -> grouped
-    down GEMM -> weighted combine.  Same contract as `moe_experts`."""
+    (moe_align), then either (KA_MOE_PREFILL=big, the default) the routed rows sorted by expert
+    (moe_sort) -> grouped gemm_big gate_up with the SwiGLU epilogue -> grouped gemm_big down
+    scattering each row back to its slot, or (gm) the grouped ring-kernel gate_up over gathered token
+    rows -> SiLU·mul -> grouped down; then the weighted combine.  Same contract as `moe_experts`."""
     lib = require()
     T, H = x.shape
     k = topk_ids.shape[1]
@@ -856,6 +870,24 @@ def moe_experts_grouped(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, to
     counts = torch.empty(El, dtype=torch.int32, device=x.device)
     lists = torch.empty((El, R), dtype=torch.int32, device=x.device)
     check(lib.ka_moe_align(_p(counts), _p(lists), _p(topk_ids), R, e0, El, st), "moe_align")
+    I = two_i // 2
+    if MOE_PREFILL == "big" and moe_big_ok(H, I, El) and x.is_contiguous():
+        chunks = (R + 255) // 256 + El
+        xs = torch.empty((R, H), dtype=x.dtype, device=x.device)
+        slot = torch.empty(R, dtype=torch.int32, device=x.device)
+        tab = torch.empty(chunks * 4, dtype=torch.int32, device=x.device)
+        check(lib.ka_moe_sort(_p(xs), _p(slot), _p(tab), _p(x), _p(counts), _p(lists), R, k, H, El, chunks, st),
+              "moe_sort")
+        act = torch.empty((R, I), dtype=x.dtype, device=x.device)   # expert-sorted rows
+        check(lib.ka_gemm_big_grouped(_p(act), _p(xs), _p(w13), _p(tab), chunks, None, R, two_i, H, H, I, El,
+                                      3, st), "gemm_big_grouped(w13)")
+        y2 = torch.empty((R, H), dtype=x.dtype, device=x.device)    # slot rows (others never read)
+        check(lib.ka_gemm_big_grouped(_p(y2), _p(act), _p(w2), _p(tab), chunks, _p(slot), R, H, I, I, H, El,
+                                      0, st), "gemm_big_grouped(w2)")
+        out = torch.empty((T, H), dtype=x.dtype, device=x.device)
+        check(lib.ka_moe_combine(_p(out), _p(y2), None, 1, _p(topk_w), _p(topk_ids), T, k, H, e0, El, st),
+              "moe_combine")
+        return out
     y1 = linear_grouped(x, w13, counts, lists, R, src_div=k)          # slot rows of local experts
     y2 = linear_grouped(silu_mul(y1), w2, counts, lists, R)          # other rows: never read
     out = torch.empty((T, H), dtype=x.dtype, device=x.device)

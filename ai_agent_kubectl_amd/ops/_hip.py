@@ -58,6 +58,7 @@ _SIGS = {
     "ka_gemm_big_ws_bytes": [],
     "ka_gemm_big_plan": [I, I, I, I, ctypes.c_size_t, P, P],
     "ka_gemm_big_tn": [I, I, I],
+    "ka_gemm_big_grouped": [P, P, P, P, I, P, I, I, I, I, I, I, I, P],
     "ka_gemm_big_err": [P, P],
     "ka_gemm_big_argmax": [P, P, P, P, I, I, I, I, P, P, I, I, P, P],
     "ka_argmax_finish": [P, P, P, P, I, I, I, P],
@@ -71,6 +72,7 @@ _SIGS = {
     "ka_moe_align": [P, P, P, I, I, I, P],
     "ka_moe_gemm": [P, P, P, P, P, I, I, I, I, I, I, I, P, P],
     "ka_moe_combine": [P, P, P, I, P, P, I, I, I, I, I, P],
+    "ka_moe_sort": [P, P, P, P, P, P, I, I, I, I, I, P],
     "ka_allreduce_oneshot": [P, P, P, P, P, P, P, I, I, I, I, I, P],
     "ka_allgather_oneshot": [P, P, P, P, P, P, P, I, I, I, I, I, P],
     "ka_allreduce_rmsnorm": [P, P, P, P, F, P, P, P, P, P, I, I, I, I, I, I, P],

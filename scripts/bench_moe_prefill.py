@@ -1,5 +1,6 @@
-"""Mixtral-8x7B MoE block at prefill token counts: the device-routed grouped MFMA path
-(ops.moe_experts_grouped, per grouped-GEMM configuration) against the host-synced sorted path
+"""Mixtral-8x7B MoE block at prefill token counts: the device-routed grouped paths
+(ops.moe_experts_grouped: expert-sorted rows on gemm_big's grouped mode, and the grouped ring kernel
+per configuration) against the host-synced sorted path
 (models/moe.py moe_sorted: one host read of the expert counts per layer + hipBLASLt per expert).
 Prints ms per block and the expert GEMMs' TFLOP/s."""
 import os
@@ -40,12 +41,15 @@ for T in (1024, 4096, 8192):
     line = [f"T={T:5d}"]
     ms = timeit(lambda: moe_sorted(x, L, cfg, 0, 1))
     line.append(f"sorted+hipBLASLt {ms:7.2f} ms ({flop / ms / 1e9:6.1f} TF/s)")
-    for c in (2, 3, 19):
-        ops.MOE_GROUPED_CFG, saved = c, ops.MOE_GROUPED_CFG
+    for mode, c in (("big", None), ("gm", 2), ("gm", 19)):
+        saved = ops.MOE_GROUPED_CFG, ops.MOE_PREFILL
+        ops.MOE_PREFILL = mode
+        ops.MOE_GROUPED_CFG = c if c is not None else saved[0]
         try:
             err = (ops.moe_experts_grouped(x, L["w13"], L["w2"], tw, tid, 0).float() - want).abs().max().item()
             ms = timeit(lambda: ops.moe_experts_grouped(x, L["w13"], L["w2"], tw, tid, 0))
         finally:
-            ops.MOE_GROUPED_CFG = saved
-        line.append(f"grouped cfg {c} {ms:7.2f} ms ({flop / ms / 1e9:6.1f} TF/s, maxdiff {err:.3f})")
+            ops.MOE_GROUPED_CFG, ops.MOE_PREFILL = saved
+        name = "grouped gemm_big" if mode == "big" else f"grouped gm cfg {c}"
+        line.append(f"{name} {ms:7.2f} ms ({flop / ms / 1e9:6.1f} TF/s, maxdiff {err:.3f})")
     print(" | ".join(line), flush=True)

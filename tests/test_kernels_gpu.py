@@ -666,16 +666,24 @@ def test_gemm_mfma_grouped_gather_scatter(src_div):
         assert torch.all(out[untouched] == 7.0), cfg
 
 
-@pytest.mark.parametrize("T", [300, 1100])
+@pytest.mark.parametrize("mode", ["big", "gm"])
+@pytest.mark.parametrize("T,skew", [(300, False), (1100, False), (2100, True)])
 @pytest.mark.parametrize("e0,el", [(0, 8), (4, 4)])
-def test_moe_experts_grouped_prefill(T, e0, el):
-    """Prefill-sized MoE block (T * k > MOE_HIP_MAX_ROWS): device routing + grouped MFMA GEMMs ==
-    fp32 reference, and == the decode-path kernels on the same rows."""
+def test_moe_experts_grouped_prefill(T, skew, e0, el, mode, monkeypatch):
+    """Prefill-sized MoE block (T * k > MOE_HIP_MAX_ROWS): device routing + the grouped expert GEMMs
+    (KA_MOE_PREFILL big: expert-sorted rows through gemm_big's grouped mode, chunks of 256 rows per
+    expert, unused chunk-table entries skipped; gm: the grouped ring kernel) == fp32 reference, and ==
+    the decode-path kernels on the same rows.  skew: expert e0 gets most rows (several chunks, others
+    few or none)."""
+    monkeypatch.setattr(ops, "MOE_PREFILL", mode)
     E, H, I, k = 8, 512, 384, 2
     x = torch.randn(T, H, device=DEV, dtype=BF)
     w13 = (torch.randn(el, 2 * I, H, device=DEV) * 0.05).to(BF)
     w2 = (torch.randn(el, H, I, device=DEV) * 0.05).to(BF)
-    tw, tid = ops.moe_topk(torch.randn(T, E, device=DEV, dtype=BF), k)
+    logits = torch.randn(T, E, device=DEV, dtype=BF)
+    if skew:
+        logits[:, e0] += 3.0
+    tw, tid = ops.moe_topk(logits, k)
     got = ops.moe_experts_grouped(x, w13, w2, tw, tid, e0)
     close(got, _moe_dense_ref(x, w13, w2, tw, tid, e0), atol=5e-2, rtol=5e-2)
     close(got, ops.moe_experts(x, w13, w2, tw, tid, e0), atol=3e-2, rtol=3e-2)
