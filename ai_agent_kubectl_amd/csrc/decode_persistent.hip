@@ -1,5 +1,7 @@
-// Persistent batch-1 decode: every decoder layer of a Llama model (TP = 1, head_dim 128, KV block 16)
-// for ONE token in ONE launch (the serving path's B = 1 hipGraph replays it once per token).
+// Persistent small-batch decode: every decoder layer of a Llama model (TP = 1, head_dim 128, KV block 16)
+// for the next token of B = 1 or 2 sequences in ONE launch (the serving path's B = 1 / 2 hipGraphs
+// replay it once per step).  Each weight byte is streamed once per step whatever B is: a wave's 1-KB
+// piece is dotted against the B activation rows staged in LDS.
 // 2.85 ms/step for Llama-3-8B against 3.45 for the ~7-kernels-per-layer chain
 // (profiles/r4/persistent_decode/README.md).
 //
@@ -27,6 +29,8 @@
 // barrier arrival and the wait, so they stream while the grid synchronises.
 #include "common.h"
 
+#include <algorithm>
+
 namespace pd {
 
 #ifndef KA_PD_RING
@@ -41,8 +45,14 @@ namespace pd {
 #ifndef KA_PD_NT
 #define KA_PD_NT 1
 #endif
-constexpr int NT = 512, NW = NT / 64, RING = KA_PD_RING, HD = 128, KBS = 16, NT_ = NT;
-static_assert((RING & (RING - 1)) == 0 && RING >= 2 && RING <= 16, "ring: a power of two <= 16");
+constexpr int NT = 512, NW = NT / 64, HD = 128, KBS = 16, NT_ = NT;
+// LDS-DMA ring slots (1 KB) per wave: KA_PD_RING (16) in every phase, except the down rows at B = 2,
+// whose two act rows (2 x I bf16) take LDS the ring gives up there (8 slots, 64 KB per CU in flight)
+template <int B>
+constexpr int ring_down() { return B == 1 ? KA_PD_RING : 8; }
+static_assert((KA_PD_RING & (KA_PD_RING - 1)) == 0 && KA_PD_RING >= 2 && KA_PD_RING <= 16, "ring: a power of two <= 16");
+constexpr int MAXB = 2;     // sequences per launch
+constexpr int XS_MIN = 29 * 1024;   // the attention leader's scratch (aliases the x rows): 28.3 KB
 
 struct Layer {
   const bf16_t* wqkv;   // [(hq + 2 hkv) 128, H]
@@ -57,20 +67,26 @@ struct Args {
   const Layer* layers;
   int L, H, hq, hkv, I;
   float eps, scale_log2;
-  const bf16_t* h0;     // [H] the token's embedding
-  bf16_t* h_out;        // [H] the residual stream after the last layer (bf16)
+  const bf16_t* h0;     // [B][H] the tokens' embeddings
+  bf16_t* h_out;        // [B][H] the residual streams after the last layer (bf16)
   bf16_t* k_cache;      // [L][NB][hkv][16][128]
   bf16_t* v_cache;      // [L][NB][hkv][128][16]
   size_t cache_layer;   // elements per layer of each cache
-  const int* pos;       // [1] position of the token
-  const int* slot;      // [1] its cache slot
-  const int* bt;        // [max_blocks] the sequence's block table
-  const int* ctx;       // [1] context length including the token
+  const int* pos;       // [B] positions of the tokens
+  const int* slot;      // [B] their cache slots
+  const int* bt;        // [B][bt_stride] the sequences' block tables
+  const int* ctx;       // [B] context lengths including the token
   const float* cos_sin; // [max_pos][128]
-  float* res;           // workspace: [H] fp32 residual
-  bf16_t* qkv;          // [(hq + 2 hkv) 128]
-  bf16_t* attn;         // [hq 128]
-  bf16_t* act;          // [I]
+  float* res;           // workspace: [B][H] fp32 residual
+  bf16_t* qkv;          // [B][(hq + 2 hkv) 128]
+  bf16_t* attn;         // [B][hq 128]
+  bf16_t* act;          // [B][I]
+  int bt_stride;        // ints per block-table row
+  int xh_bytes;         // LDS bytes per staged x / attn row of one sequence (H, hq 128 bf16)
+  int xs_bytes;         // LDS bytes per staged act row (I bf16; B = 1: the larger of the two)
+  int lds_ring;         // LDS byte offset of the QKV / O / gate_up weight rings (after the x rows)
+  int lds_ring_d;       // ... of the down rows' rings (after the act rows)
+  int lds_red;          // ... of the norm reduction (64 B), then the phases' row results (1 KB per sequence)
   int* sync;            // SYNC_BYTES: grid arrival shards, group arrivals, the error word (zeroed per launch)
   unsigned long long* stamps;   // diagnostics (nullptr: off): [G workgroups][L][16] s_memrealtime (100 MHz)
 };
@@ -239,7 +255,13 @@ KA_DEV float wave_total(float v) {
 // between the counted loads) and are returned by run(); the caller writes them after drain().
 // Every instruction between the counted loads is asm or VALU / SALU: a compiler-visible vector-memory
 // access there would get an s_waitcnt vmcnt(0) from hipcc — a drain of the whole ring.
-template <class RowFn>
+// Row results of a stream: v[b] = the row's dot product with activation row b (lane i holds row i)
+template <int B>
+struct RowVals {
+  float v[B];
+};
+
+template <int B, int RG, class RowFn>
 struct Stream {
   const bf16_t* W;
   int K, KC, total, lane;
@@ -249,7 +271,7 @@ struct Stream {
   int issued, ni, nc;   // pieces issued; row / chunk of the next piece to issue
   int rot;              // every row is read from chunk `rot` on, wrapping (see make_stream)
   KA_DEV void issue() {
-    const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)(issued & (RING - 1)) * 1024u);
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)(issued & (RG - 1)) * 1024u);
     // wave-uniform part of the byte offset (row start + chunk) -> soffset; the lane's 16 B -> voffset
     const int c = nc + rot >= KC ? nc + rot - KC : nc + rot;
     const uint32_t so = __builtin_amdgcn_readfirstlane(((uint32_t)row(ni) * (uint32_t)K + (uint32_t)(c * 512)) * 2u);
@@ -274,88 +296,117 @@ struct Stream {
       ++ni;
     }
   }
-  // the first N pieces (N < RING: the rest by top_up<N>() after the barrier wait, so the wait's polls
+  // the first N pieces (N < RG: the rest by top_up<N>() after the barrier wait, so the wait's polls
   // queue behind fewer of the CU's own pieces)
-  template <int N = RING>
+  template <int N = RG>
   KA_DEV void start() {
     issued = ni = nc = 0;
     if (total <= 0) return;
 #pragma unroll
-    for (int r = 0; r < N; ++r) issue();
+    for (int r = 0; r < (N < RG ? N : RG); ++r) issue();
   }
   template <int N>
   KA_DEV void top_up() {
     if (total <= 0) return;
 #pragma unroll
-    for (int r = N; r < RING; ++r) issue();
+    for (int r = (N < RG ? N : RG); r < RG; ++r) issue();
   }
-  // xaddr: LDS byte address of x (K bf16)
-  KA_DEV float run(uint32_t xaddr) {
-    float mine = 0.f;
+  // xaddr: LDS byte address of activation row 0 (K bf16), row b at xaddr + b xstride
+  KA_DEV RowVals<B> run(uint32_t xaddr, uint32_t xstride) {
+    RowVals<B> mine;
+#pragma unroll
+    for (int b = 0; b < B; ++b) mine.v[b] = 0.f;
     if (total <= 0) return mine;
-    float acc = 0.f;
+    float acc[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) acc[b] = 0.f;
     int cc = 0, ri = 0;
     const uint32_t lo16 = (uint32_t)lane * 16u;
     auto finish = [&]() {
       if (++cc == KC) {
         cc = 0;
-        const float v = wave_total(acc);
-        if (lane == ri) mine = v;
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+          const float v = wave_total(acc[b]);
+          if (lane == ri) mine.v[b] = v;
+          acc[b] = 0.f;
+        }
         ++ri;
-        acc = 0.f;
       }
     };
     int j = 0;
     for (; j + 1 < total; j += 2) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING - 2) : "memory");   // pieces j, j + 1 have landed
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RG - 2) : "memory");   // pieces j, j + 1 have landed
       const int xc = cc + rot >= KC ? cc + rot - KC : cc + rot;   // x chunks of pieces j, j + 1
       const int xc1 = xc + 1 == KC ? 0 : xc + 1;
-      uint4 w0, w1, x0, x1;
-      asm volatile(
-          "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
-          "s_waitcnt lgkmcnt(0)"
-          : "=&v"(w0), "=&v"(w1), "=&v"(x0), "=&v"(x1)
-          : "v"(ring + (uint32_t)(j & (RING - 1)) * 1024u + lo16), "v"(ring + (uint32_t)((j + 1) & (RING - 1)) * 1024u + lo16),
-            "v"(xaddr + (uint32_t)xc * 1024u + lo16), "v"(xaddr + (uint32_t)xc1 * 1024u + lo16)
-          : "memory");
-      issue();   // both slots are free again: refill them RING pieces ahead
+      const uint32_t r0 = ring + (uint32_t)(j & (RG - 1)) * 1024u + lo16, r1 = ring + (uint32_t)((j + 1) & (RG - 1)) * 1024u + lo16;
+      const uint32_t a0 = xaddr + (uint32_t)xc * 1024u + lo16, a1 = xaddr + (uint32_t)xc1 * 1024u + lo16;
+      uint4 w0, w1, x0[B], x1[B];
+      if constexpr (B == 1) {
+        asm volatile(
+            "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(w0), "=&v"(w1), "=&v"(x0[0]), "=&v"(x1[0])
+            : "v"(r0), "v"(r1), "v"(a0), "v"(a1)
+            : "memory");
+      } else {
+        static_assert(B == 2, "rows per launch");
+        asm volatile(
+            "ds_read_b128 %0, %6\n\tds_read_b128 %1, %7\n\tds_read_b128 %2, %8\n\tds_read_b128 %3, %9\n\t"
+            "ds_read_b128 %4, %10\n\tds_read_b128 %5, %11\n\ts_waitcnt lgkmcnt(0)"
+            : "=&v"(w0), "=&v"(w1), "=&v"(x0[0]), "=&v"(x1[0]), "=&v"(x0[1]), "=&v"(x1[1])
+            : "v"(r0), "v"(r1), "v"(a0), "v"(a1), "v"(a0 + xstride), "v"(a1 + xstride)
+            : "memory");
+      }
+      issue();   // both slots are free again: refill them RG pieces ahead
       issue();
-      acc = dot8(w0, x0, acc);
+#pragma unroll
+      for (int b = 0; b < B; ++b) acc[b] = dot8(w0, x0[b], acc[b]);
       finish();
-      acc = dot8(w1, x1, acc);
+#pragma unroll
+      for (int b = 0; b < B; ++b) acc[b] = dot8(w1, x1[b], acc[b]);
       finish();
     }
     if (j < total) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING - 1) : "memory");
-      uint4 w0, x0;
-      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
-                   : "=&v"(w0), "=&v"(x0)
-                   : "v"(ring + (uint32_t)(j & (RING - 1)) * 1024u + lo16),
-                     "v"(xaddr + (uint32_t)(cc + rot >= KC ? cc + rot - KC : cc + rot) * 1024u + lo16)
-                   : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RG - 1) : "memory");
+      const uint32_t r0 = ring + (uint32_t)(j & (RG - 1)) * 1024u + lo16;
+      const uint32_t a0 = xaddr + (uint32_t)(cc + rot >= KC ? cc + rot - KC : cc + rot) * 1024u + lo16;
+      uint4 w0, x0[B];
+      if constexpr (B == 1) {
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(w0), "=&v"(x0[0])
+                     : "v"(r0), "v"(a0)
+                     : "memory");
+      } else {
+        asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %5\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(w0), "=&v"(x0[0]), "=&v"(x0[1])
+                     : "v"(r0), "v"(a0), "v"(a0 + xstride)
+                     : "memory");
+      }
       issue();
-      acc = dot8(w0, x0, acc);
+#pragma unroll
+      for (int b = 0; b < B; ++b) acc[b] = dot8(w0, x0[b], acc[b]);
       finish();
     }
     return mine;
   }
   KA_DEV void drain() const { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 };
-template <class RowFn>
 // gw: the wave's grid-wide index.  Each wave starts its rows at chunk gw mod K/512: waves that leave
 // a grid barrier together would otherwise all read the same 1-KB column of their rows at once —
 // addresses equal modulo the row pitch, the same few HBM channels.
-KA_DEV Stream<RowFn> make_stream(const bf16_t* W, int N, int K, int n, int lane, uint32_t ring, RowFn row, int gw) {
-  Stream<RowFn> s{W, K, K / 512, n * (K / 512), lane, row, (uint32_t)N * (uint32_t)K * 2u, ring, 0, 0, 0,
-                  KA_PD_ROT ? gw % (K / 512) : 0};
+template <int B, int RG, class RowFn>
+KA_DEV Stream<B, RG, RowFn> make_stream(const bf16_t* W, int N, int K, int n, int lane, uint32_t ring, RowFn row, int gw) {
+  Stream<B, RG, RowFn> s{W, K, K / 512, n * (K / 512), lane, row, (uint32_t)N * (uint32_t)K * 2u, ring, 0, 0, 0,
+                         KA_PD_ROT ? gw % (K / 512) : 0};
   return s;
 }
 
 // x[i] = bf16(res[i] * rstd * g[i]) into LDS (every workgroup): the fp32 residual read once by 16-B
 // sc1 loads (H / 4 words, <= 8 per lane at H <= 16384) and held in registers for the scaling pass
-KA_DEV void rmsnorm_to_lds(const Args& a, const bf16_t* g, bf16_t* xs, float* red) {
+KA_DEV void rmsnorm_to_lds(const Args& a, const float* res, const bf16_t* g, bf16_t* xs, float* red) {
   const int H = a.H, n16 = H / 4;
-  const uint4* rp = reinterpret_cast<const uint4*>(a.res);
+  const uint4* rp = reinterpret_cast<const uint4*>(res);
   uint4 rv[8];
   ld4_sc1(rp + min((int)threadIdx.x, n16 - 1), rp + min((int)threadIdx.x + NT, n16 - 1),
           rp + min((int)threadIdx.x + 2 * NT, n16 - 1), rp + min((int)threadIdx.x + 3 * NT, n16 - 1),
@@ -394,28 +445,38 @@ KA_DEV void rmsnorm_to_lds(const Args& a, const bf16_t* g, bf16_t* xs, float* re
   __syncthreads();
 }
 
-// LDS layout (bytes): x / act staging [0, 29 KB) (the attention leader's scratch reuses it: x is dead
-// between the QKV rows and the O rows); the waves' weight rings [29 KB, 29 KB + 8 x RING KB); the norm
-// reduction at the end.  > 80 KB: one workgroup per CU.
-constexpr int LDS_X = 0, LDS_ATT = 0, LDS_RING = 29 * 1024, LDS_RED = LDS_RING + NW * RING * 1024;
-constexpr int LDS_OUT = LDS_RED + 64, LDS_BYTES = LDS_OUT + 1024;   // LDS_OUT: a phase's bf16 row results
+// LDS layout (bytes), phase by phase (each region is dead when the next phase's DMA reaches it):
+//   QKV / O / gate_up: the B x / attn rows (a.xh_bytes each) at 0 (the attention leader's scratch,
+//     28.3 KB, reuses it: x is dead between the QKV rows and the O rows); the waves' 16-slot weight
+//     rings at a.lds_ring;
+//   down: the B act rows (a.xs_bytes each) at 0; the waves' ring_down<B>-slot rings at a.lds_ring_d;
+// then the norm reduction and the phases' bf16 row results (1 KB per sequence) at a.lds_red, past both.
+// > 80 KB: one workgroup per CU.
+constexpr int LDS_X = 0, LDS_ATT = 0;
 
+template <int B>
 __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
+  constexpr int RG = KA_PD_RING, RGD = ring_down<B>();
   extern __shared__ __attribute__((aligned(16))) uint4 lds_u4[];
   char* const lds = reinterpret_cast<char*>(lds_u4);
   bf16_t* const xs = reinterpret_cast<bf16_t*>(lds + LDS_X);
-  float* const red = reinterpret_cast<float*>(lds + LDS_RED);
-  bf16_t* const ob = reinterpret_cast<bf16_t*>(lds + LDS_OUT);
-  // this wave's LDS-DMA weight ring (LDS byte address; dynamic LDS is the kernel's only LDS object)
-  const uint32_t xaddr = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)lds_u4 + LDS_X);
-  const uint32_t ring = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)lds_u4 + LDS_RING + (threadIdx.x >> 6) * RING * 1024);
+  const int lds_ring = a.lds_ring, xsb = a.xs_bytes, xhb = a.xh_bytes;
+  float* const red = reinterpret_cast<float*>(lds + a.lds_red);
+  bf16_t* const ob = reinterpret_cast<bf16_t*>(lds + a.lds_red + 64);   // [B][512]
+  // this wave's LDS-DMA weight rings (LDS byte addresses; dynamic LDS is the kernel's only LDS object)
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)lds_u4;
+  const uint32_t xaddr = __builtin_amdgcn_readfirstlane(lds_base + LDS_X);
+  const uint32_t ring = __builtin_amdgcn_readfirstlane(lds_base + lds_ring + (threadIdx.x >> 6) * RG * 1024);
+  const uint32_t ring_d = __builtin_amdgcn_readfirstlane(lds_base + a.lds_ring_d + (threadIdx.x >> 6) * RGD * 1024);
   const int G = gridDim.x, wg = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int gw = wg * NW + wave, nwaves = G * NW;
   const int H = a.H, hq = a.hq, hkv = a.hkv, I = a.I, Gq = hq / hkv;
   const int per_group = G / hkv, grp = wg / per_group, in_grp = wg - grp * per_group;
+  const int QKVN = (hq + 2 * hkv) * HD;
+  // the group's first B workgroups are its attention leaders, workgroup b for sequence b
+  const bool leader = in_grp < B;
+  const int lb = leader ? in_grp : 0;
   const int qkv_rows = (Gq + 2) * HD;                       // rows of one KV head's group
   const int qkv_per_wave = (qkv_rows + per_group * NW - 1) / (per_group * NW);
   const int h_per_wave = (H + nwaves - 1) / nwaves;         // O / down rows = owned residual elements
@@ -426,14 +487,19 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
 
   // residual := the embedding (each wave initialises the elements it owns)
   const int own0 = gw * h_per_wave, own1 = min(H, own0 + h_per_wave);
-  // the token's position / slot / context (fixed for the launch) and the attention loop's trip count
-  const int p = a.pos[0], slot = a.slot[0], ctx = a.ctx[0];
+  // a leader's sequence: position / slot / context (fixed for the launch) and the attention loop's trip count
+  const int p = a.pos[lb], slot = a.slot[lb], ctx = a.ctx[lb];
+  const int* const bt = a.bt + (size_t)lb * a.bt_stride;
   const int ncached = ctx - 1, nblk = (ncached + KBS - 1) / KBS;
-  // a leader wave's first 32-token chunk: context blocks 2 w, 2 w + 1 (fixed for the launch;
-  // prefetched every layer; a missing second block repeats the first: finite values, weight 0)
-  const int blk_w0 = __builtin_amdgcn_readfirstlane(2 * wave < nblk ? a.bt[2 * wave] : 0);
-  const int blk_w1 = __builtin_amdgcn_readfirstlane(2 * wave + 1 < nblk ? a.bt[2 * wave + 1] : blk_w0);
-  for (int r = own0 + lane; r < own1; r += 64) st_sc1(a.res + r, bf2f(a.h0[r]));
+  // a leader wave's first 32-token chunk: context blocks 2 w, 2 w + 1 (fixed for the launch; the first
+  // PJ of them prefetched into the idle ring every layer; a missing second block repeats the first:
+  // finite values, weight 0)
+  constexpr int PJ = RG >= 16 ? 2 : RG >= 8 ? 1 : 0;   // 8 KB (K + V of 16 tokens) per block
+  const int blk_w0 = __builtin_amdgcn_readfirstlane(2 * wave < nblk ? bt[2 * wave] : 0);
+  const int blk_w1 = __builtin_amdgcn_readfirstlane(2 * wave + 1 < nblk ? bt[2 * wave + 1] : blk_w0);
+#pragma unroll
+  for (int b = 0; b < B; ++b)
+    for (int r = own0 + lane; r < own1; r += 64) st_sc1(a.res + (size_t)b * H + r, bf2f(a.h0[(size_t)b * H + r]));
   arrive(gcnt);
 
   const int qv0 = (in_grp * NW + wave) * qkv_per_wave;
@@ -452,9 +518,9 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
   // O rows go to the workgroups that run no attention only: a leader's context loads would otherwise
   // queue behind its own O weight pieces (issued before the attention).  O's residual element != its
   // down owner is fine: each phase has one writer per element and a barrier after it.
-  const int o_per_wave = (H + (G - hkv) * NW - 1) / ((G - hkv) * NW);
-  const int ow0 = in_grp == 0 ? 0 : ((grp * (per_group - 1) + in_grp - 1) * NW + wave) * o_per_wave;
-  const int n_o = in_grp == 0 ? 0 : max(0, min(H, ow0 + o_per_wave) - ow0);
+  const int o_per_wave = (H + (G - B * hkv) * NW - 1) / ((G - B * hkv) * NW);
+  const int ow0 = leader ? 0 : ((grp * (per_group - B) + in_grp - B) * NW + wave) * o_per_wave;
+  const int n_o = leader ? 0 : max(0, min(H, ow0 + o_per_wave) - ow0);
   auto o_row = [=](int i) { return ow0 + i; };
   const int g0 = gw * i_per_wave, ng = max(0, min(I, g0 + i_per_wave) - g0);
   auto gu_row = [=](int i) { return (i & 1) ? I + g0 + (i >> 1) : g0 + (i >> 1); };   // gate, up, gate, ...
@@ -480,27 +546,33 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     // The weight pieces of each phase are issued between the arrival and the wait of the barrier before
     // it: after the arrival (its vmcnt(0) would otherwise hold the arrival back until they landed),
     // in flight while the workgroup waits for the others.
-    auto sq = make_stream(Lw.wqkv, (hq + 2 * hkv) * HD, H, nq, lane, ring, qkv_row, gw);
+    auto sq = make_stream<B, RG>(Lw.wqkv, QKVN, H, nq, lane, ring, qkv_row, gw);
     sq.template start<KA_PD_PREISSUE>();
     wait_grid(a.sync, ++nbar, G, err);
     sq.template top_up<KA_PD_PREISSUE>();
     PD_STAMP(0);
     if (st && l > 0) st[(l - 1) * 16 + 12] = st[l * 16];   // the previous layer's barrier E ends here
-    rmsnorm_to_lds(a, Lw.ln1, xs, red);
+#pragma unroll
+    for (int b = 0; b < B; ++b) rmsnorm_to_lds(a, a.res + (size_t)b * H, Lw.ln1, xs + b * (xhb / 2), red);
     PD_STAMP(1);
     {
-      const float v = sq.run(xaddr);
+      const RowVals<B> v = sq.run(xaddr, (uint32_t)xhb);
       sq.drain();
-      if (lane < nq) ob[wave * qkv_per_wave + lane] = f2bf(v);
+#pragma unroll
+      for (int b = 0; b < B; ++b)
+        if (lane < nq) ob[b * 512 + wave * qkv_per_wave + lane] = f2bf(v.v[b]);
       __syncthreads();
-      if (2 * tid < wqn) st_sc1u(a.qkv + qkv_grow(wq0 + 2 * tid), reinterpret_cast<const uint32_t*>(ob)[tid]);
+#pragma unroll
+      for (int b = 0; b < B; ++b)
+        if (2 * tid < wqn)
+          st_sc1u(a.qkv + (size_t)b * QKVN + qkv_grow(wq0 + 2 * tid), reinterpret_cast<const uint32_t*>(ob)[b * 256 + tid]);
     }
     // the O rows' weights are issued now: they stream while the group waits and attention runs
     PD_STAMP(2);
-    auto so = make_stream(Lw.wo, H, hq * HD, n_o, lane, ring, o_row, gw);
+    auto so = make_stream<B, RG>(Lw.wo, H, hq * HD, n_o, lane, ring, o_row, gw);
     arrive(a.sync + SYNC_GROUP + 32 * grp);   // this workgroup's QKV rows are published
     so.start();
-    if (in_grp == 0) {
+    if (leader) {
       // the leader (no O rows: its ring is idle now): each wave's first 32-token chunk of this layer's
       // cached K / V (blocks 2 w, 2 w + 1) into its ring by LDS-DMA, in flight while the group's QKV
       // rows finish.  K rows land XOR-swizzled (16-B chunk c16 of token t at slot c16 ^ t: the MFMA
@@ -509,7 +581,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       if (2 * wave < nblk) {
         const int tk = lane >> 4, sl = lane & 15;   // token within a 1-KB piece, slot of the lane
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < PJ; ++j) {
           const size_t boff = ((size_t)(j ? blk_w1 : blk_w0) * hkv + grp) * hs + (size_t)l * a.cache_layer;
 #pragma unroll
           for (int pc = 0; pc < 4; ++pc) {
@@ -520,8 +592,8 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
         }
       }
     }
-    if (in_grp == 0) {
-      // ---- P2: the group's attention (its first workgroup) ----
+    if (leader) {
+      // ---- P2: the group's attention for sequence lb (its leader workgroup lb) ----
       wait_for(a.sync + SYNC_GROUP + 32 * grp, (l + 1) * per_group, err);
       PD_STAMP(3);
       // scratch (LDS_ATT): per-wave P re-layout | rotated q (bf16) | new k, v (fp32) | per-wave m, l |
@@ -539,7 +611,8 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       for (int it = tid; it < (Gq + 2) * (HD / 2); it += NT) {
         const int hh = it / (HD / 2), i = it - hh * (HD / 2);
         const int base = hh < Gq ? (grp * Gq + hh) * HD : hh == Gq ? (hq + grp) * HD : (hq + hkv + grp) * HD;
-        const uint32_t w0 = ld_sc1u(a.qkv + base + (i & ~1)), w1 = ld_sc1u(a.qkv + base + HD / 2 + (i & ~1));
+        const bf16_t* const qs = a.qkv + (size_t)lb * QKVN;
+        const uint32_t w0 = ld_sc1u(qs + base + (i & ~1)), w1 = ld_sc1u(qs + base + HD / 2 + (i & ~1));
         const float x1 = (i & 1) ? hi_f(w0) : lo_f(w0), x2 = (i & 1) ? hi_f(w1) : lo_f(w1);
         if (hh <= Gq) {
           const float c = cs[i], s = cs[HD / 2 + i];
@@ -583,19 +656,20 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
 #pragma unroll
       for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
       bf16_t* const pw = pscr + wave * 16 * PSTR;
-      const char* const rb = lds + LDS_RING + wave * RING * 1024;   // the wave's first chunk (ring)
+      const char* const rb = lds + lds_ring + wave * RG * 1024;   // the wave's first chunk (ring)
       const int nch = (ncached + 31) / 32;
       for (int c = wave; c < nch; c += NW) {
         const int t0 = c * 32;
-        const bool in_ring = c == wave;
+        const bool first = c == wave;   // its first PJ blocks are in the ring
         int blk0 = 0, blk1 = 0;
-        if (!in_ring) {
-          blk0 = a.bt[2 * c];
-          blk1 = t0 + 16 < ncached ? a.bt[2 * c + 1] : blk0;
+        if (!first || PJ < 2) {
+          blk0 = first ? blk_w0 : bt[2 * c];
+          blk1 = first ? blk_w1 : t0 + 16 < ncached ? bt[2 * c + 1] : blk0;
         }
         f32x4 sc[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
+          const bool in_ring = first && j < PJ;
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int ks = 0; ks < 4; ++ks) {
@@ -613,7 +687,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
         uint4 vf[8];
 #pragma unroll
         for (int n = 0; n < 8; ++n) {
-          if (in_ring)
+          if (first && (gq >> 1) < PJ)   // lanes gq >> 1 read block gq >> 1 of the chunk
             vf[n] = *reinterpret_cast<const uint4*>(rb + (gq >> 1) * 8192 + 4096 + (n * 16 + col) * 32 + (gq & 1) * 16);
           else
             vf[n] = *reinterpret_cast<const uint4*>(vc + ((size_t)((gq >> 1) ? blk1 : blk0) * hkv + grp) * hs +
@@ -680,7 +754,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
         const float o1 = num / den;
         const float o2 = __shfl_xor(o1, 1, 64);   // d and d ^ 1 are neighbouring lanes
         if ((d & 1) == 0)
-          st_sc1u(a.attn + (grp * Gq + r) * HD + d, pack2(o1, o2));
+          st_sc1u(a.attn + (size_t)lb * hq * HD + (grp * Gq + r) * HD + d, pack2(o1, o2));
       }
       if (slot >= 0 && tid < HD) {          // append the new token (read by the NEXT launches only; after the
                                             // attention: hipcc waits for these stores before reusing their VGPRs)
@@ -694,55 +768,77 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     arrive(gcnt);
     wait_grid(a.sync, ++nbar, G, err);
     PD_STAMP(5);
-    stage_sc1(reinterpret_cast<uint4*>(lds + LDS_X), a.attn, hq * HD / 8);   // attn (sc1) -> LDS
+#pragma unroll
+    for (int b = 0; b < B; ++b)   // attn (sc1) -> LDS
+      stage_sc1(reinterpret_cast<uint4*>(lds + LDS_X + b * xhb), a.attn + (size_t)b * hq * HD, hq * HD / 8);
     vm_drain();
     __syncthreads();
     {
-      const float v = so.run(xaddr);
+      const RowVals<B> v = so.run(xaddr, (uint32_t)xhb);
       so.drain();
-      if (lane < n_o) st_sc1(a.res + ow0 + lane, ld_sc1(a.res + ow0 + lane) + bf2f(f2bf(v)));
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        float* const rr = a.res + (size_t)b * H + ow0 + lane;
+        if (lane < n_o) st_sc1(rr, ld_sc1(rr) + bf2f(f2bf(v.v[b])));
+      }
     }
     PD_STAMP(6);
-    auto sg = make_stream(Lw.w13, 2 * I, H, 2 * ng, lane, ring, gu_row, gw);
+    auto sg = make_stream<B, RG>(Lw.w13, 2 * I, H, 2 * ng, lane, ring, gu_row, gw);
     arrive(gcnt);
     sg.template start<KA_PD_PREISSUE>();
     wait_grid(a.sync, ++nbar, G, err);
     sg.template top_up<KA_PD_PREISSUE>();
     PD_STAMP(7);
     // ---- P4: norm + gate / up -> act ----
-    rmsnorm_to_lds(a, Lw.ln2, xs, red);
+#pragma unroll
+    for (int b = 0; b < B; ++b) rmsnorm_to_lds(a, a.res + (size_t)b * H, Lw.ln2, xs + b * (xhb / 2), red);
     PD_STAMP(8);
     {
-      const float v = sg.run(xaddr);   // lane 2 k: gate row k, lane 2 k + 1: its up row
+      const RowVals<B> v = sg.run(xaddr, (uint32_t)xhb);   // lane 2 k: gate row k, lane 2 k + 1: its up row
       sg.drain();
-      const float u = bf2f(f2bf(__shfl_down(v, 1, 64)));
-      const float gt = bf2f(f2bf(v));
-      if (!(lane & 1) && (lane >> 1) < ng) ob[wave * i_per_wave + (lane >> 1)] = f2bf(gt / (1.f + __expf(-gt)) * u);
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const float u = bf2f(f2bf(__shfl_down(v.v[b], 1, 64)));
+        const float gt = bf2f(f2bf(v.v[b]));
+        if (!(lane & 1) && (lane >> 1) < ng)
+          ob[b * 512 + wave * i_per_wave + (lane >> 1)] = f2bf(gt / (1.f + __expf(-gt)) * u);
+      }
       __syncthreads();
-      if (2 * tid < wan) st_sc1u(a.act + wa0 + 2 * tid, reinterpret_cast<const uint32_t*>(ob)[tid]);
+#pragma unroll
+      for (int b = 0; b < B; ++b)
+        if (2 * tid < wan)
+          st_sc1u(a.act + (size_t)b * I + wa0 + 2 * tid, reinterpret_cast<const uint32_t*>(ob)[b * 256 + tid]);
     }
     PD_STAMP(9);
-    auto sd = make_stream(Lw.w2, H, I, no, lane, ring, own_row, gw);
+    auto sd = make_stream<B, RGD>(Lw.w2, H, I, no, lane, ring_d, own_row, gw);
     arrive(gcnt);
     sd.template start<KA_PD_PREISSUE>();
     wait_grid(a.sync, ++nbar, G, err);
     sd.template top_up<KA_PD_PREISSUE>();
     PD_STAMP(10);
     // ---- P5: down rows -> residual ----
-    stage_sc1(reinterpret_cast<uint4*>(lds + LDS_X), a.act, I / 8);   // act (sc1) -> LDS
+#pragma unroll
+    for (int b = 0; b < B; ++b)   // act (sc1) -> LDS
+      stage_sc1(reinterpret_cast<uint4*>(lds + LDS_X + b * xsb), a.act + (size_t)b * I, I / 8);
     vm_drain();
     __syncthreads();
     {
-      const float v = sd.run(xaddr);
+      const RowVals<B> v = sd.run(xaddr, (uint32_t)xsb);
       sd.drain();
-      if (lane < no) st_sc1(a.res + own0 + lane, ld_sc1(a.res + own0 + lane) + bf2f(f2bf(v)));
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        float* const rr = a.res + (size_t)b * H + own0 + lane;
+        if (lane < no) st_sc1(rr, ld_sc1(rr) + bf2f(f2bf(v.v[b])));
+      }
     }
     PD_STAMP(11);
     arrive(gcnt);   // the next layer's QKV pieces are issued before the wait (top of the loop)
   }
 #undef PD_STAMP
   wait_grid(a.sync, ++nbar, G, err);
-  for (int r = own0 + lane; r < own1; r += 64) a.h_out[r] = f2bf(ld_sc1(a.res + r));
+#pragma unroll
+  for (int b = 0; b < B; ++b)
+    for (int r = own0 + lane; r < own1; r += 64) a.h_out[(size_t)b * H + r] = f2bf(ld_sc1(a.res + (size_t)b * H + r));
 }
 
 __global__ __launch_bounds__(256) void zero_sync_kernel(int* __restrict__ sync) {
@@ -761,39 +857,76 @@ static int num_cus() {
 
 }  // namespace pd
 
-// Workspace bytes: residual (fp32 H) + qkv + attn + act (bf16) + the sync words.
+// Workspace bytes for up to MAXB sequences: residual (fp32 B H) + qkv + attn + act (bf16) + the sync words.
 extern "C" size_t ka_decode_persistent_ws(int H, int hq, int hkv, int I) {
-  return pd::SYNC_BYTES + (size_t)H * 4 + (size_t)(hq + 2 * hkv) * 128 * 2 + (size_t)hq * 128 * 2 + (size_t)I * 2 + 1024;
+  return pd::SYNC_BYTES +
+         (size_t)pd::MAXB * ((size_t)H * 4 + (size_t)(hq + 2 * hkv) * 128 * 2 + (size_t)hq * 128 * 2 + (size_t)I * 2) + 1024;
 }
 
-// Every layer of a batch-1 decode step (see the header).  layers: device array of L x 6 pointers
-// (wqkv, wo, w13, w2, ln1, ln2); pos / slot / ctx: device int [1]; bt: the sequence's block table;
-// stamps: nullptr, or [G][L][16] uint64 phase timestamps (diagnostics; G <= the CU count).
+// LDS layout of a B-sequence launch (see decode_layers_kernel); returns its bytes
+static int pd_layout(int B, int H, int hq, int I, pd::Args* a) {
+  auto kb = [](int bytes) { return (bytes + 1023) / 1024 * 1024; };
+  const int xh = kb(std::max(H, hq * 128) * 2), xs = kb(std::max(std::max(H, I), hq * 128) * 2);
+  const int ring = std::max(B * (B == 1 ? xs : xh), pd::XS_MIN);
+  const int ring_d = B == 1 ? ring : B * xs;
+  const int rd = B == 1 ? KA_PD_RING : 8;
+  const int red = std::max(ring + pd::NW * KA_PD_RING * 1024, ring_d + pd::NW * rd * 1024);
+  if (a) {
+    a->xh_bytes = B == 1 ? xs : xh;
+    a->xs_bytes = xs;
+    a->lds_ring = ring;
+    a->lds_ring_d = ring_d;
+    a->lds_red = red;
+  }
+  return red + 64 + B * 1024;
+}
+
+// Largest batch (1 or 2) the persistent kernel takes for this model within the LDS of one CU; 0: none.
+extern "C" int ka_decode_persistent_max_b(int H, int hq, int I) {
+  if (pd_layout(2, H, hq, I, nullptr) <= 160 * 1024) return 2;
+  if (pd_layout(1, H, hq, I, nullptr) <= 160 * 1024) return 1;
+  return 0;
+}
+
+template <int B>
+static int pd_launch(const pd::Args& a, int G, hipStream_t stream) {
+  const int lds = pd_layout(B, a.H, a.hq, a.I, nullptr);
+  static int attr = 0;
+  if (attr < lds) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pd::decode_layers_kernel<B>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = lds;
+  }
+  hipLaunchKernelGGL(pd::decode_layers_kernel<B>, dim3(G), dim3(pd::NT), lds, stream, a);
+  return (int)hipGetLastError();
+}
+
+// Every layer of a decode step of B = 1 or 2 sequences (see the header).  layers: device array of L x 6
+// pointers (wqkv, wo, w13, w2, ln1, ln2); h0 / h_out [B][H]; pos / slot / ctx: device int [B]; bt: the
+// sequences' block tables [B][bt_stride]; stamps: nullptr, or [G][L][16] uint64 phase timestamps
+// (diagnostics; G <= the CU count).
 // Requirements: head_dim 128, block 16, hq % hkv == 0, hq / hkv <= 4, H % 512 == 0, I % 512 == 0,
-// hq * 128 % 512 == 0, the grid (the CU count, rounded down to a multiple of hkv) all resident.
+// hq * 128 % 512 == 0, the B activation rows and the rings within LDS (ka_decode_persistent_max_b),
+// the grid (the CU count, rounded down to a multiple of hkv) all resident.
 extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* layers, int L, int H, int hq, int hkv,
                                     int I, float eps, float scale, void* k_cache, void* v_cache, long cache_layer,
                                     const int* pos, const int* slot, const int* bt, const int* ctx,
-                                    const float* cos_sin, void* ws, void* stamps, hipStream_t stream) {
+                                    const float* cos_sin, void* ws, void* stamps, int B, int bt_stride,
+                                    hipStream_t stream) {
   if (L <= 0) return 0;
-  if (hq % hkv || hq / hkv > 4 || hkv > 16 || H % 512 || I % 512 || (hq * 128) % 512 || H > 16384 || I > 16384 ||
-      ws == nullptr)
+  if (B < 1 || B > pd::MAXB || hq % hkv || hq / hkv > 4 || hkv > 16 || H % 512 || I % 512 || (hq * 128) % 512 ||
+      H > 16384 ||   // rmsnorm_to_lds holds a row in 8 16-B words per thread
+      ws == nullptr || B > ka_decode_persistent_max_b(H, hq, I) || (B > 1 && bt_stride <= 0))
     return (int)hipErrorInvalidValue;
   const int G = (pd::num_cus() / hkv) * hkv;
   if (G < hkv) return (int)hipErrorInvalidValue;
   {   // every wave's rows fit its 64 lanes (lane i = row i) and the LDS result buffer
     const int per_group = G / hkv, nw = G * pd::NW;
-    if (per_group < 2) return (int)hipErrorInvalidValue;
+    if (per_group < B + 1) return (int)hipErrorInvalidValue;
     const int q = ((hq / hkv + 2) * 128 + per_group * pd::NW - 1) / (per_group * pd::NW);
     const int hpw = (H + nw - 1) / nw, ipw = (I + nw - 1) / nw;
-    const int opw = G > hkv ? (H + (G - hkv) * pd::NW - 1) / ((G - hkv) * pd::NW) : 65;
+    const int opw = (H + (G - B * hkv) * pd::NW - 1) / ((G - B * hkv) * pd::NW);
     if (q > 64 || hpw > 64 || 2 * ipw > 64 || opw > 64) return (int)hipErrorInvalidValue;
-  }
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pd::decode_layers_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, pd::LDS_BYTES);
-    attr = true;
   }
   char* w = static_cast<char*>(ws);
   pd::Args a;
@@ -818,15 +951,18 @@ extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* lay
   a.sync = reinterpret_cast<int*>(w);
   a.stamps = static_cast<unsigned long long*>(stamps);
   a.res = reinterpret_cast<float*>(w + pd::SYNC_BYTES);
-  a.qkv = reinterpret_cast<bf16_t*>(w + pd::SYNC_BYTES + (size_t)H * 4);
-  a.attn = a.qkv + (size_t)(hq + 2 * hkv) * 128;
-  a.act = a.attn + (size_t)hq * 128;
+  a.qkv = reinterpret_cast<bf16_t*>(w + pd::SYNC_BYTES + (size_t)pd::MAXB * H * 4);
+  a.attn = a.qkv + (size_t)pd::MAXB * (hq + 2 * hkv) * 128;
+  a.act = a.attn + (size_t)pd::MAXB * hq * 128;
+  a.bt_stride = bt_stride;
+  pd_layout(B, H, hq, I, &a);
   // the arrival counters and the error word start at zero in every launch.  A kernel, not
   // hipMemsetAsync: captured into a hipGraph, the memset node left the words at 0xF3C00000 on
   // ROCm 7.2 (every grid wait then ran out; scripts/debug_pd_graph.py)
   hipLaunchKernelGGL(pd::zero_sync_kernel, dim3(1), dim3(256), 0, stream, reinterpret_cast<int*>(w));
-  hipLaunchKernelGGL(pd::decode_layers_kernel, dim3(G), dim3(pd::NT), pd::LDS_BYTES, stream, a);
-  KA_CHECK_LAUNCH();
+  const int rc = (int)hipGetLastError();
+  if (rc != 0) return rc;
+  return B == 1 ? pd_launch<1>(a, G, stream) : pd_launch<2>(a, G, stream);
 }
 
 // Byte offset of the error word in the workspace (the runner reads it back with every B = 1 step).

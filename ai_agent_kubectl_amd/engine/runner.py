@@ -417,7 +417,7 @@ class ModelRunner:
             if self.graph_pool is None:
                 self.graph_pool = g.pool()
             self.graphs[B] = g
-            self.graph_persistent[B] = B == 1 and self.model.persistent_ok()
+            self.graph_persistent[B] = self.model.persistent_ok(B)
         torch.cuda.synchronize(self.device)
         return time.perf_counter() - t0
 
@@ -582,7 +582,7 @@ class ModelRunner:
         after model.persistent is turned off), the model's current setting otherwise."""
         if Bp in self.graphs:
             return self.graph_persistent.get(Bp, False)
-        return Bp == 1 and self.model.persistent_ok()
+        return self.model.persistent_ok(Bp)
 
     def _copy_err(self, persistent: bool = False) -> Optional[torch.Tensor]:
         """Queue the error word's readback behind the step just launched: [one-shot collectives,

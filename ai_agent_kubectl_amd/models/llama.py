@@ -102,6 +102,10 @@ class LlamaModel:
         # parallel/dp.py), 1 forces it on, 0 keeps the kernel chain.
         self.persistent = persistent_default()
         self._pd = None   # (layer pointer table, workspace)
+        # decode batches the persistent kernel serves (1 or 2: B = 2 streams the weights once for both
+        # sequences' rows)
+        self.persistent_max_b = int(os.environ.get("KA_PERSISTENT_MAX_B", "2"))
+        self._pd_max_b = None
         self.persistent_stamps = None   # diagnostics: int64 [CUs, L, 16] phase timestamps (scripts/)
 
     def _layer(self, i):
@@ -115,7 +119,7 @@ class LlamaModel:
         cfg = self.cfg
         eps = cfg.norm_eps
         h = ops.embedding(input_ids, self.W["embed"])
-        if meta.is_decode and input_ids.shape[0] == 1 and self.persistent_ok():
+        if meta.is_decode and self.persistent_ok(input_ids.shape[0]):
             return self._forward_persistent(h, meta, k_cache, v_cache)
         residual = None
         pending = False   # h holds this rank's partial of a row-parallel output (TP all-reduce due)
@@ -197,16 +201,22 @@ class LlamaModel:
         idx = meta.logits_indices
         return ops.rmsnorm(h.index_select(0, idx), self.W["norm"], eps, residual=residual.index_select(0, idx))
 
-    def persistent_ok(self) -> bool:
+    def persistent_ok(self, B: int = 1) -> bool:
+        """The persistent all-layers kernel takes a decode step of B sequences: B <= KA_PERSISTENT_MAX_B
+        (default 2) and within the kernel's LDS budget for this geometry (ops.decode_persistent_max_b)."""
         cfg = self.cfg
-        return (self.persistent and self.device.type == "cuda" and self._local_comm and not cfg.is_moe
+        if not (self.persistent and self.device.type == "cuda" and self._local_comm and not cfg.is_moe
                 and self.D == 128 and self.hq % self.hkv == 0 and self.hq // self.hkv <= 4
                 and cfg.hidden % 512 == 0 and cfg.intermediate % 512 == 0 and (self.hq * self.D) % 512 == 0
-                and cfg.hidden <= 16384 and cfg.intermediate <= 16384)
+                and cfg.hidden <= 16384 and 1 <= B <= self.persistent_max_b):
+            return False
+        if self._pd_max_b is None:
+            self._pd_max_b = ops.decode_persistent_max_b(cfg.hidden, self.hq, cfg.intermediate)
+        return B <= self._pd_max_b
 
     def _forward_persistent(self, h0, meta: AttnMeta, k_cache, v_cache) -> torch.Tensor:
-        """Batch-1 decode through the persistent all-layers kernel; returns the final-normed hidden
-        state [1, H] like `forward`."""
+        """Batch-1 / 2 decode through the persistent all-layers kernel; returns the final-normed hidden
+        states [B, H] like `forward`."""
         if self._pd is None:
             ptrs = [[L[k].data_ptr() for k in ("wqkv", "wo", "w13", "w2", "ln1", "ln2")] for L in self.layers]
             table = torch.tensor(ptrs, dtype=torch.int64, device=self.device)
@@ -219,7 +229,7 @@ class LlamaModel:
         assert k_cache.shape[3] == 16, "persistent decode needs KV block 16"   # [L, NB, hkv, 16, 128]
         hout = ops.decode_persistent(h0, table, len(self.layers), self.hq, self.hkv, self.cfg.intermediate,
                                      self.cfg.norm_eps, self.scale, k_cache, v_cache, meta.positions,
-                                     meta.slot_mapping, meta.block_tables[0], meta.ctx_lens, self.cos_sin, ws,
+                                     meta.slot_mapping, meta.block_tables, meta.ctx_lens, self.cos_sin, ws,
                                      self.persistent_stamps)
         return ops.rmsnorm(hout, self.W["norm"], self.cfg.norm_eps)
 

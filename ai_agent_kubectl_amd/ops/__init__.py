@@ -297,17 +297,26 @@ def decode_persistent(h0: torch.Tensor, layer_ptrs: torch.Tensor, L: int, hq: in
                       scale: float, k_cache: torch.Tensor, v_cache: torch.Tensor, positions: torch.Tensor,
                       slot_mapping: torch.Tensor, block_table: torch.Tensor, ctx_lens: torch.Tensor,
                       cos_sin: torch.Tensor, ws: torch.Tensor, stamps: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Every decoder layer of a batch-1 decode step in one persistent launch (csrc/decode_persistent.hip):
-    h0 [1, H] bf16 embedding -> the residual stream after the last layer [1, H] bf16.  layer_ptrs:
-    int64 [L, 6] device pointers (wqkv, wo, w13, w2, ln1, ln2); caches [L, NB, hkv, ...]."""
+    """Every decoder layer of a decode step of B = 1 or 2 sequences in one persistent launch
+    (csrc/decode_persistent.hip): h0 [B, H] bf16 embeddings -> the residual streams after the last
+    layer [B, H] bf16.  layer_ptrs: int64 [L, 6] device pointers (wqkv, wo, w13, w2, ln1, ln2); caches
+    [L, NB, hkv, ...]; positions / slot_mapping / ctx_lens [>= B]; block_table [>= B, max_blocks]
+    (a 1-D table is the single sequence's)."""
     lib = require()
-    H = h0.shape[-1]
+    B, H = h0.shape
     out = torch.empty_like(h0)
+    bt_stride = block_table.stride(0) if block_table.dim() == 2 else block_table.shape[0]
     check(lib.ka_decode_persistent(_p(out), _p(h0), _p(layer_ptrs), L, H, hq, hkv, I, float(eps), float(scale),
                                    _p(k_cache), _p(v_cache), k_cache[0].numel(), _p(positions), _p(slot_mapping),
-                                   _p(block_table), _p(ctx_lens), _p(cos_sin), _p(ws), _p(stamps), _stream()),
+                                   _p(block_table), _p(ctx_lens), _p(cos_sin), _p(ws), _p(stamps), B, bt_stride,
+                                   _stream()),
           "decode_persistent")
     return out
+
+
+def decode_persistent_max_b(H: int, hq: int, I: int) -> int:
+    """Largest batch (0, 1 or 2) csrc/decode_persistent.hip takes for a model (its LDS budget)."""
+    return int(require().ka_decode_persistent_max_b(H, hq, I))
 
 
 GB_BN = 256   # csrc/gemm_big.hip output tile (weight rows)

@@ -80,56 +80,57 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             out.append(f"B={B}: {e0.elapsed_time(e1) / args.reps:.3f} ms (shared blocks {int(r.h_np[r._off['nsh']])})")
-            if B == 1 and m.persistent:   # the replays' own error word (a wait that ran out = invalid timing)
+            if r.graph_persistent.get(B):   # the replays' own error word (a wait that ran out = invalid timing)
                 out.append(f"graph err {m.persistent_err()}")
         print(f"prefetch {mb:g} MB x {int(blocks)} blocks, persistent {pers}: " + ", ".join(out), flush=True)
         if m.persistent:
             print("  persistent error word:", m.persistent_err(), flush=True)
             # phase breakdown of one launch, every workgroup (stamp k = the end of phase k - 1)
-            ncu = torch.cuda.get_device_properties(0).multi_processor_count
-            m.persistent_stamps = torch.zeros((ncu, len(m.layers), 16), dtype=torch.int64, device="cuda")
-            sub = type(batch)(batch.seqs[:1], [1], is_decode=True)
-            r._pack_decode(sub, 1)
-            r.d_stage[:r._off["bt"] + r.max_blocks].copy_(r.h_stage[:r._off["bt"] + r.max_blocks])
-            h0 = m.W["embed"][:1].clone()
-            from ai_agent_kubectl_amd.models.llama import AttnMeta
-            meta = AttnMeta(positions=r._view("pos", 1), slot_mapping=r._view("slots", 1),
-                            block_tables=r._view("bt", 1), ctx_lens=r._view("ctx", 1),
-                            logits_indices=r.d_logits_idx[:1], is_decode=True)
-            for _ in range(3):
-                m._forward_persistent(h0, meta, r.k_cache, r.v_cache)
-            torch.cuda.synchronize()
-            stv = m.persistent_stamps.cpu().double() / 100.0   # 100 MHz -> us
-            G = int((stv[:, 1, 0] > 0).sum())
-            stv = stv[:G, 1:-1]                                 # layers 1 .. L-2
-            names = ["norm1", "qkv", "grp-wait", "attn", "barB", "O", "barC", "norm2", "gate_up", "barD", "down",
-                     "barE"]
-            per_layer = float((stv[:, :, 12] - stv[:, :, 0]).mean())
-            print(f"  {G} workgroups, per layer {per_layer:.1f} us", flush=True)
-            for k, n in enumerate(names):
-                ok = (stv[:, :, k + 1] > 0) & (stv[:, :, k] > 0)
-                if not ok.any():
-                    continue
-                d = (stv[:, :, k + 1] - stv[:, :, k])[ok]
-                # end-time spread across the grid at this stamp (relative to the layer's first stamp)
-                endt = (stv[:, :, k + 1] - stv[:, :, 0].min(dim=0).values)
-                print(f"  {n:9s} mean {float(d.mean()):6.1f}  p10 {float(d.quantile(0.1)):6.1f}  "
-                      f"p90 {float(d.quantile(0.9)):6.1f}  max {float(d.max()):6.1f}   end: "
-                      f"min {float(endt.min(dim=0).values.mean()):6.1f} max {float(endt.max(dim=0).values.mean()):6.1f}",
-                      flush=True)
-            lead = stv[:, :, 13] > 0   # attention leaders: RoPE / context blocks / merge
-            if lead.any():
-                sub = [("rope + K/V landed", 3, 13), ("first q.k", 13, 15), ("rest of blocks", 15, 14), ("merge", 14, 4)]
-                print("  attention: " + ", ".join(f"{n} {float((stv[:, :, b] - stv[:, :, a])[lead].mean()):.1f}"
-                                                  for n, a, b in sub), flush=True)
-            # per-XCD (wg % 8) mean gate_up / down durations: is the skew a fabric effect?
-            for k, n in ((8, "gate_up"), (10, "down")):
-                d = stv[:, :, k + 1] - stv[:, :, k]
-                xs = [float(d[x::8].mean()) for x in range(8)]
-                print(f"  {n} by XCD: " + " ".join(f"{v:.1f}" for v in xs), flush=True)
-            slow = (stv[:, :, 9] - stv[:, :, 8]).mean(dim=1)
-            print("  slowest gate_up workgroups:", [int(i) for i in slow.argsort(descending=True)[:12]], flush=True)
-            m.persistent_stamps = None
+            for PB in [b for b in (1, 2) if m.persistent_ok(b) and len(batch.seqs) >= b]:
+                ncu = torch.cuda.get_device_properties(0).multi_processor_count
+                m.persistent_stamps = torch.zeros((ncu, len(m.layers), 16), dtype=torch.int64, device="cuda")
+                sub = type(batch)(batch.seqs[:PB], [1] * PB, is_decode=True)
+                r._pack_decode(sub, PB)
+                r.d_stage[:r._off["bt"] + PB * r.max_blocks].copy_(r.h_stage[:r._off["bt"] + PB * r.max_blocks])
+                h0 = m.W["embed"][:PB].clone()
+                from ai_agent_kubectl_amd.models.llama import AttnMeta
+                meta = AttnMeta(positions=r._view("pos", PB), slot_mapping=r._view("slots", PB),
+                                block_tables=r._view("bt", PB), ctx_lens=r._view("ctx", PB),
+                                logits_indices=r.d_logits_idx[:PB], is_decode=True)
+                for _ in range(3):
+                    m._forward_persistent(h0, meta, r.k_cache, r.v_cache)
+                torch.cuda.synchronize()
+                stv = m.persistent_stamps.cpu().double() / 100.0   # 100 MHz -> us
+                G = int((stv[:, 1, 0] > 0).sum())
+                stv = stv[:G, 1:-1]                                 # layers 1 .. L-2
+                names = ["norm1", "qkv", "grp-wait", "attn", "barB", "O", "barC", "norm2", "gate_up", "barD", "down",
+                         "barE"]
+                per_layer = float((stv[:, :, 12] - stv[:, :, 0]).mean())
+                print(f"  persistent B={PB}: {G} workgroups, per layer {per_layer:.1f} us", flush=True)
+                for k, n in enumerate(names):
+                    ok = (stv[:, :, k + 1] > 0) & (stv[:, :, k] > 0)
+                    if not ok.any():
+                        continue
+                    d = (stv[:, :, k + 1] - stv[:, :, k])[ok]
+                    # end-time spread across the grid at this stamp (relative to the layer's first stamp)
+                    endt = (stv[:, :, k + 1] - stv[:, :, 0].min(dim=0).values)
+                    print(f"  {n:9s} mean {float(d.mean()):6.1f}  p10 {float(d.quantile(0.1)):6.1f}  "
+                          f"p90 {float(d.quantile(0.9)):6.1f}  max {float(d.max()):6.1f}   end: "
+                          f"min {float(endt.min(dim=0).values.mean()):6.1f} max {float(endt.max(dim=0).values.mean()):6.1f}",
+                          flush=True)
+                lead = stv[:, :, 13] > 0   # attention leaders: RoPE / context blocks / merge
+                if lead.any():
+                    sub = [("rope + K/V landed", 3, 13), ("first q.k", 13, 15), ("rest of blocks", 15, 14), ("merge", 14, 4)]
+                    print("  attention: " + ", ".join(f"{n} {float((stv[:, :, b] - stv[:, :, a])[lead].mean()):.1f}"
+                                                      for n, a, b in sub), flush=True)
+                # per-XCD (wg % 8) mean gate_up / down durations: is the skew a fabric effect?
+                for k, n in ((8, "gate_up"), (10, "down")):
+                    d = stv[:, :, k + 1] - stv[:, :, k]
+                    xs = [float(d[x::8].mean()) for x in range(8)]
+                    print(f"  {n} by XCD: " + " ".join(f"{v:.1f}" for v in xs), flush=True)
+                slow = (stv[:, :, 9] - stv[:, :, 8]).mean(dim=1)
+                print("  slowest gate_up workgroups:", [int(i) for i in slow.argsort(descending=True)[:12]], flush=True)
+                m.persistent_stamps = None
 
 
 if __name__ == "__main__":

@@ -453,40 +453,44 @@ def test_mixtral_forward_hip_vs_reference():
     assert all(len(s.output_ids) == len(be._forced) + 6 for s in seqs)
 
 
-@pytest.mark.parametrize("graphs,long_ctx", [(False, False), (True, False), (False, True)])
-def test_persistent_decode_matches_kernel_chain_and_fp32(graphs, long_ctx):
-    """csrc/decode_persistent.hip (every layer of a batch-1 decode step in one launch, grid-wide
-    arrival counters) against the per-kernel decode chain and the fp32 references, over 6 decode
-    steps of one sequence (the real Llama-3-8B layer geometry, 2 layers): hidden states within bf16
-    tolerance, the same KV appended, the tokens equal to the chain's, the error word clear — eagerly
-    and as the captured B = 1 hipGraph.  long_ctx: a ~400-token context, past the 256 tokens the
-    attention leaders prefetch into their rings (the chunk loop's global-load path)."""
+@pytest.mark.parametrize("B,graphs,long_ctx", [(1, False, False), (1, True, False), (1, False, True),
+                                                (2, False, False), (2, True, False), (2, False, True)])
+def test_persistent_decode_matches_kernel_chain_and_fp32(B, graphs, long_ctx):
+    """csrc/decode_persistent.hip (every layer of a decode step of B = 1 / 2 sequences in one launch,
+    grid-wide arrival counters, one attention leader per sequence and KV group) against the per-kernel
+    decode chain and the fp32 references, over 6 decode steps (the real Llama-3-8B layer geometry, 2
+    layers): hidden states within bf16 tolerance, the same KV appended, the tokens equal to the chain's,
+    the error word clear — eagerly and as the captured bucket-B hipGraph.  long_ctx: a ~400-token
+    context, past the tokens the attention leaders prefetch into their rings (the chunk loop's
+    global-load path); at B = 2 the two sequences differ in length."""
     from ai_agent_kubectl_amd.engine.sequence import Sequence
     from ai_agent_kubectl_amd.models.llama import AttnMeta
-    eng = _engine("llama3-8b-2l", graphs=graphs, buckets=(1,), max_batch=1, kv_cache_tokens=8192)
+    eng = _engine("llama3-8b-2l", graphs=graphs, buckets=(1, 2), max_batch=2, kv_cache_tokens=8192)
     be = EngineLLM(eng, max_new_tokens=16, ignore_eos=True)
     sch, r = eng.scheduler, eng.runner
     sch.gather_max_s = 0.0
+    sch.prefill_max_wait_s = 0.0
     m = r.model
     with torch.inference_mode():
-        ids = be.prompt_ids("list all pods in kube-system")
-        if long_ctx:
-            ids = ids + [(7 * i + 11) % 5000 + 100 for i in range(400 - len(ids))]
-        sch.add(Sequence(prompt_ids=ids, params=SamplingParams(max_new_tokens=16, ignore_eos=True)))
+        for b in range(B):
+            ids = be.prompt_ids(["list all pods in kube-system", "show services in namespace prod"][b])
+            if long_ctx and b == 0:
+                ids = ids + [(7 * i + 11) % 5000 + 100 for i in range(400 - len(ids))]
+            sch.add(Sequence(prompt_ids=ids, params=SamplingParams(max_new_tokens=16, ignore_eos=True)))
         while sch.waiting:   # a long prompt may take several (chunked) prefill steps
             b = sch.schedule()
             eng._apply(b, r.execute(b))
             sch.on_step_done(b)
         for step in range(6):
             batch = sch.schedule()
-            assert batch.is_decode and len(batch.seqs) == 1
-            r._pack_decode(batch, 1)
-            n = r._off["bt"] + r.max_blocks
+            assert batch.is_decode and len(batch.seqs) == B
+            r._pack_decode(batch, B)
+            n = r._off["bt"] + B * r.max_blocks
             r.d_stage[:n].copy_(r.h_stage[:n])
-            meta = AttnMeta(positions=r._view("pos", 1), slot_mapping=r._view("slots", 1),
-                            block_tables=r._view("bt", 1), ctx_lens=r._view("ctx", 1),
-                            logits_indices=r.d_logits_idx[:1], is_decode=True)
-            ids = r._view("ids", 1)
+            meta = AttnMeta(positions=r._view("pos", B), slot_mapping=r._view("slots", B),
+                            block_tables=r._view("bt", B), ctx_lens=r._view("ctx", B),
+                            logits_indices=r.d_logits_idx[:B], is_decode=True)
+            ids = r._view("ids", B)
             kc, vc = r.k_cache.clone(), r.v_cache.clone()
             kr, vr = r.k_cache.clone(), r.v_cache.clone()
             m.persistent = False
@@ -494,34 +498,37 @@ def test_persistent_decode_matches_kernel_chain_and_fp32(graphs, long_ctx):
             with ops.force_reference():
                 h_ref = m.forward(ids, meta, kr, vr)
             m.persistent = True
-            assert m.persistent_ok()
+            assert m.persistent_ok(B)
             kp, vp = r.k_cache.clone(), r.v_cache.clone()
             h_p = m.forward(ids, meta, kp, vp)
             torch.cuda.synchronize()
             assert m.persistent_err() == 0
             torch.testing.assert_close(h_p.float(), h_ref.float(), atol=0.1, rtol=0.05)
             torch.testing.assert_close(h_p.float(), h_chain.float(), atol=0.1, rtol=0.05)
-            slot = int(r._view("slots", 1)[0])
-            blk, off = slot // 16, slot % 16
-            # layer 0's appended K / V come from the same embedding: bf16-exact up to the norm's
-            # rounding; later layers see the fp32 residual stream (the chain's is bf16)
-            for kk, ref_c, tol in ((kp, kc, 2e-2), (vp, vc, 2e-2)):
-                got = kk[0, blk, :, off] if kk is kp else kk[0, blk, :, :, off]
-                want = ref_c[0, blk, :, off] if kk is kp else ref_c[0, blk, :, :, off]
-                torch.testing.assert_close(got.float(), want.float(), atol=tol, rtol=tol)
-            torch.testing.assert_close(kp[:, blk, :, off].float(), kc[:, blk, :, off].float(), atol=0.1, rtol=0.05)
-            torch.testing.assert_close(vp[:, blk, :, :, off].float(), vc[:, blk, :, :, off].float(), atol=0.1, rtol=0.05)
-            mask = r._view("mask", 1) if r.mask_bits is not None else None
-            tok = m.sample(h_p, r.mask_bits, mask)[:1].tolist()
-            if graphs:   # the captured B = 1 graph runs the same kernel: the same token
+            for b in range(B):
+                slot = int(r._view("slots", B)[b])
+                blk, off = slot // 16, slot % 16
+                # layer 0's appended K / V come from the same embedding: bf16-exact up to the norm's
+                # rounding; later layers see the fp32 residual stream (the chain's is bf16)
+                for kk, ref_c, tol in ((kp, kc, 2e-2), (vp, vc, 2e-2)):
+                    got = kk[0, blk, :, off] if kk is kp else kk[0, blk, :, :, off]
+                    want = ref_c[0, blk, :, off] if kk is kp else ref_c[0, blk, :, :, off]
+                    torch.testing.assert_close(got.float(), want.float(), atol=tol, rtol=tol)
+                torch.testing.assert_close(kp[:, blk, :, off].float(), kc[:, blk, :, off].float(), atol=0.1, rtol=0.05)
+                torch.testing.assert_close(vp[:, blk, :, :, off].float(), vc[:, blk, :, :, off].float(), atol=0.1,
+                                           rtol=0.05)
+            mask = r._view("mask", B) if r.mask_bits is not None else None
+            tok = m.sample(h_p, r.mask_bits, mask)[:B].tolist()
+            if graphs:   # the captured bucket-B graph runs the same kernel: the same tokens
                 r.graphs.clear()
                 r.graph_pool = None
                 r.capture_graphs(autotune=False)
-                r._pack_decode(batch, 1)          # capture_graphs reset the staging image
+                assert r.graph_persistent.get(B)
+                r._pack_decode(batch, B)          # capture_graphs reset the staging image
                 r.d_stage[:n].copy_(r.h_stage[:n])
-                r.graphs[1].replay()
+                r.graphs[B].replay()
                 torch.cuda.synchronize()
-                assert r.d_out[:1].tolist() == tok, (step, r.d_out[:1].tolist(), tok)
+                assert r.d_out[:B].tolist() == tok, (step, r.d_out[:B].tolist(), tok)
                 assert m.persistent_err() == 0
             else:   # the persistent step's cache writes are the real ones from here on
                 r.k_cache.copy_(kp)
