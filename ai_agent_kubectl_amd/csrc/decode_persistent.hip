@@ -47,9 +47,10 @@ namespace pd {
 #endif
 constexpr int NT = 512, NW = NT / 64, HD = 128, KBS = 16, NT_ = NT;
 // LDS-DMA ring slots (1 KB) per wave: KA_PD_RING (16) in every phase, except the down rows at B = 2,
-// whose two act rows (2 x I bf16) take LDS the ring gives up there (8 slots, 64 KB per CU in flight)
+// whose two act rows (2 x I bf16) take LDS the ring gives up there (12 slots, 96 KB per CU in flight;
+// 8 slots measured 16.4 us per layer for the down rows against 13.2 at B = 1)
 template <int B>
-constexpr int ring_down() { return B == 1 ? KA_PD_RING : 8; }
+constexpr int ring_down() { return B == 1 ? KA_PD_RING : 12; }
 static_assert((KA_PD_RING & (KA_PD_RING - 1)) == 0 && KA_PD_RING >= 2 && KA_PD_RING <= 16, "ring: a power of two <= 16");
 constexpr int MAXB = 2;     // sequences per launch
 constexpr int XS_MIN = 29 * 1024;   // the attention leader's scratch (aliases the x rows): 28.3 KB
@@ -263,6 +264,7 @@ struct RowVals {
 
 template <int B, int RG, class RowFn>
 struct Stream {
+  static_assert(RG >= 2 && RG <= 16 && RG % 2 == 0, "ring slots: even, <= 16 (RG - 2 pieces in flight per wait)");
   const bf16_t* W;
   int K, KC, total, lane;
   RowFn row;
@@ -271,7 +273,7 @@ struct Stream {
   int issued, ni, nc;   // pieces issued; row / chunk of the next piece to issue
   int rot;              // every row is read from chunk `rot` on, wrapping (see make_stream)
   KA_DEV void issue() {
-    const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + (uint32_t)(issued & (RG - 1)) * 1024u);
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(ring + ((uint32_t)issued % (uint32_t)RG) * 1024u);
     // wave-uniform part of the byte offset (row start + chunk) -> soffset; the lane's 16 B -> voffset
     const int c = nc + rot >= KC ? nc + rot - KC : nc + rot;
     const uint32_t so = __builtin_amdgcn_readfirstlane(((uint32_t)row(ni) * (uint32_t)K + (uint32_t)(c * 512)) * 2u);
@@ -339,7 +341,7 @@ struct Stream {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RG - 2) : "memory");   // pieces j, j + 1 have landed
       const int xc = cc + rot >= KC ? cc + rot - KC : cc + rot;   // x chunks of pieces j, j + 1
       const int xc1 = xc + 1 == KC ? 0 : xc + 1;
-      const uint32_t r0 = ring + (uint32_t)(j & (RG - 1)) * 1024u + lo16, r1 = ring + (uint32_t)((j + 1) & (RG - 1)) * 1024u + lo16;
+      const uint32_t r0 = ring + ((uint32_t)j % (uint32_t)RG) * 1024u + lo16, r1 = ring + ((uint32_t)(j + 1) % (uint32_t)RG) * 1024u + lo16;
       const uint32_t a0 = xaddr + (uint32_t)xc * 1024u + lo16, a1 = xaddr + (uint32_t)xc1 * 1024u + lo16;
       uint4 w0, w1, x0[B], x1[B];
       if constexpr (B == 1) {
@@ -369,7 +371,7 @@ struct Stream {
     }
     if (j < total) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RG - 1) : "memory");
-      const uint32_t r0 = ring + (uint32_t)(j & (RG - 1)) * 1024u + lo16;
+      const uint32_t r0 = ring + ((uint32_t)j % (uint32_t)RG) * 1024u + lo16;
       const uint32_t a0 = xaddr + (uint32_t)(cc + rot >= KC ? cc + rot - KC : cc + rot) * 1024u + lo16;
       uint4 w0, x0[B];
       if constexpr (B == 1) {
@@ -443,6 +445,59 @@ KA_DEV void rmsnorm_to_lds(const Args& a, const float* res, const bf16_t* g, bf1
     }
   }
   __syncthreads();
+}
+
+// x_b = bf16(res_b * rstd_b * g) for the B rows at once (B = 2, H <= 8192): every row's residual loaded
+// before one reduction of the B sums of squares (one workgroup barrier instead of B)
+template <int B>
+KA_DEV void rmsnorm_rows_to_lds(const Args& a, const float* res, const bf16_t* g, bf16_t* xs, int xstride, float* red) {
+  if constexpr (B == 1) {
+    rmsnorm_to_lds(a, res, g, xs, red);
+  } else {
+    const int H = a.H, n16 = H / 4;   // <= 4 NT (ka_decode_persistent_max_b)
+    uint4 rv[B][4];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const uint4* rp = reinterpret_cast<const uint4*>(res + (size_t)b * H);
+      ld4_sc1(rp + min((int)threadIdx.x, n16 - 1), rp + min((int)threadIdx.x + NT, n16 - 1),
+              rp + min((int)threadIdx.x + 2 * NT, n16 - 1), rp + min((int)threadIdx.x + 3 * NT, n16 - 1), rv[b]);
+    }
+    float ss[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      ss[b] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if ((int)threadIdx.x + k * NT < n16) {
+          const float4 f = __builtin_bit_cast(float4, rv[b][k]);
+          ss[b] += f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+        }
+      }
+      ss[b] = wave_sum(ss[b]);
+      if ((threadIdx.x & 63) == 0) red[b * NW + (threadIdx.x >> 6)] = ss[b];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      float tot = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) tot += red[b * NW + w];
+      const float rstd = rsqrtf(tot / (float)H + a.eps);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = (int)threadIdx.x + k * NT;
+        if (i < n16) {
+          const float4 f = __builtin_bit_cast(float4, rv[b][k]);
+          const uint2 gw = *reinterpret_cast<const uint2*>(g + 4 * i);
+          uint2 o;
+          o.x = pack2(f.x * rstd * lo_f(gw.x), f.y * rstd * hi_f(gw.x));
+          o.y = pack2(f.z * rstd * lo_f(gw.y), f.w * rstd * hi_f(gw.y));
+          *reinterpret_cast<uint2*>(xs + (size_t)b * xstride + 4 * i) = o;
+        }
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // LDS layout (bytes), phase by phase (each region is dead when the next phase's DMA reaches it):
@@ -552,8 +607,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     sq.template top_up<KA_PD_PREISSUE>();
     PD_STAMP(0);
     if (st && l > 0) st[(l - 1) * 16 + 12] = st[l * 16];   // the previous layer's barrier E ends here
-#pragma unroll
-    for (int b = 0; b < B; ++b) rmsnorm_to_lds(a, a.res + (size_t)b * H, Lw.ln1, xs + b * (xhb / 2), red);
+    rmsnorm_rows_to_lds<B>(a, a.res, Lw.ln1, xs, xhb / 2, red);
     PD_STAMP(1);
     {
       const RowVals<B> v = sq.run(xaddr, (uint32_t)xhb);
@@ -790,8 +844,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     sg.template top_up<KA_PD_PREISSUE>();
     PD_STAMP(7);
     // ---- P4: norm + gate / up -> act ----
-#pragma unroll
-    for (int b = 0; b < B; ++b) rmsnorm_to_lds(a, a.res + (size_t)b * H, Lw.ln2, xs + b * (xhb / 2), red);
+    rmsnorm_rows_to_lds<B>(a, a.res, Lw.ln2, xs, xhb / 2, red);
     PD_STAMP(8);
     {
       const RowVals<B> v = sg.run(xaddr, (uint32_t)xhb);   // lane 2 k: gate row k, lane 2 k + 1: its up row
@@ -869,7 +922,7 @@ static int pd_layout(int B, int H, int hq, int I, pd::Args* a) {
   const int xh = kb(std::max(H, hq * 128) * 2), xs = kb(std::max(std::max(H, I), hq * 128) * 2);
   const int ring = std::max(B * (B == 1 ? xs : xh), pd::XS_MIN);
   const int ring_d = B == 1 ? ring : B * xs;
-  const int rd = B == 1 ? KA_PD_RING : 8;
+  const int rd = B == 1 ? KA_PD_RING : 12;
   const int red = std::max(ring + pd::NW * KA_PD_RING * 1024, ring_d + pd::NW * rd * 1024);
   if (a) {
     a->xh_bytes = B == 1 ? xs : xh;
@@ -883,7 +936,7 @@ static int pd_layout(int B, int H, int hq, int I, pd::Args* a) {
 
 // Largest batch (1 or 2) the persistent kernel takes for this model within the LDS of one CU; 0: none.
 extern "C" int ka_decode_persistent_max_b(int H, int hq, int I) {
-  if (pd_layout(2, H, hq, I, nullptr) <= 160 * 1024) return 2;
+  if (H <= 4 * pd::NT * 4 && pd_layout(2, H, hq, I, nullptr) <= 160 * 1024) return 2;   // rmsnorm_rows_to_lds
   if (pd_layout(1, H, hq, I, nullptr) <= 160 * 1024) return 1;
   return 0;
 }

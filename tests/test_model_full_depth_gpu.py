@@ -7,7 +7,8 @@ the fp32 torch references (`ops.force_reference`) on the same random-init weight
 
 * a >= 1024-row prefill step through the prefill kernels, with the logits error recorded at depth
   2 / 8 / 16 / 32 (the model's first d layers, then the final norm and LM head);
-* 8 decode steps at B = 1 (the persistent all-layers kernel, eagerly and as the captured graph);
+* 8 decode steps at B = 1 and at B = 2 (the persistent all-layers kernel, eagerly and as the captured
+  graph);
 * 8 decode steps at B = 256 (the kernel chain of the headline's decode bucket, eagerly and as the
   captured graph).
 Each decode step compares the HIP forward with the reference forward on clones of the same KV cache
@@ -48,7 +49,7 @@ def _growth_ok(rows):
 
 @pytest.fixture(scope="module")
 def eng():
-    opts = EngineOptions(model="llama3-8b", device="cuda", max_batch=256, graph_buckets=(1, 256),
+    opts = EngineOptions(model="llama3-8b", device="cuda", max_batch=256, graph_buckets=(1, 2, 256),
                          kv_cache_tokens=49152, max_model_len=1024, max_batched_tokens=16384, use_graphs=True)
     e = build_engine(opts)
     assert len(e.runner.model.layers) == 32
@@ -147,7 +148,7 @@ def _decode_run(eng, B, steps=8):
             lg = m.logits(h).float()[:B]
             mask = r._view("mask", B) if r.mask_bits is not None else None
             tok = m.sample(h, r.mask_bits, mask)[:B].tolist()
-            if B == 1:
+            if B <= 2:
                 torch.cuda.synchronize()
                 assert m.persistent_err() == 0
             del kc, vc
@@ -159,7 +160,7 @@ def _decode_run(eng, B, steps=8):
             g.replay()   # the real cache gets this step's keys / values from the graph
             torch.cuda.synchronize()
             assert r.d_out[:B].tolist() == tok, step
-            if B == 1:
+            if B <= 2:
                 assert m.persistent_err() == 0
             eng._apply(batch, tok)
             sch.on_step_done(batch)
@@ -173,6 +174,18 @@ def test_full_depth_decode_b1_persistent(eng):
     assert m.persistent_ok() and eng.runner.graph_persistent.get(1)
     res = _decode_run(eng, 1)
     print("\nB=1 persistent decode, 32 layers: per-step (cos, max|d|, rel):",
+          [tuple(round(v, 4) for v in x) for x in res])
+    for cos, err, rel in res:
+        assert cos > COS_MIN and rel < REL_MAX, res
+
+
+def test_full_depth_decode_b2_persistent(eng):
+    """The persistent kernel at B = 2 (both sequences' rows against one weight stream, a leader per
+    sequence and KV group) over the full 32 layers."""
+    m = eng.runner.model
+    assert m.persistent_ok(2) and eng.runner.graph_persistent.get(2)
+    res = _decode_run(eng, 2)
+    print("\nB=2 persistent decode, 32 layers: per-step (cos, max|d|, rel):",
           [tuple(round(v, 4) for v in x) for x in res])
     for cos, err, rel in res:
         assert cos > COS_MIN and rel < REL_MAX, res
