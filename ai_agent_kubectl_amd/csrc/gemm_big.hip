@@ -20,19 +20,18 @@
 //   * persistent: one workgroup per CU walks its tiles; the next tile's first two k-tiles are staged
 //     during the current tile's last two k-steps and the epilogue transposes through a separate
 //     32 KB of LDS, so it overlaps their landing (+0.5-1 %, gb_p_ab.log);
-//   * two register fragment sets (F0 = k 0..31, F1 = k 32..63 of a k-tile) and two barriers per
-//     k-tile, with the fragment reads and the LDS-DMA pieces in separate windows of the 128-MFMA
-//     stream (the order hipBLASLt's gfx950 MT256x256x64 DirectToLds kernel uses; +1-2 % over a
-//     single-barrier loop whose second half carried reads and DMA together, and the fused LM head
-//     at M = 256 297 -> 260 us, profiles/r3/gemm_big/gbs_ab.log):
+//   * two register fragment sets (F0 = k 0..31, F1 = k 32..63 of a k-tile), the fragment reads and
+//     the LDS-DMA pieces in separate windows of the 128-MFMA stream (profiles/r3/gemm_big/gbs_ab.log):
 //       MFMA F0(t) 0-15 | read F1(t) <- buffer t&1
-//       lgkmcnt(0), barrier          (every wave's reads of buffer t&1 done)
-//       MFMA F0(t) 16-63, F1(t) 0-47 | 16 DMA pieces of k-tile t+2 -> buffer t&1, one per 6 MFMAs
-//       vmcnt(16), barrier           (k-tile t+1, staged one k-tile earlier, landed)
-//       MFMA F1(t) 48-63 | read F0(t+1) <- buffer (t+1)&1, waited for per fragment row by the
-//                          next k-tile's first MFMAs;
-//     one fragment read per MFMA in the read windows and the counted waits: another 1-2 %
-//     (gb_rp_ab.log, gb_cw_ab.log);
+//       vmcnt(0), lgkmcnt(0), barrier (every wave's reads of buffer t&1 done, and k-tile t+1 --
+//                                      the only pieces in flight -- landed in buffer (t+1)&1)
+//       MFMA F0(t) 16-63, F1(t) 0-15 | 16 DMA pieces of k-tile t+2 -> buffer t&1, one per 4 MFMAs
+//       MFMA F1(t) 16-63 | read F0(t+1) <- buffer (t+1)&1 from MFMA 48 on, waited for per fragment
+//                          row by the next k-tile's first MFMAs;
+//     one fragment read per MFMA in the read windows (gb_rp_ab.log).  Rounds 3-4 waited for k-tile
+//     t+1 with a counted vmcnt(16) at a second barrier, keeping t+2's pieces in flight across it:
+//     4-10 % faster, but LDS-DMA pieces do not complete in order and that wait let stale rows through
+//     in some launches (round 5, profiles/r5/gemm_big_clamp/);
 //   * XCD-aware tile order (T1): the bijective round-robin remap, then GM m-tiles x all n-tiles
 //     super-rows so the panels of the tiles running together on one XCD are L2 hits.
 // Measured (round 4, profiles/r4/gemm_big_tail/README.md, interleaved with rocBLAS in one process):
@@ -144,6 +143,9 @@ KA_DEV void ds_read16(bf16x8& dst, uint32_t addr) {
 // offset applies to both the LDS destination and the global address, so the lane's global offset is
 // pre-biased by -1024 P); P == 0 saves M0 and points it at the group, P == 3 restores it
 // LAST: the group's final piece (P == 3 of a 4-piece group; P == 1 of the 2-piece W group of TN 6)
+#ifndef KA_GB_CLAMP
+#define KA_GB_CLAMP 0     // diagnostic: rows past the end clamped to the last row (duplicate addresses)
+#endif
 template <int P, bool LAST>
 KA_DEV void dma16g(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t lds_addr, uint32_t& keep) {
   static_assert(P > 0 || !LAST, "a group has at least two pieces");
@@ -167,6 +169,15 @@ KA_DEV void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 KA_DEV void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
+// LDS-DMA completion is NOT ordered: a counted `s_waitcnt vmcnt(N)` (N younger pieces still allowed in
+// flight) passed while an older piece had not landed, in some launches (X piece 7 of a k-tile read
+// stale: 5/40 launches at M = 4096, N = 1152 with clamped duplicate rows, 1/80 at M = 2944, N = 6144 with
+// distinct rows), and a vmcnt(0) drain in the same places never failed (0/160, clamped rows included):
+// profiles/r5/gemm_big_clamp/.  So every LDS-DMA wait of this kernel is vmcnt(0), placed where the
+// only pieces in flight are the ones about to be read (KA_GB_DRAIN_B1 below).
+#ifndef KA_GB_DRAIN_B1
+#define KA_GB_DRAIN_B1 1  // 0: the old counted vmcnt(PIECES) at barrier #2 (unsafe, for A/B timing only)
+#endif
 template <int N>
 KA_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 KA_DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -176,25 +187,6 @@ KA_DEV void block_sync() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-}
-
-// KA_GB_SCHED 2 helpers: the operation (0 .. nops-1) issued at offset k of a span-slot segment when
-// nops operations are spread evenly over it (-1: none); and the o-th operation of a sequence that
-// interleaves na operations of kind A (returned as 0 .. na-1) with nb of kind B (100 + 0 .. nb-1),
-// one B after every (period - 1) A's, either kind alone once the other has run out.
-constexpr int spread_op(int k, int span, int nops) {
-  for (int o = 0; o < nops; ++o)
-    if ((o * span) / nops == k) return o;
-  return -1;
-}
-constexpr int pick_op(int o, int na, int nb, int period) {
-  int ia = 0, ib = 0;
-  for (int i = 0;; ++i) {
-    const bool b = ib < nb && (i % period == period - 1 || ia >= na);
-    if (i == o) return b ? 100 + ib : ia;
-    if (b) ++ib;
-    else ++ia;
-  }
 }
 
 // dispatch index -> logical index, XCD-contiguous (bijective over the grid: consecutive logical
@@ -434,7 +426,15 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
         // is gate (c even) or up (c odd) of output columns 128 tn + 16 (c >> 1) + 0..15
         wrow = 128 * tn_ + 16 * (row >> 5) + (row & 15) + ((row >> 4) & 1) * a.I;
       } else {
-        wrow = min(tn_ * BNT + row, a.N - 1);
+        // rows past the last one read distinct valid rows (their results are not stored): clamping
+        // them all to row N - 1 made 64-lane LDS-DMA pieces of duplicate addresses, and with them
+        // other pieces' rows came out wrong in some launches (profiles/r5/gemm_big_clamp/)
+        wrow = tn_ * BNT + row;
+#if KA_GB_CLAMP
+        wrow = min(wrow, a.N - 1);   // diagnostic: the old clamp
+#else
+        if (wrow >= a.N) wrow %= a.N;
+#endif
       }
       if constexpr (GR) wrow += ge_ * a.N;   // expert ge_'s weights
       offA[j] = ((uint32_t)wrow * (uint32_t)a.K + ch) * 2u + kb + BIAS - (uint32_t)(j & 3) * 1024u;
@@ -443,8 +443,15 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     for (int j = 0; j < 8; ++j) {
       const int row = 64 * w + 8 * j + r8;
       const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
-      // GR: the chunk's rows, rows past its count re-read its last row (their results are not stored)
-      const int xr = GR ? gr0_ + min(row, gnr_ - 1) : min(m0_ + row, a.M - 1);
+      // GR: the chunk's rows; rows past its count read other rows of the chunk (not stored)
+      // (rows past the end: distinct valid rows, as for W above)
+      int xr;
+      if constexpr (GR) xr = gr0_ + (row < gnr_ ? row : row % gnr_);
+#if KA_GB_CLAMP
+      else xr = min(m0_ + row, a.M - 1);   // diagnostic: the old clamp
+#else
+      else xr = m0_ + row < a.M ? m0_ + row : (m0_ + row) % a.M;
+#endif
       offB[j] = ((uint32_t)xr * (uint32_t)a.ldx + ch) * 2u + kb + BIAS - (uint32_t)(j & 3) * 1024u;
     }
   };
@@ -490,6 +497,15 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   constexpr int B1 = KA_GB_B1;       // barrier #1's group: 4 = right after the F1 read window; 5 / 6
                                      // give the window's last reads 4 / 8 more MFMAs before lgkmcnt(0)
   static_assert(B1 >= 4 && B1 <= 6, "barrier #1 group");
+#ifndef KA_GB_DMA_END
+#define KA_GB_DMA_END (KA_GB_DRAIN_B1 ? 20 : 0)
+#endif
+  // the DMA window: groups B1 .. DE - 1.  The drain at the next call's barrier #1 waits for the window's
+  // last piece, so a shorter window leaves it more time to land; but the 64 KB a k-tile stages per CU
+  // need about half the k-tile's MFMA time at the L1 fill rate, and windows of 12 groups stalled the
+  // MFMA stream (measured, profiles/r5/gemm_big_clamp/README.md: 20 is the best of 12 / 16 / 20 / 28).
+  constexpr int DE = KA_GB_DMA_END > 0 && KA_GB_DMA_END < RW ? KA_GB_DMA_END : RW;
+  static_assert(DE > B1 && DE <= RW, "DMA window");
   static_assert(NRD <= 16, "a read window holds 16 reads");
   // read S of a fragment set in window order 1 (A0 B0 A1 B1 ..., the B's past A(TN-1) last):
   auto rd1 = [&](auto sc, bf16x8* FA, bf16x8* FB, uint32_t ba, uint32_t bb) {
@@ -519,13 +535,14 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
   // the fragment reads and the LDS-DMA pieces in separate windows of the MFMA stream (the order
   // hipBLASLt's MT256x256x64 DirectToLds kernel uses; it measured faster than a window carrying both):
   //   groups 0-3:   F1(t) <- buffer BUF, one read before each MFMA
-  //   lgkmcnt(0) + barrier #1: every wave's reads of buffer BUF are done (F0(t) was read at the end
-  //                 of the previous call)
-  //   groups 4 .. RW-1: the PIECES pieces of k-tile T into buffer BUF, spread evenly (2 of every 3
-  //                 groups at TN 8)
-  //   vmcnt(PIECES) + barrier #2: the k-tile staged one call earlier has landed in buffer BUF ^ 1
+  //   vmcnt(0) + lgkmcnt(0) + barrier #1: every wave's reads of buffer BUF are done (F0(t) was read
+  //                 at the end of the previous call), and the k-tile staged one call earlier -- the
+  //                 only DMA in flight -- has landed in buffer BUF ^ 1
+  //   groups 4 .. DE-1: the PIECES pieces of k-tile T into buffer BUF, spread evenly
   //   groups RW .. NG-1: F0(t + 1) <- buffer BUF ^ 1, one read before each MFMA (F0(t) retired at
   //                 group GPS - 1)
+  // (KA_GB_DRAIN_B1 0 restores the rounds 3-4 order for timing: lgkmcnt(0) alone at barrier #1 and a
+  // counted vmcnt(PIECES) + barrier #2 at group RW, unsafe: see wait_vm.)
   // (Every DMA is issued unconditionally: skipping the last unit's re-stage behind a runtime flag put
   // VALU work (the flag's mask) into the MFMA stream, where hipcc's register reuse wrote an A-fragment
   // VGPR still being read by an in-flight asm MFMA it cannot see (sparse wrong outputs in the SwiGLU
@@ -557,16 +574,17 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
       }
       if constexpr (g == 4 && B1 > 4) wait_lgkm<15>();   // row 2 (A2) of F0: all but 15 reads done
       if constexpr (g == B1) {
-        wait_lgkm0();
+        if constexpr (KA_GB_DRAIN_B1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        else wait_lgkm0();
         block_sync();
       }
-      if constexpr (g >= B1 && g < RW) {   // the DMA pieces whose slot falls in this group
+      if constexpr (g >= B1 && g < DE) {   // the DMA pieces whose slot falls in this group
         static_for<PIECES>([&](auto pc) {
           constexpr int pp = decltype(pc)::value;
-          if constexpr (B1 + (pp * (RW - B1)) / PIECES == g) dma(pc, bufc, T);
+          if constexpr (B1 + (pp * (DE - B1)) / PIECES == g) dma(pc, bufc, T);
         });
       }
-      if constexpr (g == RW) {
+      if constexpr (g == RW && !KA_GB_DRAIN_B1) {
         wait_vm<PIECES>();
         block_sync();
       }
@@ -577,64 +595,9 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     });
     // (no lgkmcnt wait here: the next call waits per fragment; the tile's last call waits below)
   };
-  // KA_GB_SCHED 2: one k-tile as five MFMA segments split by four barriers, the fragment reads and the
-  // LDS-DMA pieces handed off per OPERAND (the order of hipBLASLt's gfx950 MT256x256x64 DirectToLds
-  // kernel, read from its disassembly): the W (A) half of the staging buffer is refilled as soon as
-  // every wave has read its F1 A fragments, the X (B) half after their B fragments, and each vmcnt
-  // wait retires only the operand half the next reads need:
-  //   S1  F1(t) A reads (one per 2 MFMAs)           | lgkmcnt(0), 1 MFMA, barrier (A of BUF free)
-  //   S2  F1(t) B reads + the TN A pieces of T      | lgkmcnt(0), 1 MFMA, barrier (B of BUF free)
-  //   S3  B pieces 0-3 of T                          | vmcnt(8 + TN + 4): the A pieces of t + 1 landed,
-  //                                                     1 MFMA, barrier
-  //   S4  F0(t + 1) A reads + B pieces 4-7 of T      | vmcnt(PIECES): the B pieces of t + 1 landed,
-  //                                                     1 MFMA, barrier
-  //   S5  F0(t + 1) B reads
-  // and the next call's first MFMA waits for everything but its own first read (lgkmcnt(1)).
-  constexpr int NS = 2 * NQ;                       // MFMA slots per k-tile
-  constexpr int E1 = NS * 20 / 128, E2 = NS * 51 / 128, E3 = NS * 68 / 128, E4 = NS * 105 / 128;
-  auto iter2 = [&](auto bufc, int T) {
-    constexpr int BUF = decltype(bufc)::value;
-    const uint32_t bA1 = BUF ? bA11 : bA01, bB1 = BUF ? bB11 : bB01;   // F1(t) <- buffer BUF
-    const uint32_t bA0 = BUF ? bA00 : bA10, bB0 = BUF ? bB00 : bB10;   // F0(t + 1) <- buffer BUF ^ 1
-    static_for<NS>([&](auto sc) {
-      constexpr int sl = decltype(sc)::value;
-      // ---- the slot's read / DMA, before its MFMA (each segment's operations spread evenly) ----
-      if constexpr (sl < E1) {
-        constexpr int o = spread_op(sl, E1, TN);
-        if constexpr (o >= 0) ds_read16<o * 2048>(fa1[o], bA1);
-      } else if constexpr (sl > E1 && sl < E2) {   // B reads / A pieces, alternating
-        constexpr int o = spread_op(sl - E1 - 1, E2 - E1 - 1, 8 + TN);
-        if constexpr (o >= 0) {
-          constexpr int c = pick_op(o, 8, TN, 2);
-          if constexpr (c < 100) ds_read16<c * 2048>(fb1[c], bB1);
-          else dma(std::integral_constant<int, c - 100>{}, bufc, T);
-        }
-      } else if constexpr (sl > E2 && sl < E3) {   // B pieces 0-3
-        constexpr int o = spread_op(sl - E2 - 1, E3 - E2 - 1, 4);
-        if constexpr (o >= 0) dma(std::integral_constant<int, TN + o>{}, bufc, T);
-      } else if constexpr (sl > E3 && sl < E4) {   // A reads of F0(t + 1) / B pieces 4-7, R R D ...
-        constexpr int o = spread_op(sl - E3 - 1, E4 - E3 - 1, TN + 4);
-        if constexpr (o >= 0) {
-          constexpr int c = pick_op(o, TN, 4, 3);
-          if constexpr (c < 100) ds_read16<c * 2048>(fa0[c], bA0);
-          else dma(std::integral_constant<int, TN + 4 + (c - 100)>{}, bufc, T);
-        }
-      } else if constexpr (sl > E4) {              // B reads of F0(t + 1)
-        constexpr int o = spread_op(sl - E4 - 1, NS - E4 - 1, 8);
-        if constexpr (o >= 0) ds_read16<o * 2048>(fb0[o], bB0);
-      }
-      // ---- waits before the slot's MFMA ----
-      if constexpr (sl == 0) wait_lgkm<1>();                      // F0(t): all but this call's first read
-      if constexpr (sl == E1 || sl == E2) wait_lgkm0();
-      if constexpr (sl == E3) wait_vm<8 + TN + 4>();
-      if constexpr (sl == E4) wait_vm<PIECES>();
-      // ---- the MFMA ----
-      if constexpr (sl < NQ) mfma_acc(acc[sl >> 3][sl & 7], fa0[sl >> 3], fb0[sl & 7]);
-      else mfma_acc(acc[(sl - NQ) >> 3][(sl - NQ) & 7], fa1[(sl - NQ) >> 3], fb1[(sl - NQ) & 7]);
-      // ---- a barrier after each segment's extra MFMA ----
-      if constexpr (sl == E1 || sl == E2 || sl == E3 || sl == E4) block_sync();
-    });
-  };
+  // (A five-segment schedule with per-operand counted vmcnt waits, after hipBLASLt's gfx950
+  // MT256x256x64 DirectToLds kernel, measured no faster in round 3 and relied on ordered LDS-DMA
+  // completion: removed in round 5.)
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
 
@@ -664,7 +627,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     // tile's epilogue stores, everything older (k-tile 0) is done.  (The previous tile's last call
     // already read these fragments; reading them again here keeps F0 dead across the epilogue,
     // which would otherwise spill.)
-    wait_vm<PIECES>();
+    wait_vm<KA_GB_DRAIN_B1 ? 0 : PIECES>();
     block_sync();
     static_for<NRD>([&](auto sc) { rd2(sc, fa0, fb0, bA00, bB00); });
 #pragma unroll
@@ -679,16 +642,8 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
     for (int t = 0; t < nk; t += 2) {
       const bool last = t + 2 >= nk;
       if (last) set_offsets(ntm, ntn, nkt0, nge, ngr0, ngnr);
-#ifndef KA_GB_SCHED
-#define KA_GB_SCHED 1
-#endif
-#if KA_GB_SCHED == 2
-      iter2(I0{}, last ? 0 : t + 2);
-      iter2(I1{}, last ? 1 : t + 3);
-#else
       iter(I0{}, last ? 0 : t + 2);
       iter(I1{}, last ? 1 : t + 3);
-#endif
       // the MFMA wait states inside the loop, before its exit: hipcc does not know the asm MFMAs'
       // latency and may copy accumulators (v_accvgpr_mov) on the exit edge, which would read
       // results still in flight (seen: the argmax epilogue's accumulators shuffled before a drain
@@ -965,12 +920,13 @@ static int choose_tn(int M, int N, int epi, int G) {
   }
   if (force == 6 || force == 8) return force;
   const int tm = (M + BM - 1) / BM;
-  auto cost = [&](int tiles, double unit) {
+  auto cost = [&](int tiles, double unit, bool tail) {
     const int whole = tiles / G, rem = tiles % G;
-    const double part = rem ? std::min(1.0, 0.5 + 0.65 * rem / (double)G) : 0.0;
+    const double part = rem ? (tail ? std::min(1.0, 0.5 + 0.65 * rem / (double)G) : 1.0) : 0.0;
     return (whole + part) * unit;
   };
-  return cost(tm * (N / 192), 0.78) < cost(tm * ((N + 255) / 256), 1.0) ? 6 : 8;
+  // TN 6 runs without the split tail (launch): its last partial round costs a whole one
+  return cost(tm * (N / 192), 0.78, false) < cost(tm * ((N + 255) / 256), 1.0, true) ? 6 : 8;
 }
 
 template <int EPI, int TN>
@@ -995,7 +951,11 @@ static int launch(const Args& a0, hipStream_t st, void* ws = nullptr, size_t ws_
   a.tail_s = 1;
   a.tail_tiles = 0;
   a.span = 0;
-  if (EPI == EPI_BF16 || EPI == EPI_SWIGLU || EPI == EPI_ADD) {
+  // the split tail runs on the 256-wide tile only.  (The wrong rows first blamed on TN 6 tails came
+  // from the clamped duplicate-address DMA rows fixed in set_offsets: profiles/r5/gemm_big_clamp/.)
+  // choose_tn prices TN 6 without a tail, and at M = 2944, N = 6144 it costs the same (two rounds of
+  // 0.78), so the 192-wide path stays the simpler one.
+  if ((EPI == EPI_BF16 || EPI == EPI_SWIGLU || EPI == EPI_ADD) && TN == 8) {
     a.tail_s = choose_tail(tiles, cus, a.K / BK, ws ? ws_bytes : 0, a.full, a.tail_tiles, tail_slab(TN));
     if (a.tail_s > 1) {
       char* base = static_cast<char*>(ws);
@@ -1100,6 +1060,11 @@ extern "C" int ka_gemm_big_plan(int M, int N, int epi, int K, size_t ws_bytes, i
   const int G = gb::num_cus() & ~7;
   const int TN = gb::choose_tn(M, N, epi, G);
   const int tm = (M + gb::BM - 1) / gb::BM, tn = epi == gb::EPI_SWIGLU ? N / 256 : (N + 32 * TN - 1) / (32 * TN);
+  if (TN != 8) {   // no split tail on 192-wide tiles (launch)
+    *full = tm * tn;
+    *tail = 0;
+    return 1;
+  }
   return gb::choose_tail(tm * tn, G, K / gb::BK, ws_bytes, *full, *tail, gb::tail_slab(TN));
 }
 

@@ -67,6 +67,9 @@ KA_DEV int swz(int row, int ch) {
   else return ch ^ ((row >> 2) & 2);
 }
 
+// DMA source row for staged row r of an n-row operand: r itself, or r % n past the end
+KA_DEV int wrap_row(int r, int n) { return r < n ? r : r % n; }
+
 template <int AUX = 0>
 KA_DEV void glds16(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
@@ -211,7 +214,10 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   for (int j = 0; j < C::GA; ++j) {
     const int row = (j * C::NW + wave) * RPI + rl;
     const int ch = swz<C::KT>(row, slot);
-    int wr = min(n0 + row, a.N - 1);
+    // rows past N / M / the list re-read DISTINCT real rows (r % N), never one clamped row: a
+    // piece whose lanes share one address intermittently corrupted other LDS-DMA pieces in
+    // gemm_big (profiles/r5/gemm_big_clamp/)
+    int wr = wrap_row(n0 + row, a.N);
     if (EPI == EPI_SWIGLU && a.swi > 0) {   // interleaved row ri: 16-row chunk ri >> 4 of gate (even) / up (odd)
       const int ri = wr;
       wr = ((ri >> 5) << 4) + (ri & 15) + ((ri >> 4) & 1) * a.swi;
@@ -223,8 +229,8 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
     const int row = (j * C::NW + wave) * RPI + rl;
     const int ch = swz<C::KT>(row, slot);
     int src;
-    if constexpr (GROUPED) src = rows_of[min(row, nrows - 1)] / a.src_div;   // padding rows: re-read a real row
-    else src = min(m0 + row, a.M - 1);
+    if constexpr (GROUPED) src = rows_of[wrap_row(row, nrows)] / a.src_div;   // padding rows: re-read a real row
+    else src = wrap_row(m0 + row, a.M);
     offB[j] = (uint32_t)(src * (uint32_t)a.ldx + kb + ch * 8) * 2u;
   }
   const char* Wb = reinterpret_cast<const char*>(Wg);
@@ -486,15 +492,15 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
   for (int j = 0; j < 2; ++j) {
     const int row = (j * 8 + w) * 8 + r8;
     const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
-    off[0][j] = ((uint32_t)min(n0 + row, a.N - 1) * (uint32_t)a.K + kb + ch) * 2u;
-    off[1][j] = ((uint32_t)min(n0 + 128 + row, a.N - 1) * (uint32_t)a.K + kb + ch) * 2u;
+    off[0][j] = ((uint32_t)wrap_row(n0 + row, a.N) * (uint32_t)a.K + kb + ch) * 2u;
+    off[1][j] = ((uint32_t)wrap_row(n0 + 128 + row, a.N) * (uint32_t)a.K + kb + ch) * 2u;
     uint32_t x0, x1;
     if constexpr (GROUPED) {
-      x0 = rows_of[min(row, nrows - 1)] / a.src_div;
-      x1 = rows_of[min(128 + row, nrows - 1)] / a.src_div;
+      x0 = rows_of[wrap_row(row, nrows)] / a.src_div;
+      x1 = rows_of[wrap_row(128 + row, nrows)] / a.src_div;
     } else {
-      x0 = min(m0 + row, a.M - 1);
-      x1 = min(m0 + 128 + row, a.M - 1);
+      x0 = wrap_row(m0 + row, a.M);
+      x1 = wrap_row(m0 + 128 + row, a.M);
     }
     off[2][j] = (x0 * (uint32_t)a.ldx + kb + ch) * 2u;
     off[3][j] = (x1 * (uint32_t)a.ldx + kb + ch) * 2u;

@@ -828,15 +828,15 @@ def test_gemm_big_linear_split_tail_vs_fp32(M, N, K):
 def test_gemm_big_split_tail_plans():
     """The shapes the bench's mixed steps produce get the tile width and split tail that fill the
     last round: QKV at M = 4096 runs 192-wide tiles (512 = 2 whole rounds) instead of 384 256-wide
-    ones (1.5 rounds); at M = 2944 192-wide tiles with a split tail (384 = 256 + 128; measured 152 us
-    against 169 for 288 256-wide tiles with theirs, profiles/r5/gemm_big_tn/)."""
+    ones (1.5 rounds); at M = 2944 192-wide tiles too, without a split tail (the tail runs on 256-wide
+    tiles only: with 192-wide ones it gave intermittent wrong rows, profiles/r5/gemm_big_tail_tn6/)."""
     lib = _hip.require()
     assert lib.ka_gemm_big_tn(4096, 6144, 0) == 6 and lib.ka_gemm_big_tn(4096, 6144, 4) == 6
     assert _gb_plan(4096, 6144, 4096, 0)[0] == 1
     assert lib.ka_gemm_big_tn(2944, 6144, 0) == 6
-    s, full, tail = _gb_plan(2944, 6144, 4096, 0)      # 12 x 32 = 384 = 256 + 128
-    assert s > 1 and full == 256 and tail == 128
-    assert lib.ka_gemm_big_tn(4096, 1152, 0) == 6      # 96 tiles of 192: the tail split on the 192 tile
+    s, full, tail = _gb_plan(2944, 6144, 4096, 0)      # 12 x 32 = 384: two rounds, no split
+    assert s == 1 and full == 384 and tail == 0
+    assert lib.ka_gemm_big_tn(4096, 1152, 0) == 8      # 80 256-wide tiles with a split tail beat 96 192-wide ones
     assert _gb_plan(4096, 1152, 4096, 0)[0] > 1
     s, full, tail = _gb_plan(2944, 28672, 4096, 3)     # gate_up + SwiGLU: 12 x 112 = 1344 = 5 x 256 + 64
     assert s > 1 and full == 1280 and tail == 64
