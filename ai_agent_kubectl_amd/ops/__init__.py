@@ -853,8 +853,12 @@ def moe_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: to
 
 # MoE prefill expert GEMMs (KA_MOE_PREFILL): "big" = expert-sorted rows through csrc/gemm_big.hip's
 # grouped mode (256 x 256 tiles, SwiGLU epilogue), "gm" = the grouped gemm_mfma ring kernel over
-# gathered rows (MOE_GROUPED_CFG)
-MOE_PREFILL = os.environ.get("KA_MOE_PREFILL", "big")
+# gathered rows (MOE_GROUPED_CFG), "auto" (default) = big from MOE_BIG_MIN_ROWS routed rows up, gm
+# below.  Mixtral block, profiles/r5/gemm_big_clamp/replan/moe_prefill.log: T = 1024 (2048 rows) gm
+# 1.12 vs big 1.31 ms; T = 4096 big 3.02 vs gm 3.16; T = 8192 big 5.24 vs gm 5.88 (sorted hipBLASLt
+# 1.51 / 3.40 / 5.66).
+MOE_PREFILL = os.environ.get("KA_MOE_PREFILL", "auto")
+MOE_BIG_MIN_ROWS = int(os.environ.get("KA_MOE_BIG_MIN_ROWS", "6144"))
 
 
 def moe_big_ok(H: int, I: int, El: int) -> bool:
@@ -866,7 +870,7 @@ def moe_big_ok(H: int, I: int, El: int) -> bool:
 def moe_experts_grouped(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
                         topk_ids: torch.Tensor, e0: int) -> torch.Tensor:
     """Prefill-sized MoE block, device-resident end to end (no host sync): routing lists
-    (moe_align), then either (KA_MOE_PREFILL=big, the default) the routed rows sorted by expert
+    (moe_align), then either (KA_MOE_PREFILL=big, or auto at >= MOE_BIG_MIN_ROWS rows) the routed rows sorted by expert
     (moe_sort) -> grouped gemm_big gate_up with the SwiGLU epilogue -> grouped gemm_big down
     scattering each row back to its slot, or (gm) the grouped ring-kernel gate_up over gathered token
     rows -> SiLU·mul -> grouped down; then the weighted combine.  Same contract as `moe_experts`."""
@@ -880,7 +884,8 @@ def moe_experts_grouped(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, to
     lists = torch.empty((El, R), dtype=torch.int32, device=x.device)
     check(lib.ka_moe_align(_p(counts), _p(lists), _p(topk_ids), R, e0, El, st), "moe_align")
     I = two_i // 2
-    if MOE_PREFILL == "big" and moe_big_ok(H, I, El) and x.is_contiguous():
+    big = MOE_PREFILL == "big" or (MOE_PREFILL == "auto" and R >= MOE_BIG_MIN_ROWS)
+    if big and moe_big_ok(H, I, El) and x.is_contiguous():
         chunks = (R + 255) // 256 + El
         xs = torch.empty((R, H), dtype=x.dtype, device=x.device)
         slot = torch.empty(R, dtype=torch.int32, device=x.device)
