@@ -40,7 +40,7 @@
 // makes gate_up + SiLU a net win, which is what the engine dispatches (ops.linear_swiglu).
 // Engine dispatch: EPI_SWIGLU (prefill / mixed-step gate_up, ops.linear_swiglu) and EPI_ARGMAX (the
 // fused LM head, ops.lm_head_argmax, per decode bucket where ModelRunner.tune_lm_head times it
-// faster).  EPI_BF16 is the plain GEMM the harness (tools/gemm_big_bench.hip) and scripts/gb_diag.py
+// faster).  EPI_BF16 is the plain GEMM the harness (tools/gemm_big_bench.hip) and profiles/r3/scripts/gb_diag.py
 // compare against rocBLAS / fp32; EPI_ADD and the split-K slabs were measured for the O / down
 // projections and decode shapes and lost there (profiles/r3/gemm_big/), so nothing dispatches them.
 // Epilogues: bf16 store; SwiGLU over the un-interleaved [gate; up] weight (the tile's W rows are

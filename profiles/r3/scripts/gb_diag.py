@@ -3,7 +3,7 @@ repeated fused-LM-head runs against fp32, for the library named by KA_HIP_LIB (d
 import math
 import os
 
-sys_path_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys_path_root = os.path.abspath(os.path.join(os.path.dirname(__file__), '..', '..', '..'))
 import sys
 
 sys.path.insert(0, sys_path_root)

@@ -8,7 +8,7 @@ import math
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), '..', '..', '..')))
 import torch  # noqa: E402
 
 from ai_agent_kubectl_amd import ops  # noqa: E402

@@ -16,7 +16,7 @@ done
 for v in c1b db1; do
   echo "== $v" >> $O/diag.log
   KA_HIP_LIB=ai_agent_kubectl_amd/ops/lib/variants/libkagent_hip_$v.so DIAG_SHAPES=4096x1152x4096,2944x6144x4096 DIAG_REPS=60 \
-    timeout -k 10 300 python -u scripts/gb_wrong_rows_diag.py >> $O/diag.log 2>&1
+    timeout -k 10 300 python -u profiles/r5/gemm_big_clamp/gb_wrong_rows_diag.py >> $O/diag.log 2>&1
   rc=$?; [ $rc -eq 0 ] || stop $v $rc
 done
 echo ALL DONE

@@ -829,7 +829,7 @@ def test_gemm_big_split_tail_plans():
     """The shapes the bench's mixed steps produce get the tile width and split tail that fill the
     last round: QKV at M = 4096 runs 192-wide tiles (512 = 2 whole rounds) instead of 384 256-wide
     ones (1.5 rounds); at M = 2944 192-wide tiles too, without a split tail (the tail runs on 256-wide
-    tiles only: with 192-wide ones it gave intermittent wrong rows, profiles/r5/gemm_big_tail_tn6/)."""
+    tiles only; choose_tn prices 192-wide tiles without one)."""
     lib = _hip.require()
     assert lib.ka_gemm_big_tn(4096, 6144, 0) == 6 and lib.ka_gemm_big_tn(4096, 6144, 4) == 6
     assert _gb_plan(4096, 6144, 4096, 0)[0] == 1
@@ -843,6 +843,26 @@ def test_gemm_big_split_tail_plans():
     assert lib.ka_gemm_big_tn(2944, 28672, 3) == 8
     assert _gb_plan(4096, 4096, 4096, 0)[0] == 1       # O: exactly one round
     assert lib.ka_gemm_big_tn(4096, 4096, 0) == 8      # (4096 is no multiple of 192)
+
+
+def test_gemm_big_alternating_launches_exact():
+    """The launch pattern that exposed unordered LDS-DMA completion (profiles/r5/gemm_big_clamp/):
+    every gemm_big launch follows an unrelated GEMM, and every result is checked whole.  With the
+    old counted vmcnt wait, 4096 x 1152 (split tail, a partial last n-tile) and 2944 x 6144 (192-wide
+    tiles, a partial last m-tile) came out wrong in 1-25 % of launches; the drained schedule never."""
+    other = torch.randn(4096, 4096, device=DEV, dtype=BF)
+    wo = (torch.randn(6144, 4096, device=DEV) / 64).to(BF)
+    for (M, N, K) in [(4096, 1152, 4096), (2944, 6144, 4096)]:
+        x = torch.randn(M, K, device=DEV, dtype=BF)
+        w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(BF)
+        want = x.float() @ w.float().t()
+        bad = 0
+        for _ in range(24):
+            ops.linear_big(other, wo)
+            err = (ops.linear_big(x, w).float() - want).abs() > 0.03 + 0.02 * want.abs()
+            bad += int(bool(err.any()))
+        assert bad == 0, f"{M}x{N}x{K}: {bad} of 24 launches wrong"
+    assert ops.gemm_big_err(torch.device(DEV)) == 0
 
 
 @pytest.mark.parametrize("M", [2944, 1100, 4096])
