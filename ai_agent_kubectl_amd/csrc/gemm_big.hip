@@ -25,8 +25,8 @@
 //       MFMA F0(t) 0-15 | read F1(t) <- buffer t&1
 //       vmcnt(0), lgkmcnt(0), barrier (every wave's reads of buffer t&1 done, and k-tile t+1 --
 //                                      the only pieces in flight -- landed in buffer (t+1)&1)
-//       MFMA F0(t) 16-63, F1(t) 0-15 | 16 DMA pieces of k-tile t+2 -> buffer t&1, one per 4 MFMAs
-//       MFMA F1(t) 16-63 | read F0(t+1) <- buffer (t+1)&1 from MFMA 48 on, waited for per fragment
+//       MFMA F0(t) 16-63, F1(t) 0-31 | 16 DMA pieces of k-tile t+2 -> buffer t&1, one per 5 MFMAs
+//       MFMA F1(t) 32-63 | read F0(t+1) <- buffer (t+1)&1 from MFMA 48 on, waited for per fragment
 //                          row by the next k-tile's first MFMAs;
 //     one fragment read per MFMA in the read windows (gb_rp_ab.log).  Rounds 3-4 waited for k-tile
 //     t+1 with a counted vmcnt(16) at a second barrier, keeping t+2's pieces in flight across it:
@@ -498,12 +498,13 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args a) {
                                      // give the window's last reads 4 / 8 more MFMAs before lgkmcnt(0)
   static_assert(B1 >= 4 && B1 <= 6, "barrier #1 group");
 #ifndef KA_GB_DMA_END
-#define KA_GB_DMA_END (KA_GB_DRAIN_B1 ? 20 : 0)
+#define KA_GB_DMA_END (KA_GB_DRAIN_B1 ? 24 : 0)
 #endif
   // the DMA window: groups B1 .. DE - 1.  The drain at the next call's barrier #1 waits for the window's
   // last piece, so a shorter window leaves it more time to land; but the 64 KB a k-tile stages per CU
   // need about half the k-tile's MFMA time at the L1 fill rate, and windows of 12 groups stalled the
-  // MFMA stream (measured, profiles/r5/gemm_big_clamp/README.md: 20 is the best of 12 / 16 / 20 / 28).
+  // MFMA stream (measured, profiles/r5/gemm_big_clamp/README.md: 12 / 16 lose 3-10 %, 20-28 are within
+  // 2 % of each other, 24 the best on the gate_up + SwiGLU shape).
   constexpr int DE = KA_GB_DMA_END > 0 && KA_GB_DMA_END < RW ? KA_GB_DMA_END : RW;
   static_assert(DE > B1 && DE <= RW, "DMA window");
   static_assert(NRD <= 16, "a read window holds 16 reads");
