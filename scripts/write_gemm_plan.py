@@ -34,18 +34,26 @@ COPY_TO = os.environ.get("PLAN_COPY_TO")   # e.g. gpurun_out/tuned: a copy after
 BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512)
 if os.environ.get("PLAN_BUCKETS"):   # re-tune (and re-write) only these buckets, e.g. "1,2,4"
     BUCKETS = tuple(int(b) for b in os.environ["PLAN_BUCKETS"].split(","))
-ONLY = os.environ.get("PLAN_ONLY", "")   # "prefill": re-tune only the prefill section (after a gemm_big change)
+# "prefill": re-tune only the prefill section (after a gemm_big change); "epilogues": only the lm_head and
+# decode_swiglu sections (the fused gemm_big / ring-kernel epilogues against the unfused plan)
+ONLY = os.environ.get("PLAN_ONLY", "")
 for model in sys.argv[1:] or ["llama3-8b"]:
     eng = build_engine(EngineOptions(model=model, device="cuda", max_batch=max(BUCKETS), graph_buckets=BUCKETS,
                                      kv_cache_tokens=65536, max_model_len=512))
     rep = {}
-    if ONLY != "prefill":
+    if ONLY not in ("prefill", "epilogues"):
         rep = eng.runner.autotune()
         print(model, len(rep), "plan entries", flush=True)
+    if ONLY == "epilogues":   # the unfused side of each comparison runs the persisted GEMM plan
+        os.environ["KA_GEMM_PLAN"] = "file"
+        print(model, "GEMM plan:", eng.runner.autotune(), flush=True)
+        os.environ["KA_GEMM_PLAN"] = "write"
+    if ONLY != "prefill":
         # the engine-start decisions persisted next to the plan (sections lm_head / decode_swiglu)
         print("lm_head:", eng.runner.tune_lm_head(), flush=True)
         print("decode_swiglu:", eng.runner.tune_swiglu(), flush=True)
-    print("prefill:", eng.runner.tune_prefill(), flush=True)
+    if ONLY != "epilogues":
+        print("prefill:", eng.runner.tune_prefill(), flush=True)
     if COPY_TO:
         os.makedirs(COPY_TO, exist_ok=True)
         shutil.copy(DEFAULT_PLAN_FILE, COPY_TO)
