@@ -34,14 +34,14 @@
 //     in some launches (round 5, profiles/r5/gemm_big_clamp/);
 //   * XCD-aware tile order (T1): the bijective round-robin remap, then GM m-tiles x all n-tiles
 //     super-rows so the panels of the tiles running together on one XCD are L2 hits.
-// Measured (round 4, profiles/r4/gemm_big_tail/README.md, interleaved with rocBLAS in one process):
-// gate_up + SwiGLU 1.05x rocBLAS (+ its separate SiLU pass) at M = 2944, QKV 0.79-0.84x at M = 2944-4096
-// (1.5 rounds of 256 x 256 tiles), O / down ~0.9x; the SwiGLU epilogue (no [M, 2I] write, no SiLU pass)
-// makes gate_up + SiLU a net win, which is what the engine dispatches (ops.linear_swiglu).
-// Engine dispatch: EPI_SWIGLU (prefill / mixed-step gate_up, ops.linear_swiglu) and EPI_ARGMAX (the
-// fused LM head, ops.lm_head_argmax, per decode bucket where ModelRunner.tune_lm_head times it
-// faster).  EPI_BF16 is the plain GEMM the harness (tools/gemm_big_bench.hip) and profiles/r3/scripts/gb_diag.py
-// compare against rocBLAS / fp32; EPI_ADD and the split-K slabs were measured for the O / down
+// Measured (round 5, after the drain fix, profiles/r5/gemm_big_clamp/, interleaved with rocBLAS in one
+// process): gate_up + SwiGLU 0.99-1.05x rocBLAS's plain GEMM (+ its separate SiLU pass); QKV on 192-wide
+// tiles 1.01-1.10x at 2048-6144 rows; O / down 0.80-0.92x.  Engine dispatch: EPI_SWIGLU (prefill /
+// mixed-step gate_up, ops.linear_swiglu), EPI_BF16 for QKV where the persisted prefill plan measured it
+// faster (ops.linear_big), the grouped mode for MoE prefill, and EPI_ARGMAX (the fused LM head,
+// ops.lm_head_argmax, per decode bucket where ModelRunner.tune_lm_head times it faster).  The harness
+// (tools/gemm_big_bench.hip) and profiles/r3/scripts/gb_diag.py compare EPI_BF16 against rocBLAS /
+// fp32; EPI_ADD and the split-K slabs were measured for the O / down
 // projections and decode shapes and lost there (profiles/r3/gemm_big/), so nothing dispatches them.
 // Epilogues: bf16 store; SwiGLU over the un-interleaved [gate; up] weight (the tile's W rows are
 // gathered as alternating 16-row gate / up chunks by the DMA source addresses, so the [M, 2I]
