@@ -704,6 +704,8 @@ static int launch_grouped(const Args& a0, int split, hipStream_t st) {
   X(4, 128, 128, 2, 2, 3, 64)    \
   X(5, 128, 64, 2, 1, 3, 64)     \
   X(12, 128, 128, 2, 2, 4, 64)    \
+  X(6, 96, 256, 2, 2, 3, 64)      \
+  X(8, 192, 128, 2, 2, 3, 64)     \
   GM_EXTRA_CFGS(X)
 // measurement-only configurations (tools/gemm_bench -DKA_GM_EXTRA): 32-deep k-steps, deeper rings
 #ifdef KA_GM_EXTRA
@@ -734,8 +736,14 @@ static int launch(const Args& a0, int split, hipStream_t st) {
 template <int EPI>
 static int dispatch(int cfg, const Args& a, int split, hipStream_t st) {
   if (cfg == 19) return launch_pp<EPI>(a, split, st);
-#define X_(id, bn, bm, wn, wm, s, kt) \
-  if (cfg == id) return launch<Cfg<bn, bm, wn, wm, s, kt>, EPI>(a, split, st);
+  // the SwiGLU epilogue pairs gate / up tiles within a wave: configurations with an odd TN lack it
+#define X_(id, bn, bm, wn, wm, s, kt)                                                    \
+  if (cfg == id) {                                                                       \
+    if constexpr (EPI == EPI_SWIGLU && Cfg<bn, bm, wn, wm, s, kt>::TN % 2 != 0)          \
+      return (int)hipErrorInvalidValue;                                                  \
+    else                                                                                 \
+      return launch<Cfg<bn, bm, wn, wm, s, kt>, EPI>(a, split, st);                      \
+  }
   GM_CFGS(X_)
 #undef X_
   return (int)hipErrorInvalidValue;

@@ -197,7 +197,7 @@ def tune_linear(groups: Dict[Tuple[int, int], List[torch.Tensor]], Ms: Sequence[
 # win at M = 32-64, 128 x 128 at 96-256, 128 x 256 / 256 x 128 / 4-stage 128 x 128 at 192-256; the
 # configurations that never won — one wave per SIMD, 32-deep rings, 64-row weight tiles, the 4-phase
 # ping-pong — were removed: profiles/r2/gemm_sweep_v*.txt)
-GM_TUNE_CFGS = (2, 3, 4, 5, 12, 19)
+GM_TUNE_CFGS = (2, 3, 4, 5, 6, 8, 12, 19)
 
 
 def gm_candidates(M: int, N: int, K: int, cfgs: Sequence[int] = ()):
