@@ -264,29 +264,11 @@ __global__ __launch_bounds__(256) void rope_kv_window_kernel(bf16_t* __restrict_
                                                              const int* __restrict__ slot_mapping, int tokens, int hq,
                                                              int hkv, const float* __restrict__ Pq, int split,
                                                              size_t pstride) {
-  constexpr int d = 128, half = 64, bs = 16, W = 16, VH = 8;
-  // [kv head of the group][dim][token] (+2 pad: the transposing writes spread over banks)
-  __shared__ bf16_t vt[VH][d][W + 2];
+  constexpr int d = 128, half = 64, bs = 16, W = 16;
+  __shared__ bf16_t vt[d][W + 2];   // [dim][token] (+2 pad: the transposing writes spread over banks)
   const int t0 = blockIdx.x * W;
   const int nt = min(W, tokens - t0);
   const int qkv_stride = (hq + 2 * hkv) * d;
-  // V of the first VH kv heads: loaded before the q / k rotation so their latency overlaps it (one
-  // 16-B load per thread and head; the load / transpose / store rounds per head were serialised
-  // round trips, about half the kernel)
-  const size_t vbase = (size_t)(hq + hkv) * d;
-  const int vj = threadIdx.x >> 4, vc = (threadIdx.x & 15) * 8;   // load phase: thread -> (token, 8-dim chunk)
-  auto load_v = [&](int h) {
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (vj < nt) {
-      const int t = t0 + vj;
-      v = ld8(qkv + (size_t)t * qkv_stride, Pq ? Pq + (size_t)t * qkv_stride : nullptr, split, pstride,
-              vbase + (size_t)h * d + vc);
-    }
-    return v;
-  };
-  uint4 vv[VH];
-#pragma unroll
-  for (int g = 0; g < VH; ++g) vv[g] = g < hkv ? load_v(g) : make_uint4(0, 0, 0, 0);
   // ---- q / k rotation: (hq + hkv) heads x 8 items of 8 rotary pairs per token, 16-B loads and
   // stores; unrolled so each thread keeps several items' loads in flight (the window grid is small:
   // ~2 workgroups per CU at an 8k-token step, so memory-level parallelism comes from the thread) ----
@@ -322,34 +304,34 @@ __global__ __launch_bounds__(256) void rope_kv_window_kernel(bf16_t* __restrict_
     *reinterpret_cast<uint4*>(dst + i) = make_uint4(o1[0], o1[1], o1[2], o1[3]);
     *reinterpret_cast<uint4*>(dst + i + half) = make_uint4(o2[0], o2[1], o2[2], o2[3]);
   }
-  // ---- V: groups of VH kv heads, 16 tokens x 128 dims each, transposed through LDS ----
+  // ---- V: per kv head, 16 tokens x 128 dims through LDS ----
   const int lj = threadIdx.x & 15;                  // store phase: lane -> token
   const int ls = slot_mapping[t0 + min(lj, nt - 1)];
   const bool lvalid = lj < nt && ls >= 0;
-  for (int h0 = 0; h0 < hkv; h0 += VH) {
-    if (h0 > 0) {
-#pragma unroll
-      for (int g = 0; g < VH; ++g) vv[g] = h0 + g < hkv ? load_v(h0 + g) : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int g = 0; g < VH; ++g) {
-      const uint32_t w[4] = {vv[g].x, vv[g].y, vv[g].z, vv[g].w};
+  const size_t vbase = (size_t)(hq + hkv) * d;
+  for (int h = 0; h < hkv; ++h) {
+    {   // load phase: thread -> (token, 8-dim chunk)
+      const int j = threadIdx.x >> 4, c = (threadIdx.x & 15) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (j < nt) {
+        const int t = t0 + j;
+        v = ld8(qkv + (size_t)t * qkv_stride, Pq ? Pq + (size_t)t * qkv_stride : nullptr, split, pstride,
+                vbase + (size_t)h * d + c);
+      }
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        vt[g][vc + 2 * k][vj] = (bf16_t)w[k];
-        vt[g][vc + 2 * k + 1][vj] = (bf16_t)(w[k] >> 16);
+        vt[c + 2 * k][j] = (bf16_t)w[k];
+        vt[c + 2 * k + 1][j] = (bf16_t)(w[k] >> 16);
       }
     }
     __syncthreads();
     if (lvalid) {
-      const int ng = min(VH, hkv - h0);
-      for (int g = 0; g < ng; ++g) {
-        bf16_t* dst = v_cache + ((size_t)(ls / bs) * hkv + h0 + g) * d * bs + ls % bs;
+      bf16_t* dst = v_cache + ((size_t)(ls / bs) * hkv + h) * d * bs + ls % bs;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int dim = (threadIdx.x >> 4) + 16 * k;
-          dst[(size_t)dim * bs] = vt[g][dim][lj];
-        }
+      for (int k = 0; k < 8; ++k) {
+        const int dim = (threadIdx.x >> 4) + 16 * k;
+        dst[(size_t)dim * bs] = vt[dim][lj];
       }
     }
     __syncthreads();

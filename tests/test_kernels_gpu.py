@@ -53,8 +53,7 @@ def _cache(nb, hkv, bs=16, d=128):
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (48, 12)])
 @pytest.mark.parametrize("T", [23, 301])
 def test_rope_kv_write(hq, hkv, T):
-    """T >= 64 takes the 16-token window kernel (V of up to 8 kv heads loaded ahead of the q / k
-    rotation and transposed through LDS; hkv = 12 takes a second, partial group of heads)."""
+    """T >= 64 takes the 16-token window kernel (V transposed through LDS, one kv head at a time)."""
     d = 128
     qkv = torch.randn(T, (hq + 2 * hkv) * d, device=DEV, dtype=BF)
     cs = ref.rope_cos_sin(4096, d, 5e5, device=DEV)
