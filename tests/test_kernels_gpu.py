@@ -689,6 +689,25 @@ def test_moe_experts_grouped_prefill(T, skew, e0, el, mode, monkeypatch):
     close(got, ops.moe_experts(x, w13, w2, tw, tid, e0), atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("T,want_big", [(300, False), (1100, True)])
+def test_moe_prefill_auto_picks_path_by_rows(T, want_big, monkeypatch):
+    """KA_MOE_PREFILL=auto: gemm_big's grouped mode from MOE_BIG_MIN_ROWS routed rows up, the grouped
+    ring kernel below (threshold lowered to 1000 rows for the test); either way == the fp32 reference."""
+    monkeypatch.setattr(ops, "MOE_PREFILL", "auto")
+    monkeypatch.setattr(ops, "MOE_BIG_MIN_ROWS", 1000)
+    ring_calls = []
+    real = ops.linear_grouped
+    monkeypatch.setattr(ops, "linear_grouped", lambda *a, **kw: ring_calls.append(1) or real(*a, **kw))
+    E, H, I, k = 8, 512, 384, 2
+    x = torch.randn(T, H, device=DEV, dtype=BF)
+    w13 = (torch.randn(E, 2 * I, H, device=DEV) * 0.05).to(BF)
+    w2 = (torch.randn(E, H, I, device=DEV) * 0.05).to(BF)
+    tw, tid = ops.moe_topk(torch.randn(T, E, device=DEV, dtype=BF), k)
+    got = ops.moe_experts_grouped(x, w13, w2, tw, tid, 0)
+    assert (len(ring_calls) == 0) == want_big
+    close(got, _moe_dense_ref(x, w13, w2, tw, tid, 0), atol=5e-2, rtol=5e-2)
+
+
 @pytest.mark.parametrize("R", [1, 29, 200, 700])
 def test_moe_local_experts_received_rows(R):
     """Receive side of the A5 all-to-all (models/moe.py `_local_experts`): rows tagged with a global
