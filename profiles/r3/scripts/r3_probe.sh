@@ -11,5 +11,5 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method threa
 tail -2 gpurun_out/lmh_tests.log
 timeout -k 10 300 python bench.py --transport asgi --steps 10 --warmup 3 --no-prefix-off-pass > gpurun_out/bench_lmh.log 2>&1 || exit 1
 tail -1 gpurun_out/bench_lmh.log | cut -c1-1200
-scripts/tcp_sched_sweep.sh "base:X=1" "hold16:KA_PREFILL_HOLD_STEPS=16 KA_PREFILL_HOLD_MAX_MS=150 KA_GATHER_MAX_MS=60" \
+profiles/scripts_archive/tcp_sched_sweep.sh "base:X=1" "hold16:KA_PREFILL_HOLD_STEPS=16 KA_PREFILL_HOLD_MAX_MS=150 KA_GATHER_MAX_MS=60" \
   "w8c8:BENCH_API_WORKERS=8 BENCH_CLIENT_PROCS=8" 2>&1 | tee gpurun_out/tcp_sweep4.txt

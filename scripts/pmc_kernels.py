@@ -1,4 +1,4 @@
-"""Workload for scripts/gpu_pmc_kernels.sh: a few dispatches of each hand-written hot kernel at its
+"""Workload for profiles/scripts_archive/gpu_pmc_kernels.sh: a few dispatches of each hand-written hot kernel at its
 serving shape — prefill attention (256 seqs x 32 new tokens, ctx 104), fused RoPE + KV append +
 decode attention (B = 256, ctx 121, QKV split-K partials), the batch-1 GEMV (gate_up, M = 1) and
 the B = 256 tile GEMM (down projection, split-K 8) — for rocprofv3 --pmc."""
