@@ -178,6 +178,12 @@ __device__ unsigned long long* g_bstamps;
 #else
 #define BSTAMP(i) do {} while (0)
 #endif
+#ifdef GM_KSTAMP
+// diagnostic build only (tools/gemm_bench.hip -DGM_KSTAMP): per-wave shader-clock cycles of the k-loop
+// phases summed over the k-steps, [block][wave][4]: wait + barrier, fragment reads + DMA issue + first
+// half's MFMA issue + reads wait, second half's MFMA issue, loop overhead
+__device__ unsigned long long* g_kstamps;
+#endif
 
 // GROUPED: blockIdx.x = n tile, blockIdx.y = chunk of BM rows over all groups in order (the grid
 // holds ceil(R / BM) + groups chunks, an upper bound computed on the host without reading counts;
@@ -351,7 +357,14 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
 #if KA_GM_PIPE == 2
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // no scalar load left in flight: lgkm counts in order
 #endif
+#ifdef GM_KSTAMP
+  unsigned long long ks[4] = {0, 0, 0, 0}, kt_e = __builtin_amdgcn_s_memtime();
+#endif
   for (int t = 0; t < nk; ++t) {
+#ifdef GM_KSTAMP
+    const unsigned long long kt_a = __builtin_amdgcn_s_memtime();
+    ks[3] += kt_a - kt_e;
+#endif
     // stage t landed (this wave's part): later stages may stay in flight
     // outstanding after this point: stages t+1 .. min(nk-1, t+STAGES-2) of this wave
     if constexpr (C::STAGES >= 3) {
@@ -360,6 +373,10 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
       wait_vm<0>();
     }
     block_sync();
+#ifdef GM_KSTAMP
+    const unsigned long long kt_b = __builtin_amdgcn_s_memtime();
+    ks[0] += kt_b - kt_a;
+#endif
     if (t == 0) BSTAMP(1);
     const int tn = t + C::STAGES - 1;
 #if KA_GM_PIPE == 2
@@ -370,7 +387,15 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
     if constexpr (C::KT == 64) {
       __builtin_amdgcn_sched_barrier(0);   // the first k-half's MFMAs stay above the second wait
       wait_frags(1);
+#ifdef GM_KSTAMP
+      const unsigned long long kt_d = __builtin_amdgcn_s_memtime();
+      ks[1] += kt_d - kt_b;
+#endif
       mma_half(1);
+#ifdef GM_KSTAMP
+      kt_e = __builtin_amdgcn_s_memtime();
+      ks[2] += kt_e - kt_d;
+#endif
     }
 #else
     read_frags(t % C::STAGES);
@@ -381,6 +406,13 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
 #endif
   }
   BSTAMP(2);
+#ifdef GM_KSTAMP
+  if (lane == 0) {
+    unsigned long long* d = g_kstamps + (((size_t)blockIdx.z * gridDim.x + blockIdx.x) * C::NW + wave) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[i] = ks[i] / (unsigned long long)max(nk, 1);
+  }
+#endif
 
   // epilogue: acc[i][j][r] = C[n = .. + i*16 + 4*grp + r][m = .. + j*16 + r16]
   const int nb = n0 + wn * C::TN * 16 + 4 * grp;

@@ -85,6 +85,12 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int warm = getenv("GB_WARM") ? atoi(getenv("GB_WARM")) : 0;   // 1: no weight rotation
+#ifdef GM_KSTAMP
+  unsigned long long* kst_;
+  const size_t nkst = (size_t)65536 * 8 * 4;   // up to 65536 blocks x 8 waves
+  CK(hipMalloc(&kst_, nkst * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(gm::g_kstamps), &kst_, sizeof(kst_)));
+#endif
 #ifdef GM_BSTAMPS
   unsigned long long* bst_;
   const size_t nbst = (size_t)65536 * 4 * 64;   // up to 65536 blocks
@@ -183,6 +189,26 @@ int main(int argc, char** argv) {
     const double us = ms * 1e3 / iters;
     const double tf = 2.0 * M * N * K / (us * 1e-6) / 1e12;
     const double tb = (wbytes + (double)M * K * 2 + (double)M * N * 2) / (us * 1e-6) / 1e12;
+#ifdef GM_KSTAMP
+    if (cfg >= 0 && cfg != 19) {   // mean shader-clock cycles per k-step and wave, by phase
+      CK(hipMemset(kst_, 0, nkst * 8));
+      run(1);
+      CK(hipStreamSynchronize(st));
+      std::vector<unsigned long long> h(nkst);
+      CK(hipMemcpy(h.data(), kst_, nkst * 8, hipMemcpyDeviceToHost));
+      double sum[4] = {0, 0, 0, 0};
+      size_t n = 0;
+      for (size_t e = 0; e < nkst / 4; ++e) {
+        const unsigned long long* v = &h[e * 4];
+        if (!v[0] && !v[1] && !v[2]) continue;
+        for (int i = 0; i < 4; ++i) sum[i] += (double)v[i];
+        ++n;
+      }
+      if (n) printf("  k-step cycles (mean of %zu waves): wait+barrier %.0f | reads+DMA+MFMA half 0+reads wait %.0f | "
+                    "MFMA half 1 issue %.0f | loop %.0f | total %.0f\n", n, sum[0] / n, sum[1] / n, sum[2] / n,
+                    sum[3] / n, (sum[0] + sum[1] + sum[2] + sum[3]) / n);
+    }
+#endif
 #ifdef GM_BSTAMPS
     if (cfg >= 0) {   // per-block timeline of one more launch (ring kernels only record stamps)
       CK(hipMemset(bst_, 0, nbst * 8));
