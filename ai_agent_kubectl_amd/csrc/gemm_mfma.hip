@@ -25,7 +25,9 @@
 //     attention, SiLU) and epilogues: bf16 store, partial slab, SwiGLU (interleaved gate_up rows,
 //     silu(g) * u computed from the accumulators: the [M, 2I] gate_up output never exists).
 // KA_HIPCC_FLAGS: -mllvm -amdgpu-mfma-vgpr-form
-// (accumulators in VGPRs with in-place MFMAs; the tables in profiles/r2/ were measured with it)
+// (accumulators in VGPRs with in-place MFMAs; the tables in profiles/r2/ were measured with it.  One
+// wave per SIMD issues 16x16x32 bf16 MFMAs every 17 clocks in this form, against 27 with the default
+// codegen: profiles/r5/mfma_rate/)
 #include "common.h"
 
 #include <utility>
