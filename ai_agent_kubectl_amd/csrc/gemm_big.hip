@@ -212,10 +212,11 @@ KA_DEV void tile_of(int L, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
 // 16 B, hipMalloc memory); 3: the sc1 loads of 2 after the fences of 1.  hipcc does not pad the
 // VMEM-store-data / VALU-write hazard around asm it cannot see, so the asm stores carry their own
 // wait states (without them a few lanes' data were corrupted: profiles/r4/gemm_big_tail/).
-// Round 5 full-matrix repeats (profiles/r5/gemm_big_tail_modes/): modes 0 and 1 (plain loads after
-// the acquire fence) read stale slab data in some launches (max err 0.17-0.23 at 2944 x 6144); modes
-// 2 and 3 were exact in every launch, and the fences of mode 3 add 24 us to the whole GEMM (167 vs
-// 143 us; rocBLAS 141).
+// Round 5 full-matrix repeats (profiles/r5/gemm_big_tail_modes/): before the LDS-DMA drain fix, modes
+// 0 and 1 read stale data in some first launches; after it, all four modes were exact in every launch
+// (48 full checks each, after_drain/), so those failures were the DMA hazard.  Mode 2 stays the
+// default because it is the fastest: 2944 x 28672 SwiGLU 639-647 us against 650-667 for the fenced
+// modes, 78-83 against 90-113 us on an all-split shape.
 #ifndef KA_GB_TAIL_MODE
 #define KA_GB_TAIL_MODE 2
 #endif
