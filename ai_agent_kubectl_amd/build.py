@@ -51,13 +51,16 @@ def file_flags(src: str):
     return []
 
 
-def build_hip(force: bool = False, verbose: bool = False, extra_flags=()) -> str:
+def build_hip(force: bool = False, verbose: bool = False, extra_flags=(), out: str = "") -> str:
+    """out: another library path (an A/B build with `extra_flags`, e.g. -DKA_GM_SCHED=0, loaded only by
+    diagnostic runs: ops/_hip.py KA_HIP_LIB + KA_HIP_LIB_DIAG=1); its objects go next to it."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = glob.glob(os.path.join(CSRC, "*.h"))
-    os.makedirs(LIB_DIR, exist_ok=True)
-    if not force and not _newer(srcs + headers, HIP_LIB):
-        return HIP_LIB
-    obj_dir = os.path.join(LIB_DIR, "obj")
+    lib = out or HIP_LIB
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    if not force and not _newer(srcs + headers, lib):
+        return lib
+    obj_dir = os.path.join(os.path.dirname(lib), "obj") if out else os.path.join(LIB_DIR, "obj")
     os.makedirs(obj_dir, exist_ok=True)
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
              "-Wno-unused-result", *extra_flags]
@@ -71,13 +74,14 @@ def build_hip(force: bool = False, verbose: bool = False, extra_flags=()) -> str
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
     with cf.ThreadPoolExecutor(max(1, jobs)) as ex:
         objs = list(ex.map(compile_one, srcs))
-    tmp = HIP_LIB + ".tmp"
+    tmp = lib + ".tmp"
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp])
-    check_lgkm_windows(verbose)
-    os.replace(tmp, HIP_LIB)
+    if not out:
+        check_lgkm_windows(verbose)
+    os.replace(tmp, lib)
     if verbose:
-        print("built", HIP_LIB)
-    return HIP_LIB
+        print("built", lib)
+    return lib
 
 
 # Kernels whose k-loops read LDS fragments with inline-asm ds_reads and wait for them with a COUNTED

@@ -45,6 +45,16 @@ namespace pd {
 #ifndef KA_PD_NT
 #define KA_PD_NT 1
 #endif
+// LDS-DMA wait schedule of the weight streams.  LDS-DMA pieces of one wave do not always complete in
+// issue order (profiles/r5/gemm_big_clamp/), so only vmcnt(0) proves that a given piece has landed.
+//   1 (default, drained halves): the ring is two halves of RING / 2 slots; a wave waits vmcnt(0) for the
+//     half it is about to read, which at that moment is the only batch it has in flight (the next half
+//     is issued right after the wait, then dotted against while the first is consumed).
+//   0 (counted, rounds 4-5): RING - 2 pieces stay in flight across each counted wait; correct only
+//     under in-order completion, kept for A/B measurements.
+#ifndef KA_PD_SAFE
+#define KA_PD_SAFE 1
+#endif
 constexpr int NT = 512, NW = NT / 64, HD = 128, KBS = 16, NT_ = NT;
 // LDS-DMA ring slots (1 KB) per wave: KA_PD_RING (16) in every phase, except the down rows at B = 2,
 // whose two act rows (2 x I bf16) take LDS the ring gives up there (12 slots, 96 KB per CU in flight;
@@ -298,20 +308,27 @@ struct Stream {
       ++ni;
     }
   }
+  static constexpr int HB = RG / 2;   // drained schedule: slots per half (one batch)
   // the first N pieces (N < RG: the rest by top_up<N>() after the barrier wait, so the wait's polls
-  // queue behind fewer of the CU's own pieces)
+  // queue behind fewer of the CU's own pieces).  Drained schedule: the first batch (half the ring)
   template <int N = RG>
   KA_DEV void start() {
     issued = ni = nc = 0;
     if (total <= 0) return;
+#if KA_PD_SAFE
+    for (int r = 0; r < min(HB, total); ++r) issue();
+#else
 #pragma unroll
     for (int r = 0; r < (N < RG ? N : RG); ++r) issue();
+#endif
   }
   template <int N>
   KA_DEV void top_up() {
+#if !KA_PD_SAFE
     if (total <= 0) return;
 #pragma unroll
     for (int r = (N < RG ? N : RG); r < RG; ++r) issue();
+#endif
   }
   // xaddr: LDS byte address of activation row 0 (K bf16), row b at xaddr + b xstride
   KA_DEV RowVals<B> run(uint32_t xaddr, uint32_t xstride) {
@@ -337,8 +354,20 @@ struct Stream {
       }
     };
     int j = 0;
+#if KA_PD_SAFE
+    // batches of HB pieces in alternating halves: wait for batch [j, j + n) (the only pieces in flight),
+    // issue the next batch into the other half (read by the batch before, whose reads have completed),
+    // then read and dot this one, two pieces at a time
+    while (j < total) {
+      const int n = min(HB, total - j);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int r = min(HB, total - j - n); r > 0; --r) issue();
+      const int je = j + n;
+      for (; j + 1 < je; j += 2) {
+#else
     for (; j + 1 < total; j += 2) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RG - 2) : "memory");   // pieces j, j + 1 have landed
+#endif
       const int xc = cc + rot >= KC ? cc + rot - KC : cc + rot;   // x chunks of pieces j, j + 1
       const int xc1 = xc + 1 == KC ? 0 : xc + 1;
       const uint32_t r0 = ring + ((uint32_t)j % (uint32_t)RG) * 1024u + lo16, r1 = ring + ((uint32_t)(j + 1) % (uint32_t)RG) * 1024u + lo16;
@@ -360,8 +389,10 @@ struct Stream {
             : "v"(r0), "v"(r1), "v"(a0), "v"(a1), "v"(a0 + xstride), "v"(a1 + xstride)
             : "memory");
       }
+#if !KA_PD_SAFE
       issue();   // both slots are free again: refill them RG pieces ahead
       issue();
+#endif
 #pragma unroll
       for (int b = 0; b < B; ++b) acc[b] = dot8(w0, x0[b], acc[b]);
       finish();
@@ -369,8 +400,12 @@ struct Stream {
       for (int b = 0; b < B; ++b) acc[b] = dot8(w1, x1[b], acc[b]);
       finish();
     }
+#if KA_PD_SAFE
+    if (j < je) {   // an odd batch: its last piece
+#else
     if (j < total) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RG - 1) : "memory");
+#endif
       const uint32_t r0 = ring + ((uint32_t)j % (uint32_t)RG) * 1024u + lo16;
       const uint32_t a0 = xaddr + (uint32_t)(cc + rot >= KC ? cc + rot - KC : cc + rot) * 1024u + lo16;
       uint4 w0, x0[B];
@@ -385,11 +420,19 @@ struct Stream {
                      : "v"(r0), "v"(a0), "v"(a0 + xstride)
                      : "memory");
       }
+#if !KA_PD_SAFE
       issue();
+#endif
 #pragma unroll
       for (int b = 0; b < B; ++b) acc[b] = dot8(w0, x0[b], acc[b]);
       finish();
+#if KA_PD_SAFE
+      ++j;
+#endif
     }
+#if KA_PD_SAFE
+    }
+#endif
     return mine;
   }
   KA_DEV void drain() const { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }

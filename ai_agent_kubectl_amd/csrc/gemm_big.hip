@@ -1015,6 +1015,9 @@ extern "C" int ka_gemm_big(void* Y, const void* R, const void* X, const void* W,
                            int epi, int gm, void* ws, size_t ws_bytes, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 128 != 0 || N % 128 != 0 || ldx % 8 != 0 || ldy % 8 != 0) return (int)hipErrorInvalidValue;
+  // 32-bit buffer-descriptor record counts (past them loads return zeros, silently)
+  if ((double)M * ldx * 2.0 >= 2147483648.0 - 4096.0 || (double)N * K * 2.0 >= 2147483648.0 - 4096.0)
+    return (int)hipErrorInvalidValue;
   gb::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), static_cast<bf16_t*>(Y),
              static_cast<const bf16_t*>(R), M, N, K, ldx, ldy, 0, 0, gm > 0 ? gm : 8, N / 2};
   switch (epi) {
@@ -1033,7 +1036,7 @@ extern "C" int ka_gemm_big(void* Y, const void* R, const void* X, const void* W,
 // (expert e, first row r0, n rows), Y rows of X[r0 .. r0 + n) W[e]^T.  W [groups][N][K] (SwiGLU:
 // [groups][2I][K], gate rows then up rows per expert).  epi 0: Y [*, ldy] row out_rows[r] for sorted
 // row r; epi 3: Y [M, ldy] sorted row r = silu(x gate^T) * (x up^T).  X [M, ldx] (M = the sorted rows'
-// capacity).  Requirements: K % 128 == 0, N % 256 == 0, groups * N * K * 2 < 2^31 - 4 KB.
+// capacity).  Requirements: K % 128 == 0, N % 256 == 0, groups * N * K * 2 and M * ldx * 2 < 2^31 - 4 KB.
 extern "C" int ka_gemm_big_grouped(void* Y, const void* X, const void* W, const int* chunk_tab, int chunks,
                                    const int* out_rows, int M, int N, int K, int ldx, int ldy, int groups, int epi,
                                    hipStream_t stream) {
@@ -1041,6 +1044,8 @@ extern "C" int ka_gemm_big_grouped(void* Y, const void* X, const void* W, const 
   if (K % 128 != 0 || N % 256 != 0 || ldx % 8 != 0 || ldy % 8 != 0 || groups < 1 || chunk_tab == nullptr ||
       (double)groups * N * K * 2.0 >= 2147483648.0 - 4096.0 || (epi == gb::EPI_BF16 && out_rows == nullptr))
     return (int)hipErrorInvalidValue;
+  // the X descriptor's record count is 32-bit too: past it the buffer loads read zeros, silently
+  if ((double)M * ldx * 2.0 >= 2147483648.0 - 4096.0) return (int)hipErrorInvalidValue;
   gb::Args a{static_cast<const bf16_t*>(X), static_cast<const bf16_t*>(W), static_cast<bf16_t*>(Y), nullptr, M, N, K,
              ldx, ldy, chunks, 0, 8, N / 2};
   a.chunk_tab = chunk_tab;

@@ -14,10 +14,10 @@
 //     wave-instruction (8 rows x 128 B); the XOR swizzle (slot = chunk ^ ((row >> 1) & 7)) is
 //     applied to the per-lane GLOBAL source address and to the ds_read_b128 address (rule 21), and
 //     makes the 16 rows a ds_read_b128 lane group touches land on 16 distinct 16-B bank slots;
-//   * STAGES-deep LDS ring, one barrier per k-step: wait for the stage being computed with a
-//     counted vmcnt (STAGES - 2 stages stay in flight across the barrier), barrier (every wave's
-//     DMA of that stage has landed, every wave is done reading the slot about to be refilled),
-//     issue the DMA of stage t + STAGES - 1, then ds_read + MFMA on stage t;
+//   * an LDS ring with stage t + 2 in flight while stage t is computed, waited for with vmcnt(0)
+//     only (KA_GM_SCHED below: LDS-DMA completion is unordered, so a wave never waits while a
+//     younger stage of its own is in flight); the barrier after the wait publishes every wave's DMA
+//     of the stage and retires the reads of the slot about to be refilled; then ds_read + MFMA;
 //   * XCD-aware tile order (T1): consecutive logical tiles share an XCD (bijective remap of the
 //     round-robin dispatch) and are grouped GM M-tiles x N so the W and X panels of the blocks
 //     running together on one XCD are L2 hits;
@@ -45,19 +45,44 @@ constexpr int BK = 64;
 
 enum Epi : int { EPI_BF16 = 0, EPI_P32 = 1, EPI_P16 = 2, EPI_SWIGLU = 3 };
 
+// LDS-DMA wait schedule of the ring kernel (KA_GM_SCHED).  LDS-DMA pieces of one wave do NOT always
+// complete in issue order (profiles/r5/gemm_big_clamp/: a younger piece that hits in L2 can retire
+// before an older one), so a counted `s_waitcnt vmcnt(N)` with N > 0 does not prove that the oldest
+// pieces have landed.  The only wait that does is vmcnt(0), so the default schedules are built so that
+// whenever a wave waits for a stage, that stage is the ONLY one it has in flight:
+//   1 (set):  the waves form two sets (w < NW/2, w >= NW/2: one wave of each set per SIMD when
+//             NW = 8); stage t is issued whole by set t & 1, three slots.  At step t set t & 1 holds
+//             only stage t (its next stage, t + 2, is issued after the barrier) and waits vmcnt(0);
+//             the other set holds only stage t + 1 and does not wait.  Same lookahead (stage t + 2
+//             issued at step t) and the same DMA pieces per SIMD per step as the counted ring.
+//   2 (pair): four slots, stages issued in pairs: at even steps every wave drains (vmcnt(0): stages
+//             t, t + 1), one barrier, then issues t + 2, t + 3; odd steps have no wait and no barrier
+//             (the even barrier already published stage t + 1 and every wave finished reading the
+//             slots refilled there).  Configurations whose four slots do not fit LDS use `set`.
+//   0 (counted, rounds 2-5): STAGES slots, vmcnt(PER (STAGES - 2)) + a barrier every step — correct
+//             only under in-order completion; kept for A/B measurements (tools/gemm_bench).
+#ifndef KA_GM_SCHED
+#define KA_GM_SCHED 1
+#endif
+
 template <int BN_, int BM_, int WN_, int WM_, int STAGES_, int BK_ = 64>
 struct Cfg {
-  static constexpr int BN = BN_, BM = BM_, WN = WN_, WM = WM_, STAGES = STAGES_, KT = BK_;
+  static constexpr int BN = BN_, BM = BM_, WN = WN_, WM = WM_, KT = BK_;
   static constexpr int NW = WN * WM, NT = 64 * NW;
   static constexpr int TN = BN / WN / 16, TM = BM / WM / 16;
   static constexpr int RB = KT * 2;                                  // bytes per staged row
   static constexpr int A_BYTES = BN * RB, B_BYTES = BM * RB;         // one k-step of W / of X
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  static constexpr int SCHED = KA_GM_SCHED == 2 ? (4 * STAGE_BYTES <= 160 * 1024 ? 2 : 1) : KA_GM_SCHED;
+  static constexpr int STAGES = SCHED == 1 ? 3 : SCHED == 2 ? 4 : STAGES_;
   static constexpr int LDS = STAGES * STAGE_BYTES;
-  static constexpr int GA = A_BYTES / (NT * 16), GB = B_BYTES / (NT * 16);   // DMAs per thread per k-step
+  // waves that issue one stage's pieces (set: half of them) and each one's DMAs per k-step
+  static constexpr int NI = SCHED == 1 ? NW / 2 : NW;
+  static constexpr int GA = A_BYTES / (NI * 64 * 16), GB = B_BYTES / (NI * 64 * 16);
   static_assert(KT == 64 || KT == 32, "k-step is 64 (128-B rows) or 32 (64-B rows)");
   static_assert(TN * WN * 16 == BN && TM * WM * 16 == BM, "tile / wave layout mismatch");
-  static_assert(GA * NT * 16 == A_BYTES && GB * NT * 16 == B_BYTES, "tile rows must fill whole DMA waves");
+  static_assert(GA * NI * 64 * 16 == A_BYTES && GB * NI * 64 * 16 == B_BYTES, "tile rows must fill whole DMA waves");
+  static_assert(SCHED != 1 || NW % 2 == 0, "set schedule: an even wave count");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
@@ -214,13 +239,16 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   const int kb = blockIdx.z * a.kps;
   const int nk = min(a.kps, a.K - kb) / C::KT;
 
-  // per-lane DMA source offsets (bytes, 32-bit): wave-instruction j covers 1 KB = RPI staged rows
+  // per-lane DMA source offsets (bytes, 32-bit): wave-instruction j covers 1 KB = RPI staged rows.
+  // Piece p = j * NI + wi of a stage is issued by issuer wi (set schedule: the wave's index in its set)
   constexpr int CPR = C::RB / 16, RPI = 64 / CPR;   // 16-B chunks per row, rows per instruction
   const int rl = lane / CPR, slot = lane % CPR;
+  const int wi = C::SCHED == 1 ? wave % C::NI : wave;
+  const int wset = C::SCHED == 1 ? wave / C::NI : 0;   // set schedule: this wave issues the stages t, t & 1 == wset
   uint32_t offA[C::GA], offB[C::GB];
 #pragma unroll
   for (int j = 0; j < C::GA; ++j) {
-    const int row = (j * C::NW + wave) * RPI + rl;
+    const int row = (j * C::NI + wi) * RPI + rl;
     const int ch = swz<C::KT>(row, slot);
     // rows past N / M / the list re-read DISTINCT real rows (r % N), never one clamped row: a
     // piece whose lanes share one address intermittently corrupted other LDS-DMA pieces in
@@ -234,7 +262,7 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   }
 #pragma unroll
   for (int j = 0; j < C::GB; ++j) {
-    const int row = (j * C::NW + wave) * RPI + rl;
+    const int row = (j * C::NI + wi) * RPI + rl;
     const int ch = swz<C::KT>(row, slot);
     int src;
     if constexpr (GROUPED) src = rows_of[wrap_row(row, nrows)] / a.src_div;   // padding rows: re-read a real row
@@ -251,23 +279,36 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
   // (build.py check_lgkm_windows verifies the k-loop's read windows in the generated assembly).
   int wnt = a.wnt;
   asm volatile("" : "+s"(wnt));
-  auto issue = [&](int stage, int t) {
+  // the wave's pieces of a stage, W pieces then X pieces; part 0 / 1: the first / second half of that
+  // list, -1: all (a call site's part is a constant: the loops fold)
+  constexpr int NPC = C::GA + C::GB, HALF_P = NPC / 2;
+  auto issue = [&](int stage, int t, int part) {
     char* sa = lds_c + stage * C::STAGE_BYTES;
     char* sb = sa + C::A_BYTES;
     const uint32_t kofs = (uint32_t)t * C::RB;
+    const int lo = part == 1 ? HALF_P : 0, hi = part == 0 ? HALF_P : NPC;
     if (!(KA_GM_ABL & 1)) {
       if (wnt) {
 #pragma unroll
-        for (int j = 0; j < C::GA; ++j) glds16<2>(Wb + offA[j] + kofs, sa + (j * C::NW + wave) * 1024);
+        for (int j = 0; j < C::GA; ++j)
+          if (j >= lo && j < hi) glds16<2>(Wb + offA[j] + kofs, sa + (j * C::NI + wi) * 1024);
       } else {
 #pragma unroll
-        for (int j = 0; j < C::GA; ++j) glds16(Wb + offA[j] + kofs, sa + (j * C::NW + wave) * 1024);
+        for (int j = 0; j < C::GA; ++j)
+          if (j >= lo && j < hi) glds16(Wb + offA[j] + kofs, sa + (j * C::NI + wi) * 1024);
       }
     }
     if (!(KA_GM_ABL & 2)) {
 #pragma unroll
-      for (int j = 0; j < C::GB; ++j) glds16(Xb + offB[j] + kofs, sb + (j * C::NW + wave) * 1024);
+      for (int j = 0; j < C::GB; ++j)
+        if (C::GA + j >= lo && C::GA + j < hi) glds16(Xb + offB[j] + kofs, sb + (j * C::NI + wi) * 1024);
     }
+  };
+  // stage t's pieces, issued by the waves that own it (every wave, or set t & 1)
+  auto issue_own = [&](int t, int part = -1) {
+    if (t >= nk) return;
+    if (C::SCHED == 1 && (t & 1) != wset) return;
+    issue(t % C::STAGES, t, part);
   };
 
   f32x4 acc[C::TN][C::TM];
@@ -351,10 +392,9 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
     for (int kk = 0; kk < C::KT / 32; ++kk) mma_half(kk);
   };
 
-  // prologue: STAGES - 1 stages in flight
+  // prologue: STAGES - 1 stages in flight (set / pair schedules: stages 0 and 1)
 #pragma unroll
-  for (int s = 0; s < C::STAGES - 1; ++s)
-    if (s < nk) issue(s, s);
+  for (int s = 0; s < (C::SCHED == 0 ? C::STAGES - 1 : 2); ++s) issue_own(s);
   constexpr int PER = C::GA + C::GB;
 #if KA_GM_PIPE == 2
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // no scalar load left in flight: lgkm counts in order
@@ -367,26 +407,55 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
     const unsigned long long kt_a = __builtin_amdgcn_s_memtime();
     ks[3] += kt_a - kt_e;
 #endif
-    // stage t landed (this wave's part): later stages may stay in flight
-    // outstanding after this point: stages t+1 .. min(nk-1, t+STAGES-2) of this wave
-    if constexpr (C::STAGES >= 3) {
+    // stage t landed (this wave's part), then the barrier publishes every wave's part
+    if constexpr (C::SCHED == 1) {
+      if ((t & 1) == wset) wait_vm<0>();   // stage t is this set's only stage in flight
+      block_sync();
+    } else if constexpr (C::SCHED == 2) {
+      if (!(t & 1)) {                      // stages t, t + 1: this wave's only pieces in flight
+        wait_vm<0>();
+        block_sync();
+      }
+    } else if constexpr (C::STAGES >= 3) {
+      // counted: stages t+1 .. min(nk-1, t+STAGES-2) of this wave stay in flight
       wait_ahead<C::STAGES - 2, PER>(min(nk - 1 - t, C::STAGES - 2));
+      block_sync();
     } else {
       wait_vm<0>();
+      block_sync();
     }
-    block_sync();
 #ifdef GM_KSTAMP
     const unsigned long long kt_b = __builtin_amdgcn_s_memtime();
     ks[0] += kt_b - kt_a;
 #endif
     if (t == 0) BSTAMP(1);
-    const int tn = t + C::STAGES - 1;
+    // refill: the slot(s) every wave finished reading before the last barrier.  KA_GM_SPLIT_ISSUE: the
+    // set / pair schedules issue twice a wave's usual pieces at once, so half of them go after the
+    // first k-half's MFMAs (issued while the matrix pipe works) instead of all ahead of them
+    auto refill = [&](int part) {
+      if constexpr (C::SCHED == 2) {
+        if (!(t & 1)) {
+          if (part != 1) issue_own(t + 2);
+          if (part != 0) issue_own(t + 3);
+        }
+      } else {
+        issue_own(t + C::STAGES - 1, part);
+      }
+    };
+#ifndef KA_GM_SPLIT_ISSUE
+#define KA_GM_SPLIT_ISSUE 1
+#endif
+    constexpr bool split_issue = KA_GM_SPLIT_ISSUE && C::SCHED != 0 && C::KT == 64;
 #if KA_GM_PIPE == 2
     read_frags_asm(t % C::STAGES);
-    if (tn < nk) issue(tn % C::STAGES, tn);
+    refill(split_issue ? 0 : -1);
     wait_frags(0);
     mma_half(0);
     if constexpr (C::KT == 64) {
+      if constexpr (split_issue) {
+        __builtin_amdgcn_sched_barrier(0);
+        refill(1);
+      }
       __builtin_amdgcn_sched_barrier(0);   // the first k-half's MFMAs stay above the second wait
       wait_frags(1);
 #ifdef GM_KSTAMP
@@ -402,7 +471,7 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(Args a) {
 #else
     read_frags(t % C::STAGES);
     __builtin_amdgcn_sched_barrier(0);
-    if (tn < nk) issue(tn % C::STAGES, tn);
+    refill(-1);
     __builtin_amdgcn_sched_barrier(0);
     mma();
 #endif
@@ -499,6 +568,19 @@ struct PP {
 //   A0 A1 (t+2):  G0 in R_b(t+1) | G1 in R_a(t+1)     (A_g of tile t last read by group g's R_b(t))
 // Waits before the barrier that ends interval 4t+7: G0 (end of C_b(t+1)) vmcnt(0), G1 (end of its
 // R_b(t+1), which issued B(t+3)) vmcnt(4).
+// KA_PP_SAFE 1: the counted vmcnt(4) of G1 is only correct under in-order LDS-DMA completion
+// (see KA_GM_SCHED), so group 0 issues every piece instead: B(t+1) in its R_a(t), A(t+1) in its R_b(t)
+// (4 pieces per wave and half-tile), and drains vmcnt(0) at the end of C_b(t) — its only pieces in
+// flight are tile t+1's — before the barrier ahead of the first read of tile t+1; group 1 never waits.
+// WAR: B(t+1) overwrites B(t-1), last read by G1's R_a(t-1) three intervals earlier; A(t+1) overwrites
+// A(t-1), last read by G1's R_b(t-1), retired before G1's C_b(t-1), one interval before G0's R_b(t).
+// KA_PP_SAFE 2 (default): both groups issue, each drains with nothing younger in flight: G0 as above
+// with its half of the pieces (B(t+1) in R_a(t), A(t+1) in R_b(t), vmcnt(0) at the end of C_b(t)); G1
+// issues its halves of A(t+1) AND B(t+1) in its R_a(t) and drains vmcnt(0) at the end of its R_b(t),
+// the barrier before G0's R_a(t+1).  WAR for G1's B(t+1): B(t-1) was last read by G1's R_a(t-1).
+#ifndef KA_PP_SAFE
+#define KA_PP_SAFE 2
+#endif
 template <int EPI, bool GROUPED = false>
 __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
@@ -521,10 +603,13 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
   const int nk = min(a.kps, a.K - kb) / BK;
 
   const int r8 = lane >> 3, slot = lane & 7;
-  uint32_t off[4][2];
+  // pieces of a half-tile issued per wave (KA_PP_SAFE: group 0 issues all 16), and the wave's index
+  constexpr int PJ = KA_PP_SAFE == 1 ? 4 : 2, PW = KA_PP_SAFE == 1 ? 4 : 8;
+  const int wq = KA_PP_SAFE == 1 ? wc : w;
+  uint32_t off[4][PJ];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = (j * 8 + w) * 8 + r8;
+  for (int j = 0; j < PJ; ++j) {
+    const int row = (j * PW + wq) * 8 + r8;
     const uint32_t ch = (uint32_t)(slot ^ ((row >> 1) & 7)) * 8;
     off[0][j] = ((uint32_t)wrap_row(n0 + row, a.N) * (uint32_t)a.K + kb + ch) * 2u;
     off[1][j] = ((uint32_t)wrap_row(n0 + 128 + row, a.N) * (uint32_t)a.K + kb + ch) * 2u;
@@ -548,10 +633,10 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
     const uint32_t kofs = (uint32_t)t * (BK * 2);
     if (h < 2 && a.wnt) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) glds16<2>(src + off[h][j] + kofs, dst + (j * 8 + w) * 1024);
+      for (int j = 0; j < PJ; ++j) glds16<2>(src + off[h][j] + kofs, dst + (j * PW + wq) * 1024);
     } else {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) glds16(src + off[h][j] + kofs, dst + (j * 8 + w) * 1024);
+      for (int j = 0; j < PJ; ++j) glds16(src + off[h][j] + kofs, dst + (j * PW + wq) * 1024);
     }
   };
 
@@ -594,6 +679,63 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
     __builtin_amdgcn_s_setprio(0);
   };
 
+#if KA_PP_SAFE == 2
+  // prologue: tile 0 (every wave its pieces), drained; then tile 1, drained by each group at its point
+  for (int h = 0; h < 4; ++h) issue(h, 0);
+  wait_vm<0>();
+  for (int h = 0; h < 4; ++h) issue(h, 1);
+  block_sync();
+  if (g == 1) block_sync();
+
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = L + (t & 1) * PP::BUF;
+    const int t1 = t == 0 ? nk : t + 1;   // tile 1 was issued whole by the prologue
+    // phase a
+    read_a(buf, 0); read_b(buf);
+    if (g == 0) { issue(2, t1); issue(3, t1); }                                   // B(t+1), G0 half
+    else { issue(0, t1); issue(1, t1); issue(2, t1); issue(3, t1); }             // A(t+1), B(t+1), G1 halves
+    block_sync();
+    mma(0);
+    block_sync();
+    // phase b
+    read_a(buf, 1);
+    if (g == 0) { issue(0, t1); issue(1, t1); }                                   // A(t+1), G0 half
+    else wait_vm<0>();                     // tile t+1: G1's only pieces in flight
+    block_sync();
+    mma(1);
+    if (g == 0) wait_vm<0>();              // tile t+1: G0's only pieces in flight
+    block_sync();
+  }
+  if (g == 0) block_sync();
+#elif KA_PP_SAFE == 1
+  // prologue: group 0 issues tile 0, drains it, issues tile 1 (drained at the end of C_b(0))
+  if (g == 0) {
+    for (int h = 0; h < 4; ++h) issue(h, 0);
+    wait_vm<0>();
+    for (int h = 0; h < 4; ++h) issue(h, 1);
+  }
+  block_sync();
+  if (g == 1) block_sync();
+
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = L + (t & 1) * PP::BUF;
+    const int t1 = t == 0 ? nk : t + 1;   // tile 1 was issued whole by the prologue
+    // phase a
+    read_a(buf, 0); read_b(buf);
+    if (g == 0) { issue(2, t1); issue(3, t1); }   // B(t+1): G0 in R_a(t)
+    block_sync();
+    mma(0);
+    block_sync();
+    // phase b
+    read_a(buf, 1);
+    if (g == 0) { issue(0, t1); issue(1, t1); }   // A(t+1): G0 in R_b(t)
+    block_sync();
+    mma(1);
+    if (g == 0) wait_vm<0>();                     // tile t+1: G0's only pieces in flight
+    block_sync();
+  }
+  if (g == 0) block_sync();
+#else
   // prologue: tiles 0 and 1 (all four half-tiles each); wait for tile 0; group 1 one barrier behind
   for (int h = 0; h < 4; ++h) issue(h, 0);
   for (int h = 0; h < 4; ++h) issue(h, 1);
@@ -622,6 +764,7 @@ __global__ __launch_bounds__(512) void gemm_pp2_kernel(Args a) {
     block_sync();
   }
   if (g == 0) block_sync();
+#endif
 
   const int nb = n0 + 128 * g + 4 * grp;
   const int mb = m0 + 64 * wc + r16;

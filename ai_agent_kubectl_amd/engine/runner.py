@@ -152,6 +152,8 @@ class ModelRunner:
         # bucket -> the captured graph holds the persistent decode kernel (its error word must be read
         # back on every replay of that graph, whatever model.persistent says now)
         self.graph_persistent: Dict[int, bool] = {}
+        # graphs taken out of service while a replay may still be queued (freed by health_check)
+        self._retired_graphs: List[object] = []
 
     # ------------------------------------------------------------------------------------------
     def _view(self, name: str, n: int) -> torch.Tensor:
@@ -571,6 +573,8 @@ class ModelRunner:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         int(probe[0].item())
+        # nothing queued before the synchronize can still be replaying a retired graph
+        self._retired_graphs.clear()
 
     def _err_word(self) -> Optional[torch.Tensor]:
         car = getattr(self.comm, "custom_ar", None)
@@ -608,10 +612,15 @@ class ModelRunner:
                                     "the step's results are stale")
         if int(h[1]):
             self.model.persistent = False   # the chain from now on: co-residency cannot be relied on
-            # a graph captured with the persistent kernel would keep replaying it: drop those graphs,
-            # their buckets run eagerly (the kernel chain) from the next step on
+            # a graph captured with the persistent kernel would keep replaying it: take those graphs
+            # out of service (their buckets run eagerly, the kernel chain, from the next step on).  The
+            # engine may already have queued a chained step that replays one of them, so the graph
+            # objects are only retired here; health_check() frees them after a device synchronize
+            # (destroying a hipGraphExec with a launch still pending is not defined)
             for b in [b for b, p in self.graph_persistent.items() if p]:
-                self.graphs.pop(b, None)
+                g = self.graphs.pop(b, None)
+                if g is not None:
+                    self._retired_graphs.append(g)
                 self.graph_persistent.pop(b, None)
             self.stats["persistent_stalls"] += 1
             logger.error("persistent decode kernel: a grid wait ran out; batch-1 decode falls back to "

@@ -119,7 +119,9 @@ class LlamaModel:
         cfg = self.cfg
         eps = cfg.norm_eps
         h = ops.embedding(input_ids, self.W["embed"])
-        if meta.is_decode and self.persistent_ok(input_ids.shape[0]):
+        if ops.reference_fp32():   # test-only fp32 truth: activations / residual in fp32 (ops.force_reference)
+            h = h.float()
+        if meta.is_decode and not ops._ref(h) and self.persistent_ok(input_ids.shape[0]):
             return self._forward_persistent(h, meta, k_cache, v_cache)
         residual = None
         pending = False   # h holds this rank's partial of a row-parallel output (TP all-reduce due)

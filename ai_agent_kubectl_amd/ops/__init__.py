@@ -19,18 +19,31 @@ from ._hip import check, require
 
 
 _FORCE_REF = False
+_REF_FP32 = False
 
 
 class force_reference:
-    """Test-only context: run the fp32 torch references even on GPU tensors (model-level parity)."""
+    """Test-only context: run the fp32 torch references even on GPU tensors (model-level parity).
+    fp32=True: the model also carries its activations and residual stream in fp32 between the ops
+    (models/llama.py), so only the weights and the KV cache are bf16 — the fp32 truth a greedy token
+    is compared against; fp32=False: every op rounds its output to bf16 as the engine's kernels do."""
+
+    def __init__(self, fp32: bool = False):
+        self.fp32 = fp32
 
     def __enter__(self):
-        global _FORCE_REF
-        self._old, _FORCE_REF = _FORCE_REF, True
+        global _FORCE_REF, _REF_FP32
+        self._old = (_FORCE_REF, _REF_FP32)
+        _FORCE_REF, _REF_FP32 = True, self.fp32
 
     def __exit__(self, *exc):
-        global _FORCE_REF
-        _FORCE_REF = self._old
+        global _FORCE_REF, _REF_FP32
+        _FORCE_REF, _REF_FP32 = self._old
+
+
+def reference_fp32() -> bool:
+    """Inside force_reference(fp32=True)."""
+    return _FORCE_REF and _REF_FP32
 
 
 def _ref(t: torch.Tensor) -> bool:
@@ -591,7 +604,7 @@ def big_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     M, K = x.shape
     N = w.shape[0]
     return (x.stride(1) == 1 and x.stride(0) % 8 == 0 and K % 128 == 0 and N % 128 == 0 and w.is_contiguous()
-            and w.shape[1] == K)
+            and w.shape[1] == K and M * x.stride(0) * 2 < 2 ** 31 - 4096 and N * K * 2 < 2 ** 31 - 4096)
 
 
 # Decode gate_up with the SwiGLU epilogue in the csrc/gemm_mfma.hip ring kernel, per decode bucket
@@ -608,8 +621,8 @@ DECODE_SWIGLU_BIG = 100
 
 
 def decode_swiglu_ok(x: torch.Tensor, w13: torch.Tensor) -> bool:
-    """Rows the ring kernel's SwiGLU epilogue takes: any M up to TILE_MAX_M (rows past M re-read row
-    M - 1); below 8 rows ModelRunner.tune_swiglu weighs it against the GEMV path with the activation in
+    """Rows the ring kernel's SwiGLU epilogue takes: any M up to TILE_MAX_M (rows past M re-read the
+    distinct rows r % M: a clamp to row M - 1 triggered LDS-DMA corruption, profiles/r5/gemm_big_clamp/); below 8 rows ModelRunner.tune_swiglu weighs it against the GEMV path with the activation in
     the down projection's staging (ops.swiglu_linear), down projection included."""
     M, K = x.shape
     return (x.is_contiguous() and w13.is_contiguous() and w13.shape[1] == K and K % 64 == 0
@@ -861,10 +874,13 @@ MOE_PREFILL = os.environ.get("KA_MOE_PREFILL", "auto")
 MOE_BIG_MIN_ROWS = int(os.environ.get("KA_MOE_BIG_MIN_ROWS", "6144"))
 
 
-def moe_big_ok(H: int, I: int, El: int) -> bool:
-    """Shapes the grouped gemm_big path takes (ka_gemm_big_grouped / ka_moe_sort requirements)."""
+def moe_big_ok(H: int, I: int, El: int, R: int = 0) -> bool:
+    """Shapes the grouped gemm_big path takes (ka_gemm_big_grouped / ka_moe_sort requirements).  R: the
+    routed rows (tokens x top-k); the [R, max(H, I)] activations must fit a 32-bit buffer descriptor
+    (Mixtral's [R, 14336] act passes 2^31 bytes at R ~ 75k), else the gm path takes the block."""
     return (H % 256 == 0 and I % 128 == 0 and El <= 64
-            and El * 2 * I * H * 2 < 2 ** 31 - 4096 and El * H * I * 2 < 2 ** 31 - 4096)
+            and El * 2 * I * H * 2 < 2 ** 31 - 4096 and El * H * I * 2 < 2 ** 31 - 4096
+            and R * max(H, I) * 2 < 2 ** 31 - 4096)
 
 
 def moe_experts_grouped(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
@@ -885,7 +901,7 @@ def moe_experts_grouped(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, to
     check(lib.ka_moe_align(_p(counts), _p(lists), _p(topk_ids), R, e0, El, st), "moe_align")
     I = two_i // 2
     big = MOE_PREFILL == "big" or (MOE_PREFILL == "auto" and R >= MOE_BIG_MIN_ROWS)
-    if big and moe_big_ok(H, I, El) and x.is_contiguous():
+    if big and moe_big_ok(H, I, El, R) and x.is_contiguous():
         chunks = (R + 255) // 256 + El
         xs = torch.empty((R, H), dtype=x.dtype, device=x.device)
         slot = torch.empty(R, dtype=torch.int32, device=x.device)

@@ -16,8 +16,23 @@ import threading
 from typing import Optional
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-# KA_HIP_LIB: load another build of the same library (A/B kernel experiments, scripts/)
-LIB_PATH = os.environ.get("KA_HIP_LIB") or os.path.join(LIB_DIR, "libkagent_hip.so")
+DEFAULT_LIB = os.path.join(LIB_DIR, "libkagent_hip.so")
+
+
+def _lib_path() -> str:
+    """The in-tree library, always, unless a diagnostic run asks for another build of it: KA_HIP_LIB is
+    honoured only together with KA_HIP_LIB_DIAG=1 (A/B kernel experiments, scripts/), so no stray
+    environment variable can route the engine, the tests or the bench to an experimental build."""
+    alt = os.environ.get("KA_HIP_LIB")
+    if alt and os.environ.get("KA_HIP_LIB_DIAG") == "1":
+        return alt
+    if alt:
+        raise RuntimeError("KA_HIP_LIB is set without KA_HIP_LIB_DIAG=1: refusing to load a non-default "
+                           f"kernel library ({alt}); unset it, or set KA_HIP_LIB_DIAG=1 for a diagnostic run")
+    return DEFAULT_LIB
+
+
+LIB_PATH = _lib_path()
 
 _lock = threading.Lock()
 _lib: Optional[ctypes.CDLL] = None

@@ -204,7 +204,7 @@ def gm_candidates(M: int, N: int, K: int, cfgs: Sequence[int] = ()):
     """(cfg, split) pairs of csrc/gemm_mfma.hip worth timing: tiles no taller than twice M and a
     grid of ~96-1024 workgroups on 256 CUs."""
     out = []
-    if K % 64 or N % 16:   # rows past M are clamped re-reads of row M - 1
+    if K % 64 or N % 16:   # rows past M re-read distinct rows r % M (never one clamped row: profiles/r5/gemm_big_clamp/)
         return out
     for cfg in cfgs or GM_TUNE_CFGS:
         bn, bm = gm_shape(cfg)

@@ -170,6 +170,33 @@ def test_persistent_stall_drops_the_persistent_graph(tiny):
         eng.healthy, eng.last_error = True, None
 
 
+def test_persistent_stall_retires_graph_until_synchronized(tiny):
+    """a stall must not destroy the persistent graph while the engine may still have
+    a chained replay of it queued.  The graph leaves service at once (no new replay can pick it) but is
+    only released by health_check(), after its device synchronize."""
+    from ai_agent_kubectl_amd.engine.runner import PersistentStall
+    eng, be = tiny
+    r, m = eng.runner, eng.runner.model
+    saved = (m.persistent, dict(r.graphs), dict(r.graph_persistent))
+    g = _FakeGraph(r, 2)
+    r.graphs[2] = g
+    r.graph_persistent[2] = True
+    try:
+        with pytest.raises(PersistentStall):
+            r._check_err(torch.tensor([0, 1], dtype=torch.int32))
+        assert 2 not in r.graphs and 2 not in r.graph_persistent
+        assert any(x is g for x in r._retired_graphs), "graph released before a synchronize"
+        r.health_check()
+        assert not r._retired_graphs
+    finally:
+        m.persistent = saved[0]
+        r.graphs.clear()
+        r.graphs.update(saved[1])
+        r.graph_persistent.clear()
+        r.graph_persistent.update(saved[2])
+        r._retired_graphs.clear()
+
+
 def test_error_word_clear_is_transparent(tiny):
     """A zero error word changes nothing (the readback rides behind every step's tokens)."""
     eng, be = tiny

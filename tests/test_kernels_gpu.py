@@ -884,6 +884,22 @@ def test_gemm_big_alternating_launches_exact():
     assert ops.gemm_big_err(torch.device(DEV)) == 0
 
 
+@pytest.mark.parametrize("amplify", [True, False])
+def test_gm_dispatched_plans_alternating_launches_exact(amplify):
+    """every (configuration, split-K, epilogue) of the ring kernels that the
+    persisted decode plan dispatches for Llama-3-8B buckets 128-512 (bf16 split-K partials included),
+    each launch right after an unrelated GEMM and checked whole against fp32 — with the duplicate-address
+    amplifier (ldx = 0: every X piece reads 8 identical rows) and without.  The kernels wait for LDS-DMA
+    with vmcnt(0) only (KA_GM_SCHED / KA_PP_SAFE), so no launch may be wrong; >= 500 launches per
+    combination: scripts/gm_plan_stress.py, profiles/r6/lds_dma_safety/."""
+    from ai_agent_kubectl_amd.ops import stress
+    combos = stress.dispatched_combos()
+    assert len(combos) >= 20, combos
+    res = stress.stress(combos, 6, amplify)
+    bad = {c: n for c, n in res.items() if n}
+    assert not bad, f"wrong launches (M, N, K, cfg, split, epi): {bad}"
+
+
 @pytest.mark.parametrize("M", [2944, 1100, 4096])
 def test_gemm_big_swiglu_split_tail_vs_fp32(M):
     """gate_up + SwiGLU epilogue with the split tail: silu(x g^T) * (x u^T) vs fp32 (the sum of the

@@ -180,3 +180,24 @@ def test_prefill_gemm_plan_buckets():
         assert not ops.use_big_gemm(x, w)   # CPU: reference path
     finally:
         ops.PREFILL_PLAN.pop((4096, 512, 256))
+
+
+def test_hip_lib_override_needs_the_diag_flag():
+    """an experimental kernel library (KA_HIP_LIB) is loaded only for an explicit
+    diagnostic run; a stray KA_HIP_LIB alone makes the import fail loudly instead of switching builds."""
+    import os
+    import subprocess
+    import sys
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = "import ai_agent_kubectl_amd.ops._hip as h; print(h.LIB_PATH)"
+    env = dict(os.environ, KA_HIP_LIB="/tmp/elsewhere/libkagent_hip.so")
+    env.pop("KA_HIP_LIB_DIAG", None)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, cwd=ROOT)
+    assert r.returncode != 0 and "KA_HIP_LIB_DIAG" in r.stderr
+    env["KA_HIP_LIB_DIAG"] = "1"
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, cwd=ROOT)
+    assert r.returncode == 0 and r.stdout.strip() == "/tmp/elsewhere/libkagent_hip.so"
+    env = dict(os.environ)
+    env.pop("KA_HIP_LIB", None)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, cwd=ROOT)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ops/lib/libkagent_hip.so")

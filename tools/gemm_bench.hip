@@ -49,6 +49,33 @@ __global__ void ref_kernel(float* out, const bf16_t* X, const bf16_t* W, const i
   out[(size_t)s * N + n] = acc;
 }
 
+// stress check: count outputs off the fp32 reference (ref [M, N] over all rows; the output of the
+// epilogue epi: 0 bf16 Y [M, ldy]; 1 / 2 fp32 / bf16 slabs P [split, M, N] summed here; 3 SwiGLU of
+// the interleaved gate / up reference into Y [M, N / 2])
+__global__ void cmp_kernel(int* bad, const float* ref, const void* Y, const void* P, int M, int N, int split,
+                           int epi, int ldy) {
+  const int NO = epi == 3 ? N / 2 : N;
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= (long)M * NO) return;
+  const int m = (int)(i / NO), c = (int)(i % NO);
+  float r, g;
+  if (epi == 3) {
+    const float gt = ref[(size_t)m * N + (c / 16) * 32 + c % 16], up = ref[(size_t)m * N + (c / 16) * 32 + 16 + c % 16];
+    r = gt / (1.f + expf(-gt)) * up;
+  } else {
+    r = ref[(size_t)m * N + c];
+  }
+  if (epi == 0 || epi == 3) {
+    g = bf2f(static_cast<const bf16_t*>(Y)[(size_t)m * ldy + c]);
+  } else {
+    g = 0.f;
+    for (int z = 0; z < split; ++z)
+      g += epi == 1 ? static_cast<const float*>(P)[((size_t)z * M + m) * N + c]
+                    : bf2f(static_cast<const bf16_t*>(P)[((size_t)z * M + m) * N + c]);
+  }
+  if (!(fabsf(g - r) <= 0.03f + 0.02f * fabsf(r))) atomicAdd(bad, 1);
+}
+
 static double now_check(std::vector<float>& ref, std::vector<uint16_t>& got, int S, int N, int ld, bool swiglu,
                         double* max_ref) {
   double err = 0, mr = 0;
@@ -85,6 +112,18 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int warm = getenv("GB_WARM") ? atoi(getenv("GB_WARM")) : 0;   // 1: no weight rotation
+  // GB_STRESS=n: after timing, n launches each preceded by an unrelated rocBLAS GEMM, every output
+  // checked against the fp32 reference (the launch pattern that exposed unordered LDS-DMA completion,
+  // profiles/r5/gemm_big_clamp/).  GB_LDX0=1: every X row aliases row 0 (ldx = 0), so each X DMA piece
+  // reads 8 identical rows: the duplicate-address amplifier of that hazard.
+  const int stress = getenv("GB_STRESS") ? atoi(getenv("GB_STRESS")) : 0;
+  const int ldx0 = getenv("GB_LDX0") ? atoi(getenv("GB_LDX0")) : 0;
+  bf16_t *OA = nullptr, *OC = nullptr;
+  if (stress > 0) {
+    CK(hipMalloc(&OA, (size_t)4096 * 4096 * 2));
+    CK(hipMalloc(&OC, (size_t)4096 * 4096 * 2));
+    hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, st, OA, (size_t)4096 * 4096, 99u, 1.0f / 64.f);
+  }
 #ifdef GM_KSTAMP
   unsigned long long* kst_;
   const size_t nkst = (size_t)65536 * 8 * 4;   // up to 65536 blocks x 8 waves
@@ -119,6 +158,7 @@ int main(int argc, char** argv) {
 
     const bool sw = epi == 3;
     const int ldy = sw ? N / 2 : N;
+    const int ldx = ldx0 ? 0 : K;
     auto run = [&](int r) -> int {
       const bf16_t* w = W + (size_t)(r % nrot) * N * K;
       if (cfg < 0) {
@@ -128,7 +168,7 @@ int main(int argc, char** argv) {
                                     rocblas_datatype_bf16_r, N, Y, rocblas_datatype_bf16_r, N,
                                     rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
       }
-      return ka_gemm_mfma(Y, P, X, w, M, N, K, K, ldy, split, cfg, epi, gm, st);
+      return ka_gemm_mfma(Y, P, X, w, M, N, K, ldx, ldy, split, cfg, epi, gm, st);
     };
     int rc = run(0);
     if (rc) {
@@ -145,7 +185,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&drows, S * 4));
     CK(hipMalloc(&dref, (size_t)S * N * 4));
     CK(hipMemcpy(drows, rows.data(), S * 4, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(ref_kernel, dim3((N + 255) / 256, S), dim3(256), 0, st, dref, X, W, drows, S, N, K, K);
+    hipLaunchKernelGGL(ref_kernel, dim3((N + 255) / 256, S), dim3(256), 0, st, dref, X, W, drows, S, N, K, ldx);
     CK(hipStreamSynchronize(st));
     std::vector<float> ref((size_t)S * N);
     CK(hipMemcpy(ref.data(), dref, ref.size() * 4, hipMemcpyDeviceToHost));
@@ -239,6 +279,41 @@ int main(int argc, char** argv) {
              q(loop, .5), q(loop, .9), q(epi_t, .5), q(end, .5), q(end, 1));
     }
 #endif
+    int wrong = -1;
+    if (stress > 0 && cfg >= 0) {
+      std::vector<int> all(M);
+      for (int s = 0; s < M; ++s) all[s] = s;
+      int *dall, *dbad;
+      float* rfull;
+      CK(hipMalloc(&dall, M * 4));
+      CK(hipMalloc(&rfull, (size_t)M * N * 4));
+      CK(hipMalloc(&dbad, stress * 4));
+      CK(hipMemset(dbad, 0, stress * 4));
+      CK(hipMemcpy(dall, all.data(), M * 4, hipMemcpyHostToDevice));
+      hipLaunchKernelGGL(ref_kernel, dim3((N + 255) / 256, M), dim3(256), 0, st, rfull, X, W, dall, M, N, K, ldx);
+      const long nout = (long)M * (sw ? N / 2 : N);
+      for (int r = 0; r < stress; ++r) {
+        const float alpha = 1.f, beta = 0.f;
+        rocblas_gemm_ex(rb, rocblas_operation_transpose, rocblas_operation_none, 4096, 4096, 4096, &alpha, OA,
+                        rocblas_datatype_bf16_r, 4096, OA, rocblas_datatype_bf16_r, 4096, &beta, OC,
+                        rocblas_datatype_bf16_r, 4096, OC, rocblas_datatype_bf16_r, 4096, rocblas_datatype_f32_r,
+                        rocblas_gemm_algo_standard, 0, 0);
+        run(0);
+        hipLaunchKernelGGL(cmp_kernel, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0, st, dbad + r, rfull, Y, P, M,
+                           N, split, epi, ldy);
+      }
+      CK(hipStreamSynchronize(st));
+      std::vector<int> hb(stress);
+      CK(hipMemcpy(hb.data(), dbad, stress * 4, hipMemcpyDeviceToHost));
+      wrong = 0;
+      int worst = 0;
+      for (int v : hb) { wrong += v > 0; worst = std::max(worst, v); }
+      printf("  stress: %d wrong of %d launches (worst launch %d bad outputs)%s\n", wrong, stress, worst,
+             ldx0 ? " [ldx 0 amplifier]" : "");
+      CK(hipFree(dall));
+      CK(hipFree(rfull));
+      CK(hipFree(dbad));
+    }
     printf("M=%5d N=%6d K=%5d cfg=%2d split=%2d epi=%d gm=%d : %8.2f us  %7.1f TF/s  %5.2f TB/s  maxerr %.3g (ref max %.3g)%s\n",
            M, N, K, cfg, split, epi, gm, us, tf, tb, err, (cfg < 0 && sw) ? 0.0 : mr,
            err > 0.02 * std::max(1.0, (cfg < 0 && sw) ? 1.0 : mr) ? "  <-- MISMATCH" : "");
