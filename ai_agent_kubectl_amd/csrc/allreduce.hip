@@ -148,11 +148,17 @@ __global__ __launch_bounds__(512) void allgather_oneshot_kernel(ArArgs a, const 
 // the reduced activation never makes a round trip through memory and one launch replaces two.
 // Arithmetic is that of all-reduce -> rmsnorm_kernel (elementwise.hip) exactly: the rank sum is
 // rounded to bf16, the residual sum is rounded to bf16, fp32 sum of squares.  hidden <= 8192.
-__global__ __launch_bounds__(512) void allreduce_rmsnorm_kernel(ArArgs a, const bf16_t* __restrict__ in,
+// split > 1: `in` holds the producing GEMM's split-K partial slabs [split, rows, hidden] (fp32, or bf16
+// when in_bf16) and this rank's contribution is their fp32 sum rounded to bf16 — what splitk_reduce
+// would have written — computed while staging it into the exchange buffer: the row-parallel O / down
+// projections of a TP rank hand their partials straight to the collective (one launch and one HBM
+// round trip fewer per projection, as the TP = 1 path's fused split-K reduce + RMSNorm).
+__global__ __launch_bounds__(512) void allreduce_rmsnorm_kernel(ArArgs a, const void* __restrict__ in,
                                                                 bf16_t* __restrict__ out, bf16_t* residual,
                                                                 const bf16_t* __restrict__ w, float eps,
                                                                 unsigned* ctr, unsigned* done, int* err, int rank,
-                                                                int world, int rows, int hidden, int cap) {
+                                                                int world, int rows, int hidden, int cap, int split,
+                                                                int in_bf16) {
   __shared__ unsigned s_epoch;
   __shared__ float red[8];
   if (threadIdx.x == 0) s_epoch = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
@@ -164,8 +170,38 @@ __global__ __launch_bounds__(512) void allreduce_rmsnorm_kernel(ArArgs a, const 
   const int beg = r0 * hidden, end = r1 * hidden;
 
   bf16_t* mine = a.data[rank] + half;
-  for (int i = beg + threadIdx.x * 8; i < end; i += blockDim.x * 8)
-    *reinterpret_cast<u32x4*>(mine + i) = *reinterpret_cast<const u32x4*>(in + i);
+  if (split <= 1 && in_bf16) {
+    const bf16_t* src = static_cast<const bf16_t*>(in);
+    for (int i = beg + threadIdx.x * 8; i < end; i += blockDim.x * 8)
+      *reinterpret_cast<u32x4*>(mine + i) = *reinterpret_cast<const u32x4*>(src + i);
+  } else {
+    const size_t ps = (size_t)rows * hidden;   // elements per slab
+    for (int i = beg + threadIdx.x * 8; i < end; i += blockDim.x * 8) {
+      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int z = 0; z < split; ++z) {
+        if (in_bf16) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(static_cast<const bf16_t*>(in) + z * ps + i);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            s[2 * k] += lo_f(v[k]);
+            s[2 * k + 1] += hi_f(v[k]);
+          }
+        } else {
+          const float* f = static_cast<const float*>(in) + z * ps + i;
+          const f32x4 v0 = *reinterpret_cast<const f32x4*>(f), v1 = *reinterpret_cast<const f32x4*>(f + 4);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            s[k] += v0[k];
+            s[4 + k] += v1[k];
+          }
+        }
+      }
+      u32x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = pack2(s[2 * k], s[2 * k + 1]);
+      *reinterpret_cast<u32x4*>(mine + i) = o;
+    }
+  }
   __threadfence_system();
   __syncthreads();
   if ((int)threadIdx.x < world) {
@@ -313,24 +349,27 @@ extern "C" int ka_allgather_oneshot(void* out, const void* in, void* const* data
   KA_CHECK_LAUNCH();
 }
 
-// in: this rank's partial [rows, hidden] bf16; out: rmsnorm(sum + residual) * w; residual (may be
-// null) is updated in place to sum + residual.  rows * hidden <= cap, hidden % 8 == 0, <= 8192;
-// nblocks (identical on every rank) <= min(rows, AR_MAX_BLOCKS).
+// in: this rank's partial [rows, hidden] bf16 (split <= 1, in_bf16 = 1), or split-K partial slabs
+// [split, rows, hidden] of fp32 (in_bf16 = 0) / bf16 (in_bf16 = 1); out: rmsnorm(sum + residual) * w;
+// residual (may be null) is updated in place to sum + residual.  rows * hidden <= cap, hidden % 8 == 0,
+// <= 8192; nblocks (identical on every rank) <= min(rows, AR_MAX_BLOCKS).
 extern "C" int ka_allreduce_rmsnorm(void* out, const void* in, void* residual, const void* w, float eps,
                                     void* const* data, void* const* flags, void* ctr, void* done, void* err, int rank,
-                                    int world, int rows, int hidden, int cap, int nblocks, hipStream_t stream) {
+                                    int world, int rows, int hidden, int cap, int nblocks, int split, int in_bf16,
+                                    hipStream_t stream) {
   if (rows <= 0) return 0;
   if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || hidden % 8 || hidden > 8192 ||
-      (long)rows * hidden > cap || nblocks < 1 || nblocks > AR_MAX_BLOCKS || nblocks > rows)
+      (long)rows * hidden > cap || nblocks < 1 || nblocks > AR_MAX_BLOCKS || nblocks > rows || split < 1 ||
+      (split == 1 && !in_bf16))
     return (int)hipErrorInvalidValue;
   ArArgs a;
   for (int p = 0; p < AR_MAX_RANKS; ++p) {
     a.data[p] = p < world ? static_cast<bf16_t*>(data[p]) : nullptr;
     a.flags[p] = p < world ? static_cast<unsigned*>(flags[p]) : nullptr;
   }
-  hipLaunchKernelGGL(allreduce_rmsnorm_kernel, dim3(nblocks), dim3(512), 0, stream, a,
-                     static_cast<const bf16_t*>(in), static_cast<bf16_t*>(out), static_cast<bf16_t*>(residual),
+  hipLaunchKernelGGL(allreduce_rmsnorm_kernel, dim3(nblocks), dim3(512), 0, stream, a, in,
+                     static_cast<bf16_t*>(out), static_cast<bf16_t*>(residual),
                      static_cast<const bf16_t*>(w), eps, static_cast<unsigned*>(ctr), static_cast<unsigned*>(done),
-                     static_cast<int*>(err), rank, world, rows, hidden, cap);
+                     static_cast<int*>(err), rank, world, rows, hidden, cap, split, in_bf16);
   KA_CHECK_LAUNCH();
 }

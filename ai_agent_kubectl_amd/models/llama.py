@@ -165,10 +165,11 @@ class LlamaModel:
                     a = self._attention(q, meta, k_cache[li], v_cache[li])
             if 0 < meta.num_tokens < T and not meta.is_decode and not pruned:
                 a[meta.num_tokens:].zero_()   # padding rows: no sequence's attention writes them
-            # TP = 1: the projections feeding a norm leave their split-K partials to the fused
-            # reduce + residual + RMSNorm kernel (ops.SplitK); with TP the row-parallel output is
-            # bf16 and the all-reduce is fused with that norm (comm.all_reduce_rmsnorm, A1)
-            fuse = self._local_comm
+            # the projections feeding a norm leave their split-K partials to the consumer
+            # (ops.SplitK): TP = 1 the fused reduce + residual + RMSNorm kernel; a TP rank's decode
+            # step the one-shot all-reduce + RMSNorm kernel, which reduces the slabs while staging its
+            # contribution (comm.all_reduce_rmsnorm, A1 / A2; comm.splitk_norm)
+            fuse = self._local_comm or (meta.is_decode and getattr(self.comm, "splitk_norm", False))
             h = ops.linear(a.reshape(a.shape[0], self.hq * self.D), L["wo"], defer_reduce=fuse,
                            bf16_partials=self.bf16_partials)
             x = self._reduce_norm(h, L["ln2"], eps, residual, True)

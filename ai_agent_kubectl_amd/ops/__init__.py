@@ -92,6 +92,12 @@ class SplitK(NamedTuple):
         return self.P.float().sum(0).to(torch.bfloat16)
 
 
+def splitk_resolve(t: SplitK) -> torch.Tensor:
+    """bf16 [M, N] sum of split-K partials (the RCCL all-reduce path of a TP rank, which cannot read
+    the slabs itself)."""
+    return t.resolve()
+
+
 def rmsnorm(x, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
             out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = rmsnorm(x (+ residual)) * w; when `residual` is given it is updated in place to x + residual.

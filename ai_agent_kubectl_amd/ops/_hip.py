@@ -91,7 +91,7 @@ _SIGS = {
     "ka_moe_sort": [P, P, P, P, P, P, I, I, I, I, I, P],
     "ka_allreduce_oneshot": [P, P, P, P, P, P, P, I, I, I, I, I, P],
     "ka_allgather_oneshot": [P, P, P, P, P, P, P, I, I, I, I, I, P],
-    "ka_allreduce_rmsnorm": [P, P, P, P, F, P, P, P, P, P, I, I, I, I, I, I, P],
+    "ka_allreduce_rmsnorm": [P, P, P, P, F, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
     "ka_ar_alloc": [P, ctypes.c_size_t],
     "ka_ar_free": [P],
     "ka_ar_get_handle": [P, P],

@@ -55,8 +55,8 @@ def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq: i
     if valid.any():
         s = slots[valid]
         blk, off = s // bs, s % bs
-        k_cache[blk, :, off, :] = k_rot[valid]
-        v_cache[blk, :, :, off] = v[valid]
+        k_cache[blk, :, off, :] = k_rot[valid].to(k_cache.dtype)
+        v_cache[blk, :, :, off] = v[valid].to(v_cache.dtype)
     return q_out
 
 

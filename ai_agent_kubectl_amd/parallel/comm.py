@@ -82,6 +82,8 @@ class LocalComm:
         from .. import ops
         return ops.rmsnorm(t, w, eps, residual=residual)
 
+    splitk_norm = True
+
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         return t
 
@@ -121,16 +123,26 @@ class TorchComm:
             self.timer.end(tok)
         return t
 
-    def all_reduce_rmsnorm(self, t: torch.Tensor, w: torch.Tensor, eps: float, residual=None) -> torch.Tensor:
-        """rmsnorm(all_reduce(t) (+ residual)) * w: one fused one-shot launch for decode-size bf16
-        rows (residual updated in place), else the all-reduce followed by the RMSNorm kernel."""
+    def all_reduce_rmsnorm(self, t, w: torch.Tensor, eps: float, residual=None) -> torch.Tensor:
+        """rmsnorm(all_reduce(t) (+ residual)) * w: one fused one-shot launch for decode-size rows
+        (residual updated in place), else the all-reduce followed by the RMSNorm kernel.  t may be the
+        split-K partials of the row-parallel projection (ops.SplitK): the one-shot kernel reduces them
+        while staging its contribution; on the RCCL path they are reduced first."""
         from .. import ops
         if self.world_size > 1 and self.custom_ar is not None and self.custom_ar.can_fuse_norm(t):
+            rows, hidden = t.shape
             self.allreduce_calls += 1
-            self.allreduce_bytes += t.numel() * t.element_size()
+            self.allreduce_bytes += rows * hidden * 2
             return self.custom_ar.all_reduce_rmsnorm(t, w, eps, residual)
+        if isinstance(t, ops.SplitK):
+            t = ops.splitk_resolve(t)
         self.all_reduce(t)
         return ops.rmsnorm(t, w, eps, residual=residual)
+
+    @property
+    def splitk_norm(self) -> bool:
+        """all_reduce_rmsnorm takes split-K partials (models/llama.py then defers the O / down reduce)."""
+        return self.custom_ar is not None
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         if self.custom_ar is not None and self.custom_ar.should_gather(t):
@@ -180,10 +192,16 @@ class VirtualRankComm:
         self.allreduce_bytes += t.numel() * t.element_size()
         return t
 
-    def all_reduce_rmsnorm(self, t: torch.Tensor, w: torch.Tensor, eps: float, residual=None) -> torch.Tensor:
+    def all_reduce_rmsnorm(self, t, w: torch.Tensor, eps: float, residual=None) -> torch.Tensor:
+        """t: bf16 rows or split-K partials (ops.SplitK, reduced inside the norm kernel as the fused
+        one-shot kernel reduces them inside the collective)."""
         from .. import ops
-        self.all_reduce(t)
+        rows, hidden = t.shape
+        self.allreduce_calls += 1
+        self.allreduce_bytes += rows * hidden * 2
         return ops.rmsnorm(t, w, eps, residual=residual)
+
+    splitk_norm = True   # all_reduce_rmsnorm takes split-K partials (models/llama.py defers the reduce)
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         return t.unsqueeze(0).expand((self.world_size,) + tuple(t.shape)).contiguous()

@@ -96,21 +96,33 @@ class OneShotAllReduce:
             self.rank, self.world, n, self.cap, self.blocks_for(n), ctypes.c_void_p(stream)), "allreduce_oneshot")
         return t
 
-    def can_fuse_norm(self, t: torch.Tensor) -> bool:
+    def can_fuse_norm(self, t) -> bool:
+        """t: a bf16 [rows, hidden] partial, or the `ops.SplitK` partial slabs of the producing GEMM."""
+        from .. import ops
+        if isinstance(t, ops.SplitK):
+            rows, hidden = t.shape
+            return (t.P.is_cuda and t.P.is_contiguous() and hidden % 8 == 0 and hidden <= 8192
+                    and 0 < rows * hidden <= self.cap)
         return self.should_use(t) and t.dim() == 2 and t.shape[1] % 8 == 0 and t.shape[1] <= 8192
 
-    def all_reduce_rmsnorm(self, t: torch.Tensor, w: torch.Tensor, eps: float, residual=None,
-                           out=None) -> torch.Tensor:
-        """rmsnorm(sum_ranks(t) (+ residual)) * w in one launch (residual updated in place)."""
-        rows, hidden = t.shape
-        out = torch.empty_like(t) if out is None else out
-        stream = torch.cuda.current_stream(t.device).cuda_stream
+    def all_reduce_rmsnorm(self, t, w: torch.Tensor, eps: float, residual=None, out=None) -> torch.Tensor:
+        """rmsnorm(sum_ranks(t) (+ residual)) * w in one launch (residual updated in place).  A SplitK
+        input is reduced over its slabs inside the same launch (no splitk_reduce kernel)."""
+        from .. import ops
+        if isinstance(t, ops.SplitK):
+            src, split, in_bf16 = t.P, t.split, int(t.is_bf16)
+            rows, hidden = t.shape
+        else:
+            src, split, in_bf16 = t, 1, 1
+            rows, hidden = t.shape
+        out = torch.empty((rows, hidden), dtype=w.dtype, device=w.device) if out is None else out
+        stream = torch.cuda.current_stream(src.device).cuda_stream
         self.check_rc(self.lib.ka_allreduce_rmsnorm(
-            ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(t.data_ptr()),
+            ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(src.data_ptr()),
             ctypes.c_void_p(residual.data_ptr() if residual is not None else 0), ctypes.c_void_p(w.data_ptr()),
             float(eps), self._data, self._flags, ctypes.c_void_p(self._ctr), ctypes.c_void_p(self._done),
             ctypes.c_void_p(self._err), self.rank, self.world, rows, hidden, self.cap, min(rows, AR_MAX_BLOCKS),
-            ctypes.c_void_p(stream)), "allreduce_rmsnorm")
+            split, in_bf16, ctypes.c_void_p(stream)), "allreduce_rmsnorm")
         return out
 
     def should_gather(self, t: torch.Tensor) -> bool:

@@ -47,6 +47,18 @@ def _worker(rank, world, port, q):
             got_out = ar.all_reduce_rmsnorm(t2, wgt, 1e-5, r2)
             torch.cuda.synchronize()
             errs.append(0.0 if torch.equal(got_out, want_out) and torch.equal(r2, r1) else 1.0)
+            # split-K partial slabs reduced inside the collective (round 6: a TP rank's O / down hand
+            # their partials to it) == splitk_reduce's bf16 sum then the collective, bit for bit
+            for pdt, split in ((torch.float32, 4), (torch.bfloat16, 8), (torch.bfloat16, 2)):
+                slabs = (torch.randn(split, rows, hidden, generator=g) * 0.3).to(pdt).cuda()
+                r3, r4 = res0.clone(), res0.clone()
+                acc = slabs[0].float()
+                for z in range(1, split):   # the kernel's order: fp32, slab 0 first
+                    acc = acc + slabs[z].float()
+                want3 = ar.all_reduce_rmsnorm(acc.to(torch.bfloat16), wgt, 1e-5, r3)
+                got4 = ar.all_reduce_rmsnorm(ops.SplitK(slabs, split), wgt, 1e-5, r4)
+                torch.cuda.synchronize()
+                errs.append(0.0 if torch.equal(got4, want3) and torch.equal(r4, r3) else 1.0)
             t3 = torch.arange(rows * 4, dtype=torch.int32, device="cuda").view(rows, 4) + 1000 * rank
             gath = ar.all_gather(t3)
             errs.append(0.0 if all(torch.equal(gath[p], t3 - 1000 * rank + 1000 * p) for p in range(world)) else 1.0)

@@ -129,6 +129,18 @@ def _decode_run(eng, B, steps=8, graph=True):
     sch.gather_max_s = 0.0
     sch.hold_steps = 0
     out = []
+    for s in list(sch.running) + list(sch.waiting):   # whatever an earlier (failed) test left behind
+        sch.abort(s)
+    try:
+        _decode_steps(eng, B, steps, graph, out, be, params)
+    finally:
+        for s in list(sch.running) + list(sch.waiting):   # the next test starts with an empty scheduler
+            sch.abort(s)
+    return out
+
+
+def _decode_steps(eng, B, steps, graph, out, be, params):
+    sch, r, m = eng.scheduler, eng.runner, eng.runner.model
     with torch.inference_mode():
         for i in range(B):
             sch.add(Sequence(prompt_ids=be.prompt_ids(QUERIES[i % len(QUERIES)] + f" #{i}"), params=params,
@@ -177,9 +189,6 @@ def _decode_run(eng, B, steps=8, graph=True):
                 assert m.persistent_err() == 0
             eng._apply(batch, tok)
             sch.on_step_done(batch)
-        for s in list(sch.running):   # the next test starts with an empty scheduler
-            sch.abort(s)
-    return out
 
 
 @pytest.mark.parametrize("B", [1, 2])
