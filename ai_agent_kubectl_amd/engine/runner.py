@@ -182,7 +182,9 @@ class ModelRunner:
         from ..ops.autotune import tune_linear
         groups = {}
         norm_fed = set()
-        local = getattr(self.model, "_local_comm", False)
+        # O / down partials feed the norm directly at TP = 1, and in a TP rank's decode step when the
+        # collective reduces them (models/llama.py `fuse`): timed with that consumer
+        local = getattr(self.model, "_local_comm", False) or getattr(self.model.comm, "splitk_norm", False)
         for L in self.model.layers:
             for k in ("wqkv", "wo", "w13", "w2"):
                 w = L.get(k)

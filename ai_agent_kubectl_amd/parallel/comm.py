@@ -25,6 +25,12 @@ from typing import List, Optional
 import torch
 
 
+# TP decode: the row-parallel O / down projections hand their split-K partials to the fused all-reduce +
+# RMSNorm (csrc/allreduce.hip reduces the slabs while staging its contribution).  0: reduce them first
+# (splitk_reduce), as before round 6.
+TP_SPLITK_NORM = os.environ.get("KA_TP_SPLITK_NORM", "1") == "1"
+
+
 class CollectiveTimer:
     """Wall time of eager all-reduces for the `rccl_allreduce_seconds` histogram.
     Device tensors: a pair of timing events on the issuing stream, resolved later by `drain()`
@@ -141,8 +147,9 @@ class TorchComm:
 
     @property
     def splitk_norm(self) -> bool:
-        """all_reduce_rmsnorm takes split-K partials (models/llama.py then defers the O / down reduce)."""
-        return self.custom_ar is not None
+        """all_reduce_rmsnorm takes split-K partials (models/llama.py then defers the O / down reduce):
+        with the one-shot kernel, unless KA_TP_SPLITK_NORM=0 (the A/B against splitk_reduce first)."""
+        return self.custom_ar is not None and TP_SPLITK_NORM
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         if self.custom_ar is not None and self.custom_ar.should_gather(t):
@@ -201,7 +208,9 @@ class VirtualRankComm:
         self.allreduce_bytes += rows * hidden * 2
         return ops.rmsnorm(t, w, eps, residual=residual)
 
-    splitk_norm = True   # all_reduce_rmsnorm takes split-K partials (models/llama.py defers the reduce)
+    @property
+    def splitk_norm(self) -> bool:   # all_reduce_rmsnorm takes split-K partials (models/llama.py defers the reduce)
+        return TP_SPLITK_NORM
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         return t.unsqueeze(0).expand((self.world_size,) + tuple(t.shape)).contiguous()

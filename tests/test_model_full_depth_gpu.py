@@ -180,7 +180,11 @@ def _decode_steps(eng, B, steps, graph, out, be, params):
                 assert m.persistent_err() == 0
             del kc, vc
             agree = sum(a == b for a, b in zip(tok, tok_ref)) / B
-            out.append(_cmp(lg, lg_ref) + (agree,))
+            # every disagreement's fp32 logit margin: how far the fp32 truth prefers its token over the
+            # HIP token (both allowed by the mask); a near-tie is smaller than the step's logit error
+            gap = max([float(lg_ref[i, tok_ref[i]] - lg_ref[i, tok[i]]) for i in range(B) if tok[i] != tok_ref[i]],
+                      default=0.0)
+            out.append(_cmp(lg, lg_ref) + (agree, gap))
             if graph:
                 g.replay()   # the real cache gets this step's keys / values from the graph
                 torch.cuda.synchronize()
@@ -245,10 +249,15 @@ AGREE_MIN = {1: 0.75, 2: 0.75, 256: 0.8}
 
 
 def _report(name, res):
-    print(f"\n{name}: per-step (cos, max|d|, rel, token agreement):",
+    print(f"\n{name}: per-step (cos, max|d|, rel, token agreement, largest fp32 margin of a disagreement):",
           [tuple(round(v, 4) for v in x) for x in res])
     agree = sum(x[3] for x in res) / len(res)
-    print(f"{name}: mean greedy-token agreement with fp32 = {agree:.4f}, max rel = {max(x[2] for x in res):.4f}")
+    print(f"{name}: mean greedy-token agreement with fp32 = {agree:.4f}, max rel = {max(x[2] for x in res):.4f}, "
+          f"largest fp32 logit margin of a disagreeing row = {max(x[4] for x in res):.4f} "
+          f"(max |dlogit| {max(x[1] for x in res):.4f})")
+    # every disagreement is a near-tie of the fp32 model: the HIP logits rank the two tokens the other
+    # way round, so the fp32 margin is at most the logit error of both (2 max |dlogit|)
+    assert all(x[4] <= 2 * x[1] + 1e-3 for x in res), res
     return agree
 
 
@@ -257,7 +266,7 @@ def test_full_depth_decode_b1_persistent(eng):
     assert m.persistent_ok() and eng.runner.graph_persistent.get(1)
     res = _decode_run(eng, 1)
     agree = _report("B=1 persistent decode, 32 layers", res)
-    for cos, err, rel, _ in res:
+    for cos, err, rel, _, _ in res:
         assert cos > COS_MIN and rel < REL_MAX, res
     assert agree >= AGREE_MIN[1], res
 
@@ -269,7 +278,7 @@ def test_full_depth_decode_b2_persistent(eng):
     assert m.persistent_ok(2) and eng.runner.graph_persistent.get(2)
     res = _decode_run(eng, 2)
     agree = _report("B=2 persistent decode, 32 layers", res)
-    for cos, err, rel, _ in res:
+    for cos, err, rel, _, _ in res:
         assert cos > COS_MIN and rel < REL_MAX, res
     assert agree >= AGREE_MIN[2], res
 
@@ -277,7 +286,7 @@ def test_full_depth_decode_b2_persistent(eng):
 def test_full_depth_decode_b256_graph(eng):
     res = _decode_run(eng, 256)
     agree = _report("B=256 decode chain, 32 layers", res)
-    for cos, err, rel, _ in res:
+    for cos, err, rel, _, _ in res:
         assert cos > COS_MIN and rel < REL_MAX, res
     assert agree >= AGREE_MIN[256], res
 
@@ -295,7 +304,7 @@ def test_full_depth_decode_b2_kernel_chain(eng):
     finally:
         m.persistent = saved
     agree = _report("B=2 decode kernel chain (no persistent kernel), 32 layers", res)
-    for cos, err, rel, _ in res:
+    for cos, err, rel, _, _ in res:
         assert cos > COS_MIN and rel < REL_MAX, res
     assert agree >= AGREE_MIN[2], res
 
@@ -312,6 +321,6 @@ def test_full_depth_decode_b256_fp32_partials(eng):
     finally:
         m.bf16_partials, m.bf16_qkv_partials = saved
     agree = _report("B=256 decode chain, fp32 split-K partials, 32 layers", res)
-    for cos, err, rel, _ in res:
+    for cos, err, rel, _, _ in res:
         assert cos > COS_MIN and rel < REL_MAX, res
     assert agree >= AGREE_MIN[256], res
