@@ -33,6 +33,8 @@
 
 namespace pd {
 
+#define KA_HD __host__ __device__ __forceinline__
+
 #ifndef KA_PD_RING
 #define KA_PD_RING 16
 #endif
@@ -59,11 +61,15 @@ constexpr int NT = 512, NW = NT / 64, HD = 128, KBS = 16, NT_ = NT;
 // LDS-DMA ring slots (1 KB) per wave: KA_PD_RING (16) in every phase, except the down rows at B = 2,
 // whose two act rows (2 x I bf16) take LDS the ring gives up there (12 slots, 96 KB per CU in flight;
 // 8 slots measured 16.4 us per layer for the down rows against 13.2 at B = 1)
-template <int B>
-constexpr int ring_down() { return B == 1 ? KA_PD_RING : 12; }
+template <int B, int RG = KA_PD_RING>
+constexpr int ring_down() { return B == 1 ? RG : (RG < 12 ? RG : 12); }
 static_assert((KA_PD_RING & (KA_PD_RING - 1)) == 0 && KA_PD_RING >= 2 && KA_PD_RING <= 16, "ring: a power of two <= 16");
 constexpr int MAXB = 2;     // sequences per launch
-constexpr int XS_MIN = 29 * 1024;   // the attention leader's scratch (aliases the x rows): 28.3 KB
+// The attention leader's scratch (aliases the x rows) for GR = 4 or 8 rows per KV group (GQA <= 4 /
+// <= 8): P re-layout 10 KB | rotated q GR x 128 bf16 | new k, v | per-wave m, l | new-token scores |
+// per-wave o [NW][GR][128] fp32
+KA_HD int scratch_bytes(int gr) { return 10240 + gr * 256 + 1024 + 2 * 8 * gr * 4 + 64 + 8 * gr * 128 * 4; }
+constexpr int XS_MIN = 29 * 1024;   // GR = 4: 28.3 KB
 
 struct Layer {
   const bf16_t* wqkv;   // [(hq + 2 hkv) 128, H]
@@ -552,9 +558,11 @@ KA_DEV void rmsnorm_rows_to_lds(const Args& a, const float* res, const bf16_t* g
 // > 80 KB: one workgroup per CU.
 constexpr int LDS_X = 0, LDS_ATT = 0;
 
-template <int B>
+// RG: weight-ring slots per wave (16; 12 where the GQA-8 attention scratch needs the LDS: the 70B
+// tensor-parallel rank, hq / hkv = 8)
+template <int B, int RG>
 __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
-  constexpr int RG = KA_PD_RING, RGD = ring_down<B>();
+  constexpr int RGD = ring_down<B, RG>();
   extern __shared__ __attribute__((aligned(16))) uint4 lds_u4[];
   char* const lds = reinterpret_cast<char*>(lds_u4);
   bf16_t* const xs = reinterpret_cast<bf16_t*>(lds + LDS_X);
@@ -695,14 +703,16 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       PD_STAMP(3);
       // scratch (LDS_ATT): per-wave P re-layout | rotated q (bf16) | new k, v (fp32) | per-wave m, l |
       // new-token scores | per-wave o of the group's q rows
+      // (GR = 4 or 8 rows per KV group: scratch_bytes)
+      const int GR = Gq > 4 ? 8 : 4;
       bf16_t* const pscr = reinterpret_cast<bf16_t*>(lds + LDS_ATT);             // [NW][16 PSTR]
-      bf16_t* const qb = reinterpret_cast<bf16_t*>(lds + LDS_ATT + 10240);       // [4][128]
-      float* const kn = reinterpret_cast<float*>(lds + LDS_ATT + 11264);         // [128]
+      bf16_t* const qb = reinterpret_cast<bf16_t*>(lds + LDS_ATT + 10240);       // [GR][128]
+      float* const kn = reinterpret_cast<float*>(lds + LDS_ATT + 10240 + GR * 256);   // [128]
       float* const vn = kn + HD;                                                  // [128]
-      float* const mo = vn + HD;                                                  // [NW][4]
-      float* const lo = mo + NW * 4;                                              // [NW][4]
-      float* const snr = lo + NW * 4;                                             // [4] (+ pad)
-      float* const oo = snr + 16;                                                 // [NW][4][128]
+      float* const mo = vn + HD;                                                  // [NW][GR]
+      float* const lo = mo + NW * GR;                                             // [NW][GR]
+      float* const snr = lo + NW * GR;                                            // [GR] (+ pad)
+      float* const oo = snr + 16;                                                 // [NW][GR][128]
       const float* cs = a.cos_sin + (size_t)p * HD;
       // RoPE (neox halves) on the group's q heads and k; v as is
       for (int it = tid; it < (Gq + 2) * (HD / 2); it += NT) {
@@ -813,17 +823,18 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
         for (int n = 0; n < 8; ++n) o[n] = mfma16x16x32(pf, as_bf16x8(vf[n]), o[n]);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // P scratch read before the next chunk's writes
       }
-      // per-wave (m, l, o) of rows 0 .. Gq - 1 (lanes gq == 0 hold rows r = 0..3) -> LDS
-      if (gq == 0) {
+      // per-wave (m, l, o) of rows 0 .. Gq - 1 (lanes gq hold rows 4 gq + r) -> LDS
+      if (4 * gq < Gq) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if (r < Gq) {
+          const int row = 4 * gq + r;
+          if (row < Gq) {
             if (col == 0) {
-              mo[wave * 4 + r] = m[r];
-              lo[wave * 4 + r] = lsum[r];
+              mo[wave * GR + row] = m[r];
+              lo[wave * GR + row] = lsum[r];
             }
 #pragma unroll
-            for (int n = 0; n < 8; ++n) oo[(wave * 4 + r) * HD + n * 16 + col] = o[n][r];
+            for (int n = 0; n < 8; ++n) oo[(wave * GR + row) * HD + n * 16 + col] = o[n][r];
           }
         }
       }
@@ -839,14 +850,14 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
         const int r = it / HD, d = it - r * HD;
         const float sn = snr[r];
         float M = sn;
-        for (int w = 0; w < NW; ++w) M = fmaxf(M, mo[w * 4 + r]);
+        for (int w = 0; w < NW; ++w) M = fmaxf(M, mo[w * GR + r]);
         float den = exp2f(sn - M), num = den * vn[d];
         for (int w = 0; w < NW; ++w) {
-          const float mw = mo[w * 4 + r];
+          const float mw = mo[w * GR + r];
           if (mw == -INFINITY) continue;
           const float e = exp2f(mw - M);
-          den += e * lo[w * 4 + r];
-          num += e * oo[(w * 4 + r) * HD + d];
+          den += e * lo[w * GR + r];
+          num += e * oo[(w * GR + r) * HD + d];
         }
         const float o1 = num / den;
         const float o2 = __shfl_xor(o1, 1, 64);   // d and d ^ 1 are neighbouring lanes
@@ -959,14 +970,20 @@ extern "C" size_t ka_decode_persistent_ws(int H, int hq, int hkv, int I) {
          (size_t)pd::MAXB * ((size_t)H * 4 + (size_t)(hq + 2 * hkv) * 128 * 2 + (size_t)hq * 128 * 2 + (size_t)I * 2) + 1024;
 }
 
+// Weight-ring slots per wave for a geometry: 16, or 12 where the GQA-8 attention scratch leaves no room
+// for 16 (gq = hq / hkv)
+static int pd_ring(int gq) { return gq > 4 ? 12 : KA_PD_RING; }
+
 // LDS layout of a B-sequence launch (see decode_layers_kernel); returns its bytes
-static int pd_layout(int B, int H, int hq, int I, pd::Args* a) {
+static int pd_layout(int B, int H, int hq, int I, pd::Args* a, int gq = 4) {
   auto kb = [](int bytes) { return (bytes + 1023) / 1024 * 1024; };
   const int xh = kb(std::max(H, hq * 128) * 2), xs = kb(std::max(std::max(H, I), hq * 128) * 2);
-  const int ring = std::max(B * (B == 1 ? xs : xh), pd::XS_MIN);
+  const int scr = gq > 4 ? kb(pd::scratch_bytes(8)) : pd::XS_MIN;
+  const int rg = pd_ring(gq);
+  const int ring = std::max(B * (B == 1 ? xs : xh), scr);
   const int ring_d = B == 1 ? ring : B * xs;
-  const int rd = B == 1 ? KA_PD_RING : 12;
-  const int red = std::max(ring + pd::NW * KA_PD_RING * 1024, ring_d + pd::NW * rd * 1024);
+  const int rd = B == 1 ? rg : std::min(rg, 12);
+  const int red = std::max(ring + pd::NW * rg * 1024, ring_d + pd::NW * rd * 1024);
   if (a) {
     a->xh_bytes = B == 1 ? xs : xh;
     a->xs_bytes = xs;
@@ -978,22 +995,24 @@ static int pd_layout(int B, int H, int hq, int I, pd::Args* a) {
 }
 
 // Largest batch (1 or 2) the persistent kernel takes for this model within the LDS of one CU; 0: none.
-extern "C" int ka_decode_persistent_max_b(int H, int hq, int I) {
-  if (H <= 4 * pd::NT * 4 && pd_layout(2, H, hq, I, nullptr) <= 160 * 1024) return 2;   // rmsnorm_rows_to_lds
-  if (pd_layout(1, H, hq, I, nullptr) <= 160 * 1024) return 1;
+// gq = hq / hkv (the attention scratch of GQA 8 takes 46 KB of LDS instead of 29)
+extern "C" int ka_decode_persistent_max_b2(int H, int hq, int I, int gq) {
+  if (H <= 4 * pd::NT * 4 && pd_layout(2, H, hq, I, nullptr, gq) <= 160 * 1024) return 2;   // rmsnorm_rows_to_lds
+  if (pd_layout(1, H, hq, I, nullptr, gq) <= 160 * 1024) return 1;
   return 0;
 }
+extern "C" int ka_decode_persistent_max_b(int H, int hq, int I) { return ka_decode_persistent_max_b2(H, hq, I, 4); }
 
-template <int B>
+template <int B, int RG>
 static int pd_launch(const pd::Args& a, int G, hipStream_t stream) {
-  const int lds = pd_layout(B, a.H, a.hq, a.I, nullptr);
+  const int lds = pd_layout(B, a.H, a.hq, a.I, nullptr, a.hq / a.hkv);
   static int attr = 0;
   if (attr < lds) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pd::decode_layers_kernel<B>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pd::decode_layers_kernel<B, RG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = lds;
   }
-  hipLaunchKernelGGL(pd::decode_layers_kernel<B>, dim3(G), dim3(pd::NT), lds, stream, a);
+  hipLaunchKernelGGL((pd::decode_layers_kernel<B, RG>), dim3(G), dim3(pd::NT), lds, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -1001,7 +1020,7 @@ static int pd_launch(const pd::Args& a, int G, hipStream_t stream) {
 // pointers (wqkv, wo, w13, w2, ln1, ln2); h0 / h_out [B][H]; pos / slot / ctx: device int [B]; bt: the
 // sequences' block tables [B][bt_stride]; stamps: nullptr, or [G][L][16] uint64 phase timestamps
 // (diagnostics; G <= the CU count).
-// Requirements: head_dim 128, block 16, hq % hkv == 0, hq / hkv <= 4, H % 512 == 0, I % 512 == 0,
+// Requirements: head_dim 128, block 16, hq % hkv == 0, hq / hkv <= 8, H % 512 == 0, I % 512 == 0,
 // hq * 128 % 512 == 0, the B activation rows and the rings within LDS (ka_decode_persistent_max_b),
 // the grid (the CU count, rounded down to a multiple of hkv) all resident.
 extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* layers, int L, int H, int hq, int hkv,
@@ -1010,9 +1029,9 @@ extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* lay
                                     const float* cos_sin, void* ws, void* stamps, int B, int bt_stride,
                                     hipStream_t stream) {
   if (L <= 0) return 0;
-  if (B < 1 || B > pd::MAXB || hq % hkv || hq / hkv > 4 || hkv > 16 || H % 512 || I % 512 || (hq * 128) % 512 ||
+  if (B < 1 || B > pd::MAXB || hq % hkv || hq / hkv > 8 || hkv > 16 || H % 512 || I % 512 || (hq * 128) % 512 ||
       H > 16384 ||   // rmsnorm_to_lds holds a row in 8 16-B words per thread
-      ws == nullptr || B > ka_decode_persistent_max_b(H, hq, I) || (B > 1 && bt_stride <= 0))
+      ws == nullptr || B > ka_decode_persistent_max_b2(H, hq, I, hq / hkv) || (B > 1 && bt_stride <= 0))
     return (int)hipErrorInvalidValue;
   const int G = (pd::num_cus() / hkv) * hkv;
   if (G < hkv) return (int)hipErrorInvalidValue;
@@ -1051,14 +1070,15 @@ extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* lay
   a.attn = a.qkv + (size_t)pd::MAXB * (hq + 2 * hkv) * 128;
   a.act = a.attn + (size_t)pd::MAXB * hq * 128;
   a.bt_stride = bt_stride;
-  pd_layout(B, H, hq, I, &a);
+  pd_layout(B, H, hq, I, &a, hq / hkv);
   // the arrival counters and the error word start at zero in every launch.  A kernel, not
   // hipMemsetAsync: captured into a hipGraph, the memset node left the words at 0xF3C00000 on
   // ROCm 7.2 (every grid wait then ran out; scripts/debug_pd_graph.py)
   hipLaunchKernelGGL(pd::zero_sync_kernel, dim3(1), dim3(256), 0, stream, reinterpret_cast<int*>(w));
   const int rc = (int)hipGetLastError();
   if (rc != 0) return rc;
-  return B == 1 ? pd_launch<1>(a, G, stream) : pd_launch<2>(a, G, stream);
+  if (pd_ring(hq / hkv) == 12 && KA_PD_RING != 12) return B == 1 ? pd_launch<1, 12>(a, G, stream) : pd_launch<2, 12>(a, G, stream);
+  return B == 1 ? pd_launch<1, KA_PD_RING>(a, G, stream) : pd_launch<2, KA_PD_RING>(a, G, stream);
 }
 
 // Byte offset of the error word in the workspace (the runner reads it back with every B = 1 step).

@@ -78,6 +78,9 @@ class LlamaModel:
         # them in fp32): a separate switch so the two can be A/B'd independently
         self.bf16_qkv_partials = os.environ.get("KA_BF16_QKV_PARTIALS", "1") == "1"
         self.layers = [self._layer(i) for i in range(cfg.num_layers)]
+        # this rank's MLP width (the TP shard of the intermediate size)
+        w13 = self.layers[0].get("w13") if self.layers else None
+        self.i_local = w13.shape[-2] // 2 if w13 is not None else cfg.intermediate // tp_size
         # prefill / mixed steps: the last layer's rows other than each sequence's last token feed
         # nothing (only the last rows reach the final norm and the LM head), so after that layer's
         # QKV + RoPE + KV append (which every row needs for later steps) it continues on the S
@@ -208,13 +211,17 @@ class LlamaModel:
         """The persistent all-layers kernel takes a decode step of B sequences: B <= KA_PERSISTENT_MAX_B
         (default 2) and within the kernel's LDS budget for this geometry (ops.decode_persistent_max_b)."""
         cfg = self.cfg
-        if not (self.persistent and self.device.type == "cuda" and self._local_comm and not cfg.is_moe
-                and self.D == 128 and self.hq % self.hkv == 0 and self.hq // self.hkv <= 4
-                and cfg.hidden % 512 == 0 and cfg.intermediate % 512 == 0 and (self.hq * self.D) % 512 == 0
+        # the kernel reduces nothing across ranks: it serves TP = 1 (LocalComm) and a virtual rank
+        # (parallel/comm.py VirtualRankComm, whose all-reduces are no-ops by definition)
+        comm_ok = self._local_comm or getattr(self.comm, "persistent_no_reduce", False)
+        I = self.i_local
+        if not (self.persistent and self.device.type == "cuda" and comm_ok and not cfg.is_moe
+                and self.D == 128 and self.hq % self.hkv == 0 and self.hq // self.hkv <= 8
+                and cfg.hidden % 512 == 0 and I % 512 == 0 and (self.hq * self.D) % 512 == 0
                 and cfg.hidden <= 16384 and 1 <= B <= self.persistent_max_b):
             return False
         if self._pd_max_b is None:
-            self._pd_max_b = ops.decode_persistent_max_b(cfg.hidden, self.hq, cfg.intermediate)
+            self._pd_max_b = ops.decode_persistent_max_b(cfg.hidden, self.hq, I, self.hq // self.hkv)
         return B <= self._pd_max_b
 
     def _forward_persistent(self, h0, meta: AttnMeta, k_cache, v_cache) -> torch.Tensor:
@@ -224,13 +231,12 @@ class LlamaModel:
             ptrs = [[L[k].data_ptr() for k in ("wqkv", "wo", "w13", "w2", "ln1", "ln2")] for L in self.layers]
             table = torch.tensor(ptrs, dtype=torch.int64, device=self.device)
             lib = ops._hip.require()
-            ws = torch.zeros(int(lib.ka_decode_persistent_ws(self.cfg.hidden, self.hq, self.hkv,
-                                                               self.cfg.intermediate)),
+            ws = torch.zeros(int(lib.ka_decode_persistent_ws(self.cfg.hidden, self.hq, self.hkv, self.i_local)),
                              dtype=torch.uint8, device=self.device)
             self._pd = (table, ws)
         table, ws = self._pd
         assert k_cache.shape[3] == 16, "persistent decode needs KV block 16"   # [L, NB, hkv, 16, 128]
-        hout = ops.decode_persistent(h0, table, len(self.layers), self.hq, self.hkv, self.cfg.intermediate,
+        hout = ops.decode_persistent(h0, table, len(self.layers), self.hq, self.hkv, self.i_local,
                                      self.cfg.norm_eps, self.scale, k_cache, v_cache, meta.positions,
                                      meta.slot_mapping, meta.block_tables, meta.ctx_lens, self.cos_sin, ws,
                                      self.persistent_stamps)

@@ -333,9 +333,10 @@ def decode_persistent(h0: torch.Tensor, layer_ptrs: torch.Tensor, L: int, hq: in
     return out
 
 
-def decode_persistent_max_b(H: int, hq: int, I: int) -> int:
-    """Largest batch (0, 1 or 2) csrc/decode_persistent.hip takes for a model (its LDS budget)."""
-    return int(require().ka_decode_persistent_max_b(H, hq, I))
+def decode_persistent_max_b(H: int, hq: int, I: int, gq: int = 4) -> int:
+    """Largest batch (0, 1 or 2) csrc/decode_persistent.hip takes for a model (its LDS budget; gq =
+    hq / hkv: the GQA-8 attention scratch takes more of it)."""
+    return int(require().ka_decode_persistent_max_b2(H, hq, I, gq))
 
 
 GB_BN = 256   # csrc/gemm_big.hip output tile (weight rows)

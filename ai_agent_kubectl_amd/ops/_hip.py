@@ -80,6 +80,7 @@ _SIGS = {
     "ka_argmax_combine": [P, P, P, I, I, P],
     "ka_decode_persistent": [P, P, P, I, I, I, I, I, F, F, P, P, ctypes.c_long, P, P, P, P, P, P, P, I, I, P],
     "ka_decode_persistent_max_b": [I, I, I],
+    "ka_decode_persistent_max_b2": [I, I, I, I],
     "ka_decode_persistent_ws": [I, I, I, I],
     "ka_decode_persistent_err": [P, P],
     "ka_decode_persistent_err_offset": [],

@@ -187,6 +187,9 @@ class VirtualRankComm:
 
     device_ordered = True
     custom_ar = None
+    # the persistent decode kernel (csrc/decode_persistent.hip) may serve this rank: its row-parallel
+    # outputs are added to the residual unreduced, which is what every all-reduce here returns
+    persistent_no_reduce = True
 
     def __init__(self, world: int, rank: int = 0):
         self.world_size, self.rank = world, rank

@@ -24,10 +24,10 @@ QUERIES = ["list all pods", "show services in namespace prod", "scale web to 3 r
            "get nodes with labels", "describe deployment api", "logs of pod api-1"]
 
 
-def _engine(model, graphs, buckets=(1, 2, 4, 8), max_batch=8, kv_cache_tokens=16384, **kw):
+def _engine(model, graphs, buckets=(1, 2, 4, 8), max_batch=8, kv_cache_tokens=16384, comm=None, **kw):
     opts = EngineOptions(model=model, device="cuda", max_batch=max_batch, graph_buckets=buckets,
                          kv_cache_tokens=kv_cache_tokens, max_model_len=512, use_graphs=graphs, **kw)
-    eng = build_engine(opts)
+    eng = build_engine(opts, comm=comm) if comm is not None else build_engine(opts)
     if graphs:
         eng.runner.capture_graphs()
     return eng
@@ -453,19 +453,29 @@ def test_mixtral_forward_hip_vs_reference():
     assert all(len(s.output_ids) == len(be._forced) + 6 for s in seqs)
 
 
-@pytest.mark.parametrize("B,graphs,long_ctx", [(1, False, False), (1, True, False), (1, False, True),
-                                                (2, False, False), (2, True, False), (2, False, True)])
-def test_persistent_decode_matches_kernel_chain_and_fp32(B, graphs, long_ctx):
+@pytest.mark.parametrize("model,B,graphs,long_ctx", [
+    ("llama3-8b-2l", 1, False, False), ("llama3-8b-2l", 1, True, False), ("llama3-8b-2l", 1, False, True),
+    ("llama3-8b-2l", 2, False, False), ("llama3-8b-2l", 2, True, False), ("llama3-8b-2l", 2, False, True),
+    ("llama3-70b-2l/tp8", 1, False, False), ("llama3-70b-2l/tp8", 1, True, False),
+    ("llama3-70b-2l/tp8", 1, False, True), ("llama3-70b-2l/tp8", 2, False, True)])
+def test_persistent_decode_matches_kernel_chain_and_fp32(model, B, graphs, long_ctx):
     """csrc/decode_persistent.hip (every layer of a decode step of B = 1 / 2 sequences in one launch,
     grid-wide arrival counters, one attention leader per sequence and KV group) against the per-kernel
     decode chain and the fp32 references, over 6 decode steps (the real Llama-3-8B layer geometry, 2
     layers): hidden states within bf16 tolerance, the same KV appended, the tokens equal to the chain's,
     the error word clear — eagerly and as the captured bucket-B hipGraph.  long_ctx: a ~400-token
     context, past the tokens the attention leaders prefetch into their rings (the chunk loop's
-    global-load path); at B = 2 the two sequences differ in length."""
+    global-load path); at B = 2 the two sequences differ in length.  "/tp8": rank 0 of Llama-3-70B at
+    TP = 8 on a virtual communicator (H 8192, 8 q heads over 1 KV head: the GQA-8 attention scratch and
+    12-slot rings; its all-reduces are no-ops in the chain and the kernel alike)."""
     from ai_agent_kubectl_amd.engine.sequence import Sequence
     from ai_agent_kubectl_amd.models.llama import AttnMeta
-    eng = _engine("llama3-8b-2l", graphs=graphs, buckets=(1, 2), max_batch=2, kv_cache_tokens=8192)
+    from ai_agent_kubectl_amd.parallel.comm import VirtualRankComm
+    kw = {}
+    if model.endswith("/tp8"):
+        model = model[:-4]
+        kw = dict(comm=VirtualRankComm(8), tp_rank=0, tp_size=8)
+    eng = _engine(model, graphs=graphs, buckets=(1, 2), max_batch=2, kv_cache_tokens=8192, **kw)
     be = EngineLLM(eng, max_new_tokens=16, ignore_eos=True)
     sch, r = eng.scheduler, eng.runner
     sch.gather_max_s = 0.0
