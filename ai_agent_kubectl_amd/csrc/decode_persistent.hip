@@ -65,6 +65,7 @@ template <int B, int RG = KA_PD_RING>
 constexpr int ring_down() { return B == 1 ? RG : (RG < 12 ? RG : 12); }
 static_assert((KA_PD_RING & (KA_PD_RING - 1)) == 0 && KA_PD_RING >= 2 && KA_PD_RING <= 16, "ring: a power of two <= 16");
 constexpr int MAXB = 2;     // sequences per launch
+constexpr int XR_MAX_RANKS = 8, XR_MAX_WG = 256, XR_MAX_H = 16384;   // the in-kernel all-reduce's limits
 // The attention leader's scratch (aliases the x rows) for GR = 4 or 8 rows per KV group (GQA <= 4 /
 // <= 8): P re-layout 10 KB | rotated q GR x 128 bf16 | new k, v | per-wave m, l | new-token scores |
 // per-wave o [NW][GR][128] fp32
@@ -106,6 +107,13 @@ struct Args {
   int lds_red;          // ... of the norm reduction (64 B), then the phases' row results (1 KB per sequence)
   int* sync;            // SYNC_BYTES: grid arrival shards, group arrivals, the error word (zeroed per launch)
   unsigned long long* stamps;   // diagnostics (nullptr: off): [G workgroups][L][16] s_memrealtime (100 MHz)
+  // tensor parallelism (world > 1): the row-parallel O / down outputs are all-reduced inside the kernel
+  // (see xreduce); world 0 / 1: added to the residual as they are (TP = 1, or a virtual rank whose
+  // collectives are no-ops)
+  int world, rank;
+  float* xdata[XR_MAX_RANKS];      // every rank's exchange halves [2][MAXB][H] fp32 (IPC-mapped, uncached)
+  unsigned* xflag[XR_MAX_RANKS];   // every rank's flags [XR_MAX_WG][XR_MAX_RANKS] (IPC-mapped, uncached)
+  unsigned* xctr;                  // this rank's epoch counter (local; 2 L per launch)
 };
 
 KA_DEV float ld_sc1(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -549,6 +557,50 @@ KA_DEV void rmsnorm_rows_to_lds(const Args& a, const float* res, const bf16_t* g
   }
 }
 
+// In-kernel all-reduce of a row-parallel projection (tensor parallelism; MI355X_MICROARCH.md hand-off
+// table, system scope).  Every rank splits the output rows over its workgroups the same way, so
+// workgroup wg of every rank owns the same rows: it publishes its partial rows into half e & 1 of its
+// own exchange buffer (uncached, IPC-mapped), releases at system scope, stores epoch e into flag
+// [wg][rank] of every peer, waits until its own flags [wg][p] reach e (bounded: the error word instead
+// of a hang), then sums the peers' rows in rank order.  Alternating halves: a rank rewrites half h at
+// epoch e + 2 only after every peer's workgroup wg signalled e + 1, i.e. finished reading e.
+// v[b] = this lane's partial of row `row` (valid when `mine`); returns the sum over ranks.
+template <int B>
+KA_DEV void xreduce(const Args& a, unsigned epoch, int wg, int row, bool mine, float (&v)[B], int* err) {
+  const size_t hb = (size_t)MAXB * a.H, half = (size_t)(epoch & 1u) * hb;
+  if (mine) {
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+      __hip_atomic_store(a.xdata[a.rank] + half + (size_t)b * a.H + row, v[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __threadfence_system();
+  __syncthreads();
+  if ((int)threadIdx.x < a.world) {
+    const int p = threadIdx.x;
+    __hip_atomic_store(a.xflag[p] + wg * XR_MAX_RANKS + a.rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned* f = a.xflag[a.rank] + wg * XR_MAX_RANKS + p;
+    int spins = 0;
+    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((++spins & 255) == 0 &&
+          (spins > (1 << 22) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // 2: a peer rank never came
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (mine) {
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      float sum = 0.f;
+      for (int p = 0; p < a.world; ++p)
+        sum += __hip_atomic_load(a.xdata[p] + half + (size_t)b * a.H + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      v[b] = sum;
+    }
+  }
+}
+
 // LDS layout (bytes), phase by phase (each region is dead when the next phase's DMA reaches it):
 //   QKV / O / gate_up: the B x / attn rows (a.xh_bytes each) at 0 (the attention leader's scratch,
 //     28.3 KB, reuses it: x is dead between the QKV rows and the O rows); the waves' 16-slot weight
@@ -590,6 +642,9 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
   int* const gcnt = grid_shard(a.sync, wg);
   int* const err = a.sync + SYNC_ERR;
   int nbar = 0;   // grid barriers passed
+  const bool tp = a.world > 1;
+  // the all-reduce epochs of this launch: base + 1 .. base + 2 L (the counter moves on at the end)
+  const unsigned ebase = tp ? __builtin_amdgcn_readfirstlane(__hip_atomic_load(a.xctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0u;
 
   // residual := the embedding (each wave initialises the elements it owns)
   const int own0 = gw * h_per_wave, own1 = min(H, own0 + h_per_wave);
@@ -882,8 +937,10 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     vm_drain();
     __syncthreads();
     {
-      const RowVals<B> v = so.run(xaddr, (uint32_t)xhb);
+      RowVals<B> v = so.run(xaddr, (uint32_t)xhb);
       so.drain();
+      // (leader workgroups own no O rows on any rank: they take no part in its all-reduce)
+      if (tp && !leader) xreduce<B>(a, ebase + 2u * (unsigned)l + 1u, wg, ow0 + lane, lane < n_o, v.v, err);
 #pragma unroll
       for (int b = 0; b < B; ++b) {
         float* const rr = a.res + (size_t)b * H + ow0 + lane;
@@ -930,8 +987,9 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     vm_drain();
     __syncthreads();
     {
-      const RowVals<B> v = sd.run(xaddr, (uint32_t)xsb);
+      RowVals<B> v = sd.run(xaddr, (uint32_t)xsb);
       sd.drain();
+      if (tp) xreduce<B>(a, ebase + 2u * (unsigned)l + 2u, wg, own0 + lane, lane < no, v.v, err);
 #pragma unroll
       for (int b = 0; b < B; ++b) {
         float* const rr = a.res + (size_t)b * H + own0 + lane;
@@ -946,6 +1004,8 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
 #pragma unroll
   for (int b = 0; b < B; ++b)
     for (int r = own0 + lane; r < own1; r += 64) a.h_out[(size_t)b * H + r] = f2bf(ld_sc1(a.res + (size_t)b * H + r));
+  // every workgroup has read the epoch base (it did so before its first barrier): move it on
+  if (tp && wg == 0 && tid == 0) __hip_atomic_store(a.xctr, ebase + 2u * (unsigned)a.L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(256) void zero_sync_kernel(int* __restrict__ sync) {
@@ -1023,17 +1083,28 @@ static int pd_launch(const pd::Args& a, int G, hipStream_t stream) {
 // Requirements: head_dim 128, block 16, hq % hkv == 0, hq / hkv <= 8, H % 512 == 0, I % 512 == 0,
 // hq * 128 % 512 == 0, the B activation rows and the rings within LDS (ka_decode_persistent_max_b),
 // the grid (the CU count, rounded down to a multiple of hkv) all resident.
-extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* layers, int L, int H, int hq, int hkv,
-                                    int I, float eps, float scale, void* k_cache, void* v_cache, long cache_layer,
-                                    const int* pos, const int* slot, const int* bt, const int* ctx,
-                                    const float* cos_sin, void* ws, void* stamps, int B, int bt_stride,
-                                    hipStream_t stream) {
+// Tensor parallelism (ka_decode_persistent_tp): world ranks (2 .. 8) of a TP group, this one `rank`;
+// xdata / xflag: host arrays of every rank's exchange buffer / flag words (IPC-mapped, uncached:
+// parallel/custom_allreduce.py pd_buffers), xctr: this rank's epoch counter (device u32, zero at
+// start, advanced by 2 L per launch on every rank alike).  The O and down projections' partial rows
+// are all-reduced inside the kernel.  KA_PD_GRID caps the grid (tests: two ranks sharing one GPU).
+extern "C" int ka_decode_persistent_tp(void* h_out, const void* h0, const void* layers, int L, int H, int hq, int hkv,
+                                       int I, float eps, float scale, void* k_cache, void* v_cache, long cache_layer,
+                                       const int* pos, const int* slot, const int* bt, const int* ctx,
+                                       const float* cos_sin, void* ws, void* stamps, int B, int bt_stride, int world,
+                                       int rank, void* const* xdata, void* const* xflag, void* xctr,
+                                       hipStream_t stream) {
   if (L <= 0) return 0;
+  if (world > 1 && (world > pd::XR_MAX_RANKS || rank < 0 || rank >= world || xdata == nullptr || xflag == nullptr ||
+                    xctr == nullptr || H > pd::XR_MAX_H))
+    return (int)hipErrorInvalidValue;
   if (B < 1 || B > pd::MAXB || hq % hkv || hq / hkv > 8 || hkv > 16 || H % 512 || I % 512 || (hq * 128) % 512 ||
       H > 16384 ||   // rmsnorm_to_lds holds a row in 8 16-B words per thread
       ws == nullptr || B > ka_decode_persistent_max_b2(H, hq, I, hq / hkv) || (B > 1 && bt_stride <= 0))
     return (int)hipErrorInvalidValue;
-  const int G = (pd::num_cus() / hkv) * hkv;
+  int cus = pd::num_cus();
+  if (const char* e = getenv("KA_PD_GRID")) cus = std::min(cus, std::max(1, atoi(e)));
+  const int G = (std::min(cus, pd::XR_MAX_WG) / hkv) * hkv;
   if (G < hkv) return (int)hipErrorInvalidValue;
   {   // every wave's rows fit its 64 lanes (lane i = row i) and the LDS result buffer
     const int per_group = G / hkv, nw = G * pd::NW;
@@ -1070,6 +1141,13 @@ extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* lay
   a.attn = a.qkv + (size_t)pd::MAXB * (hq + 2 * hkv) * 128;
   a.act = a.attn + (size_t)pd::MAXB * hq * 128;
   a.bt_stride = bt_stride;
+  a.world = world > 1 ? world : 0;
+  a.rank = rank;
+  for (int p = 0; p < pd::XR_MAX_RANKS; ++p) {
+    a.xdata[p] = (world > 1 && p < world) ? static_cast<float*>(xdata[p]) : nullptr;
+    a.xflag[p] = (world > 1 && p < world) ? static_cast<unsigned*>(xflag[p]) : nullptr;
+  }
+  a.xctr = static_cast<unsigned*>(xctr);
   pd_layout(B, H, hq, I, &a, hq / hkv);
   // the arrival counters and the error word start at zero in every launch.  A kernel, not
   // hipMemsetAsync: captured into a hipGraph, the memset node left the words at 0xF3C00000 on
@@ -1080,6 +1158,23 @@ extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* lay
   if (pd_ring(hq / hkv) == 12 && KA_PD_RING != 12) return B == 1 ? pd_launch<1, 12>(a, G, stream) : pd_launch<2, 12>(a, G, stream);
   return B == 1 ? pd_launch<1, KA_PD_RING>(a, G, stream) : pd_launch<2, KA_PD_RING>(a, G, stream);
 }
+
+extern "C" int ka_decode_persistent(void* h_out, const void* h0, const void* layers, int L, int H, int hq, int hkv,
+                                    int I, float eps, float scale, void* k_cache, void* v_cache, long cache_layer,
+                                    const int* pos, const int* slot, const int* bt, const int* ctx,
+                                    const float* cos_sin, void* ws, void* stamps, int B, int bt_stride,
+                                    hipStream_t stream) {
+  return ka_decode_persistent_tp(h_out, h0, layers, L, H, hq, hkv, I, eps, scale, k_cache, v_cache, cache_layer, pos,
+                                 slot, bt, ctx, cos_sin, ws, stamps, B, bt_stride, 0, 0, nullptr, nullptr, nullptr,
+                                 stream);
+}
+
+// Exchange bytes per rank of the in-kernel all-reduce: two halves of [MAXB][XR_MAX_H] fp32, then the
+// flags [XR_MAX_WG][XR_MAX_RANKS] u32 (parallel/custom_allreduce.py appends them to its IPC buffer).
+extern "C" size_t ka_decode_persistent_xbytes() {
+  return (size_t)2 * pd::MAXB * pd::XR_MAX_H * 4 + (size_t)pd::XR_MAX_WG * pd::XR_MAX_RANKS * 4;
+}
+extern "C" size_t ka_decode_persistent_xflag_offset() { return (size_t)2 * pd::MAXB * pd::XR_MAX_H * 4; }
 
 // Byte offset of the error word in the workspace (the runner reads it back with every B = 1 step).
 extern "C" int ka_decode_persistent_err_offset() { return pd::SYNC_ERR * 4; }

@@ -211,9 +211,12 @@ class LlamaModel:
         """The persistent all-layers kernel takes a decode step of B sequences: B <= KA_PERSISTENT_MAX_B
         (default 2) and within the kernel's LDS budget for this geometry (ops.decode_persistent_max_b)."""
         cfg = self.cfg
-        # the kernel reduces nothing across ranks: it serves TP = 1 (LocalComm) and a virtual rank
-        # (parallel/comm.py VirtualRankComm, whose all-reduces are no-ops by definition)
-        comm_ok = self._local_comm or getattr(self.comm, "persistent_no_reduce", False)
+        # TP = 1 (LocalComm), a virtual rank (parallel/comm.py VirtualRankComm, whose all-reduces are
+        # no-ops by definition), or a real TP group with the one-shot IPC buffers, whose O / down
+        # all-reduces the kernel then runs itself (KA_PERSISTENT_TP=1: opt-in until an 8-GPU node has
+        # measured it; the 2-rank-on-one-GPU test covers the protocol)
+        comm_ok = (self._local_comm or getattr(self.comm, "persistent_no_reduce", False)
+                   or self._tp_exchange() is not None)
         I = self.i_local
         if not (self.persistent and self.device.type == "cuda" and comm_ok and not cfg.is_moe
                 and self.D == 128 and self.hq % self.hkv == 0 and self.hq // self.hkv <= 8
@@ -223,6 +226,13 @@ class LlamaModel:
         if self._pd_max_b is None:
             self._pd_max_b = ops.decode_persistent_max_b(cfg.hidden, self.hq, I, self.hq // self.hkv)
         return B <= self._pd_max_b
+
+    def _tp_exchange(self):
+        """The in-kernel all-reduce's buffers of a real TP group (None: TP = 1, virtual, or not enabled)."""
+        car = getattr(self.comm, "custom_ar", None)
+        if car is None or self.tp_size <= 1 or os.environ.get("KA_PERSISTENT_TP", "0") != "1":
+            return None
+        return car.pd_exchange()
 
     def _forward_persistent(self, h0, meta: AttnMeta, k_cache, v_cache) -> torch.Tensor:
         """Batch-1 / 2 decode through the persistent all-layers kernel; returns the final-normed hidden
@@ -239,7 +249,7 @@ class LlamaModel:
         hout = ops.decode_persistent(h0, table, len(self.layers), self.hq, self.hkv, self.i_local,
                                      self.cfg.norm_eps, self.scale, k_cache, v_cache, meta.positions,
                                      meta.slot_mapping, meta.block_tables, meta.ctx_lens, self.cos_sin, ws,
-                                     self.persistent_stamps)
+                                     self.persistent_stamps, tp=self._tp_exchange())
         return ops.rmsnorm(hout, self.W["norm"], self.cfg.norm_eps)
 
     def persistent_err_word(self) -> Optional[torch.Tensor]:

@@ -315,20 +315,24 @@ def argmax_combine(vals: torch.Tensor, idxs: torch.Tensor) -> torch.Tensor:
 def decode_persistent(h0: torch.Tensor, layer_ptrs: torch.Tensor, L: int, hq: int, hkv: int, I: int, eps: float,
                       scale: float, k_cache: torch.Tensor, v_cache: torch.Tensor, positions: torch.Tensor,
                       slot_mapping: torch.Tensor, block_table: torch.Tensor, ctx_lens: torch.Tensor,
-                      cos_sin: torch.Tensor, ws: torch.Tensor, stamps: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      cos_sin: torch.Tensor, ws: torch.Tensor, stamps: Optional[torch.Tensor] = None,
+                      tp=None) -> torch.Tensor:
     """Every decoder layer of a decode step of B = 1 or 2 sequences in one persistent launch
     (csrc/decode_persistent.hip): h0 [B, H] bf16 embeddings -> the residual streams after the last
     layer [B, H] bf16.  layer_ptrs: int64 [L, 6] device pointers (wqkv, wo, w13, w2, ln1, ln2); caches
     [L, NB, hkv, ...]; positions / slot_mapping / ctx_lens [>= B]; block_table [>= B, max_blocks]
-    (a 1-D table is the single sequence's)."""
+    (a 1-D table is the single sequence's).  tp: None, or (world, rank, xdata, xflag, xctr) of a tensor-
+    parallel group (parallel/custom_allreduce.py OneShotAllReduce.pd_exchange): the row-parallel O /
+    down outputs are then all-reduced inside the kernel."""
     lib = require()
     B, H = h0.shape
     out = torch.empty_like(h0)
     bt_stride = block_table.stride(0) if block_table.dim() == 2 else block_table.shape[0]
-    check(lib.ka_decode_persistent(_p(out), _p(h0), _p(layer_ptrs), L, H, hq, hkv, I, float(eps), float(scale),
-                                   _p(k_cache), _p(v_cache), k_cache[0].numel(), _p(positions), _p(slot_mapping),
-                                   _p(block_table), _p(ctx_lens), _p(cos_sin), _p(ws), _p(stamps), B, bt_stride,
-                                   _stream()),
+    world, rank, xdata, xflag, xctr = tp if tp is not None else (0, 0, None, None, None)
+    check(lib.ka_decode_persistent_tp(_p(out), _p(h0), _p(layer_ptrs), L, H, hq, hkv, I, float(eps), float(scale),
+                                      _p(k_cache), _p(v_cache), k_cache[0].numel(), _p(positions), _p(slot_mapping),
+                                      _p(block_table), _p(ctx_lens), _p(cos_sin), _p(ws), _p(stamps), B, bt_stride,
+                                      world, rank, xdata, xflag, _p(xctr), _stream()),
           "decode_persistent")
     return out
 

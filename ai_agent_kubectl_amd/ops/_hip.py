@@ -43,6 +43,7 @@ I = ctypes.c_int
 F = ctypes.c_float
 
 _RESTYPES = {"ka_gemm_big_ws_bytes": ctypes.c_size_t, "ka_decode_persistent_ws": ctypes.c_size_t,
+             "ka_decode_persistent_xbytes": ctypes.c_size_t, "ka_decode_persistent_xflag_offset": ctypes.c_size_t,
              "ka_decode_cascade_ws": ctypes.c_size_t}
 
 _SIGS = {
@@ -79,6 +80,10 @@ _SIGS = {
     "ka_argmax_finish": [P, P, P, P, I, I, I, P],
     "ka_argmax_combine": [P, P, P, I, I, P],
     "ka_decode_persistent": [P, P, P, I, I, I, I, I, F, F, P, P, ctypes.c_long, P, P, P, P, P, P, P, I, I, P],
+    "ka_decode_persistent_tp": [P, P, P, I, I, I, I, I, F, F, P, P, ctypes.c_long, P, P, P, P, P, P, P, I, I, I, I,
+                                P, P, P, P],
+    "ka_decode_persistent_xbytes": [],
+    "ka_decode_persistent_xflag_offset": [],
     "ka_decode_persistent_max_b": [I, I, I],
     "ka_decode_persistent_max_b2": [I, I, I, I],
     "ka_decode_persistent_ws": [I, I, I, I],

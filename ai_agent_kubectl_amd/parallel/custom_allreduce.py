@@ -49,7 +49,10 @@ class OneShotAllReduce:
         self.cap = int(cap_elems) // 8 * 8
         lib, check = _lib()
         self.lib, self.check_rc = lib, check
-        self.bytes = 2 * self.cap * 2 + FLAG_BYTES
+        # + the persistent decode kernel's own exchange halves and flags (csrc/decode_persistent.hip
+        # xreduce: a separate epoch sequence, so it never shares halves with the one-shot kernels)
+        self.pd_off = 2 * self.cap * 2 + FLAG_BYTES
+        self.bytes = self.pd_off + int(lib.ka_decode_persistent_xbytes())
         base = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             check(lib.ka_ar_alloc(ctypes.byref(base), ctypes.c_size_t(self.bytes)), "ar_alloc")
@@ -76,7 +79,15 @@ class OneShotAllReduce:
         self.state = torch.zeros(4, dtype=torch.int32, device=self.device)   # ctr, done, err
         sp = self.state.data_ptr()
         self._ctr, self._done, self._err = sp, sp + 4, sp + 8
+        pf = int(lib.ka_decode_persistent_xflag_offset())
+        self._pd_data = (ctypes.c_void_p * 8)(*[p + self.pd_off for p in self.peers])
+        self._pd_flags = (ctypes.c_void_p * 8)(*[p + self.pd_off + pf for p in self.peers])
+        self.pd_ctr = torch.zeros(1, dtype=torch.int32, device=self.device)   # the kernel's epoch counter
         dist.barrier(group=group)
+
+    def pd_exchange(self):
+        """(world, rank, xdata, xflag, xctr) for ops.decode_persistent's in-kernel all-reduce."""
+        return self.world, self.rank, self._pd_data, self._pd_flags, self.pd_ctr
 
     # ------------------------------------------------------------------------------------------
     def should_use(self, t: torch.Tensor) -> bool:

@@ -28,10 +28,16 @@ def main():
     ap.add_argument("--plan-first", action="store_true",
                     help="load the GEMM plan / LM head / SwiGLU decisions before the prefill (so its steps of "
                          "<= 512 rows dispatch on them, as in serving)")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="> 1: rank 0 of a TP group on a virtual communicator (collectives left out)")
     args = ap.parse_args()
     buckets = tuple(int(b) for b in args.buckets.split(","))
+    kw, comm = {}, None
+    if args.tp > 1:
+        from ai_agent_kubectl_amd.parallel.comm import VirtualRankComm
+        kw, comm = dict(tp_rank=0, tp_size=args.tp), VirtualRankComm(args.tp)
     eng = build_engine(EngineOptions(model=args.model, device="cuda", max_batch=max(buckets), graph_buckets=buckets,
-                                     kv_cache_tokens=65536, max_model_len=512))
+                                     kv_cache_tokens=65536, max_model_len=512, **kw), comm=comm)
     r = eng.runner
     be = EngineLLM(eng, max_new_tokens=64, ignore_eos=True)
     sch = eng.scheduler

@@ -28,11 +28,12 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, model, q, overlap=False):
+def _rank(rank, world, port, model, q, overlap=False, env=None):
     try:
         sys.path.insert(0, ROOT)
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                           MASTER_PORT=str(port), KA_CUSTOM_AR="1", KA_TP_OVERLAP="force" if overlap else "0")
+        os.environ.update(env or {})
         import torch.distributed as dist
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -46,9 +47,14 @@ def _rank(rank, world, port, model, q, overlap=False):
                                          gpu_mem_fraction=0.1), comm=comm)
         eng.runner.capture_graphs(autotune=False)
         assert comm.custom_ar is not None and len(eng.runner.graphs) == 3
+        m = eng.runner.model
+        pers = (env or {}).get("KA_PERSISTENT_TP") == "1"
+        if pers:   # buckets 1 / 2 captured on the persistent kernel with its in-kernel all-reduce
+            assert m.persistent_ok(1) and eng.runner.graph_persistent.get(1), "persistent TP path not taken"
         if rank != 0:
             eng.runner.worker_loop()
             comm.custom_ar.check()
+            assert not pers or m.persistent_err() == 0, f"rank {rank}: persistent error word {m.persistent_err()}"
             q.put((rank, None, None))
             return
         be = EngineLLM(eng, max_new_tokens=6, ignore_eos=True)
@@ -73,18 +79,19 @@ def _rank(rank, world, port, model, q, overlap=False):
             replays = eng.runner.stats["graph_replays"]
             eng.runner.stop_workers()
         comm.custom_ar.check()
+        assert not pers or m.persistent_err() == 0, f"rank 0: persistent error word {m.persistent_err()}"
         q.put((0, ([s.output_ids for s in seqs], replays), None))
     except Exception:
         import traceback
         q.put((rank, None, traceback.format_exc()))
 
 
-def _run(model, world, overlap=False):
+def _run(model, world, overlap=False, env=None):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, model, q, overlap)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, model, q, overlap, env)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -138,6 +145,22 @@ def test_tp_overlapped_decode_matches_tp1():
     model = "llama3-70b-2l"
     eng1, prompts, want = _tp1(model)
     got, replays = _run(model, 4, overlap=True)
+    assert replays > 0
+    assert_same_or_near_tie(eng1, prompts, want, got)
+    del eng1
+    torch.cuda.empty_cache()
+
+
+def test_tp_persistent_decode_in_kernel_allreduce_two_ranks():
+    """The persistent all-layers decode kernel on a real TP = 2 group (KA_PERSISTENT_TP=1): each rank's
+    row-parallel O / down partial rows all-reduced INSIDE the kernel over the IPC exchange buffers
+    (csrc/decode_persistent.hip xreduce: per-workgroup epoch flags at system scope).  Two ranks share
+    this one GPU, so each grid is capped at 120 workgroups (KA_PD_GRID) for both to be resident at
+    once.  Tokens must equal TP = 1 (or differ only at a near-tie), every rank's error word clear."""
+    from tests.virtual_tp import assert_same_or_near_tie
+    model = "llama3-70b-2l"
+    eng1, prompts, want = _tp1(model)
+    got, replays = _run(model, 2, env={"KA_PERSISTENT_TP": "1", "KA_PD_GRID": "120", "KA_PERSISTENT_DECODE": "1"})
     assert replays > 0
     assert_same_or_near_tie(eng1, prompts, want, got)
     del eng1
