@@ -79,6 +79,8 @@ PRESETS: Dict[str, ModelConfig] = {
     # Llama-3-70B geometry (8 KV heads: 1 per rank at TP = 8, GQA group 8) with 2 layers: TP = 4 / 8
     # numerics on one GPU (tests/virtual_tp.py, tests/test_tp_single_gpu.py)
     "llama3-70b-2l": ModelConfig("llama3-70b-2l", "llama", 2, 8192, 64, 8, 128, 28672, 128256, 500000.0),
+    # 8 layers of Llama-3-70B: timing a TP group's decode step on one GPU (scripts/bench_tp_persistent_2rank.py)
+    "llama3-70b-8l": ModelConfig("llama3-70b-8l", "llama", 8, 8192, 64, 8, 128, 28672, 128256, 500000.0),
     # Llama-3-70B head layout (64 q / 8 kv heads: GQA 8, one KV head per rank at TP = 8) on small
     # layers: CPU multi-process TP = 8 serving tests (gloo), where the 8192-wide layers would not fit
     "llama3-70b-tiny": ModelConfig("llama3-70b-tiny", "llama", 2, 2048, 64, 8, 32, 1024, 128256, 500000.0),
