@@ -68,8 +68,10 @@ constexpr int MAXB = 2;     // sequences per launch
 constexpr int XR_MAX_RANKS = 8, XR_MAX_WG = 256, XR_MAX_H = 16384;   // the in-kernel all-reduce's limits
 // The attention leader's scratch (aliases the x rows) for GR = 4 or 8 rows per KV group (GQA <= 4 /
 // <= 8): P re-layout 10 KB | rotated q GR x 128 bf16 | new k, v | per-wave m, l | new-token scores |
-// per-wave o [NW][GR][128] fp32
-KA_HD int scratch_bytes(int gr) { return 10240 + gr * 256 + 1024 + 2 * 8 * gr * 4 + 64 + 8 * gr * 128 * 4; }
+// GR 4: per-wave o [NW][4][128] fp32.  GR 8 writes each wave's o [8][128] (4 KB) into the wave's own
+// weight ring instead, idle by then (its prefetched K / V consumed, no O rows on a leader): the 32 KB
+// of a scratch o would leave the GQA-8 geometry only 12-slot rings (and one prefetched K/V block).
+KA_HD int scratch_bytes(int gr) { return 10240 + gr * 256 + 1024 + 2 * 8 * gr * 4 + 64 + (gr > 4 ? 0 : 8 * gr * 128 * 4); }
 constexpr int XS_MIN = 29 * 1024;   // GR = 4: 28.3 KB
 
 struct Layer {
@@ -610,8 +612,8 @@ KA_DEV void xreduce(const Args& a, unsigned epoch, int wg, int row, bool mine, f
 // > 80 KB: one workgroup per CU.
 constexpr int LDS_X = 0, LDS_ATT = 0;
 
-// RG: weight-ring slots per wave (16; 12 where the GQA-8 attention scratch needs the LDS: the 70B
-// tensor-parallel rank, hq / hkv = 8)
+// RG: weight-ring slots per wave (16; 14 for B = 2 of the 70B tensor-parallel rank, hq / hkv = 8, whose
+// 16-KB x rows take the LDS; pd_ring)
 template <int B, int RG>
 __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
   constexpr int RGD = ring_down<B, RG>();
@@ -767,7 +769,11 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       float* const mo = vn + HD;                                                  // [NW][GR]
       float* const lo = mo + NW * GR;                                             // [NW][GR]
       float* const snr = lo + NW * GR;                                            // [GR] (+ pad)
-      float* const oo = snr + 16;                                                 // [NW][GR][128]
+      float* const oo = snr + 16;                                                 // [NW][4][128] (GR 4)
+      // wave w's o rows [GR][128]: the scratch (GR 4) or the wave's idle ring (GR 8, see scratch_bytes)
+      auto oo_of = [&](int w) -> float* {
+        return GR > 4 ? reinterpret_cast<float*>(lds + lds_ring + w * RG * 1024) : oo + w * GR * HD;
+      };
       const float* cs = a.cos_sin + (size_t)p * HD;
       // RoPE (neox halves) on the group's q heads and k; v as is
       for (int it = tid; it < (Gq + 2) * (HD / 2); it += NT) {
@@ -889,7 +895,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
               lo[wave * GR + row] = lsum[r];
             }
 #pragma unroll
-            for (int n = 0; n < 8; ++n) oo[(wave * GR + row) * HD + n * 16 + col] = o[n][r];
+            for (int n = 0; n < 8; ++n) oo_of(wave)[row * HD + n * 16 + col] = o[n][r];
           }
         }
       }
@@ -912,7 +918,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
           if (mw == -INFINITY) continue;
           const float e = exp2f(mw - M);
           den += e * lo[w * GR + r];
-          num += e * oo[(w * GR + r) * HD + d];
+          num += e * oo_of(w)[r * HD + d];
         }
         const float o1 = num / den;
         const float o2 = __shfl_xor(o1, 1, 64);   // d and d ^ 1 are neighbouring lanes
@@ -1030,16 +1036,16 @@ extern "C" size_t ka_decode_persistent_ws(int H, int hq, int hkv, int I) {
          (size_t)pd::MAXB * ((size_t)H * 4 + (size_t)(hq + 2 * hkv) * 128 * 2 + (size_t)hq * 128 * 2 + (size_t)I * 2) + 1024;
 }
 
-// Weight-ring slots per wave for a geometry: 16, or 12 where the GQA-8 attention scratch leaves no room
-// for 16 (gq = hq / hkv)
-static int pd_ring(int gq) { return gq > 4 ? 12 : KA_PD_RING; }
+// Weight-ring slots per wave for a geometry (gq = hq / hkv): 16, or 14 for two sequences of the GQA-8
+// geometry (their two 16-KB x rows leave room for no more)
+static int pd_ring(int gq, int B) { return gq > 4 ? (B == 1 ? 16 : 14) : KA_PD_RING; }
 
 // LDS layout of a B-sequence launch (see decode_layers_kernel); returns its bytes
 static int pd_layout(int B, int H, int hq, int I, pd::Args* a, int gq = 4) {
   auto kb = [](int bytes) { return (bytes + 1023) / 1024 * 1024; };
   const int xh = kb(std::max(H, hq * 128) * 2), xs = kb(std::max(std::max(H, I), hq * 128) * 2);
   const int scr = gq > 4 ? kb(pd::scratch_bytes(8)) : pd::XS_MIN;
-  const int rg = pd_ring(gq);
+  const int rg = pd_ring(gq, B);
   const int ring = std::max(B * (B == 1 ? xs : xh), scr);
   const int ring_d = B == 1 ? ring : B * xs;
   const int rd = B == 1 ? rg : std::min(rg, 12);
@@ -1155,7 +1161,7 @@ extern "C" int ka_decode_persistent_tp(void* h_out, const void* h0, const void* 
   hipLaunchKernelGGL(pd::zero_sync_kernel, dim3(1), dim3(256), 0, stream, reinterpret_cast<int*>(w));
   const int rc = (int)hipGetLastError();
   if (rc != 0) return rc;
-  if (pd_ring(hq / hkv) == 12 && KA_PD_RING != 12) return B == 1 ? pd_launch<1, 12>(a, G, stream) : pd_launch<2, 12>(a, G, stream);
+  if (B == 2 && pd_ring(hq / hkv, 2) == 14) return pd_launch<2, 14>(a, G, stream);
   return B == 1 ? pd_launch<1, KA_PD_RING>(a, G, stream) : pd_launch<2, KA_PD_RING>(a, G, stream);
 }
 
