@@ -78,20 +78,36 @@ struct DecodeFuse {
   float* part_ml;     // [B, hq, 2]
 };
 
+// Up to DQ_UNROLL slices are loaded before the first add (a rolled loop waited for each slice's load
+// before issuing the next: `split` serial memory latencies in the kernel's prologue); more than that
+// (no plan uses it) continue in a loop.
+constexpr int DQ_UNROLL = 4;
 __device__ __forceinline__ uint2 dq_ld4(const DecodeFuse& f, size_t off) {
   if (f.P == nullptr) return *reinterpret_cast<const uint2*>(f.qkv + off);
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
   if (f.pbf16) {   // bf16 slices (gemm_mfma EPI_P16): summed in fp32
     const bf16_t* pb = reinterpret_cast<const bf16_t*>(f.P);
-    uint2 q = *reinterpret_cast<const uint2*>(pb + off);
-    f32x4 s = f32x4{lo_f(q.x), hi_f(q.x), lo_f(q.y), hi_f(q.y)};
-    for (int k = 1; k < f.split; ++k) {
-      q = *reinterpret_cast<const uint2*>(pb + k * f.pstride + off);
-      s += f32x4{lo_f(q.x), hi_f(q.x), lo_f(q.y), hi_f(q.y)};
+    uint2 q[DQ_UNROLL];
+#pragma unroll
+    for (int k = 0; k < DQ_UNROLL; ++k)
+      if (k < f.split) q[k] = *reinterpret_cast<const uint2*>(pb + k * f.pstride + off);
+#pragma unroll
+    for (int k = 0; k < DQ_UNROLL; ++k)
+      if (k < f.split) s += f32x4{lo_f(q[k].x), hi_f(q[k].x), lo_f(q[k].y), hi_f(q[k].y)};
+    for (int k = DQ_UNROLL; k < f.split; ++k) {
+      const uint2 r = *reinterpret_cast<const uint2*>(pb + k * f.pstride + off);
+      s += f32x4{lo_f(r.x), hi_f(r.x), lo_f(r.y), hi_f(r.y)};
     }
     return make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
   }
-  f32x4 s = *reinterpret_cast<const f32x4*>(f.P + off);
-  for (int k = 1; k < f.split; ++k) s += *reinterpret_cast<const f32x4*>(f.P + k * f.pstride + off);
+  f32x4 p[DQ_UNROLL];
+#pragma unroll
+  for (int k = 0; k < DQ_UNROLL; ++k)
+    if (k < f.split) p[k] = *reinterpret_cast<const f32x4*>(f.P + k * f.pstride + off);
+#pragma unroll
+  for (int k = 0; k < DQ_UNROLL; ++k)
+    if (k < f.split) s += p[k];
+  for (int k = DQ_UNROLL; k < f.split; ++k) s += *reinterpret_cast<const f32x4*>(f.P + k * f.pstride + off);
   return make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
 }
 
@@ -108,11 +124,19 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
                                                            float scale_log2, DecodeFuse fz) {
   const int h = blockIdx.x, b = blockIdx.y;
   const int G = hq / hkv;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // fused: wave-uniform (readfirstlane), so the block-table reads below become scalar loads issued
+  // together, not vector loads each waited for before the K / V loads they address (the non-fused
+  // kernel keeps the vector form: with scalar indices it spills 3 VGPRs in the chunk loop)
+  const int lane = threadIdx.x & 63, wave = FUSED ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : threadIdx.x >> 6;
   const int col = lane & 15, grp = lane >> 4;
   int ns = 0;   // cascade: shared leading blocks, attended by cascade_prefix_kernel
+  // fused: the row's position and cache slot are read before the K loads are issued, so that waiting
+  // for them (in-order vmcnt) does not also wait for K
+  int pos_b = 0, slot_b = -1;
   if constexpr (FUSED) {
     if (fz.nshared != nullptr) ns = *fz.nshared;
+    pos_b = __builtin_amdgcn_readfirstlane(fz.positions[b]);
+    slot_b = __builtin_amdgcn_readfirstlane(fz.slot_mapping[b]);
   }
   // fused: the chunk loop covers the cached tokens only; the new one is merged from LDS
   const int ctx = ctx_lens[b] - (FUSED ? 1 : 0) - ns * KBS;
@@ -135,10 +159,18 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
   const int nchunks = (ctx + 31) >> 5;
   const size_t head_stride = (size_t)KBS * HD;  // elements per (block, head)
   uint4 kr[2][4], vr[8];
+  // Chunk c's two 16-token blocks (the second used only when the chunk reaches past its first).  The
+  // fused kernel reads them with scalar loads (uniform wave index); the second entry shares the first
+  // one's scalar-cache line.  The second index is clamped to the row.
+  const int last_entry = max_blocks - ns - 1;
+  auto blocks = [&](int c, int& blk0, int& blk1) {
+    blk0 = bt[2 * c];
+    const int e1 = bt[min(2 * c + 1, last_entry)];
+    blk1 = (c * 32 + 16 < ctx) ? e1 : blk0;
+  };
   auto load_k = [&](int c) {
-    const int t0 = c * 32;
-    const int blk0 = bt[2 * c];
-    const int blk1 = (t0 + 16 < ctx) ? bt[2 * c + 1] : blk0;
+    int blk0, blk1;
+    blocks(c, blk0, blk1);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const bf16_t* kp = k_cache + ((size_t)(j ? blk1 : blk0) * hkv + h) * head_stride + col * HD + 8 * grp;
@@ -147,8 +179,9 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
     }
   };
   auto load_v = [&](int c) {
-    const int t0 = c * 32;
-    const int blk = (grp >> 1) ? ((t0 + 16 < ctx) ? bt[2 * c + 1] : bt[2 * c]) : bt[2 * c];
+    int blk0, blk1;
+    blocks(c, blk0, blk1);
+    const int blk = (grp >> 1) ? blk1 : blk0;
     const bf16_t* vp = v_cache + ((size_t)blk * hkv + h) * head_stride + col * KBS + 8 * (grp & 1);
 #pragma unroll
     for (int n = 0; n < 8; ++n) vr[n] = *reinterpret_cast<const uint4*>(vp + (size_t)n * 16 * KBS);
@@ -164,9 +197,12 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
     const int half = HD / 2;
     const size_t stride = (size_t)(hq + 2 * hkv) * HD;
     const size_t rowoff = (size_t)b * stride;
-    const float* cs = fz.cos_sin + (size_t)fz.positions[b] * HD;
-    const int slot = fz.slot_mapping[b];   // -1: padding row (no cache write, empty output)
+    const float* cs = fz.cos_sin + (size_t)pos_b * HD;
+    const int slot = slot_b;   // -1: padding row (no cache write, empty output)
     const int blk = slot >= 0 ? slot / KBS : 0, off = slot >= 0 ? slot % KBS : 0;
+    // the new value's 4 dims (threads < 32) loaded first, so their latency overlaps the q / k items'
+    uint2 vnew = make_uint2(0u, 0u);
+    if (threadIdx.x < HD / 4) vnew = dq_ld4(fz, rowoff + (size_t)(hq + hkv + h) * HD + threadIdx.x * 4);
     // (G query heads + 1 key head) x 16 items of 4 rotary pairs
     for (int it = threadIdx.x; it < (G + 1) * 16; it += 64 * NW) {
       const int hh = it >> 4, i = (it & 15) * 4;
@@ -198,7 +234,7 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
     // value: 32 items of 4 dims -> LDS and the dim-major cache slot
     if (threadIdx.x < HD / 4) {
       const int i = threadIdx.x * 4;
-      const uint2 v = dq_ld4(fz, rowoff + (size_t)(hq + hkv + h) * HD + i);
+      const uint2 v = vnew;
       *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(new_lds) + i) = v;
       if (slot >= 0) {
       bf16_t* vd = fz.v_cache + (((size_t)blk * hkv + h) * HD + i) * KBS + off;
@@ -248,7 +284,7 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
       }
       dot += __shfl_xor(dot, 16, 64);
       dot += __shfl_xor(dot, 32, 64);
-      if (grp == 0) new_lds[HD / 2 + col] = fz.slot_mapping[b] >= 0 ? dot * scale_log2 : -INFINITY;
+      if (grp == 0) new_lds[HD / 2 + col] = slot_b >= 0 ? dot * scale_log2 : -INFINITY;
     }
     __syncthreads();   // p_lds is the chunk loop's P scratch from here on
   }
@@ -263,9 +299,17 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
   for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   bf16_t* pw = p_lds[wave];
+  // Later chunks (contexts > 32 NW tokens): K(c) and V(c) are issued together at the loop's top (both
+  // register sets are free once PV(c - NW) has read vr), so a chunk waits one memory latency instead
+  // of two (K, then V after the QK).  Issue order = use order: the compiler's counted vmcnt wait lets
+  // K through while V is still in flight (plain loads retire in order).  Prefetching K(c + NW) during
+  // chunk c instead needs kr live across the softmax: 29 VGPRs of spills at 128.
   for (int c = wave; c < nchunks; c += NW) {
     const int t0 = c * 32;
-    if (c != wave) load_k(c);   // later chunks (contexts > 32 NW tokens): fetched in the loop
+    if (c != wave) {
+      load_k(c);
+      load_v(c);
+    }
     // ---- S = Q K^T for the two 16-token halves ----
     f32x4 s[2];
 #pragma unroll
@@ -275,8 +319,6 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
       for (int ks = 0; ks < 4; ++ks) acc = mfma16x16x32(qf[ks], as_bf16x8(kr[j][ks]), acc);
       s[j] = acc;
     }
-    // ---- V fragments (issued before the softmax so their latency hides under it) ----
-    if (c != wave) load_v(c);
     // ---- online softmax over this chunk ----
     float alpha[4];
 #pragma unroll

@@ -129,16 +129,20 @@ def test_paged_decode_padding_rows_zero():
 
 
 @pytest.mark.parametrize("hq,hkv,reps", [(32, 8, 1), (64, 8, 1), (4, 1, 1), (32, 8, 23), (64, 8, 23)])
-@pytest.mark.parametrize("split", [0, 1, 4, -1, -4])
-def test_decode_attention_rope_fused(hq, hkv, reps, split):
+@pytest.mark.parametrize("split", [0, 1, 4, 6, -1, -4, -6])
+@pytest.mark.parametrize("tight", [False, True])
+def test_decode_attention_rope_fused(hq, hkv, reps, split, tight):
     """RoPE + KV append + paged decode in one kernel == rope_kv_write then attention_decode (fp32
-    torch references), on bf16 qkv and on split-K partials; cache contents identical to the
-    unfused kernels'; a padding row (slot -1, ctx 0) writes nothing and returns zeros.  reps = 23:
-    161 rows x 8 kv heads > 1024 workgroups, the 2-wave variant."""
+    torch references), on bf16 qkv and on split-K partials (6: past the prologue's 4 unrolled
+    slices); cache contents identical to the unfused kernels'; a padding row (slot -1, ctx 0) writes
+    nothing and returns zeros.  reps = 23: 162 rows x 8 kv heads > 1024 workgroups, the 2-wave
+    variant.  tight: the block table is exactly as wide as the longest context needs (9
+    blocks for 137 tokens), so the 137-token rows' last chunk, which ends in its first block, reads
+    its clamped second table entry inside the row."""
     d, nb = 128, 400 * reps
-    ctx_lens = [1, 2, 17, 100, 129, 33] * reps + [0]
+    ctx_lens = [1, 2, 17, 100, 129, 33, 137] * reps + [0]
     S = len(ctx_lens)
-    bt = _tables(S, ctx_lens, nb, 16)
+    bt = _tables(S, ctx_lens, nb, (max(ctx_lens) + 15) // 16 if tight else 16)
     ctx = torch.tensor(ctx_lens, dtype=torch.int32, device=DEV)
     btc = bt.cpu()
     slots = torch.tensor([int(btc[s, (c - 1) // 16]) * 16 + (c - 1) % 16 if c > 0 else -1
