@@ -29,40 +29,77 @@ KA_DEV void ld_part8(const PT* p, f32x4& s0, f32x4& s1) {
   }
 }
 
+// Every load a thread needs (its split-K slices, the residual, the norm weight) is issued before the
+// first use: up to UNR slices unrolled, the rest (no plan uses them) in a loop.  A rolled slice loop
+// waited for each slice before issuing the next, so a split-4 norm paid ~6 serial memory latencies.
+// The slices are still summed in order k = 0, 1, ... (bitwise the old result).
+struct f32x8_raw {
+  f32x4 a, b;
+};
+template <typename PT, typename Raw>
+KA_DEV void unpack_part8(const Raw& r, f32x4& s0, f32x4& s1) {
+  if constexpr (sizeof(PT) == 4) {
+    s0 = r.a;
+    s1 = r.b;
+  } else {
+    s0 = f32x4{lo_f(r.x), hi_f(r.x), lo_f(r.y), hi_f(r.y)};
+    s1 = f32x4{lo_f(r.z), hi_f(r.z), lo_f(r.w), hi_f(r.w)};
+  }
+}
+
 template <int NT, int MAXV, typename PT = float>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16_t* __restrict__ out, bf16_t* __restrict__ residual,
                                                      const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                      int hidden, float eps, const PT* __restrict__ P, int split,
                                                      size_t pstride) {
+  constexpr int UNR = MAXV == 1 ? (NT >= 512 ? 8 : 4) : (MAXV == 2 ? 4 : 2);
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
   const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * hidden);
   uint4* rr = residual ? reinterpret_cast<uint4*>(residual + (size_t)row * hidden) : nullptr;
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
   float v[MAXV][8];
+  uint4 g[MAXV];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int idx = threadIdx.x + i * NT;
     if (idx < nvec) {
-      uint4 a;
+      uint4 a, b = make_uint4(0u, 0u, 0u, 0u);
+      g[i] = wr[idx];
       if (P != nullptr) {
         const PT* pr = P + (size_t)row * hidden + idx * 8;
+        // raw loads first (the unpack of a bf16 slice next to its load would wait for it right there)
+        using Raw = typename std::conditional<sizeof(PT) == 4, f32x8_raw, uint4>::type;
+        Raw t[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k)
+          if (k == 0 || k < split) t[k] = *reinterpret_cast<const Raw*>(pr + k * pstride);
+        if (rr) b = rr[idx];
         f32x4 s0, s1;
-        ld_part8(pr, s0, s1);
-#pragma unroll 4
-        for (int k = 1; k < split; ++k) {
-          f32x4 t0, t1;
-          ld_part8(pr + k * pstride, t0, t1);
-          s0 += t0;
-          s1 += t1;
+        unpack_part8<PT>(t[0], s0, s1);
+#pragma unroll
+        for (int k = 1; k < UNR; ++k) {
+          if (k < split) {
+            f32x4 u0, u1;
+            unpack_part8<PT>(t[k], u0, u1);
+            s0 += u0;
+            s1 += u1;
+          }
+        }
+        for (int k = UNR; k < split; ++k) {
+          f32x4 u0, u1;
+          ld_part8(pr + k * pstride, u0, u1);
+          s0 += u0;
+          s1 += u1;
         }
         a = make_uint4(pack2(s0[0], s0[1]), pack2(s0[2], s0[3]), pack2(s1[0], s1[1]), pack2(s1[2], s1[3]));
       } else {
         a = xr[idx];
+        if (rr) b = rr[idx];
       }
       uint32_t aw[4] = {a.x, a.y, a.z, a.w};
       if (rr) {
-        uint4 b = rr[idx];
         uint32_t bw[4] = {b.x, b.y, b.z, b.w};
         uint32_t o[4];
 #pragma unroll
@@ -94,14 +131,12 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16_t* __restrict__ out, b
 #pragma unroll
   for (int i = 0; i < NT / 64; ++i) tot += red[i];
   const float scale = rsqrtf(tot / (float)hidden + eps);
-  const uint4* wr = reinterpret_cast<const uint4*>(w);
   uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * hidden);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int idx = threadIdx.x + i * NT;
     if (idx < nvec) {
-      uint4 g = wr[idx];
-      uint32_t gw[4] = {g.x, g.y, g.z, g.w};
+      uint32_t gw[4] = {g[i].x, g[i].y, g[i].z, g[i].w};
       uint32_t o[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k)

@@ -28,22 +28,38 @@ __global__ __launch_bounds__(NT) void masked_argmax_kernel(int* __restrict__ out
   const int per = (nvec_all + gridDim.y - 1) / gridDim.y;
   const int v0 = blockIdx.y * per;
   const int nvec = min(nvec_all, v0 + per);
-  for (int v = v0 + threadIdx.x; v < nvec; v += NT) {
-    const int base = v << 3;
-    uint32_t bits = 0xffu;
-    if (mrow) {
-      const int gb = base + vocab_offset;  // mask is indexed by the global token id
-      bits = (mrow[gb >> 5] >> (gb & 31)) & 0xffu;
-      if (!bits) continue;
-    }
-    uint4 q = *reinterpret_cast<const uint4*>(lr + base);
-    uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  // Batches of UN vectors per lane: the UN mask words are loaded together, then the logits of the
+  // vectors with any bit set, then all are scanned.  One vector per iteration waited for its mask
+  // word and then for its logits: two serial memory latencies per 8 tokens per lane.  Within a lane
+  // the vectors are still scanned in increasing index order.
+  constexpr int UN = 8;
+  for (int v = v0 + threadIdx.x; v < nvec; v += NT * UN) {
+    uint32_t bits[UN], raw[UN];
+    uint4 q[UN];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float x = (k & 1) ? hi_f(w[k >> 1]) : lo_f(w[k >> 1]);
-      if (((bits >> k) & 1u) && x > best) {  // strict '>' keeps the lowest index within a lane
-        best = x;
-        bidx = base + k;
+    for (int j = 0; j < UN; ++j) {
+      const int gb = ((v + j * NT) << 3) + vocab_offset;   // the mask is indexed by the global token id
+      raw[j] = 0xffffffffu;
+      if (mrow && v + j * NT < nvec) raw[j] = mrow[gb >> 5];
+    }
+#pragma unroll
+    for (int j = 0; j < UN; ++j) {
+      const int gb = ((v + j * NT) << 3) + vocab_offset;
+      bits[j] = v + j * NT < nvec ? (mrow ? (raw[j] >> (gb & 31)) & 0xffu : 0xffu) : 0u;
+      if (bits[j]) q[j] = *reinterpret_cast<const uint4*>(lr + ((v + j * NT) << 3));
+    }
+#pragma unroll
+    for (int j = 0; j < UN; ++j) {
+      if (!bits[j]) continue;
+      const int base = (v + j * NT) << 3;
+      uint32_t w[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float x = (k & 1) ? hi_f(w[k >> 1]) : lo_f(w[k >> 1]);
+        if (((bits[j] >> k) & 1u) && x > best) {  // strict '>' keeps the lowest index within a lane
+          best = x;
+          bidx = base + k;
+        }
       }
     }
   }

@@ -503,9 +503,11 @@ def test_gemm_skinny(M, N, K):
         close(got, want, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("rows,hidden,split", [(1, 4096, 2), (37, 4096, 8), (256, 4096, 4), (5, 8192, 3)])
+@pytest.mark.parametrize("rows,hidden,split", [(1, 4096, 2), (37, 4096, 8), (256, 4096, 4), (5, 8192, 3),
+                                               (3, 4096, 12), (2, 1024, 6)])
 def test_rmsnorm_fused_splitk_reduce(rows, hidden, split):
-    """rmsnorm(SplitK partials, residual) == rmsnorm(bf16(sum partials), residual)."""
+    """rmsnorm(SplitK partials, residual) == rmsnorm(bf16(sum partials), residual).  split 12 / 6 go
+    past the kernel's unrolled slices (8 at 512 threads, 4 at 256) into its remainder loop."""
     P = torch.randn(split, rows, hidden, device=DEV) * 0.5
     w = (torch.rand(hidden, device=DEV) + 0.5).to(BF)
     res0 = torch.randn(rows, hidden, device=DEV).to(BF)
