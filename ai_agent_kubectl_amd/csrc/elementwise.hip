@@ -305,25 +305,22 @@ __global__ __launch_bounds__(256) void rope_kv_window_kernel(bf16_t* __restrict_
   const int nt = min(W, tokens - t0);
   const int qkv_stride = (hq + 2 * hkv) * d;
   // ---- q / k rotation: (hq + hkv) heads x 8 items of 8 rotary pairs per token, 16-B loads and
-  // stores; unrolled so each thread keeps several items' loads in flight (the window grid is small:
-  // ~2 workgroups per CU at an 8k-token step, so memory-level parallelism comes from the thread) ----
+  // stores.  The window's slots and positions are staged in LDS first, so no item's loads wait for a
+  // global read of its token's slot / position.  The grid is small (~1 workgroup per CU at a 4k-token
+  // step, one wave per SIMD), so memory-level parallelism has to come from the thread: on the bf16
+  // path each thread issues the loads of RU items before it rotates and stores any of them ----
+  __shared__ int s_slot[W], s_pos[W];
+  if (threadIdx.x < W) {
+    const int t = t0 + min((int)threadIdx.x, nt - 1);
+    s_slot[threadIdx.x] = slot_mapping[t];
+    s_pos[threadIdx.x] = positions[t];
+  }
+  __syncthreads();
   const int per_tok = (hq + hkv) * 8;
   const int n_items = nt * per_tok;
-#pragma unroll 4
-  for (int it = threadIdx.x; it < n_items; it += 256) {
-    const int j = it / per_tok, r = it - j * per_tok;
-    const int t = t0 + j;
-    const int h = r >> 3, i = (r & 7) * 8;
-    const bf16_t* row = qkv + (size_t)t * qkv_stride;
-    const float* prow = Pq ? Pq + (size_t)t * qkv_stride : nullptr;
-    const int slot = slot_mapping[t];
-    if (h >= hq && slot < 0) continue;
-    const float* cs = cos_sin + (size_t)positions[t] * d;
-    const uint4 a = ld8(row, prow, split, pstride, (size_t)h * d + i);
-    const uint4 b = ld8(row, prow, split, pstride, (size_t)h * d + i + half);
-    const float4 c0 = *reinterpret_cast<const float4*>(cs + i), c1 = *reinterpret_cast<const float4*>(cs + i + 4);
-    const float4 s0 = *reinterpret_cast<const float4*>(cs + half + i);
-    const float4 s1 = *reinterpret_cast<const float4*>(cs + half + i + 4);
+  auto rotate_store = [&](int j, int h, int i, const uint4& a, const uint4& b, const float4& c0, const float4& c1,
+                          const float4& s0, const float4& s1) {
+    const int t = t0 + j, slot = s_slot[j];
     const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {b.x, b.y, b.z, b.w};
     const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
     const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
@@ -338,6 +335,52 @@ __global__ __launch_bounds__(256) void rope_kv_window_kernel(bf16_t* __restrict_
                          : k_cache + (((size_t)(slot / bs) * hkv + (h - hq)) * bs + slot % bs) * d;
     *reinterpret_cast<uint4*>(dst + i) = make_uint4(o1[0], o1[1], o1[2], o1[3]);
     *reinterpret_cast<uint4*>(dst + i + half) = make_uint4(o2[0], o2[1], o2[2], o2[3]);
+  };
+  if (Pq == nullptr) {
+    constexpr int RU = 4;
+    for (int it0 = threadIdx.x; it0 < n_items; it0 += 256 * RU) {
+      uint4 a[RU], b[RU];
+      float4 c0[RU], c1[RU], s0[RU], s1[RU];
+      bool ok[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int it = it0 + u * 256;
+        const int j = it / per_tok, r = it - j * per_tok, h = r >> 3, i = (r & 7) * 8;
+        ok[u] = it < n_items && (h < hq || s_slot[j] >= 0);
+        if (ok[u]) {
+          const bf16_t* row = qkv + (size_t)(t0 + j) * qkv_stride + (size_t)h * d + i;
+          const float* cs = cos_sin + (size_t)s_pos[j] * d + i;
+          a[u] = *reinterpret_cast<const uint4*>(row);
+          b[u] = *reinterpret_cast<const uint4*>(row + half);
+          c0[u] = *reinterpret_cast<const float4*>(cs);
+          c1[u] = *reinterpret_cast<const float4*>(cs + 4);
+          s0[u] = *reinterpret_cast<const float4*>(cs + half);
+          s1[u] = *reinterpret_cast<const float4*>(cs + half + 4);
+        }
+      }
+      asm volatile("" ::: "memory");   // all RU items' loads are issued before the first rotation
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        if (!ok[u]) continue;
+        const int it = it0 + u * 256;
+        const int j = it / per_tok, r = it - j * per_tok;
+        rotate_store(j, r >> 3, (r & 7) * 8, a[u], b[u], c0[u], c1[u], s0[u], s1[u]);
+      }
+    }
+  } else {   // split-K partials: ld8 sums the slices
+#pragma unroll 4
+    for (int it = threadIdx.x; it < n_items; it += 256) {
+      const int j = it / per_tok, r = it - j * per_tok;
+      const int t = t0 + j;
+      const int h = r >> 3, i = (r & 7) * 8;
+      if (h >= hq && s_slot[j] < 0) continue;
+      const float* cs = cos_sin + (size_t)s_pos[j] * d;
+      const float* prow = Pq + (size_t)t * qkv_stride;
+      const uint4 a = ld8(nullptr, prow, split, pstride, (size_t)h * d + i);
+      const uint4 b = ld8(nullptr, prow, split, pstride, (size_t)h * d + i + half);
+      rotate_store(j, h, i, a, b, *reinterpret_cast<const float4*>(cs + i), *reinterpret_cast<const float4*>(cs + i + 4),
+                   *reinterpret_cast<const float4*>(cs + half + i), *reinterpret_cast<const float4*>(cs + half + i + 4));
+    }
   }
   // ---- V: per kv head, 16 tokens x 128 dims through LDS ----
   const int lj = threadIdx.x & 15;                  // store phase: lane -> token

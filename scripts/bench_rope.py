@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ai_agent_kubectl_amd import ops  # noqa: E402
 
 HQ, HKV, D, BS = 32, 8, 128, 16
-for T in (8035, 2944):
+for T in (8035, 4077, 2944):
     NB = T // BS + 600
     kc = torch.zeros(NB, HKV, BS, D, device="cuda", dtype=torch.bfloat16)
     vc = torch.zeros(NB, HKV, D, BS, device="cuda", dtype=torch.bfloat16)
