@@ -636,21 +636,23 @@ __device__ __forceinline__ void prefill_load_tile(u32x4 (&kreg)[2], u32x4 (&vreg
                                                   int nblocks, int tile, int h, int hkv) {
   const int tid = threadIdx.x;
   const size_t head_stride = (size_t)KBS * HD;
+  // the tile's two blocks, read once per workgroup as scalar loads (tile is uniform): a per-lane
+  // bt[bi] was a vector load that every K / V load of the tile waited for
+  const int i0 = 2 * tile < nblocks ? 2 * tile : 0, i1 = 2 * tile + 1 < nblocks ? 2 * tile + 1 : 0;
+  const int blk0 = bt[__builtin_amdgcn_readfirstlane(i0)], blk1 = bt[__builtin_amdgcn_readfirstlane(i1)];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int p = tid + 256 * i;           // 512 pieces of 16 B per operand
     // K: token = p >> 4, chunk = p & 15
     {
       const int tok = p >> 4, ch = p & 15;
-      const int bi = 2 * tile + (tok >> 4);
-      const int blk = bi < nblocks ? bt[bi] : bt[0];
+      const int blk = (tok >> 4) ? blk1 : blk0;
       kreg[i] = *reinterpret_cast<const u32x4*>(k_cache + ((size_t)blk * hkv + h) * head_stride + (tok & 15) * HD + ch * 8);
     }
     // V^T: dim = p >> 2, chunk = p & 3 (chunks 0,1 from the first block, 2,3 from the second)
     {
       const int dim = p >> 2, ch = p & 3;
-      const int bi = 2 * tile + (ch >> 1);
-      const int blk = bi < nblocks ? bt[bi] : bt[0];
+      const int blk = (ch >> 1) ? blk1 : blk0;
       vreg[i] = *reinterpret_cast<const u32x4*>(v_cache + ((size_t)blk * hkv + h) * head_stride + dim * KBS + (ch & 1) * 8);
     }
   }
