@@ -78,37 +78,85 @@ struct DecodeFuse {
   float* part_ml;     // [B, hq, 2]
 };
 
-// Up to DQ_UNROLL slices are loaded before the first add (a rolled loop waited for each slice's load
-// before issuing the next: `split` serial memory latencies in the kernel's prologue); more than that
-// (no plan uses it) continue in a loop.
+// The slices are loaded DQ_UNROLL at a time, each batch issued before its first add (a rolled loop
+// waited for each slice's load before issuing the next: `split` serial memory latencies in the
+// kernel's prologue; the TP = 8 rank's QKV runs split 12).  Summed in order k = 0, 1, ...
 constexpr int DQ_UNROLL = 4;
 __device__ __forceinline__ uint2 dq_ld4(const DecodeFuse& f, size_t off) {
   if (f.P == nullptr) return *reinterpret_cast<const uint2*>(f.qkv + off);
   f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
   if (f.pbf16) {   // bf16 slices (gemm_mfma EPI_P16): summed in fp32
     const bf16_t* pb = reinterpret_cast<const bf16_t*>(f.P);
-    uint2 q[DQ_UNROLL];
+    for (int k0 = 0; k0 < f.split; k0 += DQ_UNROLL) {
+      uint2 q[DQ_UNROLL];
 #pragma unroll
-    for (int k = 0; k < DQ_UNROLL; ++k)
-      if (k < f.split) q[k] = *reinterpret_cast<const uint2*>(pb + k * f.pstride + off);
+      for (int k = 0; k < DQ_UNROLL; ++k)
+        if (k0 + k < f.split) q[k] = *reinterpret_cast<const uint2*>(pb + (k0 + k) * f.pstride + off);
 #pragma unroll
-    for (int k = 0; k < DQ_UNROLL; ++k)
-      if (k < f.split) s += f32x4{lo_f(q[k].x), hi_f(q[k].x), lo_f(q[k].y), hi_f(q[k].y)};
-    for (int k = DQ_UNROLL; k < f.split; ++k) {
-      const uint2 r = *reinterpret_cast<const uint2*>(pb + k * f.pstride + off);
-      s += f32x4{lo_f(r.x), hi_f(r.x), lo_f(r.y), hi_f(r.y)};
+      for (int k = 0; k < DQ_UNROLL; ++k)
+        if (k0 + k < f.split) s += f32x4{lo_f(q[k].x), hi_f(q[k].x), lo_f(q[k].y), hi_f(q[k].y)};
     }
     return make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
   }
-  f32x4 p[DQ_UNROLL];
+  for (int k0 = 0; k0 < f.split; k0 += DQ_UNROLL) {
+    f32x4 p[DQ_UNROLL];
 #pragma unroll
-  for (int k = 0; k < DQ_UNROLL; ++k)
-    if (k < f.split) p[k] = *reinterpret_cast<const f32x4*>(f.P + k * f.pstride + off);
+    for (int k = 0; k < DQ_UNROLL; ++k)
+      if (k0 + k < f.split) p[k] = *reinterpret_cast<const f32x4*>(f.P + (k0 + k) * f.pstride + off);
 #pragma unroll
-  for (int k = 0; k < DQ_UNROLL; ++k)
-    if (k < f.split) s += p[k];
-  for (int k = DQ_UNROLL; k < f.split; ++k) s += *reinterpret_cast<const f32x4*>(f.P + k * f.pstride + off);
+    for (int k = 0; k < DQ_UNROLL; ++k)
+      if (k0 + k < f.split) s += p[k];
+  }
   return make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
+}
+
+// N reads of dq_ld4 at once (a thread's q / k rotary halves and its new-value dims): every batch
+// issues the N reads' slices together, so the N reductions cost one round trip per batch, not N.
+template <int N>
+__device__ __forceinline__ void dq_ld4n(const DecodeFuse& f, const size_t (&off)[N], const bool (&en)[N],
+                                        uint2 (&out)[N]) {
+  if (f.P == nullptr) {
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+      if (en[n]) out[n] = *reinterpret_cast<const uint2*>(f.qkv + off[n]);
+    return;
+  }
+  f32x4 s[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) s[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (f.pbf16) {
+    const bf16_t* pb = reinterpret_cast<const bf16_t*>(f.P);
+    for (int k0 = 0; k0 < f.split; k0 += DQ_UNROLL) {
+      uint2 q[DQ_UNROLL][N];
+#pragma unroll
+      for (int k = 0; k < DQ_UNROLL; ++k)
+#pragma unroll
+        for (int n = 0; n < N; ++n)
+          if (en[n] && k0 + k < f.split) q[k][n] = *reinterpret_cast<const uint2*>(pb + (k0 + k) * f.pstride + off[n]);
+#pragma unroll
+      for (int k = 0; k < DQ_UNROLL; ++k)
+#pragma unroll
+        for (int n = 0; n < N; ++n)
+          if (en[n] && k0 + k < f.split) s[n] += f32x4{lo_f(q[k][n].x), hi_f(q[k][n].x), lo_f(q[k][n].y), hi_f(q[k][n].y)};
+    }
+  } else {   // fp32 slices: half the batch (twice the registers per slice)
+    constexpr int U = DQ_UNROLL / 2;
+    for (int k0 = 0; k0 < f.split; k0 += U) {
+      f32x4 p[U][N];
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+#pragma unroll
+        for (int n = 0; n < N; ++n)
+          if (en[n] && k0 + k < f.split) p[k][n] = *reinterpret_cast<const f32x4*>(f.P + (k0 + k) * f.pstride + off[n]);
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+#pragma unroll
+        for (int n = 0; n < N; ++n)
+          if (en[n] && k0 + k < f.split) s[n] += p[k][n];
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) out[n] = make_uint2(pack2(s[n][0], s[n][1]), pack2(s[n][2], s[n][3]));
 }
 
 // NW = waves per workgroup.  4: wave w takes the 32-token chunks w, w + 4, ... (one chunk each at
@@ -200,15 +248,19 @@ __global__ __launch_bounds__(64 * NW, 4) void paged_decode_kernel(bf16_t* __rest
     const float* cs = fz.cos_sin + (size_t)pos_b * HD;
     const int slot = slot_b;   // -1: padding row (no cache write, empty output)
     const int blk = slot >= 0 ? slot / KBS : 0, off = slot >= 0 ? slot % KBS : 0;
-    // the new value's 4 dims (threads < 32) loaded first, so their latency overlaps the q / k items'
+    // (G query heads + 1 key head) x 16 items of 4 rotary pairs; in its first item a thread < 32 also
+    // reads the new value's 4 dims, in the same batches as the item's two halves ((G + 1) * 16 >= 32)
     uint2 vnew = make_uint2(0u, 0u);
-    if (threadIdx.x < HD / 4) vnew = dq_ld4(fz, rowoff + (size_t)(hq + hkv + h) * HD + threadIdx.x * 4);
-    // (G query heads + 1 key head) x 16 items of 4 rotary pairs
     for (int it = threadIdx.x; it < (G + 1) * 16; it += 64 * NW) {
       const int hh = it >> 4, i = (it & 15) * 4;
       const size_t col0 = hh < G ? (size_t)(h * G + hh) * HD : (size_t)(hq + h) * HD;
-      const uint2 a = dq_ld4(fz, rowoff + col0 + i);
-      const uint2 c2 = dq_ld4(fz, rowoff + col0 + i + half);
+      const size_t offs[3] = {rowoff + col0 + i, rowoff + col0 + i + half,
+                              rowoff + (size_t)(hq + hkv + h) * HD + threadIdx.x * 4};
+      const bool en[3] = {true, true, it == (int)threadIdx.x && threadIdx.x < HD / 4};
+      uint2 rd[3];
+      dq_ld4n<3>(fz, offs, en, rd);
+      if (en[2]) vnew = rd[2];
+      const uint2 a = rd[0], c2 = rd[1];
       const float4 c = *reinterpret_cast<const float4*>(cs + i);
       const float4 sn = *reinterpret_cast<const float4*>(cs + half + i);
       const float x1[4] = {lo_f(a.x), hi_f(a.x), lo_f(a.y), hi_f(a.y)};

@@ -30,7 +30,7 @@ KA_DEV void ld_part8(const PT* p, f32x4& s0, f32x4& s1) {
 }
 
 // Every load a thread needs (its split-K slices, the residual, the norm weight) is issued before the
-// first use: up to UNR slices unrolled, the rest (no plan uses them) in a loop.  A rolled slice loop
+// first use: up to UNR slices unrolled, further slices UNR at a time.  A rolled slice loop
 // waited for each slice before issuing the next, so a split-4 norm paid ~6 serial memory latencies.
 // The slices are still summed in order k = 0, 1, ... (bitwise the old result).
 struct f32x8_raw {
@@ -87,11 +87,19 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16_t* __restrict__ out, b
             s1 += u1;
           }
         }
-        for (int k = UNR; k < split; ++k) {
-          f32x4 u0, u1;
-          ld_part8(pr + k * pstride, u0, u1);
-          s0 += u0;
-          s1 += u1;
+        for (int k0 = UNR; k0 < split; k0 += UNR) {   // further slices, UNR loads per wait
+#pragma unroll
+          for (int k = 0; k < UNR; ++k)
+            if (k0 + k < split) t[k] = *reinterpret_cast<const Raw*>(pr + (k0 + k) * pstride);
+#pragma unroll
+          for (int k = 0; k < UNR; ++k) {
+            if (k0 + k < split) {
+              f32x4 u0, u1;
+              unpack_part8<PT>(t[k], u0, u1);
+              s0 += u0;
+              s1 += u1;
+            }
+          }
         }
         a = make_uint4(pack2(s0[0], s0[1]), pack2(s0[2], s0[3]), pack2(s1[0], s1[1]), pack2(s1[2], s1[3]));
       } else {
