@@ -216,17 +216,58 @@ extern "C" int ka_rmsnorm_splitk(void* out, void* residual, const void* P, int s
 // RoPE (neox / rotate-half pairs (i, i + D/2)) on q and k, q -> q_out [T, Hq, D], k and v -> paged cache.
 // With P != nullptr the qkv row is the bf16-rounded sum of `split` fp32 split-K partial slabs of the
 // QKV projection (bit-identical to splitk_reduce_kernel + this kernel, one launch and HBM pass fewer).
+// The split-K slices are loaded SK_BATCH at a time, each batch issued before its first add (a rolled
+// loop waited for every slice before issuing the next); summed in order k = 0, 1, ...  N reads
+// (e.g. the gate and up halves of silu_mul) share each batch.
+constexpr int SK_BATCH = 4;
+template <int N>
+__device__ __forceinline__ void sum8_slices(const float* P, int split, size_t pstride, const size_t (&off)[N],
+                                            f32x4 (&lo)[N], f32x4 (&hi)[N]) {
+#pragma unroll
+  for (int n = 0; n < N; ++n) lo[n] = hi[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < split; k0 += SK_BATCH) {
+    f32x4 a[SK_BATCH][N], b[SK_BATCH][N];
+#pragma unroll
+    for (int k = 0; k < SK_BATCH; ++k)
+#pragma unroll
+      for (int n = 0; n < N; ++n)
+        if (k0 + k < split) {
+          a[k][n] = *reinterpret_cast<const f32x4*>(P + (k0 + k) * pstride + off[n]);
+          b[k][n] = *reinterpret_cast<const f32x4*>(P + (k0 + k) * pstride + off[n] + 4);
+        }
+#pragma unroll
+    for (int k = 0; k < SK_BATCH; ++k)
+#pragma unroll
+      for (int n = 0; n < N; ++n)
+        if (k0 + k < split) {
+          lo[n] += a[k][n];
+          hi[n] += b[k][n];
+        }
+  }
+}
+
 __device__ __forceinline__ uint2 ld4(const bf16_t* row, const float* P, int split, size_t pstride, size_t off) {
   if (P == nullptr) return *reinterpret_cast<const uint2*>(row + off);
-  f32x4 s = *reinterpret_cast<const f32x4*>(P + off);
-  for (int k = 1; k < split; ++k) s += *reinterpret_cast<const f32x4*>(P + k * pstride + off);
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < split; k0 += SK_BATCH) {
+    f32x4 a[SK_BATCH];
+#pragma unroll
+    for (int k = 0; k < SK_BATCH; ++k)
+      if (k0 + k < split) a[k] = *reinterpret_cast<const f32x4*>(P + (k0 + k) * pstride + off);
+#pragma unroll
+    for (int k = 0; k < SK_BATCH; ++k)
+      if (k0 + k < split) s += a[k];
+  }
   return make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
 }
 
 __device__ __forceinline__ uint4 ld8(const bf16_t* row, const float* P, int split, size_t pstride, size_t off) {
   if (P == nullptr) return *reinterpret_cast<const uint4*>(row + off);
-  const uint2 a = ld4(row, P, split, pstride, off), b = ld4(row, P, split, pstride, off + 4);
-  return make_uint4(a.x, a.y, b.x, b.y);
+  const size_t o[1] = {off};
+  f32x4 lo[1], hi[1];
+  sum8_slices<1>(P, split, pstride, o, lo, hi);
+  return make_uint4(pack2(lo[0][0], lo[0][1]), pack2(lo[0][2], lo[0][3]), pack2(hi[0][0], hi[0][1]),
+                    pack2(hi[0][2], hi[0][3]));
 }
 
 __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_cache,
@@ -481,8 +522,17 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(bf16_t* __restrict__ out,
     const size_t roff = (size_t)t * 2 * (size_t)inter;
     const bf16_t* r = gu ? gu + roff : nullptr;
     const float* pr = P ? P + roff : nullptr;
-    uint4 g = ld8(r, pr, split, pstride, c);
-    uint4 u = ld8(r, pr, split, pstride, (size_t)inter + c);
+    uint4 g, u;
+    if (pr == nullptr) {
+      g = *reinterpret_cast<const uint4*>(r + c);
+      u = *reinterpret_cast<const uint4*>(r + inter + c);
+    } else {   // the gate and up slices in the same batches
+      const size_t o[2] = {(size_t)c, (size_t)inter + c};
+      f32x4 lo[2], hi[2];
+      sum8_slices<2>(pr, split, pstride, o, lo, hi);
+      g = make_uint4(pack2(lo[0][0], lo[0][1]), pack2(lo[0][2], lo[0][3]), pack2(hi[0][0], hi[0][1]), pack2(hi[0][2], hi[0][3]));
+      u = make_uint4(pack2(lo[1][0], lo[1][1]), pack2(lo[1][2], lo[1][3]), pack2(hi[1][0], hi[1][1]), pack2(hi[1][2], hi[1][3]));
+    }
     uint32_t gw[4] = {g.x, g.y, g.z, g.w}, uw[4] = {u.x, u.y, u.z, u.w}, o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
