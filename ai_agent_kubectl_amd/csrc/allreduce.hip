@@ -74,12 +74,20 @@ __global__ __launch_bounds__(512) void allreduce_oneshot_kernel(ArArgs a, const 
 
   for (int i = beg + threadIdx.x * 8; i < end; i += blockDim.x * 8) {
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int p = 0; p < world; ++p) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(a.data[p] + half + i);
+    // every peer's piece is loaded before the first add (one remote round trip, not `world`);
+    // summed in rank order
+    u32x4 v[AR_MAX_RANKS];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s[2 * j] += lo_f(v[j]);
-        s[2 * j + 1] += hi_f(v[j]);
+    for (int p = 0; p < AR_MAX_RANKS; ++p)
+      if (p < world) v[p] = *reinterpret_cast<const u32x4*>(a.data[p] + half + i);
+#pragma unroll
+    for (int p = 0; p < AR_MAX_RANKS; ++p) {
+      if (p < world) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s[2 * j] += lo_f(v[p][j]);
+          s[2 * j + 1] += hi_f(v[p][j]);
+        }
       }
     }
     u32x4 o;
@@ -176,23 +184,46 @@ __global__ __launch_bounds__(512) void allreduce_rmsnorm_kernel(ArArgs a, const 
       *reinterpret_cast<u32x4*>(mine + i) = *reinterpret_cast<const u32x4*>(src + i);
   } else {
     const size_t ps = (size_t)rows * hidden;   // elements per slab
+    // the slabs are loaded AR_SK_BATCH at a time, each batch issued before its first add (a rolled
+    // loop waited for every slab); summed in slab order
+    constexpr int AR_SK_BATCH = 4;
     for (int i = beg + threadIdx.x * 8; i < end; i += blockDim.x * 8) {
       float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int z = 0; z < split; ++z) {
+      for (int z0 = 0; z0 < split; z0 += AR_SK_BATCH) {
         if (in_bf16) {
-          const u32x4 v = *reinterpret_cast<const u32x4*>(static_cast<const bf16_t*>(in) + z * ps + i);
+          u32x4 v[AR_SK_BATCH];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            s[2 * k] += lo_f(v[k]);
-            s[2 * k + 1] += hi_f(v[k]);
+          for (int z = 0; z < AR_SK_BATCH; ++z)
+            if (z0 + z < split) v[z] = *reinterpret_cast<const u32x4*>(static_cast<const bf16_t*>(in) + (z0 + z) * ps + i);
+#pragma unroll
+          for (int z = 0; z < AR_SK_BATCH; ++z) {
+            if (z0 + z < split) {
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                s[2 * k] += lo_f(v[z][k]);
+                s[2 * k + 1] += hi_f(v[z][k]);
+              }
+            }
           }
         } else {
-          const float* f = static_cast<const float*>(in) + z * ps + i;
-          const f32x4 v0 = *reinterpret_cast<const f32x4*>(f), v1 = *reinterpret_cast<const f32x4*>(f + 4);
+          f32x4 v0[AR_SK_BATCH], v1[AR_SK_BATCH];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            s[k] += v0[k];
-            s[4 + k] += v1[k];
+          for (int z = 0; z < AR_SK_BATCH; ++z) {
+            if (z0 + z < split) {
+              const float* f = static_cast<const float*>(in) + (z0 + z) * ps + i;
+              v0[z] = *reinterpret_cast<const f32x4*>(f);
+              v1[z] = *reinterpret_cast<const f32x4*>(f + 4);
+            }
+          }
+#pragma unroll
+          for (int z = 0; z < AR_SK_BATCH; ++z) {
+            if (z0 + z < split) {
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                s[k] += v0[z][k];
+                s[4 + k] += v1[z][k];
+              }
+            }
           }
         }
       }
@@ -223,17 +254,26 @@ __global__ __launch_bounds__(512) void allreduce_rmsnorm_kernel(ArArgs a, const 
       if (idx >= nvec) continue;
       const size_t e = (size_t)row * hidden + idx * 8;
       float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int p = 0; p < world; ++p) {
-        const u32x4 pv = *reinterpret_cast<const u32x4*>(a.data[p] + half + e);
+      // every peer's contribution (and the residual) is loaded before the first add, so the peer
+      // reads over xGMI overlap instead of costing one remote round trip each; summed in rank order
+      u32x4 pv[AR_MAX_RANKS];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          s[2 * k] += lo_f(pv[k]);
-          s[2 * k + 1] += hi_f(pv[k]);
+      for (int p = 0; p < AR_MAX_RANKS; ++p)
+        if (p < world) pv[p] = *reinterpret_cast<const u32x4*>(a.data[p] + half + e);
+      u32x4 b = u32x4{0u, 0u, 0u, 0u};
+      if (residual != nullptr) b = *reinterpret_cast<const u32x4*>(residual + e);
+#pragma unroll
+      for (int p = 0; p < AR_MAX_RANKS; ++p) {
+        if (p < world) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            s[2 * k] += lo_f(pv[p][k]);
+            s[2 * k + 1] += hi_f(pv[p][k]);
+          }
         }
       }
       uint32_t o[4];
       if (residual != nullptr) {
-        const u32x4 b = *reinterpret_cast<const u32x4*>(residual + e);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const uint32_t aw = pack2(s[2 * k], s[2 * k + 1]);   // the all-reduce output, bf16

@@ -567,7 +567,7 @@ KA_DEV void rmsnorm_rows_to_lds(const Args& a, const float* res, const bf16_t* g
 // of a hang), then sums the peers' rows in rank order.  Alternating halves: a rank rewrites half h at
 // epoch e + 2 only after every peer's workgroup wg signalled e + 1, i.e. finished reading e.
 // v[b] = this lane's partial of row `row` (valid when `mine`); returns the sum over ranks.
-template <int B>
+template <int B, int RG>
 KA_DEV void xreduce(const Args& a, unsigned epoch, int wg, int row, bool mine, float (&v)[B], int* err) {
   const size_t hb = (size_t)MAXB * a.H, half = (size_t)(epoch & 1u) * hb;
   if (mine) {
@@ -593,11 +593,25 @@ KA_DEV void xreduce(const Args& a, unsigned epoch, int wg, int row, bool mine, f
   }
   __syncthreads();
   if (mine) {
+    // the peers' rows are loaded XB at a time, each batch before its first add (2 remote round
+    // trips at TP = 8 instead of 8; a batch of 8 spills at this kernel's 256-VGPR budget, and so does
+    // a batch of 4 in the B = 2 / 16-slot instantiation, which keeps one peer per round trip);
+    // summed in rank order
+    constexpr int XB = (B == 2 && RG == 16) ? 1 : 4;
 #pragma unroll
     for (int b = 0; b < B; ++b) {
       float sum = 0.f;
-      for (int p = 0; p < a.world; ++p)
-        sum += __hip_atomic_load(a.xdata[p] + half + (size_t)b * a.H + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (int p0 = 0; p0 < a.world; p0 += XB) {
+        float pv[XB];
+#pragma unroll
+        for (int p = 0; p < XB; ++p)
+          if (p0 + p < a.world)
+            pv[p] = __hip_atomic_load(a.xdata[p0 + p] + half + (size_t)b * a.H + row, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+        for (int p = 0; p < XB; ++p)
+          if (p0 + p < a.world) sum += pv[p];
+      }
       v[b] = sum;
     }
   }
@@ -946,7 +960,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
       RowVals<B> v = so.run(xaddr, (uint32_t)xhb);
       so.drain();
       // (leader workgroups own no O rows on any rank: they take no part in its all-reduce)
-      if (tp && !leader) xreduce<B>(a, ebase + 2u * (unsigned)l + 1u, wg, ow0 + lane, lane < n_o, v.v, err);
+      if (tp && !leader) xreduce<B, RG>(a, ebase + 2u * (unsigned)l + 1u, wg, ow0 + lane, lane < n_o, v.v, err);
 #pragma unroll
       for (int b = 0; b < B; ++b) {
         float* const rr = a.res + (size_t)b * H + ow0 + lane;
@@ -995,7 +1009,7 @@ __global__ __launch_bounds__(NT, 1) void decode_layers_kernel(Args a) {
     {
       RowVals<B> v = sd.run(xaddr, (uint32_t)xsb);
       sd.drain();
-      if (tp) xreduce<B>(a, ebase + 2u * (unsigned)l + 2u, wg, own0 + lane, lane < no, v.v, err);
+      if (tp) xreduce<B, RG>(a, ebase + 2u * (unsigned)l + 2u, wg, own0 + lane, lane < no, v.v, err);
 #pragma unroll
       for (int b = 0; b < B; ++b) {
         float* const rr = a.res + (size_t)b * H + own0 + lane;
