@@ -252,13 +252,22 @@ static int gemv_ring_depth() {
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(bf16_t* __restrict__ Y, const float* __restrict__ P,
                                                             int split, long mn) {
   for (long i = (blockIdx.x * (long)blockDim.x + threadIdx.x) * 4; i < mn; i += (long)gridDim.x * blockDim.x * 4) {
-    float4 s = *reinterpret_cast<const float4*>(P + i);
-    for (int k = 1; k < split; ++k) {
-      const float4 t = *reinterpret_cast<const float4*>(P + (size_t)k * mn + i);
-      s.x += t.x;
-      s.y += t.y;
-      s.z += t.z;
-      s.w += t.w;
+    // slices 4 at a time, each batch issued before its first add (summed in slice order)
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k0 = 0; k0 < split; k0 += 4) {
+      float4 t[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k0 + k < split) t[k] = *reinterpret_cast<const float4*>(P + (size_t)(k0 + k) * mn + i);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k0 + k < split) {
+          s.x += t[k].x;
+          s.y += t[k].y;
+          s.z += t[k].z;
+          s.w += t[k].w;
+        }
+      }
     }
     *reinterpret_cast<uint2*>(Y + i) = make_uint2(pack2(s.x, s.y), pack2(s.z, s.w));
   }

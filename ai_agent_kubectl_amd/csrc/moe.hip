@@ -158,10 +158,24 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(bf16_t* __restrict__ o
       const float w = topk_w[t * k + j];
       if (P != nullptr) {   // the expert GEMM's split-K slices: reduce them here (fp32, no bf16 round)
         const float* pr = P + ((size_t)t * k + j) * H + c;
-        f32x4 y0 = *reinterpret_cast<const f32x4*>(pr), y1 = *reinterpret_cast<const f32x4*>(pr + 4);
-        for (int s2 = 1; s2 < split; ++s2) {
-          y0 += *reinterpret_cast<const f32x4*>(pr + s2 * pstride);
-          y1 += *reinterpret_cast<const f32x4*>(pr + s2 * pstride + 4);
+        // slices 4 at a time, each batch issued before its first add (summed in slice order)
+        f32x4 y0 = f32x4{0.f, 0.f, 0.f, 0.f}, y1 = y0;
+        for (int s0 = 0; s0 < split; s0 += 4) {
+          f32x4 a[4], b[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (s0 + q < split) {
+              a[q] = *reinterpret_cast<const f32x4*>(pr + (s0 + q) * pstride);
+              b[q] = *reinterpret_cast<const f32x4*>(pr + (s0 + q) * pstride + 4);
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (s0 + q < split) {
+              y0 += a[q];
+              y1 += b[q];
+            }
+          }
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
