@@ -35,7 +35,8 @@ BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 51
 if os.environ.get("PLAN_BUCKETS"):   # re-tune (and re-write) only these buckets, e.g. "1,2,4"
     BUCKETS = tuple(int(b) for b in os.environ["PLAN_BUCKETS"].split(","))
 # "prefill": re-tune only the prefill section (after a gemm_big change); "epilogues": only the lm_head and
-# decode_swiglu sections (the fused gemm_big / ring-kernel epilogues against the unfused plan)
+# decode_swiglu sections (the fused gemm_big / ring-kernel epilogues against the unfused plan); "decode":
+# only the decode GEMM plan (after a change to a consumer the plan times with, e.g. the norm)
 ONLY = os.environ.get("PLAN_ONLY", "")
 for model in sys.argv[1:] or ["llama3-8b"]:
     eng = build_engine(EngineOptions(model=model, device="cuda", max_batch=max(BUCKETS), graph_buckets=BUCKETS,
@@ -48,11 +49,11 @@ for model in sys.argv[1:] or ["llama3-8b"]:
         os.environ["KA_GEMM_PLAN"] = "file"
         print(model, "GEMM plan:", eng.runner.autotune(), flush=True)
         os.environ["KA_GEMM_PLAN"] = "write"
-    if ONLY != "prefill":
+    if ONLY not in ("prefill", "decode"):
         # the engine-start decisions persisted next to the plan (sections lm_head / decode_swiglu)
         print("lm_head:", eng.runner.tune_lm_head(), flush=True)
         print("decode_swiglu:", eng.runner.tune_swiglu(), flush=True)
-    if ONLY != "epilogues":
+    if ONLY not in ("epilogues", "decode"):
         print("prefill:", eng.runner.tune_prefill(), flush=True)
     if COPY_TO:
         os.makedirs(COPY_TO, exist_ok=True)
