@@ -192,6 +192,9 @@ static void launch_rmsnorm_splitk(bf16_t* o, bf16_t* r, const PT* p, int split, 
   else if (nvec <= 512)   // the split slabs are read once: 8 waves per row keep more loads in flight
     hipLaunchKernelGGL((rmsnorm_kernel<512, 1, PT>), dim3(rows), dim3(512), 0, stream, o, r, nullptr, wi, hidden, eps,
                        p, split, ps);
+  else if (nvec <= 1024 && rows <= 1024)   // hidden 8192 at decode sizes: 8 waves, 4 slices per batch
+    hipLaunchKernelGGL((rmsnorm_kernel<512, 2, PT>), dim3(rows), dim3(512), 0, stream, o, r, nullptr, wi, hidden, eps,
+                       p, split, ps);
   else
     hipLaunchKernelGGL((rmsnorm_kernel<256, 4, PT>), dim3(rows), dim3(256), 0, stream, o, r, nullptr, wi, hidden, eps,
                        p, split, ps);
