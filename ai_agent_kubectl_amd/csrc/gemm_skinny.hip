@@ -179,14 +179,33 @@ __global__ __launch_bounds__(256) void gemv_ring_kernel(const bf16_t* __restrict
     w[r][0] = *reinterpret_cast<const uint4*>(wp + c * 64);
     w[r][1] = *reinterpret_cast<const uint4*>(wp + c * 64 + 32);
   }
-  for (int p = tid; p < M * pr; p += 256) {
-    const int row = p / pr, pc = p - row * pr;
-    if constexpr (SWIGLU) {
-      const bf16_t* g = X + (size_t)row * 2 * K + k_begin + pc * 8;
-      const u32x4 v = swiglu8(*reinterpret_cast<const u32x4*>(g), *reinterpret_cast<const u32x4*>(g + K));
-      xsd[row * pr + (pc ^ (row & 7))] = __builtin_bit_cast(uint4, v);
-    } else {
-      xsd[row * pr + (pc ^ (row & 7))] = *reinterpret_cast<const uint4*>(X + (size_t)row * K + k_begin + pc * 8);
+  // X staged XB pieces per thread per batch, every batch's loads issued before its LDS stores (one
+  // piece per iteration waited for each piece's L2 round trip: M * pr / 256 of them in sequence)
+  constexpr int XB = 4;
+  for (int p0 = tid; p0 < M * pr; p0 += 256 * XB) {
+    u32x4 xa[XB], xb[XB];
+#pragma unroll
+    for (int j = 0; j < XB; ++j) {
+      const int p = p0 + j * 256;
+      if (p < M * pr) {
+        const int row = p / pr, pc = p - row * pr;
+        if constexpr (SWIGLU) {
+          const bf16_t* g = X + (size_t)row * 2 * K + k_begin + pc * 8;
+          xa[j] = *reinterpret_cast<const u32x4*>(g);
+          xb[j] = *reinterpret_cast<const u32x4*>(g + K);
+        } else {
+          xa[j] = *reinterpret_cast<const u32x4*>(X + (size_t)row * K + k_begin + pc * 8);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < XB; ++j) {
+      const int p = p0 + j * 256;
+      if (p < M * pr) {
+        const int row = p / pr, pc = p - row * pr;
+        const u32x4 v = SWIGLU ? swiglu8(xa[j], xb[j]) : xa[j];
+        xsd[row * pr + (pc ^ (row & 7))] = __builtin_bit_cast(uint4, v);
+      }
     }
   }
   __syncthreads();
@@ -235,9 +254,23 @@ __global__ __launch_bounds__(256) void gemv_ring_kernel(const bf16_t* __restrict
 
 // KA_GEMV_RING: ring depth 4 (default) or 8, 0 disables the variant (A/B runs).  Measured on
 // MI355X against the staged kernel (profiles/gemv_ring_ab.txt): ring 4 wins O / gate_up at
-// M = 1..4 by 3-10 %, ring 8 is no better, and at M = 16 the staged kernel is faster (QKV 14.5
-// vs 17.9 us), so the variant serves M <= GEMV_MAX_M.
-#define GEMV_MAX_M 4
+// M = 1..4 by 3-10 %, ring 8 is no better, and at M = 16 the staged kernel was faster (QKV 14.5
+// vs 17.9 us) while the X staging loaded one piece per wait.  With the staging batched (round 6,
+// profiles/r6/latency_chains/gemv_*): up to 8 rows the 70B TP = 8 rank's B = 8 step is 2.2 % faster on
+// the ring variant and Llama-3-8B's B = 8 within 0.4 %; 16 rows is 1.5 % slower on the 8B.
+#define GEMV_MAX_M 8
+#define GEMV_SWIGLU_MAX_M 4   // ka_gemv_swiglu (ops.GEMV_SWIGLU_MAX_M)
+// KA_GEMV_MAX_M: rows up to which ka_gemm_skinny takes the ring variant (default GEMV_MAX_M; <= 16, one
+// MFMA row tile) — an A/B switch for the batched X staging
+static int gemv_max_m() {
+  static int mm = -1;
+  if (mm < 0) {
+    const char* e = getenv("KA_GEMV_MAX_M");
+    mm = e ? atoi(e) : GEMV_MAX_M;
+    if (mm < 0 || mm > 16) mm = GEMV_MAX_M;
+  }
+  return mm;
+}
 static int gemv_ring_depth() {
   static int ring = -1;
   if (ring < 0) {
@@ -444,7 +477,7 @@ extern "C" int ka_gemm_skinny(void* Y, const void* X, const void* W, void* works
   const int mt = (M + 15) / 16;
   const size_t gemv_lds = (size_t)M * kps * 2;
   const int ring = gemv_ring_depth();
-  if (M <= GEMV_MAX_M && ring > 0 && gemv_lds <= 65536) {
+  if (M <= gemv_max_m() && ring > 0 && gemv_lds <= 65536) {
     dim3 grid((N + NW - 1) / NW, split);
     if (ring == 4)
       hipLaunchKernelGGL(gemv_ring_kernel<4>, grid, dim3(256), gemv_lds, stream, x, w, y, p, M, N, K, kps);
@@ -462,14 +495,14 @@ extern "C" int ka_gemm_skinny(void* Y, const void* X, const void* W, void* works
   KA_CHECK_LAUNCH();
 }
 
-// Y = swiglu(GU) * W^T for M <= GEMV_MAX_M (GU = [M, 2K] gate | up): the batch-1..4 down projection
+// Y = swiglu(GU) * W^T for M <= GEMV_SWIGLU_MAX_M (GU = [M, 2K] gate | up): the batch-1..4 down projection
 // with the SiLU*mul computed while staging X.  split > 1 needs the split * M * N float workspace;
 // Y == nullptr leaves the partials for a fused consumer.  Returns hipErrorInvalidValue for shapes
 // this path does not take (the caller then runs silu_mul + linear).
 extern "C" int ka_gemv_swiglu(void* Y, const void* GU, const void* W, void* workspace, int M, int N, int K,
                               int split, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (M > GEMV_MAX_M || K % 64 != 0 || N % 4 != 0 || split < 1) return (int)hipErrorInvalidValue;
+  if (M > GEMV_SWIGLU_MAX_M || K % 64 != 0 || N % 4 != 0 || split < 1) return (int)hipErrorInvalidValue;
   int kps = (K / split + 63) / 64 * 64;
   split = (K + kps - 1) / kps;
   const size_t lds = (size_t)M * kps * 2;

@@ -695,7 +695,7 @@ def linear_rows(x: torch.Tensor, w: torch.Tensor, split: int, rw: int, defer_red
     return y
 
 
-GEMV_SWIGLU_MAX_M = 4   # csrc/gemm_skinny.hip GEMV_MAX_M
+GEMV_SWIGLU_MAX_M = 4   # csrc/gemm_skinny.hip GEMV_SWIGLU_MAX_M
 
 
 def swiglu_linear(gu, w: torch.Tensor, defer_reduce: bool = False, bf16_partials: bool = False):
